@@ -1,0 +1,284 @@
+// oracle_api.cpp — TEST INFRASTRUCTURE ONLY: C ABI over the CPU restatement,
+// loaded by tests/ (ctypes), __graft_entry__.smoke() and bench.py's
+// cpu_baseline leg.  Never linked into the product library.
+//
+// oracle_step() runs one scan through the reference's three nodes with the
+// deterministic gating of SURVEY §8(d) replacing ROS timing (Appendix A Q13):
+//   imageProjection every scan -> featureAssociation every scan ->
+//   mapOptimization when FA publishes (every skipFrameNum+1 = 2nd scan) and
+//   t - t_last >= mappingProcessInterval -> SC detect once per new keyframe.
+// The raw cloud handed to mapping is the scan being mapped (Q16).
+#include "oracle_fa.h"
+#include "oracle_mo.h"
+#include <thread>
+#include <chrono>
+#include <atomic>
+#include <string>
+#include "../sc-lego-loam_amd/csrc/slo_gen.h"
+
+using namespace oracle;
+
+struct OracleStream {
+    slo_config cfg;
+    ImageProjection ip;
+    FeatureAssociation fa;
+    MapOptimization mo;
+    SCManager::DetectResult det{};
+    bool det_valid = false;
+    int scan_index = 0;
+    explicit OracleStream(const slo_config& c) : cfg(c), ip(c), fa(c), mo(c) {}
+
+    // returns bit flags: 1 = FA odometry ran, 2 = mapping ran, 4 = keyframe, 8 = detect ran
+    int step(const float* pts, int n, double t) {
+        int flags = 0;
+        det_valid = false;
+        ip.cloudHandler(pts, n);
+        fa.run(ip.segmentedCloud, ip.segMsg, ip.outlierCloud);
+        if (fa.systemInitedLM && scan_index > 0) flags |= 1;
+        if (fa.published_to_mapping) {
+            bool ran = mo.run(fa.laserCloudCornerLast, fa.laserCloudSurfLast, fa.outlierCloud, fa.transformSum, pts, n, t);
+            if (ran) flags |= 2;
+            if (ran && mo.saved_keyframe) {
+                flags |= 4;
+                det = mo.sc.detectLoopClosureID();
+                det_valid = true;
+                flags |= 8;
+            }
+        }
+        scan_index++;
+        return flags;
+    }
+};
+
+extern "C" {
+
+int oracle_config_preset(int preset, slo_config* out) { return slo_config_preset_impl(preset, out); }
+
+void* oracle_create(const slo_config* cfg, int stable_voxel) {
+    OracleStream* s = new OracleStream(*cfg);
+    s->fa.stable_voxel = stable_voxel != 0;
+    s->mo.stable_voxel = stable_voxel != 0;
+    return s;
+}
+void oracle_destroy(void* h) { delete (OracleStream*)h; }
+
+int oracle_step(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step(pts, n, t); }
+
+// image projection only (for front-end parity of a single scan)
+void oracle_image_projection(void* h, const float* pts, int n) { ((OracleStream*)h)->ip.cloudHandler(pts, n); }
+
+static int copy_cloud(const Cloud& c, float* out, int cap) {
+    int n = (int)c.size();
+    if (out) for (int i = 0; i < n && i < cap; ++i) memcpy(out + 4 * i, &c[i], 16);
+    return n;
+}
+
+// Named accessor: copies up to cap elements into out, returns the full count.
+int oracle_get(void* h, const char* name_c, void* out, int cap) {
+    OracleStream* s = (OracleStream*)h;
+    std::string name(name_c);
+    const int H = s->cfg.n_scan * s->cfg.horizon_scan;
+    auto cp = [&](const void* src, int count, int esz) {
+        if (out) memcpy(out, src, (size_t)std::min(count, cap) * esz);
+        return count;
+    };
+    if (name == "range") return cp(s->ip.rangeMat.data(), H, 4);
+    if (name == "label") return cp(s->ip.labelMat.data(), H, 4);
+    if (name == "ground") return cp(s->ip.groundMat.data(), H, 1);
+    if (name == "full_cloud") return copy_cloud(s->ip.fullCloud, (float*)out, cap);
+    if (name == "seg_pts") return copy_cloud(s->ip.segmentedCloud, (float*)out, cap);
+    int S = (int)s->ip.segmentedCloud.size();
+    if (name == "seg_ground") return cp(s->ip.segMsg.segmentedCloudGroundFlag.data(), S, 1);
+    if (name == "seg_col") return cp(s->ip.segMsg.segmentedCloudColInd.data(), S, 4);
+    if (name == "seg_range") return cp(s->ip.segMsg.segmentedCloudRange.data(), S, 4);
+    if (name == "ring_start") return cp(s->ip.segMsg.startRingIndex.data(), s->cfg.n_scan, 4);
+    if (name == "ring_end") return cp(s->ip.segMsg.endRingIndex.data(), s->cfg.n_scan, 4);
+    if (name == "orient") {
+        float o[3] = {s->ip.segMsg.startOrientation, s->ip.segMsg.endOrientation, s->ip.segMsg.orientationDiff};
+        return cp(o, 3, 4);
+    }
+    if (name == "outlier") return copy_cloud(s->ip.outlierCloud, (float*)out, cap);
+    if (name == "fa_seg_pts") return copy_cloud(s->fa.segmentedCloud, (float*)out, cap);
+    if (name == "curvature") return cp(s->fa.cloudCurvature.data(), H, 4);
+    if (name == "picked") return cp(s->fa.cloudNeighborPicked.data(), H, 4);
+    if (name == "cloud_label") return cp(s->fa.cloudLabel.data(), H, 4);
+    if (name == "smooth_ind") {
+        std::vector<int32_t> v(H);
+        for (int i = 0; i < H; ++i) v[i] = (int32_t)s->fa.cloudSmoothness[i].ind;
+        return cp(v.data(), H, 4);
+    }
+    if (name == "sharp") return copy_cloud(s->fa.cornerPointsSharp, (float*)out, cap);
+    if (name == "flat") return copy_cloud(s->fa.surfPointsFlat, (float*)out, cap);
+    if (name == "less_sharp") return copy_cloud(s->fa.cornerPointsLessSharp, (float*)out, cap);
+    if (name == "less_flat") return copy_cloud(s->fa.surfPointsLessFlat, (float*)out, cap);
+    if (name == "corner_last") return copy_cloud(s->fa.laserCloudCornerLast, (float*)out, cap);
+    if (name == "surf_last") return copy_cloud(s->fa.laserCloudSurfLast, (float*)out, cap);
+    if (name == "transform_sum") return cp(s->fa.transformSum, 6, 4);
+    if (name == "transform_cur") return cp(s->fa.transformCur, 6, 4);
+    if (name == "fa_iters") { int v[2] = {s->fa.iters_surf, s->fa.iters_corner}; return cp(v, 2, 4); }
+    if (name == "mapped") return cp(s->mo.transformAftMapped, 6, 4);
+    if (name == "tobe_mapped") return cp(s->mo.transformTobeMapped, 6, 4);
+    if (name == "mo_iters") return cp(&s->mo.lm_iters, 1, 4);
+    if (name == "n_keyframes") { int v = (int)s->mo.keyPoses.size(); return cp(&v, 1, 4); }
+    if (name == "keyposes") return cp(s->mo.keyPoses.data(), (int)s->mo.keyPoses.size() * 6, 4);
+    if (name == "raw_ds") return copy_cloud(s->mo.laserCloudRawDS, (float*)out, cap);
+    if (name == "corner_ds") return copy_cloud(s->mo.laserCloudCornerLastDS, (float*)out, cap);
+    if (name == "surf_total_ds") return copy_cloud(s->mo.laserCloudSurfTotalLastDS, (float*)out, cap);
+    if (name == "sc_desc") {
+        if (s->mo.sc.polarcontexts_.empty()) return 0;
+        auto& d = s->mo.sc.polarcontexts_.back();
+        return cp(d.data(), (int)d.size(), 8);
+    }
+    if (name == "ring_key") {
+        if (s->mo.sc.invkeys_.empty()) return 0;
+        auto& d = s->mo.sc.invkeys_.back();
+        return cp(d.data(), (int)d.size(), 8);
+    }
+    if (name == "sector_key") {
+        if (s->mo.sc.vkeys_.empty()) return 0;
+        auto& d = s->mo.sc.vkeys_.back();
+        return cp(d.data(), (int)d.size(), 8);
+    }
+    if (name == "detect") {  // loop_id, nn_idx, n_cand, cand[K] as int32; then yaw, min_dist via detect_f
+        if (!s->det_valid) return 0;
+        std::vector<int32_t> v{s->det.loop_id, s->det.nn_idx, s->det.n_cand};
+        for (int i = 0; i < s->det.n_cand; ++i) v.push_back(s->det.cand[i]);
+        return cp(v.data(), (int)v.size(), 4);
+    }
+    if (name == "detect_f") {
+        if (!s->det_valid) return 0;
+        double v[2] = {(double)s->det.yaw, s->det.min_dist};
+        return cp(v, 2, 8);
+    }
+    return -1;
+}
+
+// ---- SC unit entry points (pure functions over given descriptors)
+double oracle_sc_distance(const slo_config* cfg, const double* sc1, const double* sc2, int* shift) {
+    SCManager m(*cfg);
+    std::vector<double> a(sc1, sc1 + cfg->sc_num_ring * cfg->sc_num_sector);
+    std::vector<double> b(sc2, sc2 + cfg->sc_num_ring * cfg->sc_num_sector);
+    auto r = m.distanceBtnScanContext(a, b);
+    *shift = r.second;
+    return r.first;
+}
+void oracle_sc_make(const slo_config* cfg, const float* pts, int n, double* desc, double* ring, double* sector) {
+    SCManager m(*cfg);
+    Cloud c(n);
+    memcpy(c.data(), pts, (size_t)n * 16);
+    auto d = m.makeScancontext(c);
+    auto rk = m.makeRingkey(d);
+    auto vk = m.makeSectorkey(d);
+    memcpy(desc, d.data(), d.size() * 8);
+    memcpy(ring, rk.data(), rk.size() * 8);
+    memcpy(sector, vk.data(), vk.size() * 8);
+}
+int oracle_voxel_grid(const float* pts, int n, float leaf, int stable, float* out, int cap) {
+    Cloud c(n), o;
+    memcpy(c.data(), pts, (size_t)n * 16);
+    voxel_grid(c, leaf, o, stable != 0);
+    return copy_cloud(o, out, cap);
+}
+
+// ---- libm self-test against the host glibc (tests/test_libm.py)
+long oracle_libm_selftest(long n, unsigned long seed) {
+    uint64_t st = seed * 0x9E3779B97F4A7C15ULL + 1;
+    auto nx = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+        uint64_t r = nx();
+        float y = slo_libm::u2f((uint32_t)r), x = slo_libm::u2f((uint32_t)(r >> 32));
+        if (i & 1) { y = (float)((int32_t)(r & 0xffffff) - 0x800000) * 1e-5f; x = (float)((int32_t)((r >> 24) & 0xffffff) - 0x800000) * 1e-5f; }
+        auto same = [](float a, float b) { return slo_libm::f2u(a) == slo_libm::f2u(b) || (std::isnan(a) && std::isnan(b)); };
+        if (!same(slo_libm::atan2f_(y, x), atan2f(y, x))) bad++;
+        if (!same(slo_libm::sinf_(y), sinf(y))) bad++;
+        if (!same(slo_libm::cosf_(y), cosf(y))) bad++;
+        if (!same(slo_libm::atanf_(y), atanf(y))) bad++;
+        float u = fmodf(y, 1.0f);
+        if (!same(slo_libm::asinf_(u), asinf(u))) bad++;
+    }
+    return bad;
+}
+
+// ---- generator passthrough (same header the product library uses)
+int oracle_gen_scan(int preset, int config_id, int stream_id, int k, float* out) {
+    slo_config cfg;
+    if (slo_config_preset_impl(preset, &cfg)) return -1;
+    slo_gen::Stream s = slo_gen::make_stream(cfg, config_id, stream_id);
+    return slo_gen::stream_scan(s, k, out);
+}
+
+// ---- CPU baseline: n_threads independent streams, each processing n_scans
+// pre-generated scans (generation excluded from timing).  Returns wall
+// seconds of the processing; per-stage seconds summed over threads in stage_s[4]
+// (ip, fa, mo, sc).
+double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int warmup, double* stage_s) {
+    slo_config cfg;
+    if (slo_config_preset_impl(preset, &cfg)) return -1;
+    const int P = cfg.n_scan * cfg.horizon_scan;
+    std::vector<std::vector<float>> scans((size_t)n_threads * (n_scans + warmup));
+    {
+        std::vector<std::thread> g;
+        for (int t = 0; t < n_threads; ++t)
+            g.emplace_back([&, t]() {
+                slo_gen::Stream s = slo_gen::make_stream(cfg, config_id, t);
+                for (int k = 0; k < n_scans + warmup; ++k) {
+                    auto& v = scans[(size_t)t * (n_scans + warmup) + k];
+                    v.resize((size_t)P * 4);
+                    slo_gen::stream_scan(s, k, v.data());
+                }
+            });
+        for (auto& th : g) th.join();
+    }
+    std::vector<double> st(4 * n_threads, 0.0);
+    std::atomic<int> ready{0};
+    std::atomic<bool> go{false};
+    std::vector<double> tstart(n_threads), tend(n_threads);
+    std::vector<std::thread> th;
+    for (int t = 0; t < n_threads; ++t)
+        th.emplace_back([&, t]() {
+            OracleStream s(cfg);
+            for (int k = 0; k < warmup; ++k) s.step(scans[(size_t)t * (n_scans + warmup) + k].data(), P, 0.1 * k);
+            ready++;
+            while (!go.load()) std::this_thread::yield();
+            auto T0 = std::chrono::steady_clock::now();
+            tstart[t] = std::chrono::duration<double>(T0.time_since_epoch()).count();
+            for (int k = warmup; k < n_scans + warmup; ++k) {
+                const float* p = scans[(size_t)t * (n_scans + warmup) + k].data();
+                auto a = std::chrono::steady_clock::now();
+                s.det_valid = false;
+                s.ip.cloudHandler(p, P);
+                auto b = std::chrono::steady_clock::now();
+                s.fa.run(s.ip.segmentedCloud, s.ip.segMsg, s.ip.outlierCloud);
+                auto c = std::chrono::steady_clock::now();
+                bool kf = false;
+                if (s.fa.published_to_mapping) {
+                    bool ran = s.mo.run(s.fa.laserCloudCornerLast, s.fa.laserCloudSurfLast, s.fa.outlierCloud,
+                                        s.fa.transformSum, p, P, 0.1 * k);
+                    kf = ran && s.mo.saved_keyframe;
+                }
+                auto d = std::chrono::steady_clock::now();
+                if (kf) s.det = s.mo.sc.detectLoopClosureID();
+                auto e = std::chrono::steady_clock::now();
+                s.scan_index++;
+                st[4 * t + 0] += std::chrono::duration<double>(b - a).count();
+                st[4 * t + 1] += std::chrono::duration<double>(c - b).count();
+                st[4 * t + 2] += std::chrono::duration<double>(d - c).count();
+                st[4 * t + 3] += std::chrono::duration<double>(e - d).count();
+            }
+            tend[t] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        });
+    while (ready.load() < n_threads) std::this_thread::yield();
+    go = true;
+    for (auto& x : th) x.join();
+    double t0 = *std::min_element(tstart.begin(), tstart.end());
+    double t1 = *std::max_element(tend.begin(), tend.end());
+    if (stage_s)
+        for (int k = 0; k < 4; ++k) {
+            stage_s[k] = 0;
+            for (int t = 0; t < n_threads; ++t) stage_s[k] += st[4 * t + k];
+        }
+    return t1 - t0;
+}
+
+}  // extern "C"
