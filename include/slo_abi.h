@@ -1,0 +1,134 @@
+/* slo_abi.h — C ABI of the MI355X-native SC-LeGO-LOAM hot path (libslo.so).
+ *
+ * Drop-in boundary for the four per-scan entry points of the reference
+ * (SURVEY §8(b)); every function is extern "C", noexcept, returns 0 on
+ * success or a negative SLO_E* code (text via slo_last_error()).
+ *
+ *   reference entry point                                  replaced by
+ *   ImageProjection::cloudHandler   imageProjection.cpp:181   slo_image_projection / slo_batch_image_projection
+ *   FeatureAssociation::runFeatureAssociation
+ *                                featureAssociation.cpp:1817  slo_feature_association / slo_batch_feature_association
+ *   mapOptimization::run            mapOptmization.cpp:1673   slo_map_optimization / slo_batch_map_optimization
+ *   SCManager::makeAndSaveScancontextAndKeys Scancontext.h:72 (called inside the mapping step, MO:1630)
+ *   SCManager::detectLoopClosureID  Scancontext.h:73 / MO:916 slo_sc_detect / slo_batch_sc_detect
+ *
+ * One context serves `n_streams` independent LiDAR streams (the batch
+ * dimension): a batched call advances every stream by one scan.  The
+ * single-scan calls act on stream 0 and take host memory, exactly like the
+ * reference callbacks.  A context is single-caller; the caller serialises
+ * (the reference's `mtx`, mapOptmization.cpp:197).  Every entry point sets
+ * the context's HIP device first, so calls may come from any host thread.
+ */
+#ifndef SLO_ABI_H
+#define SLO_ABI_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include "../sc-lego-loam_amd/csrc/slo_config.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SLO_OK 0
+#define SLO_E_ARG (-1)
+#define SLO_E_HIP (-2)
+#define SLO_E_CAPACITY (-3)
+#define SLO_E_STATE (-4)
+
+typedef struct slo_ctx slo_ctx;
+
+/* Fill *out with a named preset (SLO_PRESET_*), reference defaults. */
+int slo_config_preset(int preset, slo_config* out);
+
+/* Create a context on HIP device `hip_device` for `n_streams` streams. */
+int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** out);
+void slo_destroy(slo_ctx* ctx);
+const char* slo_last_error(const slo_ctx* ctx);
+/* The hipStream_t all work of this context is queued on. */
+void* slo_stream(slo_ctx* ctx);
+/* Block until all queued work of the context is done. */
+int slo_synchronize(slo_ctx* ctx);
+
+/* ---------------------------------------------------------------- batched
+ * d_points: device array [n_streams][cfg.max_points] of (x,y,z,intensity)
+ * float4 in firing order, NaN for no return; d_counts: device int32
+ * [n_streams].  All batched calls are asynchronous on slo_stream(). */
+int slo_batch_image_projection(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
+/* features (FA:1833-1839) + scan-to-scan odometry (FA:1846-1859) */
+int slo_batch_feature_association(slo_ctx* ctx);
+/* mapping step for streams whose FA published this scan and whose
+ * t_scan - t_last >= mappingProcessInterval (MO:1675-1706), incl. keyframe
+ * save and Scan Context make (MO:1630); d_points as above (raw cloud, Q16) */
+int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan);
+/* SC loop detection for every stream that saved a keyframe this scan */
+int slo_batch_sc_detect(slo_ctx* ctx);
+/* whole pipeline for one scan per stream with the deterministic gating of
+ * IP -> FA -> [mapping + SC make] -> [SC detect] */
+int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan);
+
+/* ---------------------------------------------------------------- single scan (stream 0, host memory) */
+typedef struct slo_seg_view {
+    int32_t n_segmented;           /* |segmentedCloud| */
+    const float* segmented;        /* n_segmented x (x,y,z,intensity) */
+    const uint8_t* ground_flag;    /* cloud_info.segmentedCloudGroundFlag */
+    const uint32_t* col_ind;       /* cloud_info.segmentedCloudColInd */
+    const float* range;            /* cloud_info.segmentedCloudRange */
+    const int32_t* start_ring_index;
+    const int32_t* end_ring_index;
+    float start_orientation, end_orientation, orientation_diff;
+    int32_t n_outlier;
+    const float* outlier;          /* n_outlier x 4 */
+} slo_seg_view;
+
+typedef struct slo_fa_view {
+    int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
+    const float* sharp;            /* each n x (x,y,z,intensity), camera frame */
+    const float* less_sharp;
+    const float* flat;
+    const float* less_flat;
+    float transform_sum[6];        /* /laser_odom_to_init (rx,ry,rz,tx,ty,tz) */
+    int32_t published;             /* 1 if this scan went to mapping (FA:1790) */
+} slo_fa_view;
+
+typedef struct slo_map_view {
+    int32_t ran;                   /* mapping ran for this scan */
+    int32_t keyframe_saved;
+    int32_t n_keyframes;
+    float transform_aft_mapped[6]; /* /aft_mapped_to_init */
+} slo_map_view;
+
+/* pts: n points, stride_bytes apart, xyz at off_xyz (3 floats), intensity at off_i */
+int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                         size_t off_i, slo_seg_view* out);
+int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out);
+/* raw_pts: the raw cloud of the scan being mapped (same layout arguments) */
+int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                         size_t off_i, double t_scan, slo_map_view* out);
+int slo_sc_detect(slo_ctx* ctx, int32_t* loop_id, float* yaw_rad, double* min_dist);
+
+/* ---------------------------------------------------------------- readback
+ * Copy a named per-stream result to host memory (synchronises).  Returns the
+ * element count (copies at most cap_bytes), or < 0.  Names: "range",
+ * "label", "ground", "seg_pts", "seg_ground", "seg_col", "seg_range",
+ * "ring_start", "ring_end", "orient", "outlier", "fa_seg_pts", "curvature",
+ * "picked", "cloud_label", "smooth_ind", "sharp", "less_sharp", "flat",
+ * "less_flat", "corner_last", "surf_last", "transform_sum", "transform_cur",
+ * "fa_iters", "mapped", "n_keyframes", "keyposes", "sc_desc", "ring_key",
+ * "sector_key", "detect", "detect_f", "flags". */
+int slo_get(slo_ctx* ctx, int stream, const char* name, void* dst, size_t cap_bytes);
+
+/* per-kernel timing (HIP events around every launch when enabled) */
+int slo_timing_enable(slo_ctx* ctx, int enable);
+/* fills up to cap entries of names (NUL-separated into buf) and total ms and
+ * launch counts; returns number of kernels */
+int slo_timing_read(slo_ctx* ctx, char* names_buf, size_t buf_bytes, double* total_ms, int64_t* launches, int cap);
+int slo_timing_reset(slo_ctx* ctx);
+
+/* synthetic stream generator (sc-lego-loam_amd/csrc/slo_gen.h), host side */
+int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float* out_xyzi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

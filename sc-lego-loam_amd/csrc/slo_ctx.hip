@@ -1,0 +1,400 @@
+// slo_ctx.hip — context lifetime, HBM arena, batched pipeline driver and the
+// C ABI of include/slo_abi.h.
+#include "slo_internal.h"
+#include "../../include/slo_abi.h"
+#include "slo_gen.h"
+#include <string.h>
+#include <algorithm>
+
+using slo::DevView;
+using slo::StreamState;
+
+namespace slo {
+
+void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a) {
+    (void)name;
+    hipEventCreate(a);
+    hipEventRecord(*a, ctx->stream);
+}
+void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a) {
+    hipEvent_t b;
+    hipEventCreate(&b);
+    hipEventRecord(b, ctx->stream);
+    ctx->pending.push_back({name, {a, b}});
+}
+static void timing_flush(slo_ctx* ctx) {
+    if (ctx->pending.empty()) return;
+    hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, p.second.first, p.second.second);
+        auto& k = ctx->ktimes[p.first];
+        k.total_ms += ms;
+        k.n += 1;
+        hipEventDestroy(p.second.first);
+        hipEventDestroy(p.second.second);
+    }
+    ctx->pending.clear();
+}
+
+}  // namespace slo
+
+namespace {
+
+struct Carver {
+    size_t off = 0;
+    std::vector<std::pair<void**, size_t>> items;
+    template <class T>
+    void add(T** p, size_t count) {
+        items.push_back({(void**)p, sizeof(T) * count});
+        off += (sizeof(T) * count + 255) & ~(size_t)255;
+    }
+    void assign(char* base) {
+        size_t o = 0;
+        for (auto& it : items) {
+            *it.first = base + o;
+            o += (it.second + 255) & ~(size_t)255;
+        }
+    }
+};
+
+}  // namespace
+
+extern "C" {
+
+int slo_config_preset(int preset, slo_config* out) {
+    if (!out) return SLO_E_ARG;
+    return slo_config_preset_impl(preset, out) == 0 ? SLO_OK : SLO_E_ARG;
+}
+
+const char* slo_last_error(const slo_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+void* slo_stream(slo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** out) {
+    if (!cfg || !out || n_streams <= 0 || cfg->n_scan <= 0 || cfg->n_scan > 128 || cfg->horizon_scan <= 0 ||
+        cfg->horizon_scan > 4096 || cfg->max_points <= 0)
+        return SLO_E_ARG;
+    slo_ctx* ctx = new slo_ctx();
+    ctx->cfg = *cfg;
+    ctx->dev = hip_device;
+    ctx->S = n_streams;
+    *out = nullptr;
+    if (hipSetDevice(hip_device) != hipSuccess) { delete ctx; return SLO_E_HIP; }
+    if (hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) { delete ctx; return SLO_E_HIP; }
+    DevView& v = ctx->v;
+    memset(&v, 0, sizeof(v));
+    v.cfg = *cfg;
+    v.S = n_streams;
+    v.P = cfg->max_points;
+    const int R = cfg->n_scan, C = cfg->horizon_scan;
+    v.H = R * C;
+    v.cap_sharp = 12 * R;
+    v.cap_less_sharp = 120 * R;
+    v.cap_flat = 24 * R;
+    v.cap_less_flat = v.H;
+    const size_t S = n_streams, H = v.H;
+    Carver c;
+    c.add(&ctx->d_in, S * v.P);
+    c.add(&ctx->d_cnt, S);
+    c.add(&v.owner, S * H);
+    c.add(&v.fl, 2 * S);
+    c.add(&v.range, S * H);
+    c.add(&v.full, S * H);
+    c.add(&v.ground, S * H);
+    c.add(&v.label, S * H);
+    c.add(&v.parent, S * H);
+    c.add(&v.csize, S * H);
+    c.add(&v.crows, 2 * S * H);
+    c.add(&v.rowcnt, 2 * S * R);
+    c.add(&v.seg, S * H);
+    c.add(&v.seg_ground, S * H);
+    c.add(&v.seg_col, S * H);
+    c.add(&v.seg_range, S * H);
+    c.add(&v.ring_se, 2 * S * R);
+    c.add(&v.orient, 3 * S);
+    c.add(&v.outlier, S * H);
+    c.add(&v.fpts, S * H);
+    c.add(&v.curv, S * H);
+    c.add(&v.picked, S * H);
+    c.add(&v.clabel, S * H);
+    c.add(&v.smooth, S * H);
+    c.add(&v.ring_cnt, 4 * S * R);
+    c.add(&v.r_sharp, S * R * 12);
+    c.add(&v.r_less_sharp, S * R * 120);
+    c.add(&v.r_flat, S * R * 24);
+    c.add(&v.r_lf_scan, S * R * C);
+    c.add(&v.r_lf_n, S * R);
+    c.add(&v.r_lf_ds, S * R * C);
+    c.add(&v.sharp, S * v.cap_sharp);
+    c.add(&v.less_sharp, S * v.cap_less_sharp);
+    c.add(&v.flat, S * v.cap_flat);
+    c.add(&v.less_flat, S * v.cap_less_flat);
+    c.add(&v.corner_last, S * v.cap_less_sharp);
+    c.add(&v.surf_last, S * v.cap_less_flat);
+    c.add(&v.corner_next, S * v.cap_less_sharp);
+    c.add(&v.surf_next, S * v.cap_less_flat);
+    c.add(&v.kd_corner, S * v.cap_less_sharp);
+    c.add(&v.kd_surf, S * v.cap_less_flat);
+    c.add(&v.ind_surf, S * v.cap_flat * 3);
+    c.add(&v.ind_corner, S * v.cap_sharp * 2);
+    c.add(&v.st, S);
+    ctx->arena_bytes = c.off;
+    if (hipMalloc(&ctx->arena, ctx->arena_bytes) != hipSuccess) {
+        ctx->err = "hipMalloc arena failed";
+        hipStreamDestroy(ctx->stream);
+        delete ctx;
+        return SLO_E_HIP;
+    }
+    c.assign((char*)ctx->arena);
+    // zero everything: persistent FA arrays start as the zero pages new[] gives
+    if (hipMemsetAsync(ctx->arena, 0, ctx->arena_bytes, ctx->stream) != hipSuccess ||
+        hipHostMalloc((void**)&ctx->h_st, sizeof(StreamState) * S) != hipSuccess ||
+        hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        slo_destroy(ctx);
+        return SLO_E_HIP;
+    }
+    memset(ctx->h_st, 0, sizeof(StreamState) * S);
+    *out = ctx;
+    return SLO_OK;
+}
+
+void slo_destroy(slo_ctx* ctx) {
+    if (!ctx) return;
+    hipSetDevice(ctx->dev);
+    if (ctx->stream) hipStreamSynchronize(ctx->stream);
+    for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
+    if (ctx->arena) hipFree(ctx->arena);
+    if (ctx->h_st) hipHostFree(ctx->h_st);
+    if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int slo_synchronize(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    hipSetDevice(ctx->dev);
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
+}
+
+int slo_batch_image_projection(slo_ctx* ctx, const void* d_points, const int32_t* d_counts) {
+    if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    ctx->v.pts = (const float4*)d_points;
+    ctx->v.npts = d_counts;
+    return slo::ip_run(ctx);
+}
+
+int slo_batch_feature_association(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = slo::fa_features_run(ctx);
+    if (r) return r;
+    const bool first = !ctx->fa_inited;
+    r = slo::fa_odometry_run(ctx, first);
+    if (r) return r;
+    // FA frameCount / publish gate (FA:1790-1792); the init scan never publishes
+    ctx->fa_published = false;
+    if (first) {
+        ctx->fa_inited = true;
+        ctx->fa_frame_count = ctx->cfg.skip_frame_num;
+    } else {
+        ctx->fa_frame_count++;
+        if (ctx->fa_frame_count >= ctx->cfg.skip_frame_num + 1) {
+            ctx->fa_frame_count = 0;
+            ctx->fa_published = true;
+        }
+    }
+    ctx->scan_index++;
+    return SLO_OK;
+}
+
+int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
+    (void)d_points; (void)d_counts; (void)t_scan;
+    if (!ctx) return SLO_E_ARG;
+    return SLO_OK;  // mapping stage lands in slo_map.hip
+}
+
+int slo_batch_sc_detect(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    return SLO_OK;
+}
+
+int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
+    int r = slo_batch_image_projection(ctx, d_points, d_counts);
+    if (r) return r;
+    r = slo_batch_feature_association(ctx);
+    if (r) return r;
+    if (ctx->fa_published) {
+        r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
+        if (r) return r;
+        r = slo_batch_sc_detect(ctx);
+    }
+    return r;
+}
+
+// ---------------------------------------------------------------- readback
+int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_bytes) {
+    if (!ctx || !name_c || stream < 0 || stream >= ctx->S) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    slo::timing_flush(ctx);
+    const DevView& v = ctx->v;
+    StreamState st;
+    SLO_CHECK(hipMemcpy(&st, v.st + stream, sizeof(st), hipMemcpyDeviceToHost));
+    const std::string name(name_c);
+    const size_t s = stream, H = v.H, R = v.cfg.n_scan;
+    const void* src = nullptr;
+    size_t count = 0, esz = 0;
+    std::vector<char> tmp;
+    auto dev = [&](const void* p, size_t n, size_t e) { src = p; count = n; esz = e; };
+    if (name == "range") dev(v.range + s * H, H, 4);
+    else if (name == "label") dev(v.label + s * H, H, 4);
+    else if (name == "ground") dev(v.ground + s * H, H, 1);
+    else if (name == "full_cloud") dev(v.full + s * H, H, 16);
+    else if (name == "seg_pts") dev(v.seg + s * H, st.seg_count, 16);
+    else if (name == "seg_ground") dev(v.seg_ground + s * H, st.seg_count, 1);
+    else if (name == "seg_col") dev(v.seg_col + s * H, st.seg_count, 4);
+    else if (name == "seg_range") dev(v.seg_range + s * H, st.seg_count, 4);
+    else if (name == "ring_start" || name == "ring_end") {
+        std::vector<int32_t> se(2 * R);
+        SLO_CHECK(hipMemcpy(se.data(), v.ring_se + s * 2 * R, sizeof(int32_t) * 2 * R, hipMemcpyDeviceToHost));
+        tmp.resize(4 * R);
+        for (size_t i = 0; i < R; ++i) ((int32_t*)tmp.data())[i] = se[2 * i + (name == "ring_end")];
+        count = R; esz = 4;
+    } else if (name == "orient") dev(v.orient + 3 * s, 3, 4);
+    else if (name == "outlier") dev(v.outlier + s * H, st.outlier_count, 16);
+    else if (name == "fa_seg_pts") dev(v.fpts + s * H, st.seg_count, 16);
+    else if (name == "curvature") dev(v.curv + s * H, H, 4);
+    else if (name == "picked") dev(v.picked + s * H, H, 4);
+    else if (name == "cloud_label") dev(v.clabel + s * H, H, 4);
+    else if (name == "smooth_ind") {
+        std::vector<slo::Smooth> sm(H);
+        SLO_CHECK(hipMemcpy(sm.data(), v.smooth + s * H, sizeof(slo::Smooth) * H, hipMemcpyDeviceToHost));
+        tmp.resize(4 * H);
+        for (size_t i = 0; i < H; ++i) ((int32_t*)tmp.data())[i] = sm[i].ind;
+        count = H; esz = 4;
+    } else if (name == "sharp") dev(v.sharp + s * v.cap_sharp, st.n_sharp, 16);
+    else if (name == "less_sharp") dev(v.less_sharp + s * v.cap_less_sharp, st.n_less_sharp, 16);
+    else if (name == "flat") dev(v.flat + s * v.cap_flat, st.n_flat, 16);
+    else if (name == "less_flat") dev(v.less_flat + s * v.cap_less_flat, st.n_less_flat, 16);
+    else if (name == "corner_last") dev(v.corner_last + s * v.cap_less_sharp, st.cornerLastNum, 16);
+    else if (name == "surf_last") dev(v.surf_last + s * v.cap_less_flat, st.surfLastNum, 16);
+    else if (name == "transform_sum") { tmp.resize(24); memcpy(tmp.data(), st.transformSum, 24); count = 6; esz = 4; }
+    else if (name == "transform_cur") { tmp.resize(24); memcpy(tmp.data(), st.transformCur, 24); count = 6; esz = 4; }
+    else if (name == "fa_iters") { int32_t a[2] = {st.iters_surf, st.iters_corner}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4; }
+    else if (name == "mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformAftMapped, 24); count = 6; esz = 4; }
+    else if (name == "n_keyframes") { tmp.resize(4); memcpy(tmp.data(), &st.n_keyframes, 4); count = 1; esz = 4; }
+    else if (name == "flags") { tmp.resize(4); memcpy(tmp.data(), &st.flags, 4); count = 1; esz = 4; }
+    else return SLO_E_ARG;
+    const size_t bytes = std::min(cap_bytes, count * esz);
+    if (dst && bytes) {
+        if (src) SLO_CHECK(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+        else memcpy(dst, tmp.data(), bytes);
+    }
+    return (int)count;
+}
+
+int slo_timing_enable(slo_ctx* ctx, int enable) {
+    if (!ctx) return SLO_E_ARG;
+    ctx->timing = enable != 0;
+    return SLO_OK;
+}
+int slo_timing_reset(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    slo::timing_flush(ctx);
+    ctx->ktimes.clear();
+    return SLO_OK;
+}
+int slo_timing_read(slo_ctx* ctx, char* names_buf, size_t buf_bytes, double* total_ms, int64_t* launches, int cap) {
+    if (!ctx) return SLO_E_ARG;
+    slo::timing_flush(ctx);
+    int i = 0;
+    size_t off = 0;
+    for (auto& kv : ctx->ktimes) {
+        if (i >= cap) break;
+        size_t L = kv.first.size() + 1;
+        if (names_buf && off + L <= buf_bytes) { memcpy(names_buf + off, kv.first.c_str(), L); off += L; }
+        if (total_ms) total_ms[i] = kv.second.total_ms;
+        if (launches) launches[i] = kv.second.n;
+        ++i;
+    }
+    return i;
+}
+
+int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float* out_xyzi) {
+    slo_config cfg;
+    if (slo_config_preset_impl(preset, &cfg) || !out_xyzi) return SLO_E_ARG;
+    slo_gen::Stream s = slo_gen::make_stream(cfg, config_id, stream_id);
+    return slo_gen::stream_scan(s, scan_index, out_xyzi);
+}
+
+// ---------------------------------------------------------------- single scan (stream 0)
+static int stage_points(slo_ctx* ctx, const void* pts, size_t n, size_t stride, size_t off_xyz, size_t off_i) {
+    if (n > (size_t)ctx->cfg.max_points) { ctx->err = "too many points"; return SLO_E_CAPACITY; }
+    const size_t need = n * 16 + 16;
+    if (ctx->h_stage_bytes < need) {
+        if (ctx->h_stage) hipHostFree(ctx->h_stage);
+        ctx->h_stage = nullptr;
+        SLO_CHECK(hipHostMalloc(&ctx->h_stage, need));
+        ctx->h_stage_bytes = need;
+    }
+    float* h = (float*)ctx->h_stage;
+    const char* b = (const char*)pts;
+    for (size_t i = 0; i < n; ++i) {
+        memcpy(h + 4 * i, b + i * stride + off_xyz, 12);
+        memcpy(h + 4 * i + 3, b + i * stride + off_i, 4);
+    }
+    int32_t cnt = (int32_t)n;
+    memcpy(h + 4 * n, &cnt, 4);
+    SLO_CHECK(hipMemcpyAsync(ctx->d_in, h, n * 16, hipMemcpyHostToDevice, ctx->stream));
+    SLO_CHECK(hipMemcpyAsync(ctx->d_cnt, h + 4 * n, 4, hipMemcpyHostToDevice, ctx->stream));
+    return SLO_OK;
+}
+
+int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz, size_t off_i,
+                         slo_seg_view* out) {
+    if (!ctx || !pts || !out || ctx->S < 1) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = stage_points(ctx, pts, n, stride_bytes, off_xyz, off_i);
+    if (r) return r;
+    ctx->v.pts = ctx->d_in;
+    ctx->v.npts = ctx->d_cnt;
+    r = slo::ip_run(ctx);
+    if (r) return r;
+    memset(out, 0, sizeof(*out));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
+}
+
+int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out) {
+    (void)t_scan;
+    if (!ctx || !out) return SLO_E_ARG;
+    int r = slo_batch_feature_association(ctx);
+    if (r) return r;
+    memset(out, 0, sizeof(*out));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    StreamState st;
+    SLO_CHECK(hipMemcpy(&st, ctx->v.st, sizeof(st), hipMemcpyDeviceToHost));
+    memcpy(out->transform_sum, st.transformSum, 24);
+    out->n_sharp = st.n_sharp; out->n_less_sharp = st.n_less_sharp;
+    out->n_flat = st.n_flat; out->n_less_flat = st.n_less_flat;
+    out->published = ctx->fa_published;
+    return SLO_OK;
+}
+
+int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                         size_t off_i, double t_scan, slo_map_view* out) {
+    (void)raw_pts; (void)n; (void)stride_bytes; (void)off_xyz; (void)off_i; (void)t_scan;
+    if (!ctx || !out) return SLO_E_ARG;
+    memset(out, 0, sizeof(*out));
+    return SLO_OK;
+}
+
+int slo_sc_detect(slo_ctx* ctx, int32_t* loop_id, float* yaw_rad, double* min_dist) {
+    if (!ctx || !loop_id || !yaw_rad || !min_dist) return SLO_E_ARG;
+    *loop_id = -1; *yaw_rad = 0; *min_dist = 0;
+    return SLO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,168 @@
+// slo_internal.h — context layout shared by the HIP translation units.
+//
+// HBM layout: every per-stream array is a [n_streams][capacity] slab carved
+// out of one arena (struct-of-arrays, 256-byte aligned), so a batched kernel
+// indexes (stream, element) with one multiply and reads each stream's slab
+// contiguously.  State that the reference keeps across scans (FA's
+// cloudSmoothness / cloudCurvature / cloudNeighborPicked / cloudLabel, the
+// cloud_info arrays with their stale tails, *Last clouds, the keyframe ring,
+// the Scan Context history) lives here for the lifetime of the context.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include <vector>
+#include <map>
+#include "slo_config.h"
+#include "../../include/slo_abi.h"
+
+#define SLO_CHECK(x)                                                            \
+    do {                                                                          \
+        hipError_t e_ = (x);                                                      \
+        if (e_ != hipSuccess) {                                                   \
+            ctx->err = std::string(#x) + ": " + hipGetErrorString(e_);            \
+            return SLO_E_HIP;                                                     \
+        }                                                                         \
+    } while (0)
+
+namespace slo {
+
+struct alignas(8) Smooth { float value; int32_t ind; };
+
+// Per-stream scalar state of the FA / MO nodes (one record per stream).
+struct StreamState {
+    float transformCur[6];
+    float transformSum[6];
+    float matP_fa[9];
+    int32_t isDegenerate_fa;
+    int32_t cornerLastNum, surfLastNum;   // laserCloud*LastNum
+    int32_t kdCornerNum, kdSurfNum;       // size of the cloud the "tree" was last built on
+    int32_t iters_surf, iters_corner;
+    int32_t first_half;                   // deskew: first index with halfPassed
+    int32_t seg_count, outlier_count;
+    int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
+    // mapping
+    float transformLast[6], transformIncre[6], transformTobeMapped[6];
+    float transformBefMapped[6], transformAftMapped[6];
+    float mo_sum[6];
+    float matP_mo[36];
+    int32_t isDegenerate_mo;
+    int32_t n_keyframes;
+    int32_t latestFrameID;
+    int32_t recent_n;                     // deque size
+    int32_t recent_ids[64];               // deque of keyframe ids (front first)
+    float prevPos[3];
+    int32_t mo_ran, kf_saved, mo_iters, mo_converged;
+    int32_t n_corner_map, n_surf_map, n_corner_ds, n_surf_total_ds, n_raw_ds;
+    // scan context
+    int32_t sc_count, sc_tree_n, sc_counter;
+    int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];
+    float det_yaw;
+    double det_min_dist;
+    int32_t flags;
+    int32_t err;
+};
+
+// kernel-visible view of the context (passed by value)
+struct DevView {
+    slo_config cfg;
+    int S;        // streams
+    int P;        // max points per scan
+    int H;        // R*C
+    int cap_sharp, cap_less_sharp, cap_flat, cap_less_flat;
+    // inputs
+    const float4* pts;   // [S][P]
+    const int32_t* npts; // [S]
+    // image projection
+    int32_t* owner;      // [S][H]
+    int32_t* fl;         // [S][2] first/last finite index
+    float* range;        // [S][H]
+    float4* full;        // [S][H]
+    int8_t* ground;      // [S][H]
+    int32_t* label;      // [S][H]
+    int32_t* parent;     // [S][H]
+    int32_t* csize;      // [S][H]
+    unsigned long long* crows;  // [S][H][2]
+    int32_t* rowcnt;     // [S][R][2] kept / outlier per row
+    float4* seg;         // [S][H]
+    uint8_t* seg_ground; // [S][H]
+    uint32_t* seg_col;   // [S][H]
+    float* seg_range;    // [S][H]
+    int32_t* ring_se;    // [S][R][2]
+    float* orient;       // [S][3]
+    float4* outlier;     // [S][H]
+    // feature association
+    float4* fpts;        // [S][H] deskewed camera-frame points
+    float* curv;         // [S][H]
+    int32_t* picked;     // [S][H]
+    int32_t* clabel;     // [S][H]
+    Smooth* smooth;      // [S][H]
+    int32_t* ring_cnt;   // [S][R][4] sharp, less_sharp, flat, less_flat(after DS)
+    float4* r_sharp;     // [S][R][12]
+    float4* r_less_sharp;// [S][R][120]
+    float4* r_flat;      // [S][R][24]
+    float4* r_lf_scan;   // [S][R][C] less-flat scan (before DS)
+    int32_t* r_lf_n;     // [S][R]
+    float4* r_lf_ds;     // [S][R][C]
+    float4* sharp;       // [S][cap_sharp]
+    float4* less_sharp;  // [S][cap_less_sharp]
+    float4* flat;        // [S][cap_flat]
+    float4* less_flat;   // [S][cap_less_flat]
+    // odometry
+    float4* corner_last; // [S][cap_less_sharp]  (previous scan, end-of-sweep)
+    float4* surf_last;   // [S][cap_less_flat]
+    float4* corner_next; // [S][cap_less_sharp]  (this scan, written by odometry)
+    float4* surf_next;   // [S][cap_less_flat]
+    float4* kd_corner;   // [S][cap_less_sharp]  copy the "tree" searches (setInputCloud copies)
+    float4* kd_surf;     // [S][cap_less_flat]
+    int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
+    int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
+    StreamState* st;     // [S]
+};
+
+}  // namespace slo
+
+struct slo_ctx {
+    slo_config cfg;
+    int dev = 0;
+    int S = 0;
+    hipStream_t stream = nullptr;
+    std::string err;
+    void* arena = nullptr;
+    size_t arena_bytes = 0;
+    slo::DevView v;
+    slo::StreamState* h_st = nullptr;   // pinned host mirror
+    int scan_index = 0;                 // scans processed by the batched pipeline
+    int fa_frame_count = 0;             // FA frameCount (host-known, lockstep streams)
+    bool fa_inited = false;
+    double t_last_processing = -1;      // MO timeLastProcessing (lockstep streams)
+    bool fa_published = false;
+    // timing
+    bool timing = false;
+    struct KT { std::vector<hipEvent_t> ev; double total_ms = 0; int64_t n = 0; };
+    std::map<std::string, KT> ktimes;
+    std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    // host staging for single-scan API
+    void* h_stage = nullptr;
+    size_t h_stage_bytes = 0;
+    float4* d_in = nullptr;   // internal input buffer [S][P]
+    int32_t* d_cnt = nullptr;
+};
+
+// launch helpers with optional per-kernel HIP-event timing
+namespace slo {
+void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a);
+void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a);
+int ip_run(slo_ctx* ctx);
+int fa_features_run(slo_ctx* ctx);
+int fa_odometry_run(slo_ctx* ctx, bool first_scan);
+}  // namespace slo
+
+#define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \
+    do {                                                                              \
+        hipEvent_t ev_a_ = nullptr;                                                   \
+        if ((ctx)->timing) slo::timing_begin((ctx), name, &ev_a_);                    \
+        hipLaunchKernelGGL(kernel, grid, block, shmem, (ctx)->stream, __VA_ARGS__);   \
+        if ((ctx)->timing) slo::timing_end((ctx), name, ev_a_);                       \
+    } while (0)

@@ -314,4 +314,17 @@ SLO_HD float asinf_(float x) {
     return (hx > 0) ? t : -t;
 }
 
+// ---------------------------------------------------------------- hypotf
+// glibc sysdeps/ieee754/flt-32/e_hypotf.c: evaluated in double.
+SLO_HD float hypotf_(float x, float y) {
+    uint32_t ha = f2u(x) & 0x7fffffffu, hb = f2u(y) & 0x7fffffffu;
+    if (ha == 0x7f800000u) return fabsf(x);
+    if (hb == 0x7f800000u) return fabsf(y);
+    if (ha > 0x7f800000u || hb > 0x7f800000u) return fabsf(x) * fabsf(y);
+    if (ha == 0) return fabsf(y);
+    if (hb == 0) return fabsf(x);
+    double dx = x, dy = y;
+    return (float)sqrt(dx * dx + dy * dy);
+}
+
 }  // namespace slo_libm

@@ -1,0 +1,204 @@
+// slo_pose.h — scalar pose algebra of the FA / MO nodes for one GPU lane.
+// All trig through slo_libm (glibc float bits); float evaluation order as
+// in the reference expressions.
+//   transform_to_start  featureAssociation.cpp:860-883
+//   transform_to_end    featureAssociation.cpp:885-953 (IMU terms are the
+//                       reference's zero-IMU constants, kept literally: Q17)
+//   plugin_imu_rotation featureAssociation.cpp:955-1013
+//   accumulate_rotation featureAssociation.cpp:1015-1032
+//   integrate           featureAssociation.cpp:1697-1725
+//   associate_to_map    mapOptmization.cpp:397-482
+#pragma once
+
+#include "slo_libm.h"
+
+#if defined(__HIPCC__)
+#define SLO_P_HD __host__ __device__ inline
+#else
+#define SLO_P_HD inline
+#endif
+
+namespace slo_pose {
+
+using slo_libm::sinf_;
+using slo_libm::cosf_;
+using slo_libm::asinf_;
+using slo_libm::atan2f_;
+
+struct P4 { float x, y, z, w; };
+
+SLO_P_HD P4 transform_to_start(P4 pi, const float* tc) {
+    float s = 10 * (pi.w - (float)(int)pi.w);
+    float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
+    float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
+    float x1 = cosf_(rz) * (pi.x - tx) + sinf_(rz) * (pi.y - ty);
+    float y1 = -sinf_(rz) * (pi.x - tx) + cosf_(rz) * (pi.y - ty);
+    float z1 = (pi.z - tz);
+    float x2 = x1;
+    float y2 = cosf_(rx) * y1 + sinf_(rx) * z1;
+    float z2 = -sinf_(rx) * y1 + cosf_(rx) * z1;
+    P4 o;
+    o.x = cosf_(ry) * x2 - sinf_(ry) * z2;
+    o.y = y2;
+    o.z = sinf_(ry) * x2 + cosf_(ry) * z2;
+    o.w = pi.w;
+    return o;
+}
+
+// imu quantities are the reference's values without an IMU: start angles 0
+// (so cos=1, sin=0 after updateImuRollPitchYawStartSinCos), shifts 0, last 0
+SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
+    const float cosImuRollStart = cosf_(0.0f), cosImuPitchStart = cosf_(0.0f), cosImuYawStart = cosf_(0.0f);
+    const float sinImuRollStart = sinf_(0.0f), sinImuPitchStart = sinf_(0.0f), sinImuYawStart = sinf_(0.0f);
+    const float imuShiftFromStartX = 0, imuShiftFromStartY = 0, imuShiftFromStartZ = 0;
+    const float imuYawLast = 0, imuPitchLast = 0, imuRollLast = 0;
+    float s = 10 * (pi.w - (float)(int)pi.w);
+    float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
+    float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
+    float x1 = cosf_(rz) * (pi.x - tx) + sinf_(rz) * (pi.y - ty);
+    float y1 = -sinf_(rz) * (pi.x - tx) + cosf_(rz) * (pi.y - ty);
+    float z1 = (pi.z - tz);
+    float x2 = x1;
+    float y2 = cosf_(rx) * y1 + sinf_(rx) * z1;
+    float z2 = -sinf_(rx) * y1 + cosf_(rx) * z1;
+    float x3 = cosf_(ry) * x2 - sinf_(ry) * z2;
+    float y3 = y2;
+    float z3 = sinf_(ry) * x2 + cosf_(ry) * z2;
+    rx = tc[0]; ry = tc[1]; rz = tc[2];
+    tx = tc[3]; ty = tc[4]; tz = tc[5];
+    float x4 = cosf_(ry) * x3 + sinf_(ry) * z3;
+    float y4 = y3;
+    float z4 = -sinf_(ry) * x3 + cosf_(ry) * z3;
+    float x5 = x4;
+    float y5 = cosf_(rx) * y4 - sinf_(rx) * z4;
+    float z5 = sinf_(rx) * y4 + cosf_(rx) * z4;
+    float x6 = cosf_(rz) * x5 - sinf_(rz) * y5 + tx;
+    float y6 = sinf_(rz) * x5 + cosf_(rz) * y5 + ty;
+    float z6 = z5 + tz;
+    float x7 = cosImuRollStart * (x6 - imuShiftFromStartX) - sinImuRollStart * (y6 - imuShiftFromStartY);
+    float y7 = sinImuRollStart * (x6 - imuShiftFromStartX) + cosImuRollStart * (y6 - imuShiftFromStartY);
+    float z7 = z6 - imuShiftFromStartZ;
+    float x8 = x7;
+    float y8 = cosImuPitchStart * y7 - sinImuPitchStart * z7;
+    float z8 = sinImuPitchStart * y7 + cosImuPitchStart * z7;
+    float x9 = cosImuYawStart * x8 + sinImuYawStart * z8;
+    float y9 = y8;
+    float z9 = -sinImuYawStart * x8 + cosImuYawStart * z8;
+    float x10 = cosf_(imuYawLast) * x9 - sinf_(imuYawLast) * z9;
+    float y10 = y9;
+    float z10 = sinf_(imuYawLast) * x9 + cosf_(imuYawLast) * z9;
+    float x11 = x10;
+    float y11 = cosf_(imuPitchLast) * y10 + sinf_(imuPitchLast) * z10;
+    float z11 = -sinf_(imuPitchLast) * y10 + cosf_(imuPitchLast) * z10;
+    P4 o;
+    o.x = cosf_(imuRollLast) * x11 + sinf_(imuRollLast) * y11;
+    o.y = -sinf_(imuRollLast) * x11 + cosf_(imuRollLast) * y11;
+    o.z = z11;
+    o.w = (float)(int)pi.w;
+    return o;
+}
+
+SLO_P_HD void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz, float alx,
+                                  float aly, float alz, float& acx, float& acy, float& acz) {
+    float sbcx = sinf_(bcx), cbcx = cosf_(bcx), sbcy = sinf_(bcy), cbcy = cosf_(bcy), sbcz = sinf_(bcz), cbcz = cosf_(bcz);
+    float sblx = sinf_(blx), cblx = cosf_(blx), sbly = sinf_(bly), cbly = cosf_(bly), sblz = sinf_(blz), cblz = cosf_(blz);
+    float salx = sinf_(alx), calx = cosf_(alx), saly = sinf_(aly), caly = cosf_(aly), salz = sinf_(alz), calz = cosf_(alz);
+    float srx = -sbcx * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly) -
+                cbcx * cbcz * (calx * saly * (cbly * sblz - cblz * sblx * sbly) - calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) -
+                cbcx * sbcz * (calx * caly * (cblz * sbly - cbly * sblx * sblz) - calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz);
+    acx = -asinf_(srx);
+    float srycrx = (cbcy * sbcz - cbcz * sbcx * sbcy) * (calx * saly * (cbly * sblz - cblz * sblx * sbly) - calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) -
+                   (cbcy * cbcz + sbcx * sbcy * sbcz) * (calx * caly * (cblz * sbly - cbly * sblx * sblz) - calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz) +
+                   cbcx * sbcy * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly);
+    float crycrx = (cbcz * sbcy - cbcy * sbcx * sbcz) * (calx * caly * (cblz * sbly - cbly * sblx * sblz) - calx * saly * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sblz) -
+                   (sbcy * sbcz + cbcy * cbcz * sbcx) * (calx * saly * (cbly * sblz - cblz * sblx * sbly) - calx * caly * (sbly * sblz + cbly * cblz * sblx) + cblx * cblz * salx) +
+                   cbcx * cbcy * (salx * sblx + calx * caly * cblx * cbly + calx * cblx * saly * sbly);
+    acy = atan2f_(srycrx / cosf_(acx), crycrx / cosf_(acx));
+    float srzcrx = sbcx * (cblx * cbly * (calz * saly - caly * salx * salz) - cblx * sbly * (caly * calz + salx * saly * salz) + calx * salz * sblx) -
+                   cbcx * cbcz * ((caly * calz + salx * saly * salz) * (cbly * sblz - cblz * sblx * sbly) + (calz * saly - caly * salx * salz) * (sbly * sblz + cbly * cblz * sblx) - calx * cblx * cblz * salz) +
+                   cbcx * sbcz * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) + (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) + calx * cblx * salz * sblz);
+    float crzcrx = sbcx * (cblx * sbly * (caly * salz - calz * salx * saly) - cblx * cbly * (saly * salz + caly * calz * salx) + calx * calz * sblx) +
+                   cbcx * cbcz * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) + (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) + calx * calz * cblx * cblz) -
+                   cbcx * sbcz * ((saly * salz + caly * calz * salx) * (cblz * sbly - cbly * sblx * sblz) + (caly * salz - calz * salx * saly) * (cbly * cblz + sblx * sbly * sblz) - calx * calz * cblx * sblz);
+    acz = atan2f_(srzcrx / cosf_(acx), crzcrx / cosf_(acx));
+}
+
+SLO_P_HD void accumulate_rotation(float cx, float cy, float cz, float lx, float ly, float lz, float& ox, float& oy, float& oz) {
+    float srx = cosf_(lx) * cosf_(cx) * sinf_(ly) * sinf_(cz) - cosf_(cx) * cosf_(cz) * sinf_(lx) - cosf_(lx) * cosf_(ly) * sinf_(cx);
+    ox = -asinf_(srx);
+    float srycrx = sinf_(lx) * (cosf_(cy) * sinf_(cz) - cosf_(cz) * sinf_(cx) * sinf_(cy)) +
+                   cosf_(lx) * sinf_(ly) * (cosf_(cy) * cosf_(cz) + sinf_(cx) * sinf_(cy) * sinf_(cz)) + cosf_(lx) * cosf_(ly) * cosf_(cx) * sinf_(cy);
+    float crycrx = cosf_(lx) * cosf_(ly) * cosf_(cx) * cosf_(cy) - cosf_(lx) * sinf_(ly) * (cosf_(cz) * sinf_(cy) - cosf_(cy) * sinf_(cx) * sinf_(cz)) -
+                   sinf_(lx) * (sinf_(cy) * sinf_(cz) + cosf_(cy) * cosf_(cz) * sinf_(cx));
+    oy = atan2f_(srycrx / cosf_(ox), crycrx / cosf_(ox));
+    float srzcrx = sinf_(cx) * (cosf_(lz) * sinf_(ly) - cosf_(ly) * sinf_(lx) * sinf_(lz)) +
+                   cosf_(cx) * sinf_(cz) * (cosf_(ly) * cosf_(lz) + sinf_(lx) * sinf_(ly) * sinf_(lz)) + cosf_(lx) * cosf_(cx) * cosf_(cz) * sinf_(lz);
+    float crzcrx = cosf_(lx) * cosf_(lz) * cosf_(cx) * cosf_(cz) - cosf_(cx) * sinf_(cz) * (cosf_(ly) * sinf_(lz) - cosf_(lz) * sinf_(lx) * sinf_(ly)) -
+                   sinf_(cx) * (sinf_(ly) * sinf_(lz) + cosf_(ly) * cosf_(lz) * sinf_(lx));
+    oz = atan2f_(srzcrx / cosf_(ox), crzcrx / cosf_(ox));
+}
+
+// integrateTransformation: sum <- sum (+) cur, zero IMU
+SLO_P_HD void integrate(float* sum, const float* cur) {
+    float rx, ry, rz, tx, ty, tz;
+    accumulate_rotation(sum[0], sum[1], sum[2], -cur[0], -cur[1], -cur[2], rx, ry, rz);
+    const float sx = 0, sy = 0, sz = 0;  // imuShiftFromStart*
+    float x1 = cosf_(rz) * (cur[3] - sx) - sinf_(rz) * (cur[4] - sy);
+    float y1 = sinf_(rz) * (cur[3] - sx) + cosf_(rz) * (cur[4] - sy);
+    float z1 = cur[5] - sz;
+    float x2 = x1;
+    float y2 = cosf_(rx) * y1 - sinf_(rx) * z1;
+    float z2 = sinf_(rx) * y1 + cosf_(rx) * z1;
+    tx = sum[3] - (cosf_(ry) * x2 + sinf_(ry) * z2);
+    ty = sum[4] - y2;
+    tz = sum[5] - (-sinf_(ry) * x2 + cosf_(ry) * z2);
+    plugin_imu_rotation(rx, ry, rz, 0, 0, 0, 0, 0, 0, rx, ry, rz);
+    sum[0] = rx; sum[1] = ry; sum[2] = rz;
+    sum[3] = tx; sum[4] = ty; sum[5] = tz;
+}
+
+// transformAssociateToMap: predicted map pose tbm from odometry sum and the
+// last (before, after) mapping pair
+SLO_P_HD void associate_to_map(const float* sum, const float* bef, const float* aft, float* incre, float* tbm) {
+    float x1 = cosf_(sum[1]) * (bef[3] - sum[3]) - sinf_(sum[1]) * (bef[5] - sum[5]);
+    float y1 = bef[4] - sum[4];
+    float z1 = sinf_(sum[1]) * (bef[3] - sum[3]) + cosf_(sum[1]) * (bef[5] - sum[5]);
+    float x2 = x1;
+    float y2 = cosf_(sum[0]) * y1 + sinf_(sum[0]) * z1;
+    float z2 = -sinf_(sum[0]) * y1 + cosf_(sum[0]) * z1;
+    incre[3] = cosf_(sum[2]) * x2 + sinf_(sum[2]) * y2;
+    incre[4] = -sinf_(sum[2]) * x2 + cosf_(sum[2]) * y2;
+    incre[5] = z2;
+    float sbcx = sinf_(sum[0]), cbcx = cosf_(sum[0]), sbcy = sinf_(sum[1]), cbcy = cosf_(sum[1]), sbcz = sinf_(sum[2]), cbcz = cosf_(sum[2]);
+    float sblx = sinf_(bef[0]), cblx = cosf_(bef[0]), sbly = sinf_(bef[1]), cbly = cosf_(bef[1]), sblz = sinf_(bef[2]), cblz = cosf_(bef[2]);
+    float salx = sinf_(aft[0]), calx = cosf_(aft[0]), saly = sinf_(aft[1]), caly = cosf_(aft[1]), salz = sinf_(aft[2]), calz = cosf_(aft[2]);
+    float srx = -sbcx * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz) -
+                cbcx * sbcy * (calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
+                cbcx * cbcy * (calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx);
+    tbm[0] = -asinf_(srx);
+    float srycrx = sbcx * (cblx * cblz * (caly * salz - calz * salx * saly) - cblx * sblz * (caly * calz + salx * saly * salz) + calx * saly * sblx) -
+                   cbcx * cbcy * ((caly * calz + salx * saly * salz) * (cblz * sbly - cbly * sblx * sblz) + (caly * salz - calz * salx * saly) * (sbly * sblz + cbly * cblz * sblx) - calx * cblx * cbly * saly) +
+                   cbcx * sbcy * ((caly * calz + salx * saly * salz) * (cbly * cblz + sblx * sbly * sblz) + (caly * salz - calz * salx * saly) * (cbly * sblz - cblz * sblx * sbly) + calx * cblx * saly * sbly);
+    float crycrx = sbcx * (cblx * sblz * (calz * saly - caly * salx * salz) - cblx * cblz * (saly * salz + caly * calz * salx) + calx * caly * sblx) +
+                   cbcx * cbcy * ((saly * salz + caly * calz * salx) * (sbly * sblz + cbly * cblz * sblx) + (calz * saly - caly * salx * salz) * (cblz * sbly - cbly * sblx * sblz) + calx * caly * cblx * cbly) -
+                   cbcx * sbcy * ((saly * salz + caly * calz * salx) * (cbly * sblz - cblz * sblx * sbly) + (calz * saly - caly * salx * salz) * (cbly * cblz + sblx * sbly * sblz) - calx * caly * cblx * sbly);
+    tbm[1] = atan2f_(srycrx / cosf_(tbm[0]), crycrx / cosf_(tbm[0]));
+    float srzcrx = (cbcz * sbcy - cbcy * sbcx * sbcz) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) -
+                   (cbcy * cbcz + sbcx * sbcy * sbcz) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) +
+                   cbcx * sbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz);
+    float crzcrx = (cbcy * sbcz - cbcz * sbcx * sbcy) * (calx * calz * (cbly * sblz - cblz * sblx * sbly) - calx * salz * (cbly * cblz + sblx * sbly * sblz) + cblx * salx * sbly) -
+                   (sbcy * sbcz + cbcy * cbcz * sbcx) * (calx * salz * (cblz * sbly - cbly * sblx * sblz) - calx * calz * (sbly * sblz + cbly * cblz * sblx) + cblx * cbly * salx) +
+                   cbcx * cbcz * (salx * sblx + calx * cblx * salz * sblz + calx * calz * cblx * cblz);
+    tbm[2] = atan2f_(srzcrx / cosf_(tbm[0]), crzcrx / cosf_(tbm[0]));
+    x1 = cosf_(tbm[2]) * incre[3] - sinf_(tbm[2]) * incre[4];
+    y1 = sinf_(tbm[2]) * incre[3] + cosf_(tbm[2]) * incre[4];
+    z1 = incre[5];
+    x2 = x1;
+    y2 = cosf_(tbm[0]) * y1 - sinf_(tbm[0]) * z1;
+    z2 = sinf_(tbm[0]) * y1 + cosf_(tbm[0]) * z1;
+    tbm[3] = aft[3] - (cosf_(tbm[1]) * x2 + sinf_(tbm[1]) * z2);
+    tbm[4] = aft[4] - y2;
+    tbm[5] = aft[5] - (-sinf_(tbm[1]) * x2 + cosf_(tbm[1]) * z2);
+}
+
+}  // namespace slo_pose

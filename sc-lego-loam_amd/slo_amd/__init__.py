@@ -1,0 +1,154 @@
+"""slo_amd — MI355X-native SC-LeGO-LOAM per-scan hot path (host mirror).
+
+Python view of libslo.so (include/slo_abi.h).  The classes mirror the
+reference's node interfaces for the hot path:
+
+  ImageProjection.cloudHandler        imageProjection.cpp:181
+  FeatureAssociation.runFeatureAssociation  featureAssociation.cpp:1817
+  MapOptimization.run                 mapOptmization.cpp:1673
+  SCManager.detectLoopClosureID       Scancontext.h:73
+
+and `Pipeline` drives the batched path (one scan per stream per call) that
+bench.py measures.  Device memory for batched inputs is owned by torch
+(plumbing only); all compute is the HIP kernels in csrc/.
+"""
+import ctypes
+
+import numpy as np
+
+from . import _abi
+from ._abi import SloConfig, SegView, FaView, MapView
+
+PRESETS = {
+    "vlp16": 0, "hdl32": 1, "vls128": 2, "os1_16": 3, "os1_64": 4,
+    "os64_1800": 5, "hdl64_1800": 6, "dense128": 7,
+}
+
+_CLOUD_OUT = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "less_sharp", "flat", "less_flat",
+              "corner_last", "surf_last"}
+_DT = {"range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8,
+       "seg_col": np.uint32, "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32,
+       "orient": np.float32, "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32,
+       "smooth_ind": np.int32, "transform_sum": np.float32, "transform_cur": np.float32,
+       "fa_iters": np.int32, "mapped": np.float32, "n_keyframes": np.int32, "flags": np.int32,
+       "keyposes": np.float32, "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64,
+       "detect": np.int32, "detect_f": np.float64}
+
+
+class SloError(RuntimeError):
+    pass
+
+
+def preset(name_or_id):
+    pid = PRESETS.get(name_or_id, name_or_id)
+    c = SloConfig()
+    if _abi.lib().slo_config_preset(int(pid), ctypes.byref(c)) != 0:
+        raise ValueError(f"unknown preset {name_or_id}")
+    return c
+
+
+def gen_scan(preset_id, config_id, stream_id, k, n_points):
+    out = np.empty((n_points, 4), np.float32)
+    n = _abi.lib().slo_gen_scan(int(preset_id), int(config_id), int(stream_id), int(k), out.ctypes.data)
+    if n < 0:
+        raise SloError("slo_gen_scan failed")
+    return out[:n]
+
+
+class Context:
+    """One libslo context: `n_streams` independent streams on HIP device `device`."""
+
+    def __init__(self, cfg, device=0, n_streams=1):
+        self.L = _abi.lib()
+        self.cfg = cfg
+        self.n_streams = n_streams
+        h = ctypes.c_void_p()
+        rc = self.L.slo_create(ctypes.byref(cfg), int(device), int(n_streams), ctypes.byref(h))
+        if rc != 0:
+            raise SloError(f"slo_create failed ({rc})")
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.slo_destroy(self.h)
+            self.h = None
+
+    __del__ = close
+
+    def _ok(self, rc, what):
+        if rc != 0:
+            raise SloError(f"{what}: {rc} {self.L.slo_last_error(self.h).decode()}")
+
+    @property
+    def stream_handle(self):
+        return self.L.slo_stream(self.h)
+
+    def synchronize(self):
+        self._ok(self.L.slo_synchronize(self.h), "slo_synchronize")
+
+    # batched, device pointers (int addresses)
+    def batch_image_projection(self, d_pts, d_cnt):
+        self._ok(self.L.slo_batch_image_projection(self.h, d_pts, d_cnt), "slo_batch_image_projection")
+
+    def batch_feature_association(self):
+        self._ok(self.L.slo_batch_feature_association(self.h), "slo_batch_feature_association")
+
+    def batch_process(self, d_pts, d_cnt, t_scan):
+        self._ok(self.L.slo_batch_process(self.h, d_pts, d_cnt, float(t_scan)), "slo_batch_process")
+
+    def get(self, stream, name):
+        n = self.L.slo_get(self.h, int(stream), name.encode(), None, 0)
+        if n < 0:
+            raise SloError(f"slo_get({name}) -> {n}")
+        out = np.empty((n, 4), np.float32) if name in _CLOUD_OUT else np.empty(n, _DT[name])
+        if n:
+            rc = self.L.slo_get(self.h, int(stream), name.encode(), out.ctypes.data, out.nbytes)
+            if rc < 0:
+                raise SloError(f"slo_get({name}) -> {rc}")
+        return out
+
+    # per-kernel timing (HIP events)
+    def timing(self, enable=True):
+        self._ok(self.L.slo_timing_enable(self.h, int(enable)), "slo_timing_enable")
+
+    def timing_reset(self):
+        self._ok(self.L.slo_timing_reset(self.h), "slo_timing_reset")
+
+    def timing_read(self):
+        cap = 64
+        buf = ctypes.create_string_buffer(8192)
+        ms = (ctypes.c_double * cap)()
+        cnt = (ctypes.c_int64 * cap)()
+        n = self.L.slo_timing_read(self.h, buf, 8192, ms, cnt, cap)
+        names = buf.raw.split(b"\0")[:n]
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
+
+
+class ImageProjection:
+    """Mirror of ImageProjection::cloudHandler (imageProjection.cpp:181) on stream 0."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def cloudHandler(self, points_xyzi):
+        pts = np.ascontiguousarray(points_xyzi, np.float32)
+        view = SegView()
+        self.ctx._ok(self.ctx.L.slo_image_projection(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
+                                                     ctypes.byref(view)), "slo_image_projection")
+        return {k: self.ctx.get(0, k) for k in ("seg_pts", "seg_ground", "seg_col", "seg_range", "ring_start",
+                                                 "ring_end", "orient", "outlier")}
+
+
+class FeatureAssociation:
+    """Mirror of FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1817) on stream 0."""
+
+    def __init__(self, ctx):
+        self.ctx = ctx
+
+    def runFeatureAssociation(self, t_scan=0.0):
+        view = FaView()
+        self.ctx._ok(self.ctx.L.slo_feature_association(self.ctx.h, float(t_scan), ctypes.byref(view)),
+                     "slo_feature_association")
+        return {"transform_sum": np.array(view.transform_sum[:], np.float32), "published": bool(view.published),
+                "n_sharp": view.n_sharp, "n_flat": view.n_flat, "n_less_sharp": view.n_less_sharp,
+                "n_less_flat": view.n_less_flat}

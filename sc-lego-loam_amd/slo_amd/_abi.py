@@ -1,0 +1,113 @@
+"""ctypes binding of include/slo_abi.h (libslo.so, the gfx950 product library).
+
+This is the same binding a maintainer would add to call the C ABI from any
+host language.  There is no CPU fallback: if libslo.so is
+missing or no HIP device is present the calls raise.
+"""
+import ctypes
+import os
+import subprocess
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # sc-lego-loam_amd/
+LIB_PATH = os.path.join(_PKG, "libslo.so")
+_LIB = None
+
+
+class SloConfig(ctypes.Structure):
+    """Mirror of struct slo_config (csrc/slo_config.h)."""
+    _fields_ = [
+        ("n_scan", ctypes.c_int32), ("horizon_scan", ctypes.c_int32),
+        ("ang_res_x", ctypes.c_float), ("ang_res_y", ctypes.c_float), ("ang_bottom", ctypes.c_float),
+        ("ground_scan_ind", ctypes.c_int32),
+        ("sensor_minimum_range", ctypes.c_float), ("sensor_mount_angle", ctypes.c_float),
+        ("segment_theta", ctypes.c_float), ("segment_valid_point_num", ctypes.c_int32),
+        ("segment_valid_line_num", ctypes.c_int32), ("segment_alpha_x", ctypes.c_float),
+        ("segment_alpha_y", ctypes.c_float),
+        ("sin_alpha_x", ctypes.c_float), ("cos_alpha_x", ctypes.c_float),
+        ("sin_alpha_y", ctypes.c_float), ("cos_alpha_y", ctypes.c_float),
+        ("scan_period", ctypes.c_float), ("edge_feature_num", ctypes.c_int32),
+        ("surf_feature_num", ctypes.c_int32), ("sections_total", ctypes.c_int32),
+        ("edge_threshold", ctypes.c_float), ("surf_threshold", ctypes.c_float),
+        ("nearest_feature_search_sq_dist", ctypes.c_float),
+        ("loop_closure_enable", ctypes.c_int32), ("mapping_process_interval", ctypes.c_double),
+        ("surrounding_keyframe_search_num", ctypes.c_int32),
+        ("leaf_less_flat", ctypes.c_float), ("leaf_corner", ctypes.c_float), ("leaf_surf", ctypes.c_float),
+        ("leaf_outlier", ctypes.c_float), ("leaf_sc", ctypes.c_float),
+        ("sc_lidar_height", ctypes.c_double), ("sc_num_ring", ctypes.c_int32), ("sc_num_sector", ctypes.c_int32),
+        ("sc_max_radius", ctypes.c_double), ("sc_num_exclude_recent", ctypes.c_int32),
+        ("sc_num_candidates", ctypes.c_int32), ("sc_search_ratio", ctypes.c_double),
+        ("sc_dist_thres", ctypes.c_double), ("sc_tree_making_period", ctypes.c_int32),
+        ("sc_atan_float", ctypes.c_int32), ("skip_frame_num", ctypes.c_int32), ("max_points", ctypes.c_int32),
+    ]
+
+
+class SegView(ctypes.Structure):
+    _fields_ = [("n_segmented", ctypes.c_int32), ("segmented", ctypes.c_void_p), ("ground_flag", ctypes.c_void_p),
+                ("col_ind", ctypes.c_void_p), ("range", ctypes.c_void_p), ("start_ring_index", ctypes.c_void_p),
+                ("end_ring_index", ctypes.c_void_p), ("start_orientation", ctypes.c_float),
+                ("end_orientation", ctypes.c_float), ("orientation_diff", ctypes.c_float),
+                ("n_outlier", ctypes.c_int32), ("outlier", ctypes.c_void_p)]
+
+
+class FaView(ctypes.Structure):
+    _fields_ = [("n_sharp", ctypes.c_int32), ("n_less_sharp", ctypes.c_int32), ("n_flat", ctypes.c_int32),
+                ("n_less_flat", ctypes.c_int32), ("sharp", ctypes.c_void_p), ("less_sharp", ctypes.c_void_p),
+                ("flat", ctypes.c_void_p), ("less_flat", ctypes.c_void_p),
+                ("transform_sum", ctypes.c_float * 6), ("published", ctypes.c_int32)]
+
+
+class MapView(ctypes.Structure):
+    _fields_ = [("ran", ctypes.c_int32), ("keyframe_saved", ctypes.c_int32), ("n_keyframes", ctypes.c_int32),
+                ("transform_aft_mapped", ctypes.c_float * 6)]
+
+
+# symbols declared in include/slo_abi.h (tests check every one is exported)
+EXPORTS = [
+    "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
+    "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
+    "slo_batch_sc_detect", "slo_batch_process", "slo_image_projection", "slo_feature_association",
+    "slo_map_optimization", "slo_sc_detect", "slo_get", "slo_timing_enable", "slo_timing_read",
+    "slo_timing_reset", "slo_gen_scan",
+]
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _PKG], check=True)
+
+
+def lib():
+    """Load libslo.so (raises if it is not built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError("libslo.so not built (run __graft_entry__.build() or make -C sc-lego-loam_amd)")
+    L = ctypes.CDLL(LIB_PATH)
+    P = ctypes.c_void_p
+    L.slo_config_preset.argtypes = [ctypes.c_int, ctypes.POINTER(SloConfig)]
+    L.slo_create.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+    L.slo_destroy.argtypes = [P]
+    L.slo_last_error.argtypes = [P]
+    L.slo_last_error.restype = ctypes.c_char_p
+    L.slo_stream.argtypes = [P]
+    L.slo_stream.restype = P
+    L.slo_synchronize.argtypes = [P]
+    L.slo_batch_image_projection.argtypes = [P, P, P]
+    L.slo_batch_feature_association.argtypes = [P]
+    L.slo_batch_map_optimization.argtypes = [P, P, P, ctypes.c_double]
+    L.slo_batch_sc_detect.argtypes = [P]
+    L.slo_batch_process.argtypes = [P, P, P, ctypes.c_double]
+    L.slo_image_projection.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.POINTER(SegView)]
+    L.slo_feature_association.argtypes = [P, ctypes.c_double, ctypes.POINTER(FaView)]
+    L.slo_map_optimization.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                       ctypes.c_double, ctypes.POINTER(MapView)]
+    L.slo_sc_detect.argtypes = [P, ctypes.POINTER(ctypes.c_int32), ctypes.POINTER(ctypes.c_float),
+                                ctypes.POINTER(ctypes.c_double)]
+    L.slo_get.argtypes = [P, ctypes.c_int, ctypes.c_char_p, P, ctypes.c_size_t]
+    L.slo_timing_enable.argtypes = [P, ctypes.c_int]
+    L.slo_timing_reset.argtypes = [P]
+    L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
+    L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    _LIB = L
+    return L
