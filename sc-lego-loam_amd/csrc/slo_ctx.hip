@@ -138,6 +138,38 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.ind_surf, S * v.cap_flat * 3);
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
+    // ---- mapping + Scan Context history
+    v.KFR = 64;
+    v.KFMAX = 4096;
+    v.cap_kc = v.cap_less_sharp;
+    v.cap_ks = (int)(H / 3);
+    v.cap_ko = (int)(H / 5);
+    const int NKF = cfg->surrounding_keyframe_search_num;
+    v.cap_mc = NKF * v.cap_kc;
+    v.cap_ms = NKF * (v.cap_ks + v.cap_ko);
+    v.cap_st = (int)(H + H / 5);
+    const size_t NRS = (size_t)cfg->sc_num_ring * cfg->sc_num_sector;
+    c.add(&v.outl_cam, S * H);
+    c.add(&v.kf_corner, S * v.KFR * v.cap_kc);
+    c.add(&v.kf_surf, S * v.KFR * v.cap_ks);
+    c.add(&v.kf_outl, S * v.KFR * v.cap_ko);
+    c.add(&v.kf_n, S * v.KFR * 3);
+    c.add(&v.kf_pose, S * v.KFMAX * 6);
+    c.add(&v.map_c, S * v.cap_mc);
+    c.add(&v.map_s, S * v.cap_ms);
+    c.add(&v.map_c_ds, S * v.cap_mc);
+    c.add(&v.map_s_ds, S * v.cap_ms);
+    c.add(&v.cur_raw_ds, S * v.P);
+    c.add(&v.cur_c_ds, S * v.cap_less_sharp);
+    c.add(&v.cur_s_ds, S * H);
+    c.add(&v.cur_o_ds, S * (H / 5));
+    c.add(&v.cur_st, S * v.cap_st);
+    c.add(&v.cur_st_ds, S * v.cap_st);
+    c.add(&v.mo_part, S * SLO_MO_BLOCKS * 28);
+    c.add(&v.sc_desc, S * v.KFMAX * NRS);
+    c.add(&v.sc_ring, S * v.KFMAX * cfg->sc_num_ring);
+    c.add(&v.sc_ringd, S * v.KFMAX * cfg->sc_num_ring);
+    c.add(&v.sc_sect, S * v.KFMAX * cfg->sc_num_sector);
     ctx->arena_bytes = c.off;
     if (hipMalloc(&ctx->arena, ctx->arena_bytes) != hipSuccess) {
         ctx->err = "hipMalloc arena failed";
@@ -154,6 +186,11 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         return SLO_E_HIP;
     }
     memset(ctx->h_st, 0, sizeof(StreamState) * S);
+    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc) ||
+        slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms)) {
+        slo_destroy(ctx);
+        return SLO_E_HIP;
+    }
     *out = ctx;
     return SLO_OK;
 }
@@ -163,6 +200,9 @@ void slo_destroy(slo_ctx* ctx) {
     hipSetDevice(ctx->dev);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
+    slo::vg_free(ctx);
+    slo::grid_free(ctx->grid_c);
+    slo::grid_free(ctx->grid_s);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->h_st) hipHostFree(ctx->h_st);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
@@ -209,15 +249,36 @@ int slo_batch_feature_association(slo_ctx* ctx) {
     return SLO_OK;
 }
 
+}  // extern "C"
+
+namespace slo {
+__global__ void k_clear_flags(DevView v) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    v.st[s].mo_ran = 0;
+    v.st[s].kf_saved = 0;
+    v.st[s].det_valid = 0;
+}
+}  // namespace slo
+
+extern "C" {
+
+// Runs the mapping step if this scan reached mapping (FA published it,
+// FA:1790-1814) and the mapping interval has elapsed (MO:1685).
 int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
-    (void)d_points; (void)d_counts; (void)t_scan;
-    if (!ctx) return SLO_E_ARG;
-    return SLO_OK;  // mapping stage lands in slo_map.hip
+    if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    SLO_LAUNCH(ctx, "clear_flags", slo::k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
+    if (!ctx->fa_published) return SLO_OK;
+    if (!(t_scan - ctx->t_last_processing >= ctx->cfg.mapping_process_interval)) return SLO_OK;
+    ctx->t_last_processing = t_scan;
+    return slo::map_run(ctx, (const float4*)d_points, d_counts);
 }
 
 int slo_batch_sc_detect(slo_ctx* ctx) {
     if (!ctx) return SLO_E_ARG;
-    return SLO_OK;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::sc_detect_run(ctx);
 }
 
 int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
@@ -225,12 +286,9 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     if (r) return r;
     r = slo_batch_feature_association(ctx);
     if (r) return r;
-    if (ctx->fa_published) {
-        r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
-        if (r) return r;
-        r = slo_batch_sc_detect(ctx);
-    }
-    return r;
+    r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
+    if (r) return r;
+    return slo_batch_sc_detect(ctx);
 }
 
 // ---------------------------------------------------------------- readback
@@ -285,7 +343,38 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "fa_iters") { int32_t a[2] = {st.iters_surf, st.iters_corner}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4; }
     else if (name == "mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformAftMapped, 24); count = 6; esz = 4; }
     else if (name == "n_keyframes") { tmp.resize(4); memcpy(tmp.data(), &st.n_keyframes, 4); count = 1; esz = 4; }
-    else if (name == "flags") { tmp.resize(4); memcpy(tmp.data(), &st.flags, 4); count = 1; esz = 4; }
+    else if (name == "flags") {
+        int32_t f = (st.mo_ran ? 2 : 0) | (st.kf_saved ? 4 : 0) | (st.det_valid ? 8 : 0);
+        tmp.resize(4); memcpy(tmp.data(), &f, 4); count = 1; esz = 4;
+    }
+    else if (name == "tobe_mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformTobeMapped, 24); count = 6; esz = 4; }
+    else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
+    else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
+    else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
+    else if (name == "raw_ds") dev(v.cur_raw_ds + s * v.P, st.n_raw_ds, 16);
+    else if (name == "corner_ds") dev(v.cur_c_ds + s * v.cap_less_sharp, st.n_corner_ds, 16);
+    else if (name == "surf_total_ds") dev(v.cur_st_ds + s * v.cap_st, st.n_surf_total_ds, 16);
+    else if (name == "map_corner_ds") dev(v.map_c_ds + s * v.cap_mc, st.n_cmap_ds, 16);
+    else if (name == "map_surf_ds") dev(v.map_s_ds + s * v.cap_ms, st.n_smap_ds, 16);
+    else if (name == "sc_desc" || name == "ring_key" || name == "sector_key") {
+        if (st.sc_count == 0) { count = 0; esz = 8; }
+        else {
+            const size_t NR = v.cfg.sc_num_ring, NSc = v.cfg.sc_num_sector, k = st.sc_count - 1;
+            if (name == "sc_desc") dev(v.sc_desc + (s * v.KFMAX + k) * NR * NSc, NR * NSc, 8);
+            else if (name == "ring_key") dev(v.sc_ringd + (s * v.KFMAX + k) * NR, NR, 8);
+            else dev(v.sc_sect + (s * v.KFMAX + k) * NSc, NSc, 8);
+        }
+    } else if (name == "detect") {
+        if (!st.det_valid) { count = 0; esz = 4; }
+        else {
+            std::vector<int32_t> d{st.det_loop_id, st.det_nn_idx, st.sc_count >= v.cfg.sc_num_exclude_recent + 1 ? v.cfg.sc_num_candidates : 0};
+            for (int i = 0; i < d[2]; ++i) d.push_back(st.det_cand[i]);
+            tmp.resize(4 * d.size()); memcpy(tmp.data(), d.data(), 4 * d.size()); count = d.size(); esz = 4;
+        }
+    } else if (name == "detect_f") {
+        if (!st.det_valid) { count = 0; esz = 8; }
+        else { double d[2] = {(double)st.det_yaw, st.det_min_dist}; tmp.resize(16); memcpy(tmp.data(), d, 16); count = 2; esz = 8; }
+    }
     else return SLO_E_ARG;
     const size_t bytes = std::min(cap_bytes, count * esz);
     if (dst && bytes) {

@@ -55,6 +55,7 @@ struct StreamState {
     float prevPos[3];
     int32_t mo_ran, kf_saved, mo_iters, mo_converged;
     int32_t n_corner_map, n_surf_map, n_corner_ds, n_surf_total_ds, n_raw_ds;
+    int32_t n_surf_ds, n_outl_ds, n_st, n_cmap_ds, n_smap_ds, n_sel, map_ok;
     // scan context
     int32_t sc_count, sc_tree_n, sc_counter;
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];
@@ -119,6 +120,66 @@ struct DevView {
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
     StreamState* st;     // [S]
+    // ---- mapping (mapOptmization.cpp)
+    int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
+    int KFMAX;           // keyframe pose / Scan Context history capacity
+    int cap_kc, cap_ks, cap_ko, cap_mc, cap_ms, cap_st;
+    float4* outl_cam;    // [S][H]          outlier cloud, camera frame (adjustOutlierCloud)
+    float4* kf_corner;   // [S][KFR][cap_kc] keyframe clouds, world frame
+    float4* kf_surf;     // [S][KFR][cap_ks]
+    float4* kf_outl;     // [S][KFR][cap_ko]
+    int32_t* kf_n;       // [S][KFR][3]
+    float* kf_pose;      // [S][KFMAX][6]   cloudKeyPoses6D (x,y,z,roll,pitch,yaw)
+    float4* map_c;       // [S][cap_mc]     laserCloudCornerFromMap
+    float4* map_s;       // [S][cap_ms]     laserCloudSurfFromMap
+    float4* map_c_ds;    // [S][cap_mc]
+    float4* map_s_ds;    // [S][cap_ms]
+    float4* cur_raw_ds;  // [S][P]          laserCloudRawDS
+    float4* cur_c_ds;    // [S][cap_less_sharp]
+    float4* cur_s_ds;    // [S][H]
+    float4* cur_o_ds;    // [S][H/5]
+    float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
+    float4* cur_st_ds;   // [S][cap_st]
+    double* mo_part;     // [S][MO_BLOCKS][28] partial A^T A / A^T b / count
+    // hash grids over the DS maps (1 m cells)
+    int Tc, Ts;
+    const int32_t *gc_cnt, *gc_off, *gs_cnt, *gs_off;
+    const float4 *gc_ent, *gs_ent;
+    // ---- Scan Context history (Scancontext.h:99-106)
+    double* sc_desc;     // [S][KFMAX][NR*NS]
+    float* sc_ring;      // [S][KFMAX][NR]   invkeys (float, tree data)
+    double* sc_ringd;    // [S][KFMAX][NR]
+    double* sc_sect;     // [S][KFMAX][NS]
+};
+
+#define SLO_MO_BLOCKS 64
+
+__host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
+    return (((unsigned int)x * 73856093u) ^ ((unsigned int)y * 19349663u) ^ ((unsigned int)z * 83492791u)) &
+           (unsigned int)(T - 1);
+}
+
+struct VgParams;
+struct MapWs {  // VoxelGrid workspace
+    size_t items = 0;
+    unsigned long long *keys = nullptr, *keys2 = nullptr;
+    unsigned int *vals = nullptr, *vals2 = nullptr;
+    int *flags = nullptr, *rank = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    int32_t* off = nullptr;
+    unsigned int* bounds = nullptr;
+    VgParams* prm = nullptr;
+    int32_t* errflag = nullptr;
+    int32_t* h_total = nullptr;
+};
+struct HashGrid {
+    int T = 0;
+    size_t ent_stride = 0;
+    int32_t *cnt = nullptr, *cur = nullptr, *off = nullptr;
+    float4* ent = nullptr;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
 };
 
 }  // namespace slo
@@ -148,6 +209,10 @@ struct slo_ctx {
     size_t h_stage_bytes = 0;
     float4* d_in = nullptr;   // internal input buffer [S][P]
     int32_t* d_cnt = nullptr;
+    // mapping workspaces
+    slo::MapWs mws;
+    slo::HashGrid grid_c, grid_s;
+    bool map_ready = false;
 };
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -157,6 +222,15 @@ void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
 int fa_odometry_run(slo_ctx* ctx, bool first_scan);
+int vg_alloc(slo_ctx* ctx);
+void vg_free(slo_ctx* ctx);
+int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
+           float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);
+int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride);
+void grid_free(HashGrid& g);
+int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
+int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts);
+int sc_detect_run(slo_ctx* ctx);
 }  // namespace slo
 
 #define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \

@@ -1,0 +1,497 @@
+// slo_map.hip — scan-to-map optimisation of mapOptmization.cpp for a batch
+// of S streams: transformAssociateToMap (MO:397-482), the recent-50 keyframe
+// local map (MO:1122-1231, loopClosureEnableFlag branch including its
+// latestFrameID bookkeeping), downsampleCurrentScan (MO:1233-1263),
+// cornerOptimization / surfOptimization / LMOptimization (MO:1265-1499),
+// scan2MapOptimization (MO:1501-1522), transformUpdate (MO:484-517) and
+// saveKeyFramesAndFactor (MO:1525-1638, GTSAM replaced by its fixed point:
+// with only prior + consistent between-factors the newest estimate is its
+// initial value) with the Scan Context descriptor build of the keyframe
+// (Scancontext.cpp:151-244).
+//
+// Layout: keyframe clouds are stored once, already in the map frame
+// (transformPointCloud with the keyframe pose, MO:566-596 — the pose never
+// changes on this path, so transforming at save time equals the reference's
+// transform at deque insertion).  Each LM iteration is two launches: every
+// workgroup of a stream takes a slice of its corner+surf queries, does the
+// exact 5-NN in the 1 m hash grid, the 3x3 Jacobi / 5x3 QR of the reference
+// and accumulates A^T A, A^T b in double; a per-stream lane then sums the
+// slices in fixed order and runs the 6x6 QR / degeneracy projection.
+#include "slo_internal.h"
+#include "slo_libm.h"
+#include "slo_pose.h"
+#include "slo_linalg.h"
+#include <float.h>
+
+namespace slo {
+
+using slo_pose::P4;
+#define ST_STRIDE ((int)(sizeof(StreamState) / sizeof(int32_t)))
+
+// ---------------------------------------------------------------- prepare
+__global__ void k_mo_prepare(DevView v) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    // adjustOutlierCloud (FA:1746-1757): lidar -> camera axes
+    for (int i = threadIdx.x; i < st.outlier_count; i += blockDim.x) {
+        float4 p = v.outlier[(size_t)s * v.H + i];
+        v.outl_cam[(size_t)s * v.H + i] = make_float4(p.y, p.z, p.x, p.w);
+    }
+    if (threadIdx.x != 0) return;
+    st.mo_ran = 1;
+    st.kf_saved = 0;
+    st.mo_iters = 0;
+    st.mo_converged = 0;
+    for (int k = 0; k < 6; ++k) st.mo_sum[k] = st.transformSum[k];  // laserOdometryHandler
+    slo_pose::associate_to_map(st.mo_sum, st.transformBefMapped, st.transformAftMapped, st.transformIncre,
+                               st.transformTobeMapped);
+    // extractSurroundingKeyFrames: recent keyframe deque
+    const int nk = st.n_keyframes;
+    const int N = v.cfg.surrounding_keyframe_search_num;
+    if (nk > 0) {
+        if (st.recent_n < N) {
+            int cnt = 0;
+            int ids[64];
+            for (int i = nk - 1; i >= 0; --i) {
+                ids[cnt++] = i;  // push_front order reversed below
+                if (cnt >= N) break;
+            }
+            for (int k = 0; k < cnt; ++k) st.recent_ids[k] = ids[cnt - 1 - k];
+            st.recent_n = cnt;
+        } else if (st.latestFrameID != nk - 1) {
+            for (int k = 1; k < st.recent_n; ++k) st.recent_ids[k - 1] = st.recent_ids[k];
+            st.latestFrameID = nk - 1;
+            st.recent_ids[st.recent_n - 1] = st.latestFrameID;
+        }
+    } else {
+        st.recent_n = 0;
+    }
+    int nc = 0, ns = 0;
+    for (int k = 0; k < st.recent_n; ++k) {
+        const int slot = st.recent_ids[k] % v.KFR;
+        const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
+        nc += kn[0];
+        ns += kn[1] + kn[2];
+    }
+    if (nc > v.cap_mc) { nc = v.cap_mc; st.err |= 2; }
+    if (ns > v.cap_ms) { ns = v.cap_ms; st.err |= 2; }
+    st.n_corner_map = nc;
+    st.n_surf_map = ns;
+}
+
+// one block per deque entry (blockIdx.x) of stream blockIdx.y
+__global__ void k_mo_assemble(DevView v) {
+    const int s = blockIdx.y, e = blockIdx.x;
+    const StreamState& st = v.st[s];
+    if (e >= st.recent_n) return;
+    int oc = 0, os = 0;
+    for (int k = 0; k < e; ++k) {
+        const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + st.recent_ids[k] % v.KFR) * 3;
+        oc += kn[0];
+        os += kn[1] + kn[2];
+    }
+    const int slot = st.recent_ids[e] % v.KFR;
+    const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
+    const size_t ks = (size_t)s * v.KFR + slot;
+    for (int i = threadIdx.x; i < kn[0]; i += blockDim.x)
+        if (oc + i < v.cap_mc) v.map_c[(size_t)s * v.cap_mc + oc + i] = v.kf_corner[ks * v.cap_kc + i];
+    for (int i = threadIdx.x; i < kn[1]; i += blockDim.x)
+        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = v.kf_surf[ks * v.cap_ks + i];
+    for (int i = threadIdx.x; i < kn[2]; i += blockDim.x)
+        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = v.kf_outl[ks * v.cap_ko + i];
+}
+
+__global__ void k_mo_concat(DevView v) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    const int a = st.n_surf_ds, b = st.n_outl_ds;
+    for (int i = threadIdx.x; i < a; i += blockDim.x) v.cur_st[(size_t)s * v.cap_st + i] = v.cur_s_ds[(size_t)s * v.H + i];
+    for (int i = threadIdx.x; i < b; i += blockDim.x)
+        v.cur_st[(size_t)s * v.cap_st + a + i] = v.cur_o_ds[(size_t)s * (v.H / 5) + i];
+    if (threadIdx.x == 0) {
+        st.n_st = a + b;
+        st.map_ok = st.n_cmap_ds > 10 && st.n_smap_ds > 100;
+    }
+}
+
+// ---------------------------------------------------------------- 5-NN in the hash grid
+__device__ inline float sqd(const P4& q, float x, float y, float z) {
+    float d0 = q.x - x, d1 = q.y - y, d2 = q.z - z;
+    float r = 0.0f;
+    r += d0 * d0;
+    r += d1 * d1;
+    r += d2 * d2;
+    return r;
+}
+
+__device__ inline int knn5(const float4* ent, const int32_t* off, const int32_t* cnt, int T, int s, size_t ent_stride,
+                           const P4& q, int* oi, float* od) {
+    const int cx = (int)floorf(q.x), cy = (int)floorf(q.y), cz = (int)floorf(q.z);
+    const int base = off[(size_t)s * T];
+    int n = 0;
+    for (int dz = -1; dz <= 1; ++dz)
+        for (int dy = -1; dy <= 1; ++dy)
+            for (int dx = -1; dx <= 1; ++dx) {
+                const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
+                const unsigned int b = grid_hash(tx, ty, tz, T);
+                const int st = off[(size_t)s * T + b] - base, m = cnt[(size_t)s * T + b];
+                const float4* e = ent + (size_t)s * ent_stride + st;
+                for (int k = 0; k < m; ++k) {
+                    float4 p = e[k];
+                    if ((int)floorf(p.x) != tx || (int)floorf(p.y) != ty || (int)floorf(p.z) != tz) continue;
+                    const float d = sqd(q, p.x, p.y, p.z);
+                    const int idx = __float_as_int(p.w);
+                    if (n == 5 && (d > od[4] || (d == od[4] && idx > oi[4]))) continue;
+                    int pos = n < 5 ? n : 4;
+                    while (pos > 0 && (od[pos - 1] > d || (od[pos - 1] == d && oi[pos - 1] > idx))) {
+                        od[pos] = od[pos - 1]; oi[pos] = oi[pos - 1]; --pos;
+                    }
+                    od[pos] = d; oi[pos] = idx;
+                    if (n < 5) ++n;
+                }
+            }
+    return n;
+}
+
+// ---------------------------------------------------------------- correspondences + partial normal equations
+__global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
+    const int s = blockIdx.y;
+    const StreamState& st = v.st[s];
+    double acc[28];
+    for (int k = 0; k < 28; ++k) acc[k] = 0;
+    const bool live = st.mo_ran && st.map_ok && !st.mo_converged;
+    if (live) {
+        const float* t = st.transformTobeMapped;
+        using slo_libm::sinf_;
+        using slo_libm::cosf_;
+        const float cRoll = cosf_(t[0]), sRoll = sinf_(t[0]), cPitch = cosf_(t[1]), sPitch = sinf_(t[1]);
+        const float cYaw = cosf_(t[2]), sYaw = sinf_(t[2]);
+        const float tX = t[3], tY = t[4], tZ = t[5];
+        const float srx = sRoll, crx = cRoll, sry = sPitch, cry = cPitch, srz = sYaw, crz = cYaw;
+        const int nc = st.n_corner_ds, nsq = st.n_surf_total_ds;
+        const float4* mc = v.map_c_ds + (size_t)s * v.cap_mc;
+        const float4* ms = v.map_s_ds + (size_t)s * v.cap_ms;
+        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nc + nsq; q += gridDim.x * blockDim.x) {
+            const bool corner = q < nc;
+            float4 po4 = corner ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
+            P4 po{po4.x, po4.y, po4.z, po4.w};
+            // pointAssociateToMap (MO:534-548)
+            float x1 = cYaw * po.x - sYaw * po.y, y1 = sYaw * po.x + cYaw * po.y, z1 = po.z;
+            float x2 = x1, y2 = cRoll * y1 - sRoll * z1, z2 = sRoll * y1 + cRoll * z1;
+            P4 sel{cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, po.w};
+            int ind[5]; float dis[5];
+            int n = corner ? knn5(v.gc_ent, v.gc_off, v.gc_cnt, v.Tc, s, v.cap_mc, sel, ind, dis)
+                           : knn5(v.gs_ent, v.gs_off, v.gs_cnt, v.Ts, s, v.cap_ms, sel, ind, dis);
+            if (n < 5 || !(dis[4] < 1.0)) continue;
+            float cfx, cfy, cfz, cfw;
+            bool ok = false;
+            if (corner) {
+                float cx = 0, cy = 0, cz = 0;
+                for (int j = 0; j < 5; j++) { float4 m = mc[ind[j]]; cx += m.x; cy += m.y; cz += m.z; }
+                cx /= 5; cy /= 5; cz /= 5;
+                float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+                for (int j = 0; j < 5; j++) {
+                    float4 m = mc[ind[j]];
+                    float ax = m.x - cx, ay = m.y - cy, az = m.z - cz;
+                    a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+                    a22 += ay * ay; a23 += ay * az;
+                    a33 += az * az;
+                }
+                a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+                float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33}, D1[3], V1[9];
+                slo_la::eigen_sym(A1, 3, D1, V1);
+                if (D1[0] > 3 * D1[1]) {
+                    float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+                    float x1 = (float)(cx + 0.1 * V1[0]), y1 = (float)(cy + 0.1 * V1[1]), z1 = (float)(cz + 0.1 * V1[2]);
+                    float x2 = (float)(cx - 0.1 * V1[0]), y2 = (float)(cy - 0.1 * V1[1]), z2 = (float)(cz - 0.1 * V1[2]);
+                    float m1 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
+                    float m2 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
+                    float m3 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
+                    float a012 = sqrtf(m1 * m1 + m2 * m2 + m3 * m3);
+                    float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+                    float la = ((y1 - y2) * m1 + (z1 - z2) * m2) / a012 / l12;
+                    float lb = -((x1 - x2) * m1 - (z1 - z2) * m3) / a012 / l12;
+                    float lc = -((x1 - x2) * m2 + (y1 - y2) * m3) / a012 / l12;
+                    float ld2 = a012 / l12;
+                    float sw = (float)(1 - 0.9 * fabsf(ld2));
+                    cfx = sw * la; cfy = sw * lb; cfz = sw * lc; cfw = sw * ld2;
+                    ok = sw > 0.1;
+                }
+            } else {
+                float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3];
+                for (int j = 0; j < 5; j++) { float4 m = ms[ind[j]]; A0[j * 3] = m.x; A0[j * 3 + 1] = m.y; A0[j * 3 + 2] = m.z; }
+                slo_la::solve_qr(A0, B0, 5, 3, X0);
+                float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+                float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+                pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+                bool planeValid = true;
+                for (int j = 0; j < 5; j++) {
+                    float4 m = ms[ind[j]];
+                    if (fabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) { planeValid = false; break; }
+                }
+                if (planeValid) {
+                    float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+                    float sw = (float)(1 - 0.9 * fabsf(pd2) / sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+                    cfx = sw * pa; cfy = sw * pb; cfz = sw * pc; cfw = sw * pd2;
+                    ok = sw > 0.1;
+                }
+            }
+            if (!ok) continue;
+            const P4& p = po;
+            float arx = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * cfx +
+                        (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * cfy +
+                        (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * cfz;
+            float ary = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * cfx +
+                        ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * cfz;
+            float arz = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * cfx +
+                        (crx * crz * p.x - crx * srz * p.y) * cfy +
+                        ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * cfz;
+            const double a[6] = {arx, ary, arz, cfx, cfy, cfz};
+            const double b = -cfw;
+            int k = 0;
+            for (int i = 0; i < 6; ++i)
+                for (int j = i; j < 6; ++j) acc[k++] += a[i] * a[j];
+            for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * b;
+            acc[27] += 1.0;
+        }
+    }
+    // block reduction (fixed order)
+    __shared__ double sh[4][28];
+    for (int o = 32; o > 0; o >>= 1)
+        for (int k = 0; k < 28; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < 28; ++k) sh[w][k] = acc[k];
+    __syncthreads();
+    if (threadIdx.x < 28) {
+        double r = sh[0][threadIdx.x];
+        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) r += sh[ww][threadIdx.x];
+        v.mo_part[((size_t)s * SLO_MO_BLOCKS + blockIdx.x) * 28 + threadIdx.x] = r;
+    }
+}
+
+// LMOptimization tail (MO:1445-1498) for one stream
+__global__ void k_mo_solve(DevView v, int iterCount) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    if (threadIdx.x != 0) return;
+    if (!(st.mo_ran && st.map_ok && !st.mo_converged)) return;
+    double acc[28];
+    for (int k = 0; k < 28; ++k) acc[k] = 0;
+    for (int b = 0; b < SLO_MO_BLOCKS; ++b)
+        for (int k = 0; k < 28; ++k) acc[k] += v.mo_part[((size_t)s * SLO_MO_BLOCKS + b) * 28 + k];
+    st.mo_iters = iterCount + 1;
+    const int nsel = (int)acc[27];
+    st.n_sel = nsel;
+    if (nsel < 50) return;  // LMOptimization returns false, loop continues
+    float AtA[36], AtB[6], X[6];
+    int k = 0;
+    for (int i = 0; i < 6; ++i)
+        for (int j = i; j < 6; ++j) { AtA[i * 6 + j] = (float)acc[k]; AtA[j * 6 + i] = (float)acc[k]; ++k; }
+    for (int i = 0; i < 6; ++i) AtB[i] = (float)acc[21 + i];
+    slo_la::solve_qr(AtA, AtB, 6, 6, X);
+    if (iterCount == 0) {
+        float E[6], V[36], V2[36], Vi[36];
+        slo_la::eigen_sym(AtA, 6, E, V);
+        for (int i = 0; i < 36; ++i) V2[i] = V[i];
+        st.isDegenerate_mo = 0;
+        for (int i = 5; i >= 0; i--) {
+            if (E[i] < 100.0f) {
+                for (int j = 0; j < 6; j++) V2[i * 6 + j] = 0;
+                st.isDegenerate_mo = 1;
+            } else break;
+        }
+        slo_la::inv(V, 6, Vi);
+        slo_la::mul(Vi, V2, 6, 6, 6, st.matP_mo);
+    }
+    if (st.isDegenerate_mo) {
+        float X2[6];
+        for (int i = 0; i < 6; ++i) X2[i] = X[i];
+        slo_la::mul(st.matP_mo, X2, 6, 6, 1, X);
+    }
+    for (int i = 0; i < 6; ++i) st.transformTobeMapped[i] += X[i];
+    double r0 = X[0] * 57.29578f, r1 = X[1] * 57.29578f, r2 = X[2] * 57.29578f;
+    double t0 = X[3] * 100, t1 = X[4] * 100, t2 = X[5] * 100;
+    float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
+    float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
+    if (deltaR < 0.05 && deltaT < 0.05) st.mo_converged = 1;
+}
+
+// ---------------------------------------------------------------- keyframe + Scan Context make
+__device__ inline unsigned int ford(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float unord(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// Eigen 3.3 SSE2 packet-order sum (Appendix A Q12d), stride in elements
+__device__ inline double eigen_sum(const double* x, int n, int stride) {
+    if (n < 2) return n ? x[0] : 0.0;
+    const int a2 = (n / 4) * 4, a1 = (n / 2) * 2;
+    double p0a = x[0], p0b = x[stride];
+    if (a1 > 2) {
+        double p1a = x[2 * stride], p1b = x[3 * stride];
+        for (int i = 4; i < a2; i += 4) {
+            p0a += x[i * stride]; p0b += x[(i + 1) * stride];
+            p1a += x[(i + 2) * stride]; p1b += x[(i + 3) * stride];
+        }
+        p0a += p1a; p0b += p1b;
+        if (a1 > a2) { p0a += x[a2 * stride]; p0b += x[(a2 + 1) * stride]; }
+    }
+    double r = p0a + p0b;
+    for (int i = a1; i < n; ++i) r += x[i * stride];
+    return r;
+}
+
+__device__ inline float sc_xy2theta(float x, float y, int atan_float) {
+    auto at = [&](float t) -> double { return atan_float ? (double)slo_libm::atanf_(t) : atan((double)t); };
+    if ((x >= 0) & (y >= 0)) return (float)((180 / M_PI) * at(y / x));
+    if ((x < 0) & (y >= 0)) return (float)(180 - ((180 / M_PI) * at(y / (-x))));
+    if ((x < 0) & (y < 0)) return (float)(180 + ((180 / M_PI) * at(y / x)));
+    if ((x >= 0) & (y < 0)) return (float)(360 - ((180 / M_PI) * at((-y) / x)));
+    return __builtin_nanf("");
+}
+
+__global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    __shared__ int save;
+    __shared__ float pose[6];
+    __shared__ int kfid;
+    if (threadIdx.x == 0) {
+        save = 0;
+        if (st.mo_ran) {
+            if (st.map_ok)  // scan2MapOptimization -> transformUpdate
+                for (int i = 0; i < 6; i++) { st.transformBefMapped[i] = st.mo_sum[i]; st.transformAftMapped[i] = st.transformTobeMapped[i]; }
+            // saveKeyFramesAndFactor
+            float cx = st.transformAftMapped[3], cy = st.transformAftMapped[4], cz = st.transformAftMapped[5];
+            float dx = st.prevPos[0] - cx, dy = st.prevPos[1] - cy, dz = st.prevPos[2] - cz;
+            bool saveThis = !(sqrtf(dx * dx + dy * dy + dz * dz) < 0.3);
+            if ((saveThis || st.n_keyframes == 0) && st.n_keyframes < v.KFMAX) {
+                st.prevPos[0] = cx; st.prevPos[1] = cy; st.prevPos[2] = cz;
+                float est[6];
+                if (st.n_keyframes == 0) {
+                    for (int i = 0; i < 6; ++i) { st.transformLast[i] = st.transformTobeMapped[i]; est[i] = st.transformTobeMapped[i]; }
+                } else {
+                    for (int i = 0; i < 6; ++i) est[i] = st.transformAftMapped[i];
+                }
+                pose[0] = est[3]; pose[1] = est[4]; pose[2] = est[5];
+                pose[3] = est[0]; pose[4] = est[1]; pose[5] = est[2];
+                kfid = st.n_keyframes;
+                float* kp = v.kf_pose + ((size_t)s * v.KFMAX + kfid) * 6;
+                for (int i = 0; i < 6; ++i) kp[i] = pose[i];
+                st.n_keyframes = kfid + 1;
+                if (st.n_keyframes > 1)
+                    for (int i = 0; i < 6; ++i) {
+                        st.transformAftMapped[i] = est[i]; st.transformLast[i] = est[i]; st.transformTobeMapped[i] = est[i];
+                    }
+                st.kf_saved = 1;
+                save = 1;
+            }
+        }
+    }
+    __syncthreads();
+    if (!save) return;
+    // keyframe clouds in the map frame (transformPointCloud, MO:566-596)
+    using slo_libm::sinf_;
+    using slo_libm::cosf_;
+    const float ctRoll = cosf_(pose[3]), stRoll = sinf_(pose[3]), ctPitch = cosf_(pose[4]), stPitch = sinf_(pose[4]);
+    const float ctYaw = cosf_(pose[5]), stYaw = sinf_(pose[5]);
+    const int slot = kfid % v.KFR;
+    const size_t ks = (size_t)s * v.KFR + slot;
+    const int n3[3] = {min(st.n_corner_ds, v.cap_kc), min(st.n_surf_ds, v.cap_ks), min(st.n_outl_ds, v.cap_ko)};
+    const float4* src[3] = {v.cur_c_ds + (size_t)s * v.cap_less_sharp, v.cur_s_ds + (size_t)s * v.H,
+                            v.cur_o_ds + (size_t)s * (v.H / 5)};
+    float4* dst[3] = {v.kf_corner + ks * v.cap_kc, v.kf_surf + ks * v.cap_ks, v.kf_outl + ks * v.cap_ko};
+    for (int c = 0; c < 3; ++c)
+        for (int i = threadIdx.x; i < n3[c]; i += blockDim.x) {
+            float4 p = src[c][i];
+            float x1 = ctYaw * p.x - stYaw * p.y, y1 = stYaw * p.x + ctYaw * p.y, z1 = p.z;
+            float x2 = x1, y2 = ctRoll * y1 - stRoll * z1, z2 = stRoll * y1 + ctRoll * z1;
+            dst[c][i] = make_float4(ctPitch * x2 + stPitch * z2 + pose[0], y2 + pose[1], -stPitch * x2 + ctPitch * z2 + pose[2], p.w);
+        }
+    if (threadIdx.x < 3) v.kf_n[ks * 3 + threadIdx.x] = n3[threadIdx.x];
+    // Scan Context make (Scancontext.cpp:151-244) on laserCloudRawDS
+    const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
+    __shared__ unsigned int cell[20 * 60];
+    __shared__ double desc[20 * 60];
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
+    __syncthreads();
+    const int nraw = st.n_raw_ds;
+    const float4* raw = v.cur_raw_ds + (size_t)s * v.P;
+    for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
+        float4 p0 = raw[i];
+        float px = p0.x, py = p0.y;
+        float pz = (float)(p0.z + v.cfg.sc_lidar_height);
+        float azim_range = sqrtf(px * px + py * py);
+        float azim_angle = sc_xy2theta(px, py, v.cfg.sc_atan_float);
+        if (azim_range > v.cfg.sc_max_radius) continue;
+        int ring_idx = max(min(NR, (int)ceil((azim_range / v.cfg.sc_max_radius) * NR)), 1);
+        double sc = ceil((azim_angle / 360.0) * NS);
+        int sraw = isnan(sc) ? INT_MIN : (int)sc;
+        int sctor_idx = max(min(NS, sraw), 1);
+        atomicMax(&cell[(ring_idx - 1) * NS + (sctor_idx - 1)], ford(pz));
+    }
+    __syncthreads();
+    double* hd = v.sc_desc + ((size_t)s * v.KFMAX + kfid) * NR * NS;
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) {
+        float f = unord(cell[i]);
+        double d = (f == -1000.0f) ? 0.0 : (double)f;
+        desc[i] = d;
+        hd[i] = d;
+    }
+    __syncthreads();
+    if (threadIdx.x < NR) {
+        double rk = eigen_sum(desc + threadIdx.x * NS, NS, 1) / (double)NS;
+        v.sc_ringd[((size_t)s * v.KFMAX + kfid) * NR + threadIdx.x] = rk;
+        v.sc_ring[((size_t)s * v.KFMAX + kfid) * NR + threadIdx.x] = (float)rk;
+    } else if (threadIdx.x >= 64 && threadIdx.x < 64 + NS) {
+        const int c = threadIdx.x - 64;
+        v.sc_sect[((size_t)s * v.KFMAX + kfid) * NS + c] = eigen_sum(desc + c, NR, NS) / (double)NR;
+    }
+    if (threadIdx.x == 0) st.sc_count = kfid + 1;
+}
+
+int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
+    DevView& v = ctx->v;
+    const int S = ctx->S;
+    const int SS = ST_STRIDE;
+    StreamState* st0 = v.st;
+    auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
+    SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.cfg.surrounding_keyframe_search_num, S), dim3(256), 0, v);
+    // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263)
+    int r;
+    if ((r = vg_run(ctx, "map_corner", v.map_c, v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner,
+                    v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc))) return r;
+    if ((r = vg_run(ctx, "map_surf", v.map_s, v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf,
+                    v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms))) return r;
+    if ((r = vg_run(ctx, "raw", d_points, v.P, d_counts, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
+                    fld(&StreamState::n_raw_ds), SS, v.P))) return r;
+    if ((r = vg_run(ctx, "corner", v.corner_last, v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS,
+                    v.cfg.leaf_corner, v.cur_c_ds, v.cap_less_sharp, fld(&StreamState::n_corner_ds), SS,
+                    v.cap_less_sharp))) return r;
+    if ((r = vg_run(ctx, "surf", v.surf_last, v.cap_less_flat, fld(&StreamState::surfLastNum), SS, v.cfg.leaf_surf,
+                    v.cur_s_ds, v.H, fld(&StreamState::n_surf_ds), SS, v.H))) return r;
+    if ((r = vg_run(ctx, "outlier", v.outl_cam, v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier,
+                    v.cur_o_ds, v.H / 5, fld(&StreamState::n_outl_ds), SS, v.H / 5))) return r;
+    SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
+    if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
+                    v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;
+    // hash grids over the DS maps
+    if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
+    if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
+    v.Tc = ctx->grid_c.T; v.gc_cnt = ctx->grid_c.cnt; v.gc_off = ctx->grid_c.off; v.gc_ent = ctx->grid_c.ent;
+    v.Ts = ctx->grid_s.T; v.gs_cnt = ctx->grid_s.cnt; v.gs_off = ctx->grid_s.off; v.gs_ent = ctx->grid_s.ent;
+    for (int it = 0; it < 10; ++it) {
+        SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(SLO_MO_BLOCKS, S), dim3(256), 0, v);
+        SLO_LAUNCH(ctx, "mo_solve", k_mo_solve, dim3(S), dim3(64), 0, v, it);
+    }
+    SLO_LAUNCH(ctx, "mo_finish", k_mo_finish, dim3(S), dim3(256), 0, v);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+}  // namespace slo

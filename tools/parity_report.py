@@ -1,6 +1,6 @@
 """Run synthetic streams through libslo (GPU) and the oracle (CPU) side by
 side and report per-stage parity.  Used by tests/test_gpu_parity.py and run
-directly on the GPU box:  python tools/parity_report.py --streams 2 --scans 6
+directly on the GPU box:  python tools/parity_report.py --streams 2 --scans 12
 """
 import argparse
 import json
@@ -20,44 +20,74 @@ from parity_util import mismatch, seg_class  # noqa: E402
 
 FRONT = ["range", "ground", "seg_pts", "seg_ground", "seg_col", "seg_range", "ring_start", "ring_end", "orient",
          "outlier", "fa_seg_pts", "sharp", "flat", "corner_last", "surf_last"]
+MAPPED = ["raw_ds", "corner_ds", "surf_total_ds"]
+SC = ["sc_desc", "ring_key", "sector_key"]
 
 
-def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True):
+def posediff(a, b):
+    return float(np.max(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)))) if len(a) else 0.0
+
+
+def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1):
     import torch
     cfg = slo_amd.preset(preset_id)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, n_streams)
     ors = [O.OracleStream(O.preset(preset_id), stable_voxel=True) for _ in range(n_streams)]
     report = []
-    max_pose = 0.0
+    worst = {"odom": 0.0, "map": 0.0, "keypose": 0.0}
+    counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0}
     for k in range(n_scans):
         scans = [O.gen_scan(preset_id, config_id, s, k) for s in range(n_streams)]
         pts = torch.from_numpy(np.stack(scans)).cuda()
         cnt = torch.full((n_streams,), P, dtype=torch.int32, device="cuda")
-        ctx.batch_image_projection(pts.data_ptr(), cnt.data_ptr())
-        ctx.batch_feature_association()
+        ctx.batch_process(pts.data_ptr(), cnt.data_ptr(), 0.1 * k)
         ctx.synchronize()
         for s in range(n_streams):
-            ors[s].step(scans[s], 0.1 * k)
-            row = {"scan": k, "stream": s}
-            for name in FRONT:
-                row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
-            lab_g, lab_o = ctx.get(s, "label"), ors[s].get("label")
-            row["label_class"] = int((seg_class(lab_g) != seg_class(lab_o)).sum())
-            S = len(ors[s].get("seg_pts"))
-            for name in ("curvature", "picked", "cloud_label", "smooth_ind"):
-                row[name] = mismatch(ctx.get(s, name)[:S], ors[s].get(name)[:S])
-            tg, to = ctx.get(s, "transform_sum"), ors[s].get("transform_sum")
-            d = float(np.max(np.abs(tg.astype(np.float64) - to.astype(np.float64))))
-            row["pose_maxdiff"] = d
-            row["fa_iters_gpu"] = ctx.get(s, "fa_iters").tolist()
-            row["fa_iters_cpu"] = ors[s].get("fa_iters").tolist()
-            max_pose = max(max_pose, d)
+            fl_o = ors[s].step(scans[s], 0.1 * k)
+            fl_g = int(ctx.get(s, "flags")[0])
+            row = {"scan": k, "stream": s, "flags_cpu": fl_o & 14, "flags_gpu": fl_g}
+            check_front = front and (k % every == 0)
+            if check_front:
+                for name in FRONT:
+                    row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
+                row["label_class"] = int((seg_class(ctx.get(s, "label")) != seg_class(ors[s].get("label"))).sum())
+                S = len(ors[s].get("seg_pts"))
+                for name in ("curvature", "picked", "cloud_label", "smooth_ind"):
+                    row[name] = mismatch(ctx.get(s, name)[:S], ors[s].get(name)[:S])
+            row["odom"] = posediff(ctx.get(s, "transform_sum"), ors[s].get("transform_sum"))
+            worst["odom"] = max(worst["odom"], row["odom"])
+            if fl_o & 2:
+                row["mapped"] = posediff(ctx.get(s, "mapped"), ors[s].get("mapped"))
+                worst["map"] = max(worst["map"], row["mapped"])
+                row["mo_iters"] = [int(ctx.get(s, "mo_iters")[0]), int(ors[s].get("mo_iters")[0])]
+                for name in MAPPED:
+                    row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
+                kg, ko = ctx.get(s, "keyposes"), ors[s].get("keyposes")
+                row["n_kf"] = [len(kg) // 6, len(ko) // 6]
+                if len(kg) == len(ko):
+                    worst["keypose"] = max(worst["keypose"], posediff(kg, ko))
+            if fl_o & 4:
+                for name in SC:
+                    row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
+            if fl_o & 8:
+                dg, do = ctx.get(s, "detect"), ors[s].get("detect")
+                row["detect_gpu"] = dg.tolist()
+                row["detect_cpu"] = do.tolist()
+                counts["detects"] += 1
+                if len(dg) == 0 or len(do) == 0 or dg[0] != do[0] or not np.array_equal(dg, do):
+                    counts["detect_mismatch"] += 1
+                if len(do) and do[0] >= 0:
+                    counts["loops"] += 1
+                fg, fo = ctx.get(s, "detect_f"), ors[s].get("detect_f")
+                row["sc_min_dist"] = [float(fg[1]) if len(fg) else None, float(fo[1]) if len(fo) else None]
+            counts["bit_mismatch"] += sum(v for kk, v in row.items() if isinstance(v, int) and v != 0 and kk not in
+                                          ("scan", "stream", "flags_cpu", "flags_gpu"))
             report.append(row)
             if verbose:
                 print(json.dumps(row), flush=True)
     ctx.close()
-    return report, max_pose
+    return report, worst, counts
 
 
 if __name__ == "__main__":
@@ -65,7 +95,8 @@ if __name__ == "__main__":
     ap.add_argument("--preset", type=int, default=5)
     ap.add_argument("--config", type=int, default=2)
     ap.add_argument("--streams", type=int, default=2)
-    ap.add_argument("--scans", type=int, default=6)
+    ap.add_argument("--scans", type=int, default=12)
+    ap.add_argument("--every", type=int, default=1, help="front-end bit checks every N scans")
     a = ap.parse_args()
-    rep, mp = run(a.preset, a.config, a.streams, a.scans)
-    print("max pose diff", mp)
+    rep, worst, counts = run(a.preset, a.config, a.streams, a.scans, every=a.every)
+    print("SUMMARY", json.dumps({"worst": worst, "counts": counts}))
