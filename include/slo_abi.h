@@ -106,6 +106,20 @@ int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out);
 int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t stride_bytes, size_t off_xyz,
                          size_t off_i, double t_scan, slo_map_view* out);
 int slo_sc_detect(slo_ctx* ctx, int32_t* loop_id, float* yaw_rad, double* min_dist);
+/* SCManager::makeAndSaveScancontextAndKeys (Scancontext.cpp:230) on stream 0:
+ * pts is the already downsampled cloud, as in the reference call (MO:1630) */
+int slo_sc_make_and_save(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                         size_t off_i);
+/* batched: VoxelGrid(0.5) + makeAndSaveScancontextAndKeys for every stream
+ * (used to seed the Scan Context history, e.g. from a previous session) */
+int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
+
+/* ---------------------------------------------------------------- multi-GPU records
+ * Pack one fixed-size record per stream (odometry pose, mapped pose,
+ * keyframe count, loop result, newest ring key) into device memory d_out
+ * [n_streams][slo_record_floats()] for the RCCL all-gather. */
+int slo_pack_records(slo_ctx* ctx, void* d_out);
+int slo_record_floats(void);
 
 /* ---------------------------------------------------------------- readback
  * Copy a named per-stream result to host memory (synchronises).  Returns the
@@ -127,6 +141,9 @@ int slo_timing_reset(slo_ctx* ctx);
 
 /* synthetic stream generator (sc-lego-loam_amd/csrc/slo_gen.h), host side */
 int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float* out_xyzi);
+/* n_streams x n_scans scans, layout [scan][stream][max_points][4], host threads */
+int slo_gen_batch(int preset, int config_id, int stream0, int n_streams, int scan0, int n_scans, float* out,
+                  int n_threads);
 
 #ifdef __cplusplus
 }

@@ -212,11 +212,12 @@ int oracle_gen_scan(int preset, int config_id, int stream_id, int k, float* out)
 // pre-generated scans (generation excluded from timing).  Returns wall
 // seconds of the processing; per-stage seconds summed over threads in stage_s[4]
 // (ip, fa, mo, sc).
-double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int warmup, double* stage_s) {
+double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int warmup, int history, double* stage_s) {
     slo_config cfg;
     if (slo_config_preset_impl(preset, &cfg)) return -1;
     const int P = cfg.n_scan * cfg.horizon_scan;
     std::vector<std::vector<float>> scans((size_t)n_threads * (n_scans + warmup));
+    std::vector<OracleStream*> streams(n_threads, nullptr);
     {
         std::vector<std::thread> g;
         for (int t = 0; t < n_threads; ++t)
@@ -226,6 +227,20 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
                     auto& v = scans[(size_t)t * (n_scans + warmup) + k];
                     v.resize((size_t)P * 4);
                     slo_gen::stream_scan(s, k, v.data());
+                }
+                // Scan Context history of `history` earlier scans (same as
+                // slo_batch_sc_make in bench.py): VoxelGrid(0.5) + make&save
+                streams[t] = new OracleStream(cfg);
+                std::vector<float> buf((size_t)P * 4);
+                for (int h = 0; h < history; ++h) {
+                    slo_gen::stream_scan(s, h - history, buf.data());
+                    Cloud c, ds;
+                    for (int i = 0; i < P; ++i) {
+                        const float* p = &buf[4 * (size_t)i];
+                        if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) c.push_back({p[0], p[1], p[2], p[3]});
+                    }
+                    voxel_grid(c, cfg.leaf_sc, ds, false);
+                    streams[t]->mo.sc.makeAndSaveScancontextAndKeys(ds);
                 }
             });
         for (auto& th : g) th.join();
@@ -237,7 +252,7 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
     std::vector<std::thread> th;
     for (int t = 0; t < n_threads; ++t)
         th.emplace_back([&, t]() {
-            OracleStream s(cfg);
+            OracleStream& s = *streams[t];
             for (int k = 0; k < warmup; ++k) s.step(scans[(size_t)t * (n_scans + warmup) + k].data(), P, 0.1 * k);
             ready++;
             while (!go.load()) std::this_thread::yield();
@@ -271,6 +286,7 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
     while (ready.load() < n_threads) std::this_thread::yield();
     go = true;
     for (auto& x : th) x.join();
+    for (auto* p : streams) delete p;
     double t0 = *std::min_element(tstart.begin(), tstart.end());
     double t1 = *std::max_element(tend.begin(), tend.end());
     if (stage_s)

@@ -5,6 +5,8 @@
 #include "slo_gen.h"
 #include <string.h>
 #include <algorithm>
+#include <atomic>
+#include <thread>
 
 using slo::DevView;
 using slo::StreamState;
@@ -187,10 +189,14 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     }
     memset(ctx->h_st, 0, sizeof(StreamState) * S);
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc) ||
-        slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms)) {
+        slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms) ||
+        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 13, v.cap_less_sharp) ||
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
+    v.Toc = ctx->grid_oc.T; v.goc_cnt = ctx->grid_oc.cnt; v.goc_off = ctx->grid_oc.off; v.goc_ent = ctx->grid_oc.ent;
+    v.Tos = ctx->grid_os.T; v.gos_cnt = ctx->grid_os.cnt; v.gos_off = ctx->grid_os.off; v.gos_ent = ctx->grid_os.ent;
     *out = ctx;
     return SLO_OK;
 }
@@ -203,6 +209,8 @@ void slo_destroy(slo_ctx* ctx) {
     slo::vg_free(ctx);
     slo::grid_free(ctx->grid_c);
     slo::grid_free(ctx->grid_s);
+    slo::grid_free(ctx->grid_oc);
+    slo::grid_free(ctx->grid_os);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->h_st) hipHostFree(ctx->h_st);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
@@ -480,9 +488,72 @@ int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t str
     return SLO_OK;
 }
 
+int slo_sc_make_and_save(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                         size_t off_i) {
+    if (!ctx || (!pts && n)) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = stage_points(ctx, pts, n, stride_bytes, off_xyz, off_i);
+    if (r) return r;
+    // one workgroup = stream 0
+    r = slo::sc_make_run(ctx, ctx->d_in, (size_t)ctx->cfg.max_points, ctx->d_cnt, 1, 1);
+    if (r) return r;
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
+}
+
 int slo_sc_detect(slo_ctx* ctx, int32_t* loop_id, float* yaw_rad, double* min_dist) {
     if (!ctx || !loop_id || !yaw_rad || !min_dist) return SLO_E_ARG;
-    *loop_id = -1; *yaw_rad = 0; *min_dist = 0;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = slo::sc_detect_run_one(ctx);
+    if (r) return r;
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    StreamState st;
+    SLO_CHECK(hipMemcpy(&st, ctx->v.st, sizeof(st), hipMemcpyDeviceToHost));
+    *loop_id = st.det_loop_id;
+    *yaw_rad = st.det_yaw;
+    *min_dist = st.det_min_dist;
+    return SLO_OK;
+}
+
+int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_counts) {
+    if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    DevView& v = ctx->v;
+    const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
+    int r = slo::vg_run(ctx, "raw", (const float4*)d_points, v.P, d_counts, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
+                        &v.st->n_raw_ds, SS, v.P);
+    if (r) return r;
+    return slo::sc_make_run(ctx, v.cur_raw_ds, v.P, &v.st->n_raw_ds, SS, ctx->S);
+}
+
+int slo_pack_records(slo_ctx* ctx, void* d_out) {
+    if (!ctx || !d_out) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::pack_records_run(ctx, (float*)d_out);
+}
+
+int slo_record_floats(void) { return SLO_RECORD_FLOATS; }
+
+int slo_gen_batch(int preset, int config_id, int stream0, int n_streams, int scan0, int n_scans, float* out,
+                  int n_threads) {
+    slo_config cfg;
+    if (slo_config_preset_impl(preset, &cfg) || !out || n_streams <= 0 || n_scans <= 0) return SLO_E_ARG;
+    const size_t P = (size_t)cfg.max_points;
+    std::vector<slo_gen::Stream> st;
+    for (int s = 0; s < n_streams; ++s) st.push_back(slo_gen::make_stream(cfg, config_id, stream0 + s));
+    std::atomic<int> next{0};
+    auto work = [&]() {
+        while (true) {
+            int j = next++;
+            if (j >= n_streams * n_scans) break;
+            int s = j / n_scans, k = j % n_scans;
+            // layout [scan][stream][P][4]
+            slo_gen::stream_scan(st[s], scan0 + k, out + ((size_t)k * n_streams + s) * P * 4);
+        }
+    };
+    std::vector<std::thread> th;
+    for (int t = 0; t < std::max(1, n_threads); ++t) th.emplace_back(work);
+    for (auto& t : th) t.join();
     return SLO_OK;
 }
 

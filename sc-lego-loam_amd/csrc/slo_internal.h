@@ -141,6 +141,10 @@ struct DevView {
     float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
     float4* cur_st_ds;   // [S][cap_st]
     double* mo_part;     // [S][MO_BLOCKS][28] partial A^T A / A^T b / count
+    // hash grids over the odometry "kd-tree" clouds (1 m cells)
+    int Toc, Tos;
+    const int32_t *goc_cnt, *goc_off, *gos_cnt, *gos_off;
+    const float4 *goc_ent, *gos_ent;
     // hash grids over the DS maps (1 m cells)
     int Tc, Ts;
     const int32_t *gc_cnt, *gc_off, *gs_cnt, *gs_off;
@@ -153,6 +157,7 @@ struct DevView {
 };
 
 #define SLO_MO_BLOCKS 64
+#define SLO_RECORD_FLOATS 40
 
 __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
     return (((unsigned int)x * 73856093u) ^ ((unsigned int)y * 19349663u) ^ ((unsigned int)z * 83492791u)) &
@@ -211,7 +216,7 @@ struct slo_ctx {
     int32_t* d_cnt = nullptr;
     // mapping workspaces
     slo::MapWs mws;
-    slo::HashGrid grid_c, grid_s;
+    slo::HashGrid grid_c, grid_s, grid_oc, grid_os;
     bool map_ready = false;
 };
 
@@ -230,7 +235,10 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts);
+int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams);
 int sc_detect_run(slo_ctx* ctx);
+int sc_detect_run_one(slo_ctx* ctx);
+int pack_records_run(slo_ctx* ctx, float* d_out);
 }  // namespace slo
 
 #define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \

@@ -318,6 +318,8 @@ __global__ void k_mo_solve(DevView v, int iterCount) {
 }
 
 // ---------------------------------------------------------------- keyframe + Scan Context make
+__device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
+
 __device__ inline unsigned int ford(float f) {
     unsigned int u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -413,14 +415,36 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
             dst[c][i] = make_float4(ctPitch * x2 + stPitch * z2 + pose[0], y2 + pose[1], -stPitch * x2 + ctPitch * z2 + pose[2], p.w);
         }
     if (threadIdx.x < 3) v.kf_n[ks * 3 + threadIdx.x] = n3[threadIdx.x];
-    // Scan Context make (Scancontext.cpp:151-244) on laserCloudRawDS
+    // Scan Context make on laserCloudRawDS (MO:1626-1631)
+    sc_make_block(v, s, v.cur_raw_ds + (size_t)s * v.P, st.n_raw_ds);
+}
+
+// makeAndSaveScancontextAndKeys on an already downsampled cloud (public SC API)
+__global__ void __launch_bounds__(256) k_sc_make(DevView v, const float4* pts, size_t stride, const int32_t* n,
+                                                 int n_stride) {
+    const int s = blockIdx.x;
+    sc_make_block(v, s, pts + (size_t)s * stride, n[(size_t)s * n_stride]);
+}
+
+int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams) {
+    SLO_LAUNCH(ctx, "sc_make", k_sc_make, dim3(n_streams), dim3(256), 0, ctx->v, pts, stride, n, n_stride);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+// SCManager::makeScancontext + makeRingkey/SectorkeyFromScancontext +
+// history append (Scancontext.cpp:151-244), one workgroup
+__device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw) {
+    StreamState& st = v.st[s];
     const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
     __shared__ unsigned int cell[20 * 60];
     __shared__ double desc[20 * 60];
+    __shared__ int hid;
+    if (threadIdx.x == 0) hid = st.sc_count;
     for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
     __syncthreads();
-    const int nraw = st.n_raw_ds;
-    const float4* raw = v.cur_raw_ds + (size_t)s * v.P;
+    const int kfid = hid;
+    if (kfid >= v.KFMAX) return;
     for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
         float4 p0 = raw[i];
         float px = p0.x, py = p0.y;

@@ -39,12 +39,39 @@ __device__ inline float sqdist_flann(const P4& q, const float4& p) {  // ((0+d0^
     return r;
 }
 
-// exact 1-NN over kd[0..n): (distance, index) lexicographic minimum
-__device__ inline void nn1(const float4* kd, int n, const P4& q, int& bi, float& bd) {
+// exact 1-NN in the 1 m hash grid of the "tree" cloud: shells of cells at
+// Chebyshev distance r = 0,1,..; every point outside shells <= r is more than
+// r metres away, so once the best float distance is < r^2 nothing unseen can
+// beat or tie it (fl(d) is monotone in the exact distance).  r stops at
+// rmax = ceil(sqrt(nearestFeatureSearchSqDist)): anything further fails the
+// gate anyway, as it would after the reference's exact FLANN search.
+// Ties -> lowest index.
+__device__ inline void nn1_grid(const float4* ent, const int32_t* off, const int32_t* cnt, int T, int s,
+                                size_t es, int rmax, const P4& q, int& bi, float& bd) {
     bi = -1; bd = FLT_MAX;
-    for (int j = 0; j < n; ++j) {
-        float d = sqdist_flann(q, kd[j]);
-        if (d < bd) { bd = d; bi = j; }
+    if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return;
+    const int cx = (int)floorf(q.x), cy = (int)floorf(q.y), cz = (int)floorf(q.z);
+    const int base = off[(size_t)s * T];
+    const float4* E = ent + (size_t)s * es;
+    for (int r = 0; r <= rmax; ++r) {
+        for (int dz = -r; dz <= r; ++dz)
+            for (int dy = -r; dy <= r; ++dy) {
+                const bool edge = (dz == -r || dz == r || dy == -r || dy == r);
+                for (int dx = -r; dx <= r; dx += (edge ? 1 : 2 * r > 0 ? 2 * r : 1)) {
+                    const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
+                    const unsigned int b = grid_hash(tx, ty, tz, T);
+                    const int st = off[(size_t)s * T + b] - base, m = cnt[(size_t)s * T + b];
+                    for (int k = 0; k < m; ++k) {
+                        const float4 p = E[st + k];
+                        if ((int)floorf(p.x) != tx || (int)floorf(p.y) != ty || (int)floorf(p.z) != tz) continue;
+                        const float d = sqdist_flann(q, p);
+                        const int idx = __float_as_int(p.w);
+                        if (d < bd || (d == bd && idx < bi)) { bd = d; bi = idx; }
+                    }
+                    if (r == 0) break;
+                }
+            }
+        if (r >= 1 && bd < (float)(r * r)) break;
     }
 }
 
@@ -133,8 +160,8 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
     const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
     const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
     const int cornerLastNum = st.cornerLastNum, surfLastNum = st.surfLastNum;
-    const int kdCN = st.kdCornerNum, kdSN = st.kdSurfNum;
     const float gate = v.cfg.nearest_feature_search_sq_dist;
+    const int rmax = (int)ceilf(sqrtf(gate));
     int iters_surf = 0, iters_corner = 0;
 
     if (!(cornerLastNum < 10 || surfLastNum < 100)) {
@@ -163,8 +190,7 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
                 P4 sel = slo_pose::transform_to_start(po, tc);
                 if (iterCount % 5 == 0) {
                     int ci; float cd;
-                    // every lane of the wave sweeps the same targets (broadcast loads)
-                    nn1(kds, kdSN, sel, ci, cd);
+                    nn1_grid(v.gos_ent, v.gos_off, v.gos_cnt, v.Tos, s, v.cap_less_flat, rmax, sel, ci, cd);
                     int closest = -1, i2 = -1, i3 = -1;
                     if (active && cd < gate && ci >= 0 && ci < surfLastNum) {
                         closest = ci;
@@ -256,7 +282,7 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
                 P4 sel = slo_pose::transform_to_start(po, tc);
                 if (iterCount % 5 == 0) {
                     int ci; float cd;
-                    nn1(kdc, kdCN, sel, ci, cd);
+                    nn1_grid(v.goc_ent, v.goc_off, v.goc_cnt, v.Toc, s, v.cap_less_sharp, rmax, sel, ci, cd);
                     int closest = -1, i2 = -1;
                     if (active && cd < gate && ci >= 0 && ci < cornerLastNum) {
                         closest = ci;
@@ -364,7 +390,11 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);
     std::swap(ctx->v.surf_last, ctx->v.surf_next);
-    return 0;
+    // setInputCloud: hash grids over the (possibly unchanged) tree clouds
+    const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
+    int r = grid_build(ctx, ctx->grid_oc, v.kd_corner, v.cap_less_sharp, &v.st->kdCornerNum, SS);
+    if (r) return r;
+    return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
 }
 
 }  // namespace slo

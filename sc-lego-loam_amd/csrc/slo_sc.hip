@@ -201,4 +201,39 @@ int sc_detect_run(slo_ctx* ctx) {
     return 0;
 }
 
+__global__ void k_sc_force(DevView v) { v.st[0].kf_saved = 1; }
+
+// detectLoopClosureID on stream 0 only (single-scan API)
+int sc_detect_run_one(slo_ctx* ctx) {
+    SLO_LAUNCH(ctx, "sc_force", k_sc_force, dim3(1), dim3(1), 0, ctx->v);
+    SLO_LAUNCH(ctx, "sc_detect", k_sc_detect, dim3(1), dim3(256), 0, ctx->v);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+// Per-stream record shared across ranks by the RCCL all-gather (SURVEY §8(e)
+// mode M): odometry pose, mapped pose, keyframe count, loop result and the
+// newest ring key.  40 floats = 160 B per stream.
+__global__ void k_pack_records(DevView v, float* out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    const StreamState& st = v.st[s];
+    float* o = out + (size_t)s * SLO_RECORD_FLOATS;
+    for (int k = 0; k < 6; ++k) { o[k] = st.transformSum[k]; o[6 + k] = st.transformAftMapped[k]; }
+    o[12] = (float)st.n_keyframes;
+    o[13] = (float)st.kf_saved;
+    o[14] = st.det_valid ? (float)st.det_loop_id : -2.0f;
+    o[15] = st.det_valid ? (float)st.det_min_dist : 0.0f;
+    const int NR = v.cfg.sc_num_ring;
+    const float* rk = st.sc_count > 0 ? v.sc_ring + ((size_t)s * v.KFMAX + st.sc_count - 1) * NR : nullptr;
+    for (int k = 0; k < 20; ++k) o[16 + k] = (rk && k < NR) ? rk[k] : 0.0f;
+    o[36] = (float)st.sc_count; o[37] = (float)st.err; o[38] = 0; o[39] = 0;
+}
+
+int pack_records_run(slo_ctx* ctx, float* d_out) {
+    SLO_LAUNCH(ctx, "pack_records", k_pack_records, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v, d_out);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
 }  // namespace slo

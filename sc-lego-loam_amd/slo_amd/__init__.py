@@ -48,6 +48,17 @@ def preset(name_or_id):
     return c
 
 
+def gen_batch(preset_id, config_id, stream0, n_streams, scan0, n_scans, n_points, n_threads=8, out=None):
+    """[n_scans][n_streams][n_points][4] float32 synthetic scans (host threads)."""
+    if out is None:
+        out = np.empty((n_scans, n_streams, n_points, 4), np.float32)
+    rc = _abi.lib().slo_gen_batch(int(preset_id), int(config_id), int(stream0), int(n_streams), int(scan0),
+                                  int(n_scans), out.ctypes.data, int(n_threads))
+    if rc != 0:
+        raise SloError("slo_gen_batch failed")
+    return out
+
+
 def gen_scan(preset_id, config_id, stream_id, k, n_points):
     out = np.empty((n_points, 4), np.float32)
     n = _abi.lib().slo_gen_scan(int(preset_id), int(config_id), int(stream_id), int(k), out.ctypes.data)
@@ -96,6 +107,21 @@ class Context:
 
     def batch_process(self, d_pts, d_cnt, t_scan):
         self._ok(self.L.slo_batch_process(self.h, d_pts, d_cnt, float(t_scan)), "slo_batch_process")
+
+    def batch_sc_make(self, d_pts, d_cnt):
+        self._ok(self.L.slo_batch_sc_make(self.h, d_pts, d_cnt), "slo_batch_sc_make")
+
+    def pack_records(self, d_out):
+        self._ok(self.L.slo_pack_records(self.h, d_out), "slo_pack_records")
+
+    def sc_make_and_save(self, pts_xyzi):
+        pts = np.ascontiguousarray(pts_xyzi, np.float32)
+        self._ok(self.L.slo_sc_make_and_save(self.h, pts.ctypes.data, len(pts), 16, 0, 12), "slo_sc_make_and_save")
+
+    def sc_detect(self):
+        lid, yaw, md = ctypes.c_int32(), ctypes.c_float(), ctypes.c_double()
+        self._ok(self.L.slo_sc_detect(self.h, ctypes.byref(lid), ctypes.byref(yaw), ctypes.byref(md)), "slo_sc_detect")
+        return int(lid.value), float(yaw.value), float(md.value)
 
     def get(self, stream, name):
         n = self.L.slo_get(self.h, int(stream), name.encode(), None, 0)

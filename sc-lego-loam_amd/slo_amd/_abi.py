@@ -66,8 +66,9 @@ EXPORTS = [
     "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
     "slo_batch_sc_detect", "slo_batch_process", "slo_image_projection", "slo_feature_association",
-    "slo_map_optimization", "slo_sc_detect", "slo_get", "slo_timing_enable", "slo_timing_read",
-    "slo_timing_reset", "slo_gen_scan",
+    "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
+    "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
+    "slo_gen_batch",
 ]
 
 
@@ -109,5 +110,10 @@ def lib():
     L.slo_timing_reset.argtypes = [P]
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
+    L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
+    L.slo_sc_make_and_save.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
+    L.slo_batch_sc_make.argtypes = [P, P, P]
+    L.slo_pack_records.argtypes = [P, P]
+    L.slo_record_floats.argtypes = []
     _LIB = L
     return L
