@@ -71,9 +71,8 @@ def main():
     import torch.distributed as dist
     import slo_amd
 
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from slo_amd import dist as sdist
+    rank, world, local = sdist.env_rank()
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -90,7 +89,8 @@ def main():
 
     # ---- inputs (host generation, then resident in HBM)
     t_gen = time.time()
-    host = slo_amd.gen_batch(pid, a.config_id, rank * S, S, 0, ntot, P, gthreads)
+    stream0, _ = sdist.stream_shard(rank, world, S)
+    host = slo_amd.gen_batch(pid, a.config_id, stream0, S, 0, ntot, P, gthreads)
     dev = torch.from_numpy(host).to(f"cuda:{local}")
     del host
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
@@ -105,7 +105,7 @@ def main():
     chunk = 8
     for h0 in range(-a.history, 0, chunk):
         nh = min(chunk, -h0)
-        hist = slo_amd.gen_batch(pid, a.config_id, rank * S, S, h0, nh, P, gthreads)
+        hist = slo_amd.gen_batch(pid, a.config_id, stream0, S, h0, nh, P, gthreads)
         for h in range(nh):
             d = torch.from_numpy(hist[h]).to(f"cuda:{local}")
             ctx.batch_sc_make(d.data_ptr(), cnt.data_ptr())
@@ -118,7 +118,7 @@ def main():
         if world > 1:
             ctx.pack_records(rec.data_ptr())
             with torch.cuda.stream(ext):
-                dist.all_gather_into_tensor(gathered, rec)
+                sdist.gather_records(rec, gathered)
 
     for k in range(a.warmup):
         step(k)
@@ -134,10 +134,7 @@ def main():
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = sdist.max_over_ranks(el, f"cuda:{local}")
     scans = S * a.steps * world
     value = scans / el
 

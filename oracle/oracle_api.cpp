@@ -180,6 +180,42 @@ int oracle_voxel_grid(const float* pts, int n, float leaf, int stable, float* ou
     return copy_cloud(o, out, cap);
 }
 
+// ---- Scan Context session (SCManager alone): add = VoxelGrid(leaf_sc) of the
+// finite points + makeAndSaveScancontextAndKeys; detect = detectLoopClosureID.
+void* oracle_sc_session_create(const slo_config* cfg) { return new SCManager(*cfg); }
+void oracle_sc_session_destroy(void* h) { delete (SCManager*)h; }
+// returns the DS size; ring_key_f (NR floats) = the tree row just appended
+int oracle_sc_session_add(void* h, const float* pts, int n, int stable, float* ring_key_f) {
+    SCManager* m = (SCManager*)h;
+    Cloud c, ds;
+    for (int i = 0; i < n; ++i) {
+        const float* p = pts + 4 * (size_t)i;
+        if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) c.push_back({p[0], p[1], p[2], p[3]});
+    }
+    voxel_grid(c, m->cfg.leaf_sc, ds, stable != 0);
+    m->makeAndSaveScancontextAndKeys(ds);
+    if (ring_key_f) memcpy(ring_key_f, m->invkeys_mat_.back().data(), sizeof(float) * m->NR);
+    return (int)ds.size();
+}
+// out_i: loop_id, nn_idx, n_cand, cand[K]; out_f: yaw, min_dist
+void oracle_sc_session_detect(void* h, int* out_i, double* out_f) {
+    auto r = ((SCManager*)h)->detectLoopClosureID();
+    out_i[0] = r.loop_id; out_i[1] = r.nn_idx; out_i[2] = r.n_cand;
+    for (int c = 0; c < r.n_cand; ++c) out_i[3 + c] = r.cand[c];
+    out_f[0] = r.yaw; out_f[1] = r.min_dist;
+}
+// exact K-NN of the restatement over `n` rows of `data` (the ring-key tree
+// snapshot) in nanoflann's float L2 order; unfilled slots stay 0 / FLT_MAX
+void oracle_sc_knn(const slo_config* cfg, const float* data, int n, const float* q, int K, int* idx, float* dist) {
+    SCManager m(*cfg);
+    for (int t = 0; t < n; ++t)
+        m.invkeys_to_search_.emplace_back(data + (size_t)t * m.NR, data + (size_t)(t + 1) * m.NR);
+    std::vector<int> ci;
+    std::vector<float> cd;
+    m.knn_search(q, K, ci, cd);
+    for (int c = 0; c < K; ++c) { idx[c] = ci[c]; dist[c] = cd[c]; }
+}
+
 // ---- libm self-test against the host glibc (tests/test_libm.py)
 long oracle_libm_selftest(long n, unsigned long seed) {
     uint64_t st = seed * 0x9E3779B97F4A7C15ULL + 1;

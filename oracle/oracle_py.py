@@ -73,6 +73,14 @@ def lib():
                                      ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_voxel_grid.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_int]
+        L.oracle_sc_session_create.restype = ctypes.c_void_p
+        L.oracle_sc_session_create.argtypes = [ctypes.POINTER(SloConfig)]
+        L.oracle_sc_session_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_sc_session_add.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_void_p]
+        L.oracle_sc_session_detect.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_sc_knn.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                    ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _LIB = L
     return _LIB
 
@@ -102,6 +110,45 @@ _DTYPES = {
 }
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
            "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds"}
+
+
+class SCSession:
+    """SCManager alone: add() = VoxelGrid(leaf_sc) + makeAndSaveScancontextAndKeys,
+    detect() = detectLoopClosureID (Scancontext.cpp:230-338)."""
+
+    def __init__(self, cfg, stable_voxel=False):
+        self.cfg = cfg
+        self.stable = int(stable_voxel)
+        self.h = lib().oracle_sc_session_create(ctypes.byref(cfg))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().oracle_sc_session_destroy(self.h)
+            self.h = None
+
+    def add(self, pts):
+        pts = np.ascontiguousarray(pts, np.float32)
+        key = np.empty(self.cfg.sc_num_ring, np.float32)
+        n = lib().oracle_sc_session_add(self.h, pts.ctypes.data, len(pts), self.stable, key.ctypes.data)
+        return n, key
+
+    def detect(self):
+        oi = np.zeros(3 + 64, np.int32)
+        of = np.zeros(2, np.float64)
+        lib().oracle_sc_session_detect(self.h, oi.ctypes.data, of.ctypes.data)
+        return {"loop_id": int(oi[0]), "nn_idx": int(oi[1]), "cand": oi[3:3 + oi[2]].copy(),
+                "yaw": float(of[0]), "min_dist": float(of[1])}
+
+
+def sc_knn(cfg, data, q, K):
+    """Exact K-NN of the restatement over ring-key rows `data` (n x NR float32)."""
+    data = np.ascontiguousarray(data, np.float32)
+    q = np.ascontiguousarray(q, np.float32)
+    idx = np.zeros(K, np.int32)
+    dist = np.zeros(K, np.float32)
+    lib().oracle_sc_knn(ctypes.byref(cfg), data.ctypes.data, len(data), q.ctypes.data, K, idx.ctypes.data,
+                        dist.ctypes.data)
+    return idx, dist
 
 
 class OracleStream:

@@ -178,6 +178,23 @@ struct SCManager {
         return result;
     }
 
+    // exact K-NN over the tree snapshot (SCc:286-289); distance-sorted, ties
+    // by index; unfilled slots stay index 0, as with the reference's
+    // zero-initialised candidate_indexes (SCc:282)
+    void knn_search(const float* q, int K, std::vector<int>& ci, std::vector<float>& cd) const {
+        ci.assign(K, 0);
+        cd.assign(K, FLT_MAX);
+        int cnt = 0;
+        for (int t = 0; t < (int)invkeys_to_search_.size(); ++t) {
+            float d = l2_nf(q, invkeys_to_search_[t].data(), NR);
+            if (cnt == K && !(d < cd[K - 1])) continue;
+            int pos = cnt < K ? cnt : K - 1;
+            while (pos > 0 && cd[pos - 1] > d) { cd[pos] = cd[pos - 1]; ci[pos] = ci[pos - 1]; --pos; }
+            cd[pos] = d; ci[pos] = t;
+            if (cnt < K) ++cnt;
+        }
+    }
+
     struct DetectResult { int loop_id; float yaw; double min_dist; int nn_idx; int n_cand; int cand[64]; };
 
     DetectResult detectLoopClosureID() {
@@ -191,19 +208,9 @@ struct SCManager {
         }
         tree_making_period_conter = tree_making_period_conter + 1;
         const int K = cfg.sc_num_candidates;
-        // exact K-NN (unfilled slots stay index 0, as with the reference's
-        // zero-initialised candidate_indexes)
-        std::vector<int> ci(K, 0);
-        std::vector<float> cd(K, FLT_MAX);
-        int cnt = 0;
-        for (int t = 0; t < (int)invkeys_to_search_.size(); ++t) {
-            float d = l2_nf(curr_key.data(), invkeys_to_search_[t].data(), NR);
-            if (cnt == K && !(d < cd[K - 1])) continue;
-            int pos = cnt < K ? cnt : K - 1;
-            while (pos > 0 && cd[pos - 1] > d) { cd[pos] = cd[pos - 1]; ci[pos] = ci[pos - 1]; --pos; }
-            cd[pos] = d; ci[pos] = t;
-            if (cnt < K) ++cnt;
-        }
+        std::vector<int> ci;
+        std::vector<float> cd;
+        knn_search(curr_key.data(), K, ci, cd);
         double min_dist = 10000000;
         int nn_align = 0, nn_idx = 0;
         res.n_cand = K;

@@ -74,7 +74,11 @@ void* slo_stream(slo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** out) {
     if (!cfg || !out || n_streams <= 0 || cfg->n_scan <= 0 || cfg->n_scan > 128 || cfg->horizon_scan <= 0 ||
-        cfg->horizon_scan > 4096 || cfg->max_points <= 0)
+        cfg->horizon_scan > 4096 || cfg->max_points <= 0 || cfg->sc_num_candidates < 1 ||
+        cfg->sc_num_candidates > SLO_SC_MAX_K || cfg->sc_num_ring < 1 || cfg->sc_num_ring > 64 ||
+        cfg->sc_num_sector < 1 || cfg->sc_num_sector > SLO_SC_MAX_SECTOR ||
+        cfg->sc_num_ring * cfg->sc_num_sector > SLO_SC_MAX_CELLS || cfg->surrounding_keyframe_search_num < 1 ||
+        cfg->surrounding_keyframe_search_num + 2 > 64 || cfg->sc_tree_making_period < 1)
         return SLO_E_ARG;
     slo_ctx* ctx = new slo_ctx();
     ctx->cfg = *cfg;
@@ -142,7 +146,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.st, S);
     // ---- mapping + Scan Context history
     v.KFR = 64;
-    v.KFMAX = 4096;
+    v.KFMAX = SLO_KFMAX;
     v.cap_kc = v.cap_less_sharp;
     v.cap_ks = (int)(H / 3);
     v.cap_ko = (int)(H / 5);
@@ -449,11 +453,33 @@ static int stage_points(slo_ctx* ctx, const void* pts, size_t n, size_t stride, 
     return SLO_OK;
 }
 
+// copy `bytes` of device memory into view slot `slot`; returns the host pointer
+static const void* view_copy(slo_ctx* ctx, int slot, const void* dsrc, size_t bytes, int* rc) {
+    auto& b = ctx->h_view[slot];
+    b.resize(std::max<size_t>(bytes, 16));
+    if (bytes) {
+        hipError_t e = hipMemcpy(b.data(), dsrc, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) { ctx->err = hipGetErrorString(e); *rc = SLO_E_HIP; }
+    }
+    return b.data();
+}
+
+// The three node-level entry points drive a one-stream context exactly like
+// the reference callbacks; a batched context must use slo_batch_*.
+static int single_stream(slo_ctx* ctx) {
+    if (ctx->S != 1) { ctx->err = "single-scan entry points need a context with n_streams == 1"; return SLO_E_STATE; }
+    return SLO_OK;
+}
+
+// ImageProjection::cloudHandler (IP:181-196): copyPointCloud .. cloudSegmentation;
+// *out mirrors /segmented_cloud, /segmented_cloud_info and /outlier_cloud.
 int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz, size_t off_i,
                          slo_seg_view* out) {
-    if (!ctx || !pts || !out || ctx->S < 1) return SLO_E_ARG;
+    if (!ctx || (!pts && n) || !out) return SLO_E_ARG;
+    int r = single_stream(ctx);
+    if (r) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
-    int r = stage_points(ctx, pts, n, stride_bytes, off_xyz, off_i);
+    r = stage_points(ctx, pts, n, stride_bytes, off_xyz, off_i);
     if (r) return r;
     ctx->v.pts = ctx->d_in;
     ctx->v.npts = ctx->d_cnt;
@@ -461,30 +487,76 @@ int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
     if (r) return r;
     memset(out, 0, sizeof(*out));
     SLO_CHECK(hipStreamSynchronize(ctx->stream));
-    return SLO_OK;
+    const DevView& v = ctx->v;
+    StreamState st;
+    SLO_CHECK(hipMemcpy(&st, v.st, sizeof(st), hipMemcpyDeviceToHost));
+    const int R = v.cfg.n_scan;
+    int rc = SLO_OK;
+    out->n_segmented = st.seg_count;
+    out->segmented = (const float*)view_copy(ctx, 0, v.seg, 16 * (size_t)st.seg_count, &rc);
+    out->ground_flag = (const uint8_t*)view_copy(ctx, 1, v.seg_ground, (size_t)st.seg_count, &rc);
+    out->col_ind = (const uint32_t*)view_copy(ctx, 2, v.seg_col, 4 * (size_t)st.seg_count, &rc);
+    out->range = (const float*)view_copy(ctx, 3, v.seg_range, 4 * (size_t)st.seg_count, &rc);
+    const int32_t* se = (const int32_t*)view_copy(ctx, 4, v.ring_se, 8 * (size_t)R, &rc);
+    for (int i = 0; i < R; ++i) { ctx->h_ring[0][i] = se[2 * i]; ctx->h_ring[1][i] = se[2 * i + 1]; }
+    out->start_ring_index = ctx->h_ring[0];
+    out->end_ring_index = ctx->h_ring[1];
+    const float* o = (const float*)view_copy(ctx, 5, v.orient, 12, &rc);
+    out->start_orientation = o[0]; out->end_orientation = o[1]; out->orientation_diff = o[2];
+    out->n_outlier = st.outlier_count;
+    out->outlier = (const float*)view_copy(ctx, 6, v.outlier, 16 * (size_t)st.outlier_count, &rc);
+    return rc;
 }
 
+// FeatureAssociation::runFeatureAssociation (FA:1817-1859) on the result of
+// the previous slo_image_projection.  sharp/flat are this scan's features
+// (start of sweep); less_sharp/less_flat are laserCloudCornerLast /
+// laserCloudSurfLast after TransformToEnd (what FA publishes, FA:1790-1814).
 int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out) {
-    (void)t_scan;
+    (void)t_scan;  // the non-IMU path never reads the stamp (Q13)
     if (!ctx || !out) return SLO_E_ARG;
-    int r = slo_batch_feature_association(ctx);
+    int r = single_stream(ctx);
+    if (r) return r;
+    r = slo_batch_feature_association(ctx);
     if (r) return r;
     memset(out, 0, sizeof(*out));
     SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    const DevView& v = ctx->v;
     StreamState st;
-    SLO_CHECK(hipMemcpy(&st, ctx->v.st, sizeof(st), hipMemcpyDeviceToHost));
+    SLO_CHECK(hipMemcpy(&st, v.st, sizeof(st), hipMemcpyDeviceToHost));
+    int rc = SLO_OK;
     memcpy(out->transform_sum, st.transformSum, 24);
-    out->n_sharp = st.n_sharp; out->n_less_sharp = st.n_less_sharp;
-    out->n_flat = st.n_flat; out->n_less_flat = st.n_less_flat;
+    out->n_sharp = st.n_sharp; out->n_flat = st.n_flat;
+    out->n_less_sharp = st.cornerLastNum; out->n_less_flat = st.surfLastNum;
+    out->sharp = (const float*)view_copy(ctx, 7, v.sharp, 16 * (size_t)st.n_sharp, &rc);
+    out->flat = (const float*)view_copy(ctx, 8, v.flat, 16 * (size_t)st.n_flat, &rc);
+    out->less_sharp = (const float*)view_copy(ctx, 9, v.corner_last, 16 * (size_t)st.cornerLastNum, &rc);
+    out->less_flat = (const float*)view_copy(ctx, 10, v.surf_last, 16 * (size_t)st.surfLastNum, &rc);
     out->published = ctx->fa_published;
-    return SLO_OK;
+    return rc;
 }
 
+// mapOptimization::run (MO:1673-1706) minus GTSAM / publishing: gating on the
+// FA publish and mappingProcessInterval, then transformAssociateToMap ..
+// saveKeyFramesAndFactor incl. makeAndSaveScancontextAndKeys on the raw scan.
 int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t stride_bytes, size_t off_xyz,
                          size_t off_i, double t_scan, slo_map_view* out) {
-    (void)raw_pts; (void)n; (void)stride_bytes; (void)off_xyz; (void)off_i; (void)t_scan;
-    if (!ctx || !out) return SLO_E_ARG;
+    if (!ctx || (!raw_pts && n) || !out) return SLO_E_ARG;
+    int r = single_stream(ctx);
+    if (r) return r;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    r = stage_points(ctx, raw_pts, n, stride_bytes, off_xyz, off_i);
+    if (r) return r;
+    r = slo_batch_map_optimization(ctx, ctx->d_in, ctx->d_cnt, t_scan);
+    if (r) return r;
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    StreamState st;
+    SLO_CHECK(hipMemcpy(&st, ctx->v.st, sizeof(st), hipMemcpyDeviceToHost));
     memset(out, 0, sizeof(*out));
+    out->ran = st.mo_ran;
+    out->keyframe_saved = st.kf_saved;
+    out->n_keyframes = st.n_keyframes;
+    memcpy(out->transform_aft_mapped, st.transformAftMapped, 24);
     return SLO_OK;
 }
 

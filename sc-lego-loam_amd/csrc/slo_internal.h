@@ -158,6 +158,14 @@ struct DevView {
 
 #define SLO_MO_BLOCKS 64
 #define SLO_RECORD_FLOATS 40
+#define SLO_KFMAX 4096          // keyframe pose / Scan Context history capacity per stream
+#define SLO_SC_MAX_K 64         // NUM_CANDIDATES_FROM_TREE limit (C5 uses 50)
+#define SLO_SC_MAX_SECTOR 64
+#define SLO_SC_MAX_CELLS 1200   // PC_NUM_RING * PC_NUM_SECTOR limit (20 x 60)
+// StreamState::err bits (sticky; read with slo_get(.., "err"))
+#define SLO_ERR_KEYFRAMES 1     // keyframe pose history full: keyframe dropped
+#define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
+#define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud
 
 __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
     return (((unsigned int)x * 73856093u) ^ ((unsigned int)y * 19349663u) ^ ((unsigned int)z * 83492791u)) &
@@ -212,6 +220,8 @@ struct slo_ctx {
     // host staging for single-scan API
     void* h_stage = nullptr;
     size_t h_stage_bytes = 0;
+    std::vector<char> h_view[16];       // backing store of the single-scan views
+    int32_t h_ring[2][128];
     float4* d_in = nullptr;   // internal input buffer [S][P]
     int32_t* d_cnt = nullptr;
     // mapping workspaces

@@ -371,6 +371,7 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
             float cx = st.transformAftMapped[3], cy = st.transformAftMapped[4], cz = st.transformAftMapped[5];
             float dx = st.prevPos[0] - cx, dy = st.prevPos[1] - cy, dz = st.prevPos[2] - cz;
             bool saveThis = !(sqrtf(dx * dx + dy * dy + dz * dz) < 0.3);
+            if ((saveThis || st.n_keyframes == 0) && st.n_keyframes >= v.KFMAX) st.err |= SLO_ERR_KEYFRAMES;
             if ((saveThis || st.n_keyframes == 0) && st.n_keyframes < v.KFMAX) {
                 st.prevPos[0] = cx; st.prevPos[1] = cy; st.prevPos[2] = cz;
                 float est[6];
@@ -415,6 +416,8 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
             dst[c][i] = make_float4(ctPitch * x2 + stPitch * z2 + pose[0], y2 + pose[1], -stPitch * x2 + ctPitch * z2 + pose[2], p.w);
         }
     if (threadIdx.x < 3) v.kf_n[ks * 3 + threadIdx.x] = n3[threadIdx.x];
+    if (threadIdx.x == 0 && (n3[0] < st.n_corner_ds || n3[1] < st.n_surf_ds || n3[2] < st.n_outl_ds))
+        st.err |= SLO_ERR_MAP_CAPACITY;
     // Scan Context make on laserCloudRawDS (MO:1626-1631)
     sc_make_block(v, s, v.cur_raw_ds + (size_t)s * v.P, st.n_raw_ds);
 }
@@ -444,7 +447,10 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
     for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
     __syncthreads();
     const int kfid = hid;
-    if (kfid >= v.KFMAX) return;
+    if (kfid >= v.KFMAX) {
+        if (threadIdx.x == 0) st.err |= SLO_ERR_SC_HISTORY;
+        return;
+    }
     for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
         float4 p0 = raw[i];
         float px = p0.x, py = p0.y;

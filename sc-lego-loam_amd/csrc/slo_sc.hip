@@ -43,7 +43,16 @@ struct ESum {
     __device__ double get() const { return (a0 + a2) + (a1 + a3); }  // valid for n % 4 == 0, n >= 4
 };
 
-#define SC_K 64
+#define SC_K SLO_SC_MAX_K
+#define SC_NS SLO_SC_MAX_SECTOR
+
+__device__ inline unsigned long long wave_min_u64(unsigned long long x) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(x, o, 64);
+        x = y < x ? y : x;
+    }
+    return x;
+}
 
 __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     const int s = blockIdx.x;
@@ -56,12 +65,13 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector, K = v.cfg.sc_num_candidates;
     const int N = st.sc_count;
     __shared__ int s_treen, s_skip;
-    __shared__ Cand lists[256][10];
+    __shared__ unsigned long long keys[SLO_KFMAX];   // (f32 L2 bits << 32 | index) of the snapshot
+    __shared__ unsigned long long wmin[4];
     __shared__ int cands[SC_K];
-    __shared__ double sim[7 * 60];
-    __shared__ int simok[7 * 60];
+    __shared__ double sim[7 * SC_NS];
+    __shared__ int simok[7 * SC_NS];
     __shared__ double dist7[7];
-    __shared__ double shnorm[64];
+    __shared__ double shnorm[SC_NS];
     __shared__ int shifts[7];
     __shared__ double cdist[SC_K];
     __shared__ int calign[SC_K];
@@ -81,34 +91,33 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     if (s_skip) return;
     const size_t hb = (size_t)s * v.KFMAX;
     const float* q = v.sc_ring + (hb + N - 1) * NR;
-    // ---- exact K-NN over the snapshot
-    Cand loc[10];
-    int cnt = 0;
-    for (int j = tid; j < s_treen; j += blockDim.x) {
-        Cand c{l2_nf(q, v.sc_ring + (hb + j) * NR, NR), j};
-        if (cnt == K && !cand_less(c, loc[K - 1])) continue;
-        int pos = cnt < K ? cnt : K - 1;
-        while (pos > 0 && cand_less(c, loc[pos - 1])) { loc[pos] = loc[pos - 1]; --pos; }
-        loc[pos] = c;
-        if (cnt < K) ++cnt;
-    }
-    for (int k = 0; k < 10; ++k) lists[tid][k] = k < cnt ? loc[k] : Cand{FLT_MAX, INT_MAX};
+    // ---- exact K-NN over the snapshot: distances once into LDS as
+    // order-preserving (distance, index) keys (L2 >= 0, so the float bits sort
+    // like the values), then K rounds of block-wide "smallest key above the
+    // previous pick".  Ties resolve to the lower index; slots beyond the
+    // snapshot size stay 0, as with the reference's zero-initialised
+    // candidate_indexes (SCc:282).
+    const int n = s_treen;
+    for (int j = tid; j < n; j += blockDim.x)
+        keys[j] = ((unsigned long long)__float_as_uint(l2_nf(q, v.sc_ring + (hb + j) * NR, NR)) << 32) |
+                  (unsigned int)j;
     __syncthreads();
-    for (int half = blockDim.x / 2; half > 0; half >>= 1) {
-        if (tid < half) {
-            Cand m[10];
-            int a = 0, b = 0;
-            for (int k = 0; k < K; ++k) {
-                const Cand& x = lists[tid][a];
-                const Cand& y = lists[tid + half][b];
-                if (cand_less(y, x)) { m[k] = y; ++b; } else { m[k] = x; ++a; }
-            }
-            for (int k = 0; k < K; ++k) lists[tid][k] = m[k];
+    unsigned long long prev = 0;
+    for (int k = 0; k < K; ++k) {
+        unsigned long long best = ~0ull;
+        for (int j = tid; j < n; j += blockDim.x) {
+            const unsigned long long x = keys[j];
+            if ((k == 0 || x > prev) && x < best) best = x;
         }
+        best = wave_min_u64(best);
+        if ((tid & 63) == 0) wmin[tid >> 6] = best;
+        __syncthreads();
+        best = wmin[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) best = wmin[w] < best ? wmin[w] : best;
+        if (tid == 0) cands[k] = best == ~0ull ? 0 : (int)(best & 0xffffffffu);
+        prev = best;
         __syncthreads();
     }
-    if (tid < K) cands[tid] = lists[0][tid].i == INT_MAX ? 0 : lists[0][tid].i;
-    __syncthreads();
     const double* sc1 = v.sc_desc + (hb + N - 1) * NR * NS;
     const double* vk1 = v.sc_sect + (hb + N - 1) * NS;
     for (int c = 0; c < K; ++c) {

@@ -151,31 +151,87 @@ class Context:
         return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
 
 
-class ImageProjection:
-    """Mirror of ImageProjection::cloudHandler (imageProjection.cpp:181) on stream 0."""
+def _arr(ptr, n, dtype, cols=None):
+    """Copy a view array (context-owned host memory) into numpy."""
+    shape = (n, cols) if cols else (n,)
+    if not n or not ptr:
+        return np.empty(shape, dtype)
+    nbytes = n * (cols or 1) * np.dtype(dtype).itemsize
+    return np.frombuffer(ctypes.string_at(ptr, nbytes), dtype).reshape(shape).copy()
+
+
+class _Node:
+    """Single-scan node mirrors share one one-stream Context (the reference
+    runs the nodes as separate processes joined by topics; here the topics are
+    the context's device buffers)."""
 
     def __init__(self, ctx):
+        if ctx.n_streams != 1:
+            raise SloError("node mirrors need a Context with n_streams == 1 (use the batch_* calls otherwise)")
         self.ctx = ctx
+
+
+class ImageProjection(_Node):
+    """Mirror of ImageProjection::cloudHandler (imageProjection.cpp:181-196).
+
+    Returns the /segmented_cloud, /segmented_cloud_info and /outlier_cloud
+    contents as numpy arrays."""
 
     def cloudHandler(self, points_xyzi):
         pts = np.ascontiguousarray(points_xyzi, np.float32)
-        view = SegView()
+        v = SegView()
         self.ctx._ok(self.ctx.L.slo_image_projection(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
-                                                     ctypes.byref(view)), "slo_image_projection")
-        return {k: self.ctx.get(0, k) for k in ("seg_pts", "seg_ground", "seg_col", "seg_range", "ring_start",
-                                                 "ring_end", "orient", "outlier")}
+                                                     ctypes.byref(v)), "slo_image_projection")
+        R = self.ctx.cfg.n_scan
+        return {
+            "seg_pts": _arr(v.segmented, v.n_segmented, np.float32, 4),
+            "seg_ground": _arr(v.ground_flag, v.n_segmented, np.uint8),
+            "seg_col": _arr(v.col_ind, v.n_segmented, np.uint32),
+            "seg_range": _arr(v.range, v.n_segmented, np.float32),
+            "ring_start": _arr(v.start_ring_index, R, np.int32),
+            "ring_end": _arr(v.end_ring_index, R, np.int32),
+            "orient": np.array([v.start_orientation, v.end_orientation, v.orientation_diff], np.float32),
+            "outlier": _arr(v.outlier, v.n_outlier, np.float32, 4),
+        }
 
 
-class FeatureAssociation:
-    """Mirror of FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1817) on stream 0."""
+class FeatureAssociation(_Node):
+    """Mirror of FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1817-1859)."""
+
+    def runFeatureAssociation(self, t_scan=0.0):
+        v = FaView()
+        self.ctx._ok(self.ctx.L.slo_feature_association(self.ctx.h, float(t_scan), ctypes.byref(v)),
+                     "slo_feature_association")
+        return {"transform_sum": np.array(v.transform_sum[:], np.float32), "published": bool(v.published),
+                "sharp": _arr(v.sharp, v.n_sharp, np.float32, 4), "flat": _arr(v.flat, v.n_flat, np.float32, 4),
+                "corner_last": _arr(v.less_sharp, v.n_less_sharp, np.float32, 4),
+                "surf_last": _arr(v.less_flat, v.n_less_flat, np.float32, 4)}
+
+
+class MapOptimization(_Node):
+    """Mirror of mapOptimization::run (mapOptmization.cpp:1673-1706) minus
+    GTSAM and publishing; `raw_xyzi` is the scan's raw cloud (/os1_points)."""
+
+    def run(self, raw_xyzi, t_scan):
+        pts = np.ascontiguousarray(raw_xyzi, np.float32)
+        v = MapView()
+        self.ctx._ok(self.ctx.L.slo_map_optimization(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
+                                                     float(t_scan), ctypes.byref(v)), "slo_map_optimization")
+        return {"ran": bool(v.ran), "keyframe_saved": bool(v.keyframe_saved), "n_keyframes": v.n_keyframes,
+                "transform_aft_mapped": np.array(v.transform_aft_mapped[:], np.float32)}
+
+
+class SCManager:
+    """Mirror of the public SCManager API (Scancontext.h:63-73) on stream 0 of
+    a Context: makeAndSaveScancontextAndKeys / detectLoopClosureID."""
 
     def __init__(self, ctx):
         self.ctx = ctx
 
-    def runFeatureAssociation(self, t_scan=0.0):
-        view = FaView()
-        self.ctx._ok(self.ctx.L.slo_feature_association(self.ctx.h, float(t_scan), ctypes.byref(view)),
-                     "slo_feature_association")
-        return {"transform_sum": np.array(view.transform_sum[:], np.float32), "published": bool(view.published),
-                "n_sharp": view.n_sharp, "n_flat": view.n_flat, "n_less_sharp": view.n_less_sharp,
-                "n_less_flat": view.n_less_flat}
+    def makeAndSaveScancontextAndKeys(self, scan_down_xyzi):
+        self.ctx.sc_make_and_save(scan_down_xyzi)
+
+    def detectLoopClosureID(self):
+        """-> (loop_id, yaw_rad) like the reference's std::pair<int, float>."""
+        lid, yaw, _ = self.ctx.sc_detect()
+        return lid, yaw

@@ -1,0 +1,50 @@
+"""Multi-GPU layout of the batched path (mode M).
+
+One process per GPU.  Streams are independent (each owns its pose chain,
+local map and Scan Context history), so rank r owns the contiguous global
+stream ids [r*S, (r+1)*S) and the data path needs no collective: every rank
+advances its own S streams one scan per step (weak scaling).  The only
+exchange is one batched all-gather per step of a fixed 160-byte record per
+stream (odometry pose, mapped pose, keyframe count, loop result, newest ring
+key; slo_pack_records), so every rank sees every stream's state for
+cross-stream (multi-session) loop candidates.  Over RCCL that is
+world*S*160 B, latency-bound and far below xGMI bandwidth.
+"""
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    import os
+    return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
+            int(os.environ.get("LOCAL_RANK", "0")))
+
+
+def stream_shard(rank, world, streams_per_rank):
+    """(first global stream id, count) owned by `rank`."""
+    if not (0 <= rank < world) or streams_per_rank <= 0:
+        raise ValueError("bad shard")
+    return rank * streams_per_rank, streams_per_rank
+
+
+def gather_records(rec, out=None):
+    """All-gather the [S, F] per-stream records of every rank into
+    [world*S, F], rank-major (= global stream order)."""
+    world = dist.get_world_size()
+    if out is None:
+        out = torch.empty((world * rec.shape[0], rec.shape[1]), dtype=rec.dtype, device=rec.device)
+    if dist.get_backend() == "gloo":   # CPU rehearsal: gloo has no all_gather_into_tensor
+        parts = list(out.view(world, *rec.shape).unbind(0))
+        dist.all_gather(parts, rec)
+    else:
+        dist.all_gather_into_tensor(out, rec)
+    return out
+
+
+def max_over_ranks(seconds, device="cpu"):
+    """The slowest rank's time (bench.py reports whole-job throughput)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(seconds)
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())

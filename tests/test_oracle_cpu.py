@@ -1,0 +1,102 @@
+"""CPU tests of the oracle (test infrastructure): the restated glibc libm and
+libstdc++ introsort against the host's, the Scan Context K-NN against the
+reference's own nanoflann tree (committed fixture), and the oracle against
+its committed stage fingerprints (tests/golden/make_golden.py)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLD = os.path.join(HERE, "golden")
+
+
+def test_libm_restatement_matches_glibc():
+    # atan2f, sinf, cosf, atanf, asinf bit-for-bit vs the host glibc
+    for seed in (1, 7, 12345):
+        assert O.lib().oracle_libm_selftest(300000, seed) == 0
+
+
+def test_introsort_restatement_matches_libstdcxx(tmp_path):
+    exe = tmp_path / "introsort_check"
+    src = os.path.join(HERE, "cpp", "introsort_check.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), src], check=True)
+    bad, cases = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
+    assert cases > 900 and bad == 0
+
+
+@pytest.fixture(scope="module")
+def sc_gold():
+    with np.load(os.path.join(GOLD, "sc_loop_hdl64.npz"), allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+@pytest.mark.parametrize("K", [10, 50])
+def test_sc_knn_matches_reference_nanoflann(sc_gold, K):
+    """Exact K-NN of the restatement == the reference's nanoflann tree
+    (oracle/_ref/nanoflann_pin built from /root/reference's headers)."""
+    cfg = O.preset(int(sc_gold["preset"]))
+    keys = sc_gold["ring_keys"]
+    nf_i, nf_d = sc_gold[f"nf_idx{K}"], sc_gold[f"nf_dist{K}"]
+    checked = 0
+    for q, (j, snap) in enumerate(zip(sc_gold["query_frame"], sc_gold["snapshot"])):
+        idx, dist = O.sc_knn(cfg, keys[:snap], keys[j], K)
+        m = min(K, int(snap))
+        assert np.array_equal(dist[:m].view(np.uint32), nf_d[q][:m].view(np.uint32)), q
+        # same neighbours; order only free inside equal-distance groups
+        for d in np.unique(dist[:m]):
+            assert set(idx[:m][dist[:m] == d]) == set(nf_i[q][:m][nf_d[q][:m] == d])
+        # unfilled slots keep the zero-initialised index (Scancontext.cpp:282)
+        assert (nf_i[q][m:] == 0).all() and (idx[m:] == 0).all()
+        checked += 1
+    assert checked == len(sc_gold["query_frame"]) > 100
+
+
+def test_sc_session_reproduces_fixture_prefix(sc_gold):
+    """First 60 keyframes: ring keys and detect results are bit-identical."""
+    pid, cid, sid, step = (int(sc_gold[k]) for k in ("preset", "config", "stream", "step"))
+    cfg = O.preset(pid)
+    ses = O.SCSession(cfg, stable_voxel=True)
+    for j in range(60):
+        n, key = ses.add(O.gen_scan(pid, cid, sid, j * step))
+        assert n == sc_gold["n_ds"][j]
+        assert np.array_equal(key.view(np.uint32), sc_gold["ring_keys"][j].view(np.uint32))
+        d = ses.detect()
+        assert d["loop_id"] == sc_gold["loop_id"][j] and d["nn_idx"] == sc_gold["nn_idx"][j]
+        assert np.float64(d["min_dist"]).view(np.uint64) == sc_gold["min_dist"][j].view(np.uint64)
+
+
+def test_sc_fixture_has_true_and_early_loops(sc_gold):
+    lid = sc_gold["loop_id"]
+    assert (lid[:50] == -1).all()                 # < 51 contexts: early return (SCc:257-261)
+    assert sc_gold["snapshot"][0] == 1            # first tree: 51 - NUM_EXCLUDE_RECENT rows
+    assert (lid[205:] >= 0).sum() > 20            # the second lap closes loops
+
+
+@pytest.mark.parametrize("name", ["vlp16", "hdl64"])
+def test_oracle_front_fingerprints(name):
+    with open(os.path.join(GOLD, f"front_{name}.json")) as f:
+        gold = json.load(f)
+    import fingerprint as F
+    rows = F.oracle_rows(O, gold["preset"], gold["config"], len(gold["scans"]))
+    for got, want in zip(rows, gold["scans"]):
+        assert got == want, (name, want["scan"])
+
+
+def test_voxel_grid_stable_and_sorted_orders_agree_as_sets():
+    """The GPU VoxelGrid keeps input order inside a voxel ("stable"); PCL's
+    std::sort does not.  Same voxels, same counts, centroids within rounding."""
+    pts = O.gen_scan(6, 3, 0, 5)
+    pts = pts[np.isfinite(pts[:, :3]).all(1)]
+    outs = []
+    for stable in (0, 1):
+        out = np.empty_like(pts)
+        n = O.lib().oracle_voxel_grid(pts.ctypes.data, len(pts), 0.5, stable, out.ctypes.data, len(out))
+        outs.append(out[:n])
+    a, b = outs
+    assert len(a) == len(b) > 1000
+    np.testing.assert_allclose(a, b, rtol=0, atol=2e-5)

@@ -28,7 +28,11 @@ def posediff(a, b):
     return float(np.max(np.abs(np.asarray(a, np.float64) - np.asarray(b, np.float64)))) if len(a) else 0.0
 
 
-def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1):
+def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1, n_points=None,
+        scan_fn=None):
+    """n_points(k, s) -> points of stream s's scan k handed over (ragged and
+    empty scans; default: all); scan_fn(k, s) -> the scan itself (default: the
+    synthetic generator)."""
     import torch
     cfg = slo_amd.preset(preset_id)
     P = cfg.max_points
@@ -36,17 +40,19 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
     ors = [O.OracleStream(O.preset(preset_id), stable_voxel=True) for _ in range(n_streams)]
     report = []
     worst = {"odom": 0.0, "map": 0.0, "keypose": 0.0}
-    counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0}
+    counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0, "flag_mismatch": 0}
     for k in range(n_scans):
-        scans = [O.gen_scan(preset_id, config_id, s, k) for s in range(n_streams)]
+        scans = [scan_fn(k, s) if scan_fn else O.gen_scan(preset_id, config_id, s, k) for s in range(n_streams)]
+        ns = [min(P, n_points(k, s)) if n_points else P for s in range(n_streams)]
         pts = torch.from_numpy(np.stack(scans)).cuda()
-        cnt = torch.full((n_streams,), P, dtype=torch.int32, device="cuda")
+        cnt = torch.tensor(ns, dtype=torch.int32, device="cuda")
         ctx.batch_process(pts.data_ptr(), cnt.data_ptr(), 0.1 * k)
         ctx.synchronize()
         for s in range(n_streams):
-            fl_o = ors[s].step(scans[s], 0.1 * k)
+            fl_o = ors[s].step(scans[s][:ns[s]], 0.1 * k)
             fl_g = int(ctx.get(s, "flags")[0])
             row = {"scan": k, "stream": s, "flags_cpu": fl_o & 14, "flags_gpu": fl_g}
+            counts["flag_mismatch"] += int((fl_o & 14) != fl_g)
             check_front = front and (k % every == 0)
             if check_front:
                 for name in FRONT:
