@@ -26,6 +26,7 @@
 #include <vector>
 #include <algorithm>
 #include <limits>
+#include "../sc-lego-loam_amd/csrc/slo_ddsum.h"
 
 namespace oracle {
 
@@ -200,26 +201,25 @@ struct KdTree {
 // output in k order (GEMMSingleMul<float,double>), result rounded to float.
 // AtB (single-column output) goes through the transposed-B branch, which
 // keeps two accumulators (even / odd k) and adds them at the end.
+// matAtA = matAt * matA, matAtB = matAt * matB (cv::Mat GEMM on float Mats,
+// FA:1324-1326 / 1425-1427, MO:1445-1447).  OpenCV's accumulation order is
+// unpinned (Q11); products of floats are exact in double and the sum is
+// taken in double-double and rounded once (slo_ddsum.h), which is the
+// correctly rounded float of the exact sum — the same value the GPU's tree
+// reduction produces.
 inline void gemm_AtA(const std::vector<float>& A, int n, int m, float* AtA) {
     for (int i = 0; i < m; ++i)
         for (int j = 0; j < m; ++j) {
-            double s = 0;
-            for (int k = 0; k < n; ++k) s += (double)A[k * m + i] * (double)A[k * m + j];
-            AtA[i * m + j] = (float)s;
+            slo_dd::DD s = slo_dd::zero();
+            for (int k = 0; k < n; ++k) slo_dd::add(s, (double)A[k * m + i] * (double)A[k * m + j]);
+            AtA[i * m + j] = slo_dd::to_float(s);
         }
 }
 inline void gemm_AtB(const std::vector<float>& A, const std::vector<float>& B, int n, int m, float* AtB) {
     for (int i = 0; i < m; ++i) {
-        double s0 = 0, s1 = 0;
-        int k = 0;
-        for (; k <= n - 4; k += 4) {
-            s0 += (double)A[k * m + i] * (double)B[k];
-            s1 += (double)A[(k + 1) * m + i] * (double)B[k + 1];
-            s0 += (double)A[(k + 2) * m + i] * (double)B[k + 2];
-            s1 += (double)A[(k + 3) * m + i] * (double)B[k + 3];
-        }
-        for (; k < n; ++k) s0 += (double)A[k * m + i] * (double)B[k];
-        AtB[i] = (float)(s0 + s1);
+        slo_dd::DD s = slo_dd::zero();
+        for (int k = 0; k < n; ++k) slo_dd::add(s, (double)A[k * m + i] * (double)B[k]);
+        AtB[i] = slo_dd::to_float(s);
     }
 }
 // small dense C = A(r x k) * B(k x c), double accumulation

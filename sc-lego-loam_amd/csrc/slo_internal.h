@@ -15,6 +15,7 @@
 #include <vector>
 #include <map>
 #include "slo_config.h"
+#include "slo_ddsum.h"
 #include "../../include/slo_abi.h"
 
 #define SLO_CHECK(x)                                                            \
@@ -140,7 +141,7 @@ struct DevView {
     float4* cur_o_ds;    // [S][H/5]
     float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
     float4* cur_st_ds;   // [S][cap_st]
-    double* mo_part;     // [S][MO_BLOCKS][28] partial A^T A / A^T b / count
+    double* mo_part;     // [S][MO_BLOCKS][SLO_MO_PART] partial A^T A / A^T b (double-double) + count
     // hash grids over the odometry "kd-tree" clouds (1 m cells)
     int Toc, Tos;
     const int32_t *goc_cnt, *goc_off, *gos_cnt, *gos_off;
@@ -157,6 +158,7 @@ struct DevView {
 };
 
 #define SLO_MO_BLOCKS 64
+#define SLO_MO_PART 55          // 27 double-double sums (21 AtA + 6 AtB) + correspondence count
 #define SLO_RECORD_FLOATS 40
 #define SLO_KFMAX 4096          // keyframe pose / Scan Context history capacity per stream
 #define SLO_SC_MAX_K 64         // NUM_CANDIDATES_FROM_TREE limit (C5 uses 50)

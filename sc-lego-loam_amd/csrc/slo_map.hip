@@ -157,8 +157,9 @@ __device__ inline int knn5(const float4* ent, const int32_t* off, const int32_t*
 __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
     const int s = blockIdx.y;
     const StreamState& st = v.st[s];
-    double acc[28];
-    for (int k = 0; k < 28; ++k) acc[k] = 0;
+    slo_dd::DD acc[27];
+    for (int k = 0; k < 27; ++k) acc[k] = slo_dd::zero();
+    int nsel = 0;
     const bool live = st.mo_ran && st.map_ok && !st.mo_converged;
     if (live) {
         const float* t = st.transformTobeMapped;
@@ -250,23 +251,38 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
             const double b = -cfw;
             int k = 0;
             for (int i = 0; i < 6; ++i)
-                for (int j = i; j < 6; ++j) acc[k++] += a[i] * a[j];
-            for (int i = 0; i < 6; ++i) acc[21 + i] += a[i] * b;
-            acc[27] += 1.0;
+                for (int j = i; j < 6; ++j) slo_dd::add(acc[k++], a[i] * a[j]);
+            for (int i = 0; i < 6; ++i) slo_dd::add(acc[21 + i], a[i] * b);
+            ++nsel;
         }
     }
-    // block reduction (fixed order)
-    __shared__ double sh[4][28];
-    for (int o = 32; o > 0; o >>= 1)
-        for (int k = 0; k < 28; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+    // block reduction of the double-double partial sums (order-independent
+    // after the final rounding, slo_ddsum.h)
+    __shared__ slo_dd::DD sh[4][27];
+    __shared__ int shn[4];
+    for (int o = 32; o > 0; o >>= 1) {
+        for (int k = 0; k < 27; ++k) {
+            slo_dd::DD y{__shfl_xor(acc[k].hi, o, 64), __shfl_xor(acc[k].lo, o, 64)};
+            slo_dd::merge(acc[k], y);
+        }
+        nsel += __shfl_xor(nsel, o, 64);
+    }
     const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 28; ++k) sh[w][k] = acc[k];
+    if ((threadIdx.x & 63) == 0) {
+        for (int k = 0; k < 27; ++k) sh[w][k] = acc[k];
+        shn[w] = nsel;
+    }
     __syncthreads();
-    if (threadIdx.x < 28) {
-        double r = sh[0][threadIdx.x];
-        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) r += sh[ww][threadIdx.x];
-        v.mo_part[((size_t)s * SLO_MO_BLOCKS + blockIdx.x) * 28 + threadIdx.x] = r;
+    double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + blockIdx.x) * SLO_MO_PART;
+    if (threadIdx.x < 27) {
+        slo_dd::DD r = sh[0][threadIdx.x];
+        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) slo_dd::merge(r, sh[ww][threadIdx.x]);
+        part[2 * threadIdx.x] = r.hi;
+        part[2 * threadIdx.x + 1] = r.lo;
+    } else if (threadIdx.x == 27) {
+        int n = shn[0];
+        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) n += shn[ww];
+        part[54] = (double)n;
     }
 }
 
@@ -276,19 +292,25 @@ __global__ void k_mo_solve(DevView v, int iterCount) {
     StreamState& st = v.st[s];
     if (threadIdx.x != 0) return;
     if (!(st.mo_ran && st.map_ok && !st.mo_converged)) return;
-    double acc[28];
-    for (int k = 0; k < 28; ++k) acc[k] = 0;
-    for (int b = 0; b < SLO_MO_BLOCKS; ++b)
-        for (int k = 0; k < 28; ++k) acc[k] += v.mo_part[((size_t)s * SLO_MO_BLOCKS + b) * 28 + k];
+    slo_dd::DD acc[27];
+    for (int k = 0; k < 27; ++k) acc[k] = slo_dd::zero();
+    int nsel = 0;
+    for (int b = 0; b < SLO_MO_BLOCKS; ++b) {
+        const double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + b) * SLO_MO_PART;
+        for (int k = 0; k < 27; ++k) slo_dd::merge(acc[k], slo_dd::DD{part[2 * k], part[2 * k + 1]});
+        nsel += (int)part[54];
+    }
     st.mo_iters = iterCount + 1;
-    const int nsel = (int)acc[27];
     st.n_sel = nsel;
     if (nsel < 50) return;  // LMOptimization returns false, loop continues
     float AtA[36], AtB[6], X[6];
     int k = 0;
     for (int i = 0; i < 6; ++i)
-        for (int j = i; j < 6; ++j) { AtA[i * 6 + j] = (float)acc[k]; AtA[j * 6 + i] = (float)acc[k]; ++k; }
-    for (int i = 0; i < 6; ++i) AtB[i] = (float)acc[21 + i];
+        for (int j = i; j < 6; ++j) {
+            const float f = slo_dd::to_float(acc[k++]);
+            AtA[i * 6 + j] = f; AtA[j * 6 + i] = f;
+        }
+    for (int i = 0; i < 6; ++i) AtB[i] = slo_dd::to_float(acc[21 + i]);
     slo_la::solve_qr(AtA, AtB, 6, 6, X);
     if (iterCount == 0) {
         float E[6], V[36], V2[36], Vi[36];

@@ -8,11 +8,12 @@
 // loop (the iterations are sequential; the streams are independent), so no
 // host round trip happens per iteration.  Per iteration every lane
 // transforms its queries, (every 5th iteration) finds the exact nearest
-// neighbour by a brute-force sweep that all lanes of a wave take in lockstep
-// (one broadcast load per target), walks the ring-ordered target cloud for
-// the 2nd/3rd points exactly as the reference (including Q7's bound), and
-// accumulates its rows of A^T A / A^T b in double; a wave-shuffle + LDS tree
-// reduces them and lane 0 runs the 3x3 QR / Jacobi / degeneracy projection.
+// neighbour in a 1 m hash grid over the "kd-tree" cloud (rebuilt after every
+// scan by fa_odometry_run, like setInputCloud), walks the ring-ordered target
+// cloud for the 2nd/3rd points exactly as the reference (including Q7's
+// bound), and accumulates its rows of A^T A / A^T b in double-double
+// (slo_ddsum.h); a wave-shuffle + LDS tree reduces them and lane 0 rounds once
+// to float and runs the 3x3 QR / Jacobi / degeneracy projection.
 // Nearest-neighbour ties resolve to the lowest index (FLANN's tie order is
 // traversal dependent).
 #include "slo_internal.h"
@@ -75,11 +76,15 @@ __device__ inline void nn1_grid(const float4* ent, const int32_t* off, const int
     }
 }
 
-// block-wide sum of NV doubles + one int; result valid in lane 0 of wave 0
+// block-wide double-double sum of NV terms + one int (slo_ddsum.h); result
+// valid in lane 0 of wave 0
 template <int NV>
-__device__ inline void block_reduce(double* acc, int& cnt, double* sh, int* shi) {
+__device__ inline void block_reduce(slo_dd::DD* acc, int& cnt, slo_dd::DD* sh, int* shi) {
     for (int o = 32; o > 0; o >>= 1) {
-        for (int k = 0; k < NV; ++k) acc[k] += __shfl_xor(acc[k], o, 64);
+        for (int k = 0; k < NV; ++k) {
+            slo_dd::DD y{__shfl_xor(acc[k].hi, o, 64), __shfl_xor(acc[k].lo, o, 64)};
+            slo_dd::merge(acc[k], y);
+        }
         cnt += __shfl_xor(cnt, o, 64);
     }
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -92,18 +97,26 @@ __device__ inline void block_reduce(double* acc, int& cnt, double* sh, int* shi)
         for (int k = 0; k < NV; ++k) acc[k] = sh[k];
         cnt = shi[0];
         for (int ww = 1; ww < nw; ++ww) {
-            for (int k = 0; k < NV; ++k) acc[k] += sh[ww * NV + k];
+            for (int k = 0; k < NV; ++k) slo_dd::merge(acc[k], sh[ww * NV + k]);
             cnt += shi[ww];
         }
     }
 }
 
+// one row of matA / matB into AtA (upper) / AtB; float products are exact in double
+__device__ inline void accumulate9(slo_dd::DD* acc, double A0, double A1, double A2, double B) {
+    slo_dd::add(acc[0], A0 * A0); slo_dd::add(acc[1], A0 * A1); slo_dd::add(acc[2], A0 * A2);
+    slo_dd::add(acc[3], A1 * A1); slo_dd::add(acc[4], A1 * A2); slo_dd::add(acc[5], A2 * A2);
+    slo_dd::add(acc[6], A0 * B); slo_dd::add(acc[7], A1 * B); slo_dd::add(acc[8], A2 * B);
+}
+
 // lane-0 tail shared by calculateTransformationSurf/Corner (FA:1324-1377)
-__device__ inline bool solve_step(StreamState& st, const double* acc, int iterCount, float* X) {
-    // acc: AtA(00,01,02,11,12,22), AtB(0,1,2)
-    float AtA[9] = {(float)acc[0], (float)acc[1], (float)acc[2], (float)acc[1], (float)acc[3],
-                    (float)acc[4], (float)acc[2], (float)acc[4], (float)acc[5]};
-    float AtB[3] = {(float)acc[6], (float)acc[7], (float)acc[8]};
+__device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int iterCount, float* X) {
+    // acc: AtA(00,01,02,11,12,22), AtB(0,1,2); matAtA / matAtB are float Mats
+    float r[9];
+    for (int k = 0; k < 9; ++k) r[k] = slo_dd::to_float(acc[k]);
+    float AtA[9] = {r[0], r[1], r[2], r[1], r[3], r[4], r[2], r[4], r[5]};
+    float AtB[3] = {r[6], r[7], r[8]};
     slo_la::solve_qr(AtA, AtB, 3, 3, X);
     if (iterCount == 0) {
         float E[3], V[9], V2[9], Vi[9];
@@ -153,7 +166,7 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
 
     __shared__ float tc[6];
     __shared__ int s_ctl;      // 0 = go on, 1 = skip solve (continue), 2 = break
-    __shared__ double sh[4 * 9];
+    __shared__ slo_dd::DD sh[4 * 9];
     __shared__ int shi[4];
     if (tid == 0) for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
     __syncthreads();
@@ -169,7 +182,8 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
         const int nq = st.n_flat;
         int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
         for (int iterCount = 0; iterCount < 25; iterCount++) {
-            double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            slo_dd::DD acc[9];
+            for (int k = 0; k < 9; ++k) acc[k] = slo_dd::zero();
             int cnt = 0;
             float srx = slo_libm::sinf_(tc[0]), crx = slo_libm::cosf_(tc[0]);
             float sry = slo_libm::sinf_(tc[1]), cry = slo_libm::cosf_(tc[1]);
@@ -234,9 +248,7 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
                         float aty = -b6 * cx + c4 * cy + b2 * cz;
                         float bb = (float)(-0.05 * cw);
                         double A0 = arx, A1 = arz, A2 = aty, B = bb;
-                        acc[0] += A0 * A0; acc[1] += A0 * A1; acc[2] += A0 * A2;
-                        acc[3] += A1 * A1; acc[4] += A1 * A2; acc[5] += A2 * A2;
-                        acc[6] += A0 * B; acc[7] += A1 * B; acc[8] += A2 * B;
+                        accumulate9(acc, A0, A1, A2, B);
                         cnt++;
                     }
                 }
@@ -265,7 +277,8 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
         const int nc = st.n_sharp;
         int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
         for (int iterCount = 0; iterCount < 25; iterCount++) {
-            double acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
+            slo_dd::DD acc[9];
+            for (int k = 0; k < 9; ++k) acc[k] = slo_dd::zero();
             int cnt = 0;
             float srx = slo_libm::sinf_(tc[0]), crx = slo_libm::cosf_(tc[0]);
             float sry = slo_libm::sinf_(tc[1]), cry = slo_libm::cosf_(tc[1]);
@@ -326,9 +339,7 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
                         float atz = b7 * cx - srx * cy - b3 * cz;
                         float bb = (float)(-0.05 * cw);
                         double A0 = ary, A1 = atx, A2 = atz, B = bb;
-                        acc[0] += A0 * A0; acc[1] += A0 * A1; acc[2] += A0 * A2;
-                        acc[3] += A1 * A1; acc[4] += A1 * A2; acc[5] += A2 * A2;
-                        acc[6] += A0 * B; acc[7] += A1 * B; acc[8] += A2 * B;
+                        accumulate9(acc, A0, A1, A2, B);
                         cnt++;
                     }
                 }
