@@ -124,6 +124,8 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
     if (name == "raw_ds") return copy_cloud(s->mo.laserCloudRawDS, (float*)out, cap);
     if (name == "corner_ds") return copy_cloud(s->mo.laserCloudCornerLastDS, (float*)out, cap);
     if (name == "surf_total_ds") return copy_cloud(s->mo.laserCloudSurfTotalLastDS, (float*)out, cap);
+    if (name == "map_corner_ds") return copy_cloud(s->mo.lastCornerMapDS, (float*)out, cap);
+    if (name == "map_surf_ds") return copy_cloud(s->mo.lastSurfMapDS, (float*)out, cap);
     if (name == "sc_desc") {
         if (s->mo.sc.polarcontexts_.empty()) return 0;
         auto& d = s->mo.sc.polarcontexts_.back();

@@ -219,8 +219,11 @@ struct ImageProjection {
     void cloudHandler(const float* pts, int n) {
         resetParameters();
         copyPointCloud(pts, n);
-        if (laserCloudIn.empty()) return;  // (reference would read points[0] of an empty cloud: UB)
-        findStartEndAngle();
+        // An empty cloud (no finite point) makes the reference read points[0]
+        // of an empty vector (IP:201: undefined).  Defined here, as in the
+        // GPU path: the orientations keep their previous values and every
+        // other stage runs on an image with no returns.
+        if (!laserCloudIn.empty()) findStartEndAngle();
         projectPointCloud();
         groundRemoval();
         cloudSegmentation();

@@ -36,6 +36,7 @@ struct MapOptimization {
     Cloud laserCloudCornerLastDS, laserCloudSurfLastDS, laserCloudOutlierLastDS;
     Cloud laserCloudSurfTotalLast, laserCloudSurfTotalLastDS;
     Cloud laserCloudCornerFromMap, laserCloudSurfFromMap, laserCloudCornerFromMapDS, laserCloudSurfFromMapDS;
+    Cloud lastCornerMapDS, lastSurfMapDS;   // the last run's DS maps (parity checks only)
     Cloud laserCloudOri, coeffSel;
     KdTree kdtreeCornerFromMap, kdtreeSurfFromMap;
     bool isDegenerate = false;
@@ -415,6 +416,9 @@ struct MapOptimization {
         downsampleCurrentScan();
         scan2MapOptimization();
         saveKeyFramesAndFactor();
+        // clearCloud (MO:1640): the DS maps are kept aside for parity checks
+        lastCornerMapDS.swap(laserCloudCornerFromMapDS);
+        lastSurfMapDS.swap(laserCloudSurfFromMapDS);
         laserCloudCornerFromMap.clear(); laserCloudSurfFromMap.clear();
         laserCloudCornerFromMapDS.clear(); laserCloudSurfFromMapDS.clear();
         return true;

@@ -109,7 +109,7 @@ _DTYPES = {
     "detect_f": np.float64,
 }
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
-           "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds"}
+           "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"}
 
 
 class SCSession:

@@ -145,15 +145,19 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
     // ---- mapping + Scan Context history
-    v.KFR = 64;
+    // Capacities are worst-case bounds, so no cloud is ever clipped: a
+    // VoxelGrid output is no larger than its input, the surf DS of a scan is
+    // a subset-DS of <= H points, the outlier cloud keeps every 5th column
+    // (IP:341-345) of at most R rows.
+    const int NKF = cfg->surrounding_keyframe_search_num;
+    v.KFR = NKF + 2;     // keyframe cloud slots: the recent-NKF deque + the one being added
     v.KFMAX = SLO_KFMAX;
     v.cap_kc = v.cap_less_sharp;
-    v.cap_ks = (int)(H / 3);
-    v.cap_ko = (int)(H / 5);
-    const int NKF = cfg->surrounding_keyframe_search_num;
+    v.cap_ks = (int)H;
+    v.cap_ko = R * ((C + 4) / 5);
     v.cap_mc = NKF * v.cap_kc;
     v.cap_ms = NKF * (v.cap_ks + v.cap_ko);
-    v.cap_st = (int)(H + H / 5);
+    v.cap_st = (int)H + v.cap_ko;
     const size_t NRS = (size_t)cfg->sc_num_ring * cfg->sc_num_sector;
     c.add(&v.outl_cam, S * H);
     c.add(&v.kf_corner, S * v.KFR * v.cap_kc);
@@ -168,7 +172,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.cur_raw_ds, S * v.P);
     c.add(&v.cur_c_ds, S * v.cap_less_sharp);
     c.add(&v.cur_s_ds, S * H);
-    c.add(&v.cur_o_ds, S * (H / 5));
+    c.add(&v.cur_o_ds, S * v.cap_ko);
     c.add(&v.cur_st, S * v.cap_st);
     c.add(&v.cur_st_ds, S * v.cap_st);
     c.add(&v.mo_part, S * SLO_MO_BLOCKS * SLO_MO_PART);

@@ -73,8 +73,8 @@ __global__ void k_mo_prepare(DevView v) {
         nc += kn[0];
         ns += kn[1] + kn[2];
     }
-    if (nc > v.cap_mc) { nc = v.cap_mc; st.err |= 2; }
-    if (ns > v.cap_ms) { ns = v.cap_ms; st.err |= 2; }
+    if (nc > v.cap_mc) { nc = v.cap_mc; st.err |= SLO_ERR_MAP_CAPACITY; }
+    if (ns > v.cap_ms) { ns = v.cap_ms; st.err |= SLO_ERR_MAP_CAPACITY; }
     st.n_corner_map = nc;
     st.n_surf_map = ns;
 }
@@ -107,7 +107,7 @@ __global__ void k_mo_concat(DevView v) {
     const int a = st.n_surf_ds, b = st.n_outl_ds;
     for (int i = threadIdx.x; i < a; i += blockDim.x) v.cur_st[(size_t)s * v.cap_st + i] = v.cur_s_ds[(size_t)s * v.H + i];
     for (int i = threadIdx.x; i < b; i += blockDim.x)
-        v.cur_st[(size_t)s * v.cap_st + a + i] = v.cur_o_ds[(size_t)s * (v.H / 5) + i];
+        v.cur_st[(size_t)s * v.cap_st + a + i] = v.cur_o_ds[(size_t)s * v.cap_ko + i];
     if (threadIdx.x == 0) {
         st.n_st = a + b;
         st.map_ok = st.n_cmap_ds > 10 && st.n_smap_ds > 100;
@@ -428,7 +428,7 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
     const size_t ks = (size_t)s * v.KFR + slot;
     const int n3[3] = {min(st.n_corner_ds, v.cap_kc), min(st.n_surf_ds, v.cap_ks), min(st.n_outl_ds, v.cap_ko)};
     const float4* src[3] = {v.cur_c_ds + (size_t)s * v.cap_less_sharp, v.cur_s_ds + (size_t)s * v.H,
-                            v.cur_o_ds + (size_t)s * (v.H / 5)};
+                            v.cur_o_ds + (size_t)s * v.cap_ko};
     float4* dst[3] = {v.kf_corner + ks * v.cap_kc, v.kf_surf + ks * v.cap_ks, v.kf_outl + ks * v.cap_ko};
     for (int c = 0; c < 3; ++c)
         for (int i = threadIdx.x; i < n3[c]; i += blockDim.x) {
@@ -528,7 +528,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     if ((r = vg_run(ctx, "surf", v.surf_last, v.cap_less_flat, fld(&StreamState::surfLastNum), SS, v.cfg.leaf_surf,
                     v.cur_s_ds, v.H, fld(&StreamState::n_surf_ds), SS, v.H))) return r;
     if ((r = vg_run(ctx, "outlier", v.outl_cam, v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier,
-                    v.cur_o_ds, v.H / 5, fld(&StreamState::n_outl_ds), SS, v.H / 5))) return r;
+                    v.cur_o_ds, v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko))) return r;
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
     if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
                     v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;

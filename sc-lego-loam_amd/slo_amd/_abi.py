@@ -83,6 +83,14 @@ def lib():
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise RuntimeError("libslo.so not built (run __graft_entry__.build() or make -C sc-lego-loam_amd)")
+    # One HIP runtime per process: PyTorch bundles its own libamdhip64.so.7
+    # (same soname as /opt/rocm's).  Whichever is loaded first serves both, and
+    # torch cannot initialise on the system one, so load torch's first when
+    # torch is in use (bench, tests); libslo then binds to it.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     P = ctypes.c_void_p
     L.slo_config_preset.argtypes = [ctypes.c_int, ctypes.POINTER(SloConfig)]

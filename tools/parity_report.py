@@ -20,7 +20,7 @@ from parity_util import mismatch, seg_class  # noqa: E402
 
 FRONT = ["range", "ground", "seg_pts", "seg_ground", "seg_col", "seg_range", "ring_start", "ring_end", "orient",
          "outlier", "fa_seg_pts", "sharp", "flat", "corner_last", "surf_last"]
-MAPPED = ["raw_ds", "corner_ds", "surf_total_ds"]
+MAPPED = ["raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"]
 SC = ["sc_desc", "ring_key", "sector_key"]
 
 
@@ -68,7 +68,10 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 worst["map"] = max(worst["map"], row["mapped"])
                 row["mo_iters"] = [int(ctx.get(s, "mo_iters")[0]), int(ors[s].get("mo_iters")[0])]
                 for name in MAPPED:
-                    row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
+                    g, o = ctx.get(s, name), ors[s].get(name)
+                    row[name] = mismatch(g, o)
+                    if row[name] < 0:
+                        row[name + "_len"] = [len(g), len(o)]
                 kg, ko = ctx.get(s, "keyposes"), ors[s].get("keyposes")
                 row["n_kf"] = [len(kg) // 6, len(ko) // 6]
                 if len(kg) == len(ko):
