@@ -8,17 +8,19 @@ A step = one scan of every stream on this rank through the whole pipeline
 (slo_batch_process: the reference's imageProjection -> featureAssociation ->
 mapOptimization + SCManager, with the deterministic gating of SURVEY §8(d):
 mapping on every 4th scan, SC detect per saved keyframe).  Each rank owns
---streams independent streams (weak scaling); per step the ranks all-gather a
-160-byte record per stream (poses + newest SC ring key) over RCCL.
-Inputs are generated on the host and resident in HBM before timing.  Each
-stream's Scan Context history is seeded with --history earlier scans of its
-own trajectory so loop detection does its full 10-NN + 10-candidate work.
+--streams independent streams (weak scaling, slo_amd/dist.py); per step the
+ranks all-gather a 160-byte record per stream (poses + newest SC ring key)
+over RCCL.  Inputs are generated on the host and resident in HBM before
+timing.  Each stream's Scan Context history is seeded with --history earlier
+scans of its own trajectory so loop detection does its full K-NN + K
+candidate-distance work.
 
-The roofline object prices the dominant kernel (largest share of the timed
-device time, from HIP events on the context's stream in a separate
-instrumented pass) by its algorithmic bytes / average launch duration against
-HBM peak.  cpu_baseline times the oracle (the C++ restatement of the
-reference, oracle/) on this host's cores with the same workload, rank 0 only.
+roofline: the dominant kernel (largest share of device time, HIP events on the
+context's stream in a separate instrumented pass) priced by its algorithmic
+bytes (DESIGN.md "Roofline", from the per-stream counts of the last profiled
+step) / its average launch duration, against HBM peak.  cpu_baseline: the
+oracle (oracle/, C++ restatement of the reference path) on this host's cores,
+rank 0 at N = 1, a bounded sample of the same workload.
 """
 import argparse
 import json
@@ -29,9 +31,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sc-lego-loam_amd"))
 
-import numpy as np  # noqa: E402
-
-HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md); 6290 measured float4 copy
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md:36); 6290 measured float4 copy
+METRIC = "scans/sec end-to-end (proj+feat+LM+SC), 64-ring 1800-col, 1/2/4/8 GPU"
 
 
 def parse():
@@ -39,29 +40,50 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--streams", type=int, default=64, help="streams per GPU")
+    ap.add_argument("--streams", type=int, default=192, help="streams per GPU")
     ap.add_argument("--preset", default="hdl64_1800")
     ap.add_argument("--config-id", type=int, default=3)
     ap.add_argument("--history", type=int, default=60, help="seeded Scan Context history per stream")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--cpu-scans", type=int, default=48, help="scans per CPU thread in the baseline (0 = skip)")
+    ap.add_argument("--cpu-scans", type=int, default=40, help="scans per CPU thread in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
     return ap.parse_args()
 
 
-def kernel_bytes(name, st, cfg):
-    """Algorithmic HBM bytes per launch of the kernels we price (SURVEY §8(d),
-    DESIGN.md "roofline"); st = summed per-stream counts of this rank."""
+def stream_counts(ctx, S):
+    """Per-stream sizes of the last step (for algorithmic bytes)."""
+    import numpy as np
+    names = ["flat", "sharp", "surf_last", "corner_last", "seg_pts", "corner_ds", "surf_total_ds",
+             "map_corner_ds", "map_surf_ds"]
+    c = {n: np.array([ctx.get(s, n).shape[0] for s in range(S)], np.int64) for n in names}
+    c["fa_iters"] = np.array([ctx.get(s, "fa_iters") for s in range(S)], np.int64)
+    c["mo_iters"] = np.array([int(ctx.get(s, "mo_iters")[0]) for s in range(S)], np.int64)
+    return c
+
+
+def algo_bytes(name, c, cfg, S, steps, map_steps):
+    """Algorithmic HBM bytes of ALL launches of `name` in the profiled window
+    (SURVEY §8(d) per-unit figures; points are 16 B).  None = not priced."""
     H = cfg.n_scan * cfg.horizon_scan
-    S = st["streams"]
-    if name == "ip_project":    # read 16 B point, scatter 4 B owner
-        return S * cfg.max_points * 20
-    if name == "ip_image":      # owner 4 + point 16 (+2 ground pair reads on gsi rows) ; write range 4, full 16, ground 1, label 4, parent 4, csize 4, rows 16
-        return S * H * (4 + 16 + 53) + S * cfg.horizon_scan * cfg.ground_scan_ind * 2 * 20
-    if name == "fa_odometry":   # per search iteration: queries read the target clouds once (broadcast)
-        return st["odom_bytes"]
-    if name == "mo_corr":       # per LM iteration: query 16 B + 27-cell candidate reads + 5 neighbours
-        return st["mocorr_bytes"]
+    P = cfg.max_points
+    if name == "ip_project":      # read the point, scatter a 4 B owner
+        return steps * S * P * (16 + 4)
+    if name == "ip_image":        # owner + point in; range, full cloud, ground, label, CC init out
+        return steps * S * H * (4 + 16 + 4 + 16 + 1 + 4 + 8)
+    if name == "fa_extract":      # curvature, smoothness, picked, label, points per segmented point
+        return steps * int(c["seg_pts"].sum()) * (4 + 8 + 4 + 4 + 16)
+    srch = lambda it: (it + 4) // 5  # noqa: E731  search iterations actually run
+    if name == "fa_search_surf":  # per search: queries + 3 indices, the target cloud once
+        return steps * int((srch(c["fa_iters"][:, 0]) * (c["flat"] * 28 + c["surf_last"] * 16)).sum())
+    if name == "fa_search_corner":
+        return steps * int((srch(c["fa_iters"][:, 1]) * (c["sharp"] * 24 + c["corner_last"] * 16)).sum())
+    if name == "fa_iter_surf":    # per iteration: query + 3 indices + 3 matched points
+        return steps * int((c["fa_iters"][:, 0] * c["flat"] * (16 + 12 + 48)).sum())
+    if name == "fa_iter_corner":
+        return steps * int((c["fa_iters"][:, 1] * c["sharp"] * (16 + 8 + 32)).sum())
+    if name == "mo_corr":         # per iteration: query + 5 neighbours (96 B, SURVEY §8(d)) + the maps once
+        per = (c["corner_ds"] + c["surf_total_ds"]) * 96 + (c["map_corner_ds"] + c["map_surf_ds"]) * 16
+        return map_steps * int((c["mo_iters"] * per).sum())
     return None
 
 
@@ -70,8 +92,8 @@ def main():
     import torch
     import torch.distributed as dist
     import slo_amd
-
     from slo_amd import dist as sdist
+
     rank, world, local = sdist.env_rank()
     torch.cuda.set_device(local)
     if world > 1:
@@ -90,9 +112,10 @@ def main():
     # ---- inputs (host generation, then resident in HBM)
     t_gen = time.time()
     stream0, _ = sdist.stream_shard(rank, world, S)
-    host = slo_amd.gen_batch(pid, a.config_id, stream0, S, 0, ntot, P, gthreads)
-    dev = torch.from_numpy(host).to(f"cuda:{local}")
-    del host
+    dev = torch.empty((ntot, S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+    for k0 in range(0, ntot, 4):
+        nk = min(4, ntot - k0)
+        dev[k0:k0 + nk].copy_(torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, k0, nk, P, gthreads)))
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
 
     ctx = slo_amd.Context(cfg, local, S)
@@ -102,14 +125,12 @@ def main():
     ext = torch.cuda.ExternalStream(ctx.stream_handle)
 
     # seed Scan Context history (makeAndSaveScancontextAndKeys) in chunks
-    chunk = 8
-    for h0 in range(-a.history, 0, chunk):
-        nh = min(chunk, -h0)
-        hist = slo_amd.gen_batch(pid, a.config_id, stream0, S, h0, nh, P, gthreads)
+    for h0 in range(-a.history, 0, 4):
+        nh = min(4, -h0)
+        hist = torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, h0, nh, P, gthreads)).cuda(local)
         for h in range(nh):
-            d = torch.from_numpy(hist[h]).to(f"cuda:{local}")
-            ctx.batch_sc_make(d.data_ptr(), cnt.data_ptr())
-            ctx.synchronize()
+            ctx.batch_sc_make(hist[h].data_ptr(), cnt.data_ptr())
+        ctx.synchronize()
         del hist
     t_gen = time.time() - t_gen
 
@@ -133,57 +154,34 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    el = time.perf_counter() - t0
-    el = sdist.max_over_ranks(el, f"cuda:{local}")
-    scans = S * a.steps * world
-    value = scans / el
+    el = sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
+    value = S * a.steps * world / el
+    errs = sum(int(ctx.get(s, "err")[0]) != 0 for s in range(S))
 
     # ---- instrumented pass: per-kernel HIP-event times on the context stream
-    roof = None
-    kt = {}
+    roof, kt = None, {}
     if a.profile_steps > 0:
         ctx.timing(True)
         ctx.timing_reset()
         k0 = a.warmup + a.steps
-        st_counts = {"streams": S, "odom_bytes": 0, "mocorr_bytes": 0}
+        map_steps = 0
         for k in range(k0, k0 + a.profile_steps):
             step(k)
-        ctx.synchronize()
+            ctx.synchronize()
+            map_steps += int(int(ctx.get(0, "flags")[0]) & 2 != 0)
         kt = ctx.timing_read()
         ctx.timing(False)
-        # algorithmic bytes for the odometry sweep and mapping correspondences
-        ns = [ctx.get(s, "surf_last").shape[0] for s in range(S)]
-        nc = [ctx.get(s, "corner_last").shape[0] for s in range(S)]
-        nf = [ctx.get(s, "flat").shape[0] for s in range(S)]
-        nsh = [ctx.get(s, "sharp").shape[0] for s in range(S)]
-        it = [ctx.get(s, "fa_iters") for s in range(S)]
-        # per launch: every search iteration (iter % 5 == 0) of each wave sweeps
-        # the whole target cloud once (16 B/pt, broadcast) ; the other
-        # iterations read queries + 2-3 neighbours (16 B each)
-        ob = 0
-        for s in range(S):
-            srch_s = (int(it[s][0]) + 4) // 5
-            srch_c = (int(it[s][1]) + 4) // 5
-            waves_s = max(1, (nf[s] + 63) // 64)
-            waves_c = max(1, (nsh[s] + 63) // 64)
-            ob += srch_s * waves_s * ns[s] * 16 + srch_c * waves_c * nc[s] * 16
-            ob += int(it[s][0]) * nf[s] * 64 + int(it[s][1]) * nsh[s] * 48
-        st_counts["odom_bytes"] = ob
+        counts = stream_counts(ctx, S)
         total_ms = sum(v[0] for v in kt.values())
-        dom = max(kt.items(), key=lambda kv: kv[1][0]) if kt else None
-        if dom:
-            name, (ms, n) = dom
-            avg_s = ms / 1e3 / max(1, n)
-            b = kernel_bytes(name, st_counts, cfg)
-            if b is not None and avg_s > 0:
-                ach = b / avg_s / 1e9
-                roof = {"bound": "hbm", "achieved": round(ach, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 5), "traffic": None, "kernel": name,
-                        "avg_launch_us": round(avg_s * 1e6, 2), "share_of_device_time": round(ms / total_ms, 4)}
-            else:
-                roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                        "traffic": None, "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
-                        "share_of_device_time": round(ms / total_ms, 4)}
+        name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
+        avg_s = ms / 1e3 / max(1, n)
+        b = algo_bytes(name, counts, cfg, S, a.profile_steps, map_steps)
+        ach = b / n / avg_s / 1e9 if b is not None else None
+        roof = {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
+                "traffic": None, "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
+                "bytes_per_launch": int(b / n) if b is not None else None,
+                "share_of_device_time": round(ms / total_ms, 4)}
 
     # ---- CPU baseline (oracle = C++ restatement of the reference), rank 0, N = 1
     cpu = None
@@ -194,27 +192,28 @@ def main():
         th = a.cpu_threads or max(1, min(16, ncpu))
         stage = (ctypes.c_double * 4)()
         secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, 4, a.history, stage)
+        per_stream = a.cpu_scans / (sum(stage) / th)
         cpu = {"value": round(th * a.cpu_scans / secs, 3), "unit": "scans/s", "cores": th, "kind": "port",
                "sample": f"{th} independent {a.preset} streams x {a.cpu_scans} scans (after 4 warm-up scans, "
-                         f"{a.history}-entry SC history), oracle/ C++ restatement -O2, one stream per thread",
-               "seconds": round(secs, 2),
+                         f"{a.history}-entry SC history), oracle/ C++ restatement g++ -O2, one stream per thread",
+               "seconds": round(secs, 2), "one_stream_scans_per_s": round(per_stream, 3),
                "stage_seconds": {"ip": round(stage[0], 2), "fa": round(stage[1], 2), "mo": round(stage[2], 2),
                                  "sc": round(stage[3], 2)}}
 
     if rank == 0:
         out = {
-            "metric": "scans/sec end-to-end (proj+feat+LM+SC), 64-ring 1800-col",
-            "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-            "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+            "metric": METRIC, "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10",
                        "preset": a.preset, "streams_per_gpu": S, "scans_per_step": S * world,
                        "sc_history_seed": a.history, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
+            "stream_errors": errs,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
-            "gen_seconds": round(t_gen, 1),
+            "setup_seconds": round(t_gen, 1),
         }
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -196,15 +196,21 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         return SLO_E_HIP;
     }
     memset(ctx->h_st, 0, sizeof(StreamState) * S);
-    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc) ||
-        slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms) ||
-        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 13, v.cap_less_sharp) ||
-        slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat)) {
+    // Grid cells (powers of two, GridView): the map grids answer 5-NN within
+    // 1 m (MO:1281/1364) in 0.5 m cells (rings <= 2, usually done after 1);
+    // the odometry grids answer 1-NN within 5 m (nearestFeatureSearchSqDist):
+    // 1 m cells.
+    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
+        slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms, 0.5f) ||
+        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 13, v.cap_less_sharp, 1.0f) ||
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat, 1.0f)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
-    v.Toc = ctx->grid_oc.T; v.goc_cnt = ctx->grid_oc.cnt; v.goc_off = ctx->grid_oc.off; v.goc_ent = ctx->grid_oc.ent;
-    v.Tos = ctx->grid_os.T; v.gos_cnt = ctx->grid_os.cnt; v.gos_off = ctx->grid_os.off; v.gos_ent = ctx->grid_os.ent;
+    v.g_oc = slo::grid_view(ctx->grid_oc);
+    v.g_os = slo::grid_view(ctx->grid_os);
+    v.g_mc = slo::grid_view(ctx->grid_c);
+    v.g_ms = slo::grid_view(ctx->grid_s);
     *out = ctx;
     return SLO_OK;
 }

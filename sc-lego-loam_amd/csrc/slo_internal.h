@@ -41,6 +41,7 @@ struct StreamState {
     int32_t kdCornerNum, kdSurfNum;       // size of the cloud the "tree" was last built on
     int32_t iters_surf, iters_corner;
     int32_t first_half;                   // deskew: first index with halfPassed
+    int32_t odo_phase;                    // odometry control between launches (slo_odom.hip)
     int32_t seg_count, outlier_count;
     int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
     // mapping
@@ -64,6 +65,20 @@ struct StreamState {
     double det_min_dist;
     int32_t flags;
     int32_t err;
+};
+
+// Spatial hash grid over one [S][es] cloud (built by grid_build): cell edge
+// `cell` is a power of two, so floor(x * inv) is floor(x / cell) exactly and
+// "a point in a cell r rings away is more than (r-1)*cell away" holds in float
+// arithmetic too — the searches rely on it to stop early and stay exact.
+// Bucket b of stream s holds ent[s*es + off[s*T+b] - off[s*T] .. + cnt[s*T+b]],
+// each entry (x, y, z, point index as int bits).
+struct GridView {
+    int T;
+    float inv, cell;
+    size_t es;
+    const int32_t *cnt, *off;
+    const float4* ent;
 };
 
 // kernel-visible view of the context (passed by value)
@@ -142,14 +157,8 @@ struct DevView {
     float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
     float4* cur_st_ds;   // [S][cap_st]
     double* mo_part;     // [S][MO_BLOCKS][SLO_MO_PART] partial A^T A / A^T b (double-double) + count
-    // hash grids over the odometry "kd-tree" clouds (1 m cells)
-    int Toc, Tos;
-    const int32_t *goc_cnt, *goc_off, *gos_cnt, *gos_off;
-    const float4 *goc_ent, *gos_ent;
-    // hash grids over the DS maps (1 m cells)
-    int Tc, Ts;
-    const int32_t *gc_cnt, *gc_off, *gs_cnt, *gs_off;
-    const float4 *gc_ent, *gs_ent;
+    // hash grids: odometry "kd-tree" clouds (corner / surf) and the DS maps
+    GridView g_oc, g_os, g_mc, g_ms;
     // ---- Scan Context history (Scancontext.h:99-106)
     double* sc_desc;     // [S][KFMAX][NR*NS]
     float* sc_ring;      // [S][KFMAX][NR]   invkeys (float, tree data)
@@ -173,6 +182,35 @@ __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
     return (((unsigned int)x * 73856093u) ^ ((unsigned int)y * 19349663u) ^ ((unsigned int)z * 83492791u)) &
            (unsigned int)(T - 1);
 }
+__host__ __device__ inline int grid_cell(float x, float inv) { return (int)floorf(x * inv); }
+
+// Visit every grid point of stream s in the cells at Chebyshev ring r around
+// cell (cx, cy, cz): f(point) for points of exactly those cells (buckets are
+// shared by hash collisions, so membership is re-checked).
+template <class F>
+__device__ inline void grid_ring(const GridView& g, int s, int cx, int cy, int cz, int r, F&& f) {
+    const size_t gb = (size_t)s * g.T;
+    const int base = g.off[gb];
+    const float4* E = g.ent + (size_t)s * g.es;
+    for (int dz = -r; dz <= r; ++dz)
+        for (int dy = -r; dy <= r; ++dy) {
+            const bool edge = (dz == -r || dz == r || dy == -r || dy == r);
+            const int step = (edge || r == 0) ? 1 : 2 * r;
+            for (int dx = -r; dx <= r; dx += step) {
+                const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
+                const unsigned int b = grid_hash(tx, ty, tz, g.T);
+                const int m = g.cnt[gb + b];
+                if (m == 0) continue;
+                const float4* e = E + (g.off[gb + b] - base);
+                for (int k = 0; k < m; ++k) {
+                    const float4 p = e[k];
+                    if (grid_cell(p.x, g.inv) != tx || grid_cell(p.y, g.inv) != ty || grid_cell(p.z, g.inv) != tz)
+                        continue;
+                    f(p);
+                }
+            }
+        }
+}
 
 struct VgParams;
 struct MapWs {  // VoxelGrid workspace
@@ -190,6 +228,7 @@ struct MapWs {  // VoxelGrid workspace
 };
 struct HashGrid {
     int T = 0;
+    float cell = 1.0f;
     size_t ent_stride = 0;
     int32_t *cnt = nullptr, *cur = nullptr, *off = nullptr;
     float4* ent = nullptr;
@@ -243,7 +282,8 @@ int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);
-int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride);
+int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell);
+GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts);

@@ -124,32 +124,30 @@ __device__ inline float sqd(const P4& q, float x, float y, float z) {
     return r;
 }
 
-__device__ inline int knn5(const float4* ent, const int32_t* off, const int32_t* cnt, int T, int s, size_t ent_stride,
-                           const P4& q, int* oi, float* od) {
-    const int cx = (int)floorf(q.x), cy = (int)floorf(q.y), cz = (int)floorf(q.z);
-    const int base = off[(size_t)s * T];
+// Exact 5-NN (sorted by (distance, index)) among the map points within 1 m —
+// the only ones the reference accepts (pointSearchSqDis[4] < 1.0, MO:1281 /
+// 1364).  Rings of cells grow outward; after ring r every unseen point is at
+// least r*cell away, so the search stops as soon as the 5th distance is below
+// (r*cell)^2, and it never needs rings beyond ceil(1 m / cell).
+__device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float* od) {
+    const int cx = grid_cell(q.x, g.inv), cy = grid_cell(q.y, g.inv), cz = grid_cell(q.z, g.inv);
+    const int rmax = (int)ceilf(g.inv);
     int n = 0;
-    for (int dz = -1; dz <= 1; ++dz)
-        for (int dy = -1; dy <= 1; ++dy)
-            for (int dx = -1; dx <= 1; ++dx) {
-                const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
-                const unsigned int b = grid_hash(tx, ty, tz, T);
-                const int st = off[(size_t)s * T + b] - base, m = cnt[(size_t)s * T + b];
-                const float4* e = ent + (size_t)s * ent_stride + st;
-                for (int k = 0; k < m; ++k) {
-                    float4 p = e[k];
-                    if ((int)floorf(p.x) != tx || (int)floorf(p.y) != ty || (int)floorf(p.z) != tz) continue;
-                    const float d = sqd(q, p.x, p.y, p.z);
-                    const int idx = __float_as_int(p.w);
-                    if (n == 5 && (d > od[4] || (d == od[4] && idx > oi[4]))) continue;
-                    int pos = n < 5 ? n : 4;
-                    while (pos > 0 && (od[pos - 1] > d || (od[pos - 1] == d && oi[pos - 1] > idx))) {
-                        od[pos] = od[pos - 1]; oi[pos] = oi[pos - 1]; --pos;
-                    }
-                    od[pos] = d; oi[pos] = idx;
-                    if (n < 5) ++n;
-                }
+    for (int r = 0; r <= rmax; ++r) {
+        grid_ring(g, s, cx, cy, cz, r, [&](const float4& p) {
+            const float d = sqd(q, p.x, p.y, p.z);
+            const int idx = __float_as_int(p.w);
+            if (n == 5 && (d > od[4] || (d == od[4] && idx > oi[4]))) return;
+            int pos = n < 5 ? n : 4;
+            while (pos > 0 && (od[pos - 1] > d || (od[pos - 1] == d && oi[pos - 1] > idx))) {
+                od[pos] = od[pos - 1]; oi[pos] = oi[pos - 1]; --pos;
             }
+            od[pos] = d; oi[pos] = idx;
+            if (n < 5) ++n;
+        });
+        const float reach = (float)r * g.cell;
+        if (r >= 1 && n == 5 && od[4] < reach * reach) break;
+    }
     return n;
 }
 
@@ -181,8 +179,7 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
             float x2 = x1, y2 = cRoll * y1 - sRoll * z1, z2 = sRoll * y1 + cRoll * z1;
             P4 sel{cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, po.w};
             int ind[5]; float dis[5];
-            int n = corner ? knn5(v.gc_ent, v.gc_off, v.gc_cnt, v.Tc, s, v.cap_mc, sel, ind, dis)
-                           : knn5(v.gs_ent, v.gs_off, v.gs_cnt, v.Ts, s, v.cap_ms, sel, ind, dis);
+            int n = corner ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
             if (n < 5 || !(dis[4] < 1.0)) continue;
             float cfx, cfy, cfz, cfw;
             bool ok = false;
@@ -535,8 +532,6 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     // hash grids over the DS maps
     if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
     if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
-    v.Tc = ctx->grid_c.T; v.gc_cnt = ctx->grid_c.cnt; v.gc_off = ctx->grid_c.off; v.gc_ent = ctx->grid_c.ent;
-    v.Ts = ctx->grid_s.T; v.gs_cnt = ctx->grid_s.cnt; v.gs_off = ctx->grid_s.off; v.gs_ent = ctx->grid_s.ent;
     for (int it = 0; it < 10; ++it) {
         SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(SLO_MO_BLOCKS, S), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_solve", k_mo_solve, dim3(S), dim3(64), 0, v, it);

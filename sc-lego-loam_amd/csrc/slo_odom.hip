@@ -4,16 +4,15 @@
 // (FA:1270-1478), integrateTransformation (FA:1697-1725) and
 // publishCloudsLast (FA:1759-1788) / checkSystemInitialization (FA:1605-1637).
 //
-// One 256-thread workgroup owns one stream for the whole <=25+25 iteration
-// loop (the iterations are sequential; the streams are independent), so no
-// host round trip happens per iteration.  Per iteration every lane
-// transforms its queries, (every 5th iteration) finds the exact nearest
-// neighbour in a 1 m hash grid over the "kd-tree" cloud (rebuilt after every
-// scan by fa_odometry_run, like setInputCloud), walks the ring-ordered target
-// cloud for the 2nd/3rd points exactly as the reference (including Q7's
-// bound), and accumulates its rows of A^T A / A^T b in double-double
+// The correspondence searches (every 5th iteration) run one thread per query
+// across the whole chip: exact nearest neighbour in a hash grid over the
+// "kd-tree" cloud (rebuilt after every scan by fa_odometry_run, like
+// setInputCloud), then the ring-ordered walk for the 2nd/3rd points exactly as
+// the reference (including Q7's bound).  The iterations run one workgroup per
+// stream: every lane accumulates its rows of A^T A / A^T b in double-double
 // (slo_ddsum.h); a wave-shuffle + LDS tree reduces them and lane 0 rounds once
-// to float and runs the 3x3 QR / Jacobi / degeneracy projection.
+// to float and runs the 3x3 QR / Jacobi / degeneracy projection.  No host
+// round trip happens per iteration (launch structure below).
 // Nearest-neighbour ties resolve to the lowest index (FLANN's tie order is
 // traversal dependent).
 #include "slo_internal.h"
@@ -40,39 +39,26 @@ __device__ inline float sqdist_flann(const P4& q, const float4& p) {  // ((0+d0^
     return r;
 }
 
-// exact 1-NN in the 1 m hash grid of the "tree" cloud: shells of cells at
-// Chebyshev distance r = 0,1,..; every point outside shells <= r is more than
-// r metres away, so once the best float distance is < r^2 nothing unseen can
-// beat or tie it (fl(d) is monotone in the exact distance).  r stops at
-// rmax = ceil(sqrt(nearestFeatureSearchSqDist)): anything further fails the
-// gate anyway, as it would after the reference's exact FLANN search.
+// Exact 1-NN in the hash grid of the "tree" cloud: rings of cells at
+// Chebyshev distance r = 0,1,..; every point outside rings <= r is more than
+// r*cell away, so once the best float distance is < (r*cell)^2 nothing unseen
+// can beat or tie it (fl(d) is monotone in the exact distance, GridView).  The
+// rings stop where the nearestFeatureSearchSqDist gate lies: anything further
+// fails it anyway, as it would after the reference's exact FLANN search.
 // Ties -> lowest index.
-__device__ inline void nn1_grid(const float4* ent, const int32_t* off, const int32_t* cnt, int T, int s,
-                                size_t es, int rmax, const P4& q, int& bi, float& bd) {
+__device__ inline void nn1_grid(const GridView& g, int s, float gate, const P4& q, int& bi, float& bd) {
     bi = -1; bd = FLT_MAX;
     if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return;
-    const int cx = (int)floorf(q.x), cy = (int)floorf(q.y), cz = (int)floorf(q.z);
-    const int base = off[(size_t)s * T];
-    const float4* E = ent + (size_t)s * es;
+    const int cx = grid_cell(q.x, g.inv), cy = grid_cell(q.y, g.inv), cz = grid_cell(q.z, g.inv);
+    const int rmax = (int)ceilf(sqrtf(gate) * g.inv);
     for (int r = 0; r <= rmax; ++r) {
-        for (int dz = -r; dz <= r; ++dz)
-            for (int dy = -r; dy <= r; ++dy) {
-                const bool edge = (dz == -r || dz == r || dy == -r || dy == r);
-                for (int dx = -r; dx <= r; dx += (edge ? 1 : 2 * r > 0 ? 2 * r : 1)) {
-                    const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
-                    const unsigned int b = grid_hash(tx, ty, tz, T);
-                    const int st = off[(size_t)s * T + b] - base, m = cnt[(size_t)s * T + b];
-                    for (int k = 0; k < m; ++k) {
-                        const float4 p = E[st + k];
-                        if ((int)floorf(p.x) != tx || (int)floorf(p.y) != ty || (int)floorf(p.z) != tz) continue;
-                        const float d = sqdist_flann(q, p);
-                        const int idx = __float_as_int(p.w);
-                        if (d < bd || (d == bd && idx < bi)) { bd = d; bi = idx; }
-                    }
-                    if (r == 0) break;
-                }
-            }
-        if (r >= 1 && bd < (float)(r * r)) break;
+        grid_ring(g, s, cx, cy, cz, r, [&](const float4& p) {
+            const float d = sqdist_flann(q, p);
+            const int idx = __float_as_int(p.w);
+            if (d < bd || (d == bd && idx < bi)) { bd = d; bi = idx; }
+        });
+        const float reach = (float)r * g.cell;
+        if (r >= 1 && bd < reach * reach) break;
     }
 }
 
@@ -139,253 +125,288 @@ __device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int it
     return true;
 }
 
-__global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) {
+// ---------------------------------------------------------------- launch structure
+// The 25 + 25 Gauss-Newton iterations of a stream are sequential, the streams
+// independent.  Each phase (surf, then corner) runs as 5 rounds of
+//   k_fa_search<PH>  one thread per query, S x ceil(cap/256) workgroups: the
+//                    correspondence search of iteration 5b (findCorresponding*
+//                    runs when iterCount % 5 == 0, FA:1157 / 1046) — the
+//                    expensive part, spread over the whole chip;
+//   k_fa_iter<PH>    one workgroup per stream: iterations 5b .. 5b+4 (residuals,
+//                    double-double normal equations, lane-0 solve, convergence).
+// StreamState::odo_phase carries the control flow between launches:
+// 0 = surf running, 1 = corner running, 2 = solved (or skipped), 3 = init scan.
+
+__global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
     const int tid = threadIdx.x, T = blockDim.x;
-    const float4* sharp = v.sharp + (size_t)s * v.cap_sharp;
-    const float4* flat = v.flat + (size_t)s * v.cap_flat;
-    const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
-    const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
-    float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
-    float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
-    float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
-    float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
     const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
-
-    if (first_scan) {  // checkSystemInitialization: swap, build trees, no odometry
+    if (first_scan) {  // checkSystemInitialization (FA:1605-1637): swap, build trees, no odometry
+        const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
+        const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
+        float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
+        float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
+        float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
+        float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
         for (int i = tid; i < nLS; i += T) { cnext[i] = lsharp[i]; kdc[i] = lsharp[i]; }
         for (int i = tid; i < nLF; i += T) { snext[i] = lflat[i]; kds[i] = lflat[i]; }
         if (tid == 0) {
             st.cornerLastNum = nLS; st.surfLastNum = nLF;
             st.kdCornerNum = nLS; st.kdSurfNum = nLF;
             st.iters_surf = st.iters_corner = 0;
+            st.odo_phase = 3;
         }
         return;
     }
+    if (tid == 0) {  // updateTransformation (FA:1666-1672)
+        st.iters_surf = st.iters_corner = 0;
+        st.odo_phase = (st.cornerLastNum < 10 || st.surfLastNum < 100) ? 2 : 0;
+    }
+}
 
+// findCorrespondingSurfFeatures (FA:1155-1268) / ...CornerFeatures
+// (FA:1044-1153) for one query: exact 1-NN in the tree cloud, then the
+// ring-ordered walk for the 2nd (and 3rd) points within +-2.5 rings.
+template <int PH>
+__global__ void __launch_bounds__(256) k_fa_search(DevView v) {
+    const int s = blockIdx.y;
+    const StreamState& st = v.st[s];
+    if (st.odo_phase != PH) return;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int nq = PH == 0 ? st.n_flat : st.n_sharp;
+    if (i >= nq) return;
+    const float gate = v.cfg.nearest_feature_search_sq_dist;
+    float tc[6];
+    for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    if (PH == 0) {
+        const float4* flat = v.flat + (size_t)s * v.cap_flat;
+        const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
+        const int surfLastNum = st.surfLastNum;
+        const P4 sel = slo_pose::transform_to_start(ld4(flat, i), tc);
+        int ci; float cd;
+        nn1_grid(v.g_os, s, gate, sel, ci, cd);
+        int closest = -1, i2 = -1, i3 = -1;
+        if (cd < gate && ci >= 0 && ci < surfLastNum) {
+            closest = ci;
+            const int cscan = (int)slast[closest].w;
+            float m2 = gate, m3 = gate;
+            for (int j = closest + 1; j < nq && j < surfLastNum; j++) {   // Q7: bounded by the flat count
+                const float4 t = slast[j];
+                if ((int)t.w > cscan + 2.5) break;
+                const float d = sq3_ref(t, sel);
+                if ((int)t.w <= cscan) { if (d < m2) { m2 = d; i2 = j; } }
+                else { if (d < m3) { m3 = d; i3 = j; } }
+            }
+            for (int j = closest - 1; j >= 0; j--) {
+                const float4 t = slast[j];
+                if ((int)t.w < cscan - 2.5) break;
+                const float d = sq3_ref(t, sel);
+                if ((int)t.w >= cscan) { if (d < m2) { m2 = d; i2 = j; } }
+                else { if (d < m3) { m3 = d; i3 = j; } }
+            }
+        }
+        int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
+        ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
+    } else {
+        const float4* sharp = v.sharp + (size_t)s * v.cap_sharp;
+        const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
+        const int cornerLastNum = st.cornerLastNum;
+        const P4 sel = slo_pose::transform_to_start(ld4(sharp, i), tc);
+        int ci; float cd;
+        nn1_grid(v.g_oc, s, gate, sel, ci, cd);
+        int closest = -1, i2 = -1;
+        if (cd < gate && ci >= 0 && ci < cornerLastNum) {
+            closest = ci;
+            const int cscan = (int)clast[closest].w;
+            float m2 = gate;
+            for (int j = closest + 1; j < nq && j < cornerLastNum; j++) {  // Q7: bounded by the sharp count
+                const float4 t = clast[j];
+                if ((int)t.w > cscan + 2.5) break;
+                const float d = sq3_ref(t, sel);
+                if ((int)t.w > cscan) { if (d < m2) { m2 = d; i2 = j; } }
+            }
+            for (int j = closest - 1; j >= 0; j--) {
+                const float4 t = clast[j];
+                if ((int)t.w < cscan - 2.5) break;
+                const float d = sq3_ref(t, sel);
+                if ((int)t.w < cscan) { if (d < m2) { m2 = d; i2 = j; } }
+            }
+        }
+        int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
+        indc[2 * i] = closest; indc[2 * i + 1] = i2;
+    }
+}
+
+// iterations iter0 .. iter0+4 of calculateTransformationSurf (FA:1270-1377)
+// or ...Corner (FA:1379-1478) for one stream
+template <int PH>
+__global__ void __launch_bounds__(256) k_fa_iter(DevView v, int iter0) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    if (st.odo_phase != PH) return;
+    const int tid = threadIdx.x, T = blockDim.x;
     __shared__ float tc[6];
     __shared__ int s_ctl;      // 0 = go on, 1 = skip solve (continue), 2 = break
     __shared__ slo_dd::DD sh[4 * 9];
     __shared__ int shi[4];
-    if (tid == 0) for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    if (tid < 6) tc[tid] = st.transformCur[tid];
+    if (tid == 0) s_ctl = 0;
     __syncthreads();
-    const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
-    const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
-    const int cornerLastNum = st.cornerLastNum, surfLastNum = st.surfLastNum;
-    const float gate = v.cfg.nearest_feature_search_sq_dist;
-    const int rmax = (int)ceilf(sqrtf(gate));
-    int iters_surf = 0, iters_corner = 0;
-
-    if (!(cornerLastNum < 10 || surfLastNum < 100)) {
-        // ------------------------------------------------ surf phase
-        const int nq = st.n_flat;
-        int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
-        for (int iterCount = 0; iterCount < 25; iterCount++) {
-            slo_dd::DD acc[9];
-            for (int k = 0; k < 9; ++k) acc[k] = slo_dd::zero();
-            int cnt = 0;
-            float srx = slo_libm::sinf_(tc[0]), crx = slo_libm::cosf_(tc[0]);
-            float sry = slo_libm::sinf_(tc[1]), cry = slo_libm::cosf_(tc[1]);
-            float srz = slo_libm::sinf_(tc[2]), crz = slo_libm::cosf_(tc[2]);
-            float tx = tc[3], ty = tc[4], tz = tc[5];
-            float a1 = crx * sry * srz; float a2 = crx * crz * sry; float a3 = srx * sry; float a4 = tx * a1 - ty * a2 - tz * a3;
-            float a5 = srx * srz; float a6 = crz * srx; float a7 = ty * a6 - tz * crx - tx * a5;
-            float a8 = crx * cry * srz; float a9 = crx * cry * crz; float a10 = cry * srx; float a11 = tz * a10 + ty * a9 - tx * a8;
-            float b1 = -crz * sry - cry * srx * srz; float b2 = cry * crz * srx - sry * srz;
-            float b5 = cry * crz - srx * sry * srz; float b6 = cry * srz + crz * srx * sry;
-            float c1 = -b6; float c2 = b5; float c3 = tx * b6 - ty * b5; float c4 = -crx * crz; float c5 = crx * srz; float c6 = ty * c5 + tx * -c4;
-            float c7 = b2; float c8 = -b1; float c9 = tx * -b2 - ty * -b1;
-            const int rounds = (nq + T - 1) / T;
-            for (int rd = 0; rd < rounds; ++rd) {
-                const int i = rd * T + tid;
-                const bool active = i < nq;
-                P4 po = active ? ld4(flat, i) : P4{0, 0, 0, 0};
-                P4 sel = slo_pose::transform_to_start(po, tc);
-                if (iterCount % 5 == 0) {
-                    int ci; float cd;
-                    nn1_grid(v.gos_ent, v.gos_off, v.gos_cnt, v.Tos, s, v.cap_less_flat, rmax, sel, ci, cd);
-                    int closest = -1, i2 = -1, i3 = -1;
-                    if (active && cd < gate && ci >= 0 && ci < surfLastNum) {
-                        closest = ci;
-                        int cscan = (int)slast[closest].w;
-                        float m2 = gate, m3 = gate;
-                        for (int j = closest + 1; j < nq && j < surfLastNum; j++) {
-                            if ((int)slast[j].w > cscan + 2.5) break;
-                            float d = sq3_ref(slast[j], sel);
-                            if ((int)slast[j].w <= cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                            else { if (d < m3) { m3 = d; i3 = j; } }
-                        }
-                        for (int j = closest - 1; j >= 0; j--) {
-                            if ((int)slast[j].w < cscan - 2.5) break;
-                            float d = sq3_ref(slast[j], sel);
-                            if ((int)slast[j].w >= cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                            else { if (d < m3) { m3 = d; i3 = j; } }
-                        }
-                    }
-                    if (active) { ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3; }
-                }
-                if (!active) continue;
+    const int nq = PH == 0 ? st.n_flat : st.n_sharp;
+    const float4* qp = PH == 0 ? v.flat + (size_t)s * v.cap_flat : v.sharp + (size_t)s * v.cap_sharp;
+    const float4* last = PH == 0 ? v.surf_last + (size_t)s * v.cap_less_flat
+                                 : v.corner_last + (size_t)s * v.cap_less_sharp;
+    const int32_t* ind = PH == 0 ? v.ind_surf + (size_t)s * v.cap_flat * 3 : v.ind_corner + (size_t)s * v.cap_sharp * 2;
+    int iterCount = iter0;
+    for (; iterCount < iter0 + 5; iterCount++) {
+        slo_dd::DD acc[9];
+        for (int k = 0; k < 9; ++k) acc[k] = slo_dd::zero();
+        int cnt = 0;
+        const float srx = slo_libm::sinf_(tc[0]), crx = slo_libm::cosf_(tc[0]);
+        const float sry = slo_libm::sinf_(tc[1]), cry = slo_libm::cosf_(tc[1]);
+        const float srz = slo_libm::sinf_(tc[2]), crz = slo_libm::cosf_(tc[2]);
+        const float tx = tc[3], ty = tc[4], tz = tc[5];
+        for (int i = tid; i < nq; i += T) {
+            const P4 po = ld4(qp, i);
+            const P4 sel = slo_pose::transform_to_start(po, tc);
+            const P4& p = po;
+            if (PH == 0) {
                 const int j1 = ind[3 * i], j2 = ind[3 * i + 1], j3 = ind[3 * i + 2];
-                if (j2 >= 0 && j3 >= 0) {
-                    float4 t1 = slast[j1], t2 = slast[j2], t3 = slast[j3];
-                    float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
-                    float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
-                    float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
-                    float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
-                    float ps = sqrtf(pa * pa + pb * pb + pc * pc);
-                    pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-                    float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-                    float sw = 1;
-                    if (iterCount >= 5)
-                        sw = (float)(1 - 1.8 * fabsf(pd2) / sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
-                    if (sw > 0.1 && pd2 != 0) {
-                        float cx = sw * pa, cy = sw * pb, cz = sw * pc, cw = sw * pd2;
-                        const P4& p = po;
-                        float arx = (-a1 * p.x + a2 * p.y + a3 * p.z + a4) * cx + (a5 * p.x - a6 * p.y + crx * p.z + a7) * cy +
-                                    (a8 * p.x - a9 * p.y - a10 * p.z + a11) * cz;
-                        float arz = (c1 * p.x + c2 * p.y + c3) * cx + (c4 * p.x - c5 * p.y + c6) * cy + (c7 * p.x + c8 * p.y + c9) * cz;
-                        float aty = -b6 * cx + c4 * cy + b2 * cz;
-                        float bb = (float)(-0.05 * cw);
-                        double A0 = arx, A1 = arz, A2 = aty, B = bb;
-                        accumulate9(acc, A0, A1, A2, B);
-                        cnt++;
-                    }
-                }
+                if (!(j2 >= 0 && j3 >= 0)) continue;
+                const float4 t1 = last[j1], t2 = last[j2], t3 = last[j3];
+                float pa = (t2.y - t1.y) * (t3.z - t1.z) - (t3.y - t1.y) * (t2.z - t1.z);
+                float pb = (t2.z - t1.z) * (t3.x - t1.x) - (t3.z - t1.z) * (t2.x - t1.x);
+                float pc = (t2.x - t1.x) * (t3.y - t1.y) - (t3.x - t1.x) * (t2.y - t1.y);
+                float pd = -(pa * t1.x + pb * t1.y + pc * t1.z);
+                const float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+                pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+                const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+                float sw = 1;
+                if (iterCount >= 5)
+                    sw = (float)(1 - 1.8 * fabsf(pd2) / sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+                if (!(sw > 0.1 && pd2 != 0)) continue;
+                const float cx = sw * pa, cy = sw * pb, cz = sw * pc, cw = sw * pd2;
+                // calculateTransformationSurf (FA:1282-1318): rows d/d(rx, rz, ty)
+                const float a1 = crx * sry * srz; const float a2 = crx * crz * sry; const float a3 = srx * sry;
+                const float a4 = tx * a1 - ty * a2 - tz * a3;
+                const float a5 = srx * srz; const float a6 = crz * srx; const float a7 = ty * a6 - tz * crx - tx * a5;
+                const float a8 = crx * cry * srz; const float a9 = crx * cry * crz; const float a10 = cry * srx;
+                const float a11 = tz * a10 + ty * a9 - tx * a8;
+                const float b1 = -crz * sry - cry * srx * srz; const float b2 = cry * crz * srx - sry * srz;
+                const float b5 = cry * crz - srx * sry * srz; const float b6 = cry * srz + crz * srx * sry;
+                const float c1 = -b6; const float c2 = b5; const float c3 = tx * b6 - ty * b5;
+                const float c4 = -crx * crz; const float c5 = crx * srz; const float c6 = ty * c5 + tx * -c4;
+                const float c7 = b2; const float c8 = -b1; const float c9 = tx * -b2 - ty * -b1;
+                const float arx = (-a1 * p.x + a2 * p.y + a3 * p.z + a4) * cx + (a5 * p.x - a6 * p.y + crx * p.z + a7) * cy +
+                                  (a8 * p.x - a9 * p.y - a10 * p.z + a11) * cz;
+                const float arz = (c1 * p.x + c2 * p.y + c3) * cx + (c4 * p.x - c5 * p.y + c6) * cy +
+                                  (c7 * p.x + c8 * p.y + c9) * cz;
+                const float aty = -b6 * cx + c4 * cy + b2 * cz;
+                const float bb = (float)(-0.05 * cw);
+                accumulate9(acc, arx, arz, aty, bb);
+                cnt++;
+            } else {
+                const int j1 = ind[2 * i], j2 = ind[2 * i + 1];
+                if (!(j2 >= 0)) continue;
+                const float4 t1 = last[j1], t2 = last[j2];
+                const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+                const float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
+                const float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
+                const float m22 = ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1));
+                const float m33 = ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1));
+                const float a012 = sqrtf(m11 * m11 + m22 * m22 + m33 * m33);
+                const float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
+                const float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
+                const float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
+                const float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
+                const float ld2 = a012 / l12;
+                float sw = 1;
+                if (iterCount >= 5) sw = (float)(1 - 1.8 * fabsf(ld2));
+                if (!(sw > 0.1 && ld2 != 0)) continue;
+                const float cx = sw * la, cy = sw * lb, cz = sw * lc, cw = sw * ld2;
+                // calculateTransformationCorner (FA:1391-1421): rows d/d(ry, tx, tz)
+                const float b1 = -crz * sry - cry * srx * srz; const float b2 = cry * crz * srx - sry * srz;
+                const float b3 = crx * cry; const float b4 = tx * -b1 + ty * -b2 + tz * b3;
+                const float b5 = cry * crz - srx * sry * srz; const float b6 = cry * srz + crz * srx * sry;
+                const float b7 = crx * sry; const float b8 = tz * b7 - ty * b6 - tx * b5;
+                const float c5 = crx * srz;
+                const float ary = (b1 * p.x + b2 * p.y - b3 * p.z + b4) * cx + (b5 * p.x + b6 * p.y - b7 * p.z + b8) * cz;
+                const float atx = -b5 * cx + c5 * cy + b1 * cz;
+                const float atz = b7 * cx - srx * cy - b3 * cz;
+                const float bb = (float)(-0.05 * cw);
+                accumulate9(acc, ary, atx, atz, bb);
+                cnt++;
             }
-            block_reduce<9>(acc, cnt, sh, shi);
-            iters_surf = iterCount + 1;
-            if (tid == 0) {
-                s_ctl = 0;
-                if (cnt < 10) s_ctl = 1;
-                else {
-                    float X[3];
-                    solve_step(st, acc, iterCount, X);
-                    tc[0] += X[0]; tc[2] += X[1]; tc[4] += X[2];
-                    for (int k = 0; k < 6; k++) if (isnan(tc[k])) tc[k] = 0;
-                    double r0 = X[0] * 180.0 / M_PI, r1 = X[1] * 180.0 / M_PI;
-                    double t2 = (double)(X[2] * 100);
-                    float deltaR = (float)sqrt(r0 * r0 + r1 * r1);
-                    float deltaT = (float)sqrt(t2 * t2);
-                    if (deltaR < 0.1 && deltaT < 0.1) s_ctl = 2;
-                }
-            }
-            __syncthreads();
-            if (s_ctl == 2) break;
         }
-        // ------------------------------------------------ corner phase
-        const int nc = st.n_sharp;
-        int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
-        for (int iterCount = 0; iterCount < 25; iterCount++) {
-            slo_dd::DD acc[9];
-            for (int k = 0; k < 9; ++k) acc[k] = slo_dd::zero();
-            int cnt = 0;
-            float srx = slo_libm::sinf_(tc[0]), crx = slo_libm::cosf_(tc[0]);
-            float sry = slo_libm::sinf_(tc[1]), cry = slo_libm::cosf_(tc[1]);
-            float srz = slo_libm::sinf_(tc[2]), crz = slo_libm::cosf_(tc[2]);
-            float tx = tc[3], ty = tc[4], tz = tc[5];
-            float b1 = -crz * sry - cry * srx * srz; float b2 = cry * crz * srx - sry * srz; float b3 = crx * cry; float b4 = tx * -b1 + ty * -b2 + tz * b3;
-            float b5 = cry * crz - srx * sry * srz; float b6 = cry * srz + crz * srx * sry; float b7 = crx * sry; float b8 = tz * b7 - ty * b6 - tx * b5;
-            float c5 = crx * srz;
-            const int rounds = (nc + T - 1) / T;
-            for (int rd = 0; rd < rounds; ++rd) {
-                const int i = rd * T + tid;
-                const bool active = i < nc;
-                P4 po = active ? ld4(sharp, i) : P4{0, 0, 0, 0};
-                P4 sel = slo_pose::transform_to_start(po, tc);
-                if (iterCount % 5 == 0) {
-                    int ci; float cd;
-                    nn1_grid(v.goc_ent, v.goc_off, v.goc_cnt, v.Toc, s, v.cap_less_sharp, rmax, sel, ci, cd);
-                    int closest = -1, i2 = -1;
-                    if (active && cd < gate && ci >= 0 && ci < cornerLastNum) {
-                        closest = ci;
-                        int cscan = (int)clast[closest].w;
-                        float m2 = gate;
-                        for (int j = closest + 1; j < nc && j < cornerLastNum; j++) {
-                            if ((int)clast[j].w > cscan + 2.5) break;
-                            float d = sq3_ref(clast[j], sel);
-                            if ((int)clast[j].w > cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                        }
-                        for (int j = closest - 1; j >= 0; j--) {
-                            if ((int)clast[j].w < cscan - 2.5) break;
-                            float d = sq3_ref(clast[j], sel);
-                            if ((int)clast[j].w < cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                        }
-                    }
-                    if (active) { indc[2 * i] = closest; indc[2 * i + 1] = i2; }
+        block_reduce<9>(acc, cnt, sh, shi);
+        if (tid == 0) {
+            if (PH == 0) st.iters_surf = iterCount + 1; else st.iters_corner = iterCount + 1;
+            s_ctl = 0;
+            if (cnt < 10) s_ctl = 1;
+            else {
+                float X[3];
+                solve_step(st, acc, iterCount, X);
+                if (PH == 0) { tc[0] += X[0]; tc[2] += X[1]; tc[4] += X[2]; }
+                else { tc[1] += X[0]; tc[3] += X[1]; tc[5] += X[2]; }
+                for (int k = 0; k < 6; k++) if (isnan(tc[k])) tc[k] = 0;
+                float deltaR, deltaT;
+                if (PH == 0) {
+                    const double r0 = X[0] * 180.0 / M_PI, r1 = X[1] * 180.0 / M_PI;
+                    const double t2 = (double)(X[2] * 100);
+                    deltaR = (float)sqrt(r0 * r0 + r1 * r1);
+                    deltaT = (float)sqrt(t2 * t2);
+                } else {
+                    const double r0 = X[0] * 180.0 / M_PI;
+                    const double t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
+                    deltaR = (float)sqrt(r0 * r0);
+                    deltaT = (float)sqrt(t1 * t1 + t2 * t2);
                 }
-                if (!active) continue;
-                const int j1 = indc[2 * i], j2 = indc[2 * i + 1];
-                if (j2 >= 0) {
-                    float4 t1 = clast[j1], t2 = clast[j2];
-                    float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-                    float x1 = t1.x, y1 = t1.y, z1 = t1.z, x2 = t2.x, y2 = t2.y, z2 = t2.z;
-                    float m11 = ((x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1));
-                    float m22 = ((x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1));
-                    float m33 = ((y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1));
-                    float a012 = sqrtf(m11 * m11 + m22 * m22 + m33 * m33);
-                    float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
-                    float la = ((y1 - y2) * m11 + (z1 - z2) * m22) / a012 / l12;
-                    float lb = -((x1 - x2) * m11 - (z1 - z2) * m33) / a012 / l12;
-                    float lc = -((x1 - x2) * m22 + (y1 - y2) * m33) / a012 / l12;
-                    float ld2 = a012 / l12;
-                    float sw = 1;
-                    if (iterCount >= 5) sw = (float)(1 - 1.8 * fabsf(ld2));
-                    if (sw > 0.1 && ld2 != 0) {
-                        float cx = sw * la, cy = sw * lb, cz = sw * lc, cw = sw * ld2;
-                        const P4& p = po;
-                        float ary = (b1 * p.x + b2 * p.y - b3 * p.z + b4) * cx + (b5 * p.x + b6 * p.y - b7 * p.z + b8) * cz;
-                        float atx = -b5 * cx + c5 * cy + b1 * cz;
-                        float atz = b7 * cx - srx * cy - b3 * cz;
-                        float bb = (float)(-0.05 * cw);
-                        double A0 = ary, A1 = atx, A2 = atz, B = bb;
-                        accumulate9(acc, A0, A1, A2, B);
-                        cnt++;
-                    }
-                }
+                if (deltaR < 0.1 && deltaT < 0.1) s_ctl = 2;
             }
-            block_reduce<9>(acc, cnt, sh, shi);
-            iters_corner = iterCount + 1;
-            if (tid == 0) {
-                s_ctl = 0;
-                if (cnt < 10) s_ctl = 1;
-                else {
-                    float X[3];
-                    solve_step(st, acc, iterCount, X);
-                    tc[1] += X[0]; tc[3] += X[1]; tc[5] += X[2];
-                    for (int k = 0; k < 6; k++) if (isnan(tc[k])) tc[k] = 0;
-                    double r0 = X[0] * 180.0 / M_PI;
-                    double t1 = (double)(X[1] * 100), t2 = (double)(X[2] * 100);
-                    float deltaR = (float)sqrt(r0 * r0);
-                    float deltaT = (float)sqrt(t1 * t1 + t2 * t2);
-                    if (deltaR < 0.1 && deltaT < 0.1) s_ctl = 2;
-                }
-            }
-            __syncthreads();
-            if (s_ctl == 2) break;
         }
+        __syncthreads();
+        if (s_ctl == 2) break;
     }
     if (tid == 0) {
         for (int k = 0; k < 6; ++k) st.transformCur[k] = tc[k];
+        if (s_ctl == 2 || iterCount >= 25) st.odo_phase = PH + 1;
+    }
+}
+
+// integrateTransformation (FA:1697-1725) + publishCloudsLast (FA:1759-1788)
+__global__ void __launch_bounds__(256) k_fa_odo_finish(DevView v) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    if (st.odo_phase == 3) return;
+    const int tid = threadIdx.x, T = blockDim.x;
+    __shared__ float tc[6];
+    if (tid == 0) {
+        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
         slo_pose::integrate(st.transformSum, tc);
-        st.iters_surf = iters_surf;
-        st.iters_corner = iters_corner;
     }
     __syncthreads();
-    // publishCloudsLast: TransformToEnd into the next *Last buffers
+    const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
+    const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
+    const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
+    float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
+    float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
+    // TransformToEnd into the next *Last buffers; the "trees" are rebuilt
+    // (setInputCloud copies) only when both clouds are big enough
+    const bool rebuild = nLS > 10 && nLF > 100;
+    float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
+    float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
     for (int i = tid; i < nLS; i += T) {
-        P4 q = slo_pose::transform_to_end(ld4(lsharp, i), tc);
-        cnext[i] = make_float4(q.x, q.y, q.z, q.w);
+        const P4 q = slo_pose::transform_to_end(ld4(lsharp, i), tc);
+        const float4 o = make_float4(q.x, q.y, q.z, q.w);
+        cnext[i] = o;
+        if (rebuild) kdc[i] = o;
     }
     for (int i = tid; i < nLF; i += T) {
-        P4 q = slo_pose::transform_to_end(ld4(lflat, i), tc);
-        snext[i] = make_float4(q.x, q.y, q.z, q.w);
-    }
-    __syncthreads();
-    const bool rebuild = nLS > 10 && nLF > 100;
-    if (rebuild) {
-        for (int i = tid; i < nLS; i += T) kdc[i] = cnext[i];
-        for (int i = tid; i < nLF; i += T) kds[i] = snext[i];
+        const P4 q = slo_pose::transform_to_end(ld4(lflat, i), tc);
+        const float4 o = make_float4(q.x, q.y, q.z, q.w);
+        snext[i] = o;
+        if (rebuild) kds[i] = o;
     }
     if (tid == 0) {
         st.cornerLastNum = nLS;
@@ -396,7 +417,20 @@ __global__ void __launch_bounds__(256) k_fa_odometry(DevView v, int first_scan) 
 
 int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     DevView& v = ctx->v;
-    SLO_LAUNCH(ctx, "fa_odometry", k_fa_odometry, dim3(ctx->S), dim3(256), 0, v, first_scan ? 1 : 0);
+    const int S = ctx->S;
+    SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
+    if (!first_scan) {
+        const dim3 gs((v.cap_flat + 255) / 256, S), gc((v.cap_sharp + 255) / 256, S);
+        for (int b = 0; b < 5; ++b) {
+            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search<0>, gs, dim3(256), 0, v);
+            SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
+        }
+        for (int b = 0; b < 5; ++b) {
+            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search<1>, gc, dim3(256), 0, v);
+            SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
+        }
+    }
+    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);

@@ -216,47 +216,56 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     return 0;
 }
 
-// ---------------------------------------------------------------- hash grid (1 m cells)
-__global__ void k_grid_count(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, int32_t* cnt) {
+// ---------------------------------------------------------------- spatial hash grid
+__global__ void k_grid_count(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
+                             int32_t* cnt) {
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        float4 p = pts[(size_t)s * stride + i];
-        unsigned int b = grid_hash((int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z), T);
+        const float4 p = pts[(size_t)s * stride + i];
+        const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
         atomicAdd(&cnt[(size_t)s * T + b], 1);
     }
 }
 
-__global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T,
+__global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
                                const int32_t* off, int32_t* cur, float4* ent, size_t ent_stride) {
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
     const int base = off[(size_t)s * T];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        float4 p = pts[(size_t)s * stride + i];
-        unsigned int b = grid_hash((int)floorf(p.x), (int)floorf(p.y), (int)floorf(p.z), T);
-        int pos = off[(size_t)s * T + b] - base + atomicAdd(&cur[(size_t)s * T + b], 1);
+        const float4 p = pts[(size_t)s * stride + i];
+        const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
+        const int pos = off[(size_t)s * T + b] - base + atomicAdd(&cur[(size_t)s * T + b], 1);
         ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
     }
 }
 
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride) {
     const int S = ctx->S;
+    const float inv = 1.0f / g.cell;
     SLO_CHECK(hipMemsetAsync(g.cnt, 0, sizeof(int32_t) * (size_t)S * g.T, ctx->stream));
     SLO_CHECK(hipMemsetAsync(g.cur, 0, sizeof(int32_t) * (size_t)S * g.T, ctx->stream));
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
-    SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, g.cnt);
+    SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
     size_t tb = g.temp_bytes;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)((size_t)S * g.T), ctx->stream));
-    SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, g.off,
-               g.cur, g.ent, g.ent_stride);
+    SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
+               g.off, g.cur, g.ent, g.ent_stride);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
 
-int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride) {
+// cell: power-of-two edge length in metres (exact floor(x / cell), GridView)
+int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) {
     const int S = ctx->S;
+    int e2;
+    if (T <= 0 || (T & (T - 1)) || !(cell > 0) || frexpf(cell, &e2) != 0.5f) {
+        ctx->err = "grid_alloc: T and cell must be powers of two";
+        return SLO_E_ARG;
+    }
     g.T = T;
+    g.cell = cell;
     g.ent_stride = ent_stride;
     SLO_CHECK(hipMalloc(&g.cnt, sizeof(int32_t) * (size_t)S * T));
     SLO_CHECK(hipMalloc(&g.cur, sizeof(int32_t) * (size_t)S * T));
@@ -267,6 +276,18 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride) {
     g.temp_bytes = tb;
     SLO_CHECK(hipMalloc(&g.temp, tb));
     return 0;
+}
+
+GridView grid_view(const HashGrid& g) {
+    GridView v;
+    v.T = g.T;
+    v.cell = g.cell;
+    v.inv = 1.0f / g.cell;
+    v.es = g.ent_stride;
+    v.cnt = g.cnt;
+    v.off = g.off;
+    v.ent = g.ent;
+    return v;
 }
 
 void grid_free(HashGrid& g) {
