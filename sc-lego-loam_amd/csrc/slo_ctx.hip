@@ -141,6 +141,8 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.surf_next, S * v.cap_less_flat);
     c.add(&v.kd_corner, S * v.cap_less_sharp);
     c.add(&v.kd_surf, S * v.cap_less_flat);
+    c.add(&v.roff_cur, S * 2 * (R + 1));
+    c.add(&v.roff_last, S * 2 * (R + 1));
     c.add(&v.ind_surf, S * v.cap_flat * 3);
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
@@ -198,16 +200,14 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     memset(ctx->h_st, 0, sizeof(StreamState) * S);
     // Grid cells (powers of two, GridView): the map grids answer 5-NN within
     // 1 m (MO:1281/1364) in 0.5 m cells (rings <= 2, usually done after 1);
-    // the odometry grids answer 1-NN within 5 m (nearestFeatureSearchSqDist):
-    // 1 m cells.
+    // the odometry surf grid answers 1-NN within 5 m (nearestFeatureSearchSqDist)
+    // in 1 m cells; the sparse corner cloud is searched by brute force.
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms, 0.5f) ||
-        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 13, v.cap_less_sharp, 1.0f) ||
         slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat, 1.0f)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
-    v.g_oc = slo::grid_view(ctx->grid_oc);
     v.g_os = slo::grid_view(ctx->grid_os);
     v.g_mc = slo::grid_view(ctx->grid_c);
     v.g_ms = slo::grid_view(ctx->grid_s);

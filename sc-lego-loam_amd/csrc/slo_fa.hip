@@ -332,6 +332,11 @@ __global__ void k_fa_gather(DevView v) {
         off[threadIdx.x][R] = a;
     }
     __syncthreads();
+    // ring boundaries of less_sharp / less_flat (the odometry's ring windows)
+    for (int r = threadIdx.x; r <= R; r += blockDim.x) {
+        v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + r] = off[1][r];
+        v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + r] = min(off[3][r], v.cap_less_flat);
+    }
     StreamState& st = v.st[s];
     if (threadIdx.x == 0) {
         st.n_sharp = off[0][R]; st.n_less_sharp = off[1][R]; st.n_flat = off[2][R];

@@ -133,6 +133,8 @@ struct DevView {
     float4* surf_next;   // [S][cap_less_flat]
     float4* kd_corner;   // [S][cap_less_sharp]  copy the "tree" searches (setInputCloud copies)
     float4* kd_surf;     // [S][cap_less_flat]
+    int32_t* roff_cur;   // [S][2][R+1] first index of each ring in less_sharp / less_flat
+    int32_t* roff_last;  // [S][2][R+1] the same for corner_last / surf_last
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
     StreamState* st;     // [S]
@@ -183,6 +185,17 @@ __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
            (unsigned int)(T - 1);
 }
 __host__ __device__ inline int grid_cell(float x, float inv) { return (int)floorf(x * inv); }
+
+// XCD-aware 1-D grids for (stream, chunk) work: blocks b and b + 8 share an
+// XCD (MI355X_MICROARCH.md "Workgroup dispatch"), so stream s goes to the XCD
+// of blocks == s (mod 8) and all NB chunks of a stream share that XCD's L2.
+// Grid size xcd_grid(S, NB); blocks with s >= S exit.
+__host__ __device__ inline int xcd_grid(int S, int NB) { return ((S + 7) / 8) * 8 * NB; }
+__device__ inline void xcd_stream_chunk(int b, int NB, int& s, int& chunk) {
+    const int x = b & 7, k = b >> 3;
+    s = (k / NB) * 8 + x;
+    chunk = k % NB;
+}
 
 // Visit every grid point of stream s in the cells at Chebyshev ring r around
 // cell (cx, cy, cz): f(point) for points of exactly those cells (buckets are

@@ -13,10 +13,11 @@
 // (transformPointCloud with the keyframe pose, MO:566-596 — the pose never
 // changes on this path, so transforming at save time equals the reference's
 // transform at deque insertion).  Each LM iteration is two launches: every
-// workgroup of a stream takes a slice of its corner+surf queries, does the
-// exact 5-NN in the 1 m hash grid, the 3x3 Jacobi / 5x3 QR of the reference
-// and accumulates A^T A, A^T b in double; a per-stream lane then sums the
-// slices in fixed order and runs the 6x6 QR / degeneracy projection.
+// workgroup of a stream takes a contiguous slice of its corner+surf queries,
+// does the exact 5-NN in the hash grid, the 3x3 Jacobi / 5x3 QR of the
+// reference and accumulates A^T A, A^T b in double-double (slo_ddsum.h); a
+// per-stream lane then merges the slices, rounds once to float and runs the
+// 6x6 QR / degeneracy projection.
 #include "slo_internal.h"
 #include "slo_libm.h"
 #include "slo_pose.h"
@@ -152,8 +153,14 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
 }
 
 // ---------------------------------------------------------------- correspondences + partial normal equations
+// XCD-aware grid (xcd_stream_chunk): a stream's SLO_MO_BLOCKS workgroups share
+// one XCD's L2, and each takes a contiguous run of the (voxel-ordered, hence
+// spatially coherent) queries, so the map cells a workgroup walks are mostly
+// the ones its neighbours just pulled in.
 __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
-    const int s = blockIdx.y;
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, SLO_MO_BLOCKS, s, chunk);
+    if (s >= v.S) return;
     const StreamState& st = v.st[s];
     slo_dd::DD acc[27];
     for (int k = 0; k < 27; ++k) acc[k] = slo_dd::zero();
@@ -170,7 +177,9 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
         const int nc = st.n_corner_ds, nsq = st.n_surf_total_ds;
         const float4* mc = v.map_c_ds + (size_t)s * v.cap_mc;
         const float4* ms = v.map_s_ds + (size_t)s * v.cap_ms;
-        for (int q = blockIdx.x * blockDim.x + threadIdx.x; q < nc + nsq; q += gridDim.x * blockDim.x) {
+        const int nq = nc + nsq, per = (nq + SLO_MO_BLOCKS - 1) / SLO_MO_BLOCKS;
+        const int q0 = chunk * per, q1 = min(nq, q0 + per);
+        for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
             const bool corner = q < nc;
             float4 po4 = corner ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
             P4 po{po4.x, po4.y, po4.z, po4.w};
@@ -270,7 +279,7 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
         shn[w] = nsel;
     }
     __syncthreads();
-    double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + blockIdx.x) * SLO_MO_PART;
+    double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + chunk) * SLO_MO_PART;
     if (threadIdx.x < 27) {
         slo_dd::DD r = sh[0][threadIdx.x];
         for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) slo_dd::merge(r, sh[ww][threadIdx.x]);
@@ -533,7 +542,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
     if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
     for (int it = 0; it < 10; ++it) {
-        SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(SLO_MO_BLOCKS, S), dim3(256), 0, v);
+        SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_solve", k_mo_solve, dim3(S), dim3(64), 0, v, it);
     }
     SLO_LAUNCH(ctx, "mo_finish", k_mo_finish, dim3(S), dim3(256), 0, v);

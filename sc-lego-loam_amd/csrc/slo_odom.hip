@@ -137,6 +137,12 @@ __device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int it
 // StreamState::odo_phase carries the control flow between launches:
 // 0 = surf running, 1 = corner running, 2 = solved (or skipped), 3 = init scan.
 
+// the clouds becoming *Last keep the ring structure of less_sharp / less_flat
+__device__ inline void copy_ring_offsets(const DevView& v, int s) {
+    const int n = 2 * (v.cfg.n_scan + 1);
+    for (int k = threadIdx.x; k < n; k += blockDim.x) v.roff_last[(size_t)s * n + k] = v.roff_cur[(size_t)s * n + k];
+}
+
 __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
@@ -151,6 +157,7 @@ __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan)
         float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
         for (int i = tid; i < nLS; i += T) { cnext[i] = lsharp[i]; kdc[i] = lsharp[i]; }
         for (int i = tid; i < nLF; i += T) { snext[i] = lflat[i]; kds[i] = lflat[i]; }
+        copy_ring_offsets(v, s);
         if (tid == 0) {
             st.cornerLastNum = nLS; st.surfLastNum = nLF;
             st.kdCornerNum = nLS; st.kdSurfNum = nLF;
@@ -165,73 +172,108 @@ __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan)
     }
 }
 
+// min of sq3_ref over a[j0..j1) visited upward / downward with the
+// reference's strict '<' (so ties keep the first index met)
+__device__ inline void walk_up(const float4* a, int j0, int j1, const P4& q, float& m, int& mi) {
+#pragma unroll 4
+    for (int j = j0; j < j1; ++j) {
+        const float d = sq3_ref(a[j], q);
+        if (d < m) { m = d; mi = j; }
+    }
+}
+__device__ inline void walk_down(const float4* a, int j0, int j1, const P4& q, float& m, int& mi) {
+#pragma unroll 4
+    for (int j = j1 - 1; j >= j0; --j) {
+        const float d = sq3_ref(a[j], q);
+        if (d < m) { m = d; mi = j; }
+    }
+}
+
 // findCorrespondingSurfFeatures (FA:1155-1268) / ...CornerFeatures
 // (FA:1044-1153) for one query: exact 1-NN in the tree cloud, then the
 // ring-ordered walk for the 2nd (and 3rd) points within +-2.5 rings.
+//
+// The *Last clouds are concatenated ring by ring, so the reference's walk —
+// step away from `closest` until the ring leaves [cscan-2, cscan+2], sorting
+// each point into "same/lower ring" or "other ring" by its ring — is exactly a
+// min over four index ranges cut at the ring boundaries (roff_last), in the
+// same visiting order: forward over [closest+1, ...) bounded by Q7's
+// min(query count, cloud size), then backward from closest-1.
+//
+// 1-NN: surf (dense, ~10^4-10^5 points) through the 1 m hash grid; corner
+// (sparse, <= 120 R points) by brute force, the cloud streamed through LDS in
+// 256-point tiles shared by the workgroup's 256 queries (lowest index wins
+// ties: strict '<' in index order).
 template <int PH>
-__global__ void __launch_bounds__(256) k_fa_search(DevView v) {
-    const int s = blockIdx.y;
+__global__ void __launch_bounds__(256) k_fa_search(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
     const StreamState& st = v.st[s];
     if (st.odo_phase != PH) return;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    const int i = chunk * blockDim.x + threadIdx.x;
     const int nq = PH == 0 ? st.n_flat : st.n_sharp;
-    if (i >= nq) return;
+    if (chunk * (int)blockDim.x >= nq) return;   // whole workgroup idle (uniform)
+    const bool active = i < nq;
     const float gate = v.cfg.nearest_feature_search_sq_dist;
+    const int R = v.cfg.n_scan;
     float tc[6];
     for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    const float4* qp = PH == 0 ? v.flat + (size_t)s * v.cap_flat : v.sharp + (size_t)s * v.cap_sharp;
+    const P4 sel = slo_pose::transform_to_start(ld4(qp, active ? i : 0), tc);
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + (PH == 0 ? 1 : 0)) * (R + 1);
+    auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
+    int ci; float cd;
     if (PH == 0) {
-        const float4* flat = v.flat + (size_t)s * v.cap_flat;
+        nn1_grid(v.g_os, s, gate, sel, ci, cd);
+    } else {
+        __shared__ float4 tile[256];
+        const float4* kd = v.kd_corner + (size_t)s * v.cap_less_sharp;
+        const int n = st.kdCornerNum;
+        ci = -1; cd = FLT_MAX;
+        const bool fin = isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z);
+        for (int t0 = 0; t0 < n; t0 += 256) {
+            __syncthreads();
+            if (t0 + (int)threadIdx.x < n) tile[threadIdx.x] = kd[t0 + threadIdx.x];
+            __syncthreads();
+            const int m = min(256, n - t0);
+            if (active && fin)
+                for (int k = 0; k < m; ++k) {
+                    const float d = sqdist_flann(sel, tile[k]);
+                    if (d < cd) { cd = d; ci = t0 + k; }
+                }
+        }
+    }
+    if (!active) return;
+    if (PH == 0) {
         const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
         const int surfLastNum = st.surfLastNum;
-        const P4 sel = slo_pose::transform_to_start(ld4(flat, i), tc);
-        int ci; float cd;
-        nn1_grid(v.g_os, s, gate, sel, ci, cd);
         int closest = -1, i2 = -1, i3 = -1;
         if (cd < gate && ci >= 0 && ci < surfLastNum) {
             closest = ci;
             const int cscan = (int)slast[closest].w;
+            const int lim = min(nq, surfLastNum);                        // Q7: bounded by the flat count
+            const int e0 = ring_first(cscan + 1), e2 = ring_first(cscan + 3);
+            const int b0 = ring_first(cscan), b2 = ring_first(cscan - 2);
             float m2 = gate, m3 = gate;
-            for (int j = closest + 1; j < nq && j < surfLastNum; j++) {   // Q7: bounded by the flat count
-                const float4 t = slast[j];
-                if ((int)t.w > cscan + 2.5) break;
-                const float d = sq3_ref(t, sel);
-                if ((int)t.w <= cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                else { if (d < m3) { m3 = d; i3 = j; } }
-            }
-            for (int j = closest - 1; j >= 0; j--) {
-                const float4 t = slast[j];
-                if ((int)t.w < cscan - 2.5) break;
-                const float d = sq3_ref(t, sel);
-                if ((int)t.w >= cscan) { if (d < m2) { m2 = d; i2 = j; } }
-                else { if (d < m3) { m3 = d; i3 = j; } }
-            }
+            walk_up(slast, closest + 1, min(e0, lim), sel, m2, i2);         // ring == cscan
+            walk_up(slast, max(closest + 1, e0), min(e2, lim), sel, m3, i3); // cscan < ring <= cscan+2
+            walk_down(slast, b0, closest, sel, m2, i2);                      // ring == cscan
+            walk_down(slast, b2, min(b0, closest), sel, m3, i3);             // cscan-2 <= ring < cscan
         }
         int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
         ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
     } else {
-        const float4* sharp = v.sharp + (size_t)s * v.cap_sharp;
         const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
         const int cornerLastNum = st.cornerLastNum;
-        const P4 sel = slo_pose::transform_to_start(ld4(sharp, i), tc);
-        int ci; float cd;
-        nn1_grid(v.g_oc, s, gate, sel, ci, cd);
         int closest = -1, i2 = -1;
         if (cd < gate && ci >= 0 && ci < cornerLastNum) {
             closest = ci;
             const int cscan = (int)clast[closest].w;
+            const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
             float m2 = gate;
-            for (int j = closest + 1; j < nq && j < cornerLastNum; j++) {  // Q7: bounded by the sharp count
-                const float4 t = clast[j];
-                if ((int)t.w > cscan + 2.5) break;
-                const float d = sq3_ref(t, sel);
-                if ((int)t.w > cscan) { if (d < m2) { m2 = d; i2 = j; } }
-            }
-            for (int j = closest - 1; j >= 0; j--) {
-                const float4 t = clast[j];
-                if ((int)t.w < cscan - 2.5) break;
-                const float d = sq3_ref(t, sel);
-                if ((int)t.w < cscan) { if (d < m2) { m2 = d; i2 = j; } }
-            }
+            walk_up(clast, max(closest + 1, ring_first(cscan + 1)), min(ring_first(cscan + 3), lim), sel, m2, i2);
+            walk_down(clast, ring_first(cscan - 2), min(ring_first(cscan), closest), sel, m2, i2);
         }
         int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
         indc[2 * i] = closest; indc[2 * i + 1] = i2;
@@ -408,6 +450,7 @@ __global__ void __launch_bounds__(256) k_fa_odo_finish(DevView v) {
         snext[i] = o;
         if (rebuild) kds[i] = o;
     }
+    copy_ring_offsets(v, s);
     if (tid == 0) {
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;
@@ -420,13 +463,13 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
     if (!first_scan) {
-        const dim3 gs((v.cap_flat + 255) / 256, S), gc((v.cap_sharp + 255) / 256, S);
+        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 255) / 256;
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search<0>, gs, dim3(256), 0, v);
+            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search<0>, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
             SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
         }
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search<1>, gc, dim3(256), 0, v);
+            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search<1>, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
@@ -435,10 +478,9 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);
     std::swap(ctx->v.surf_last, ctx->v.surf_next);
-    // setInputCloud: hash grids over the (possibly unchanged) tree clouds
+    // setInputCloud: hash grid over the (possibly unchanged) surf tree cloud
+    // (the corner tree is searched by brute force, k_fa_search<1>)
     const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
-    int r = grid_build(ctx, ctx->grid_oc, v.kd_corner, v.cap_less_sharp, &v.st->kdCornerNum, SS);
-    if (r) return r;
     return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
 }
 
