@@ -372,6 +372,7 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "tobe_mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformTobeMapped, 24); count = 6; esz = 4; }
     else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
+    else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
     else if (name == "raw_ds") dev(v.cur_raw_ds + s * v.P, st.n_raw_ds, 16);
     else if (name == "corner_ds") dev(v.cur_c_ds + s * v.cap_less_sharp, st.n_corner_ds, 16);

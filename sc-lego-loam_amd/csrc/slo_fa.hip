@@ -11,10 +11,10 @@
 //     values persisted from earlier scans (Appendix A Q5).
 //   extractFeatures (FA:680-784): rings are independent except through the
 //     stale cloudSmoothness[4] entry of ring 0 (Q5), so ring 0 runs first and
-//     rings 1..R-1 then run in parallel, one wavefront each.  The six sector
-//     sorts of a ring run in six lanes with an exact restatement of
-//     libstdc++'s introsort (slo_introsort.h, Q4/Q6); the greedy picks are
-//     sequential per ring as in the reference.
+//     rings 1..R-1 then run in parallel, one workgroup each, staged in LDS
+//     (k_fa_extract: wave rank sorts with the exact libstdc++ introsort
+//     restatement for sectors holding ties, Q4/Q6; the greedy picks are
+//     sequential per ring as in the reference).
 //   per-ring VoxelGrid(0.2) (FA:778-782): one block per ring, bitonic sort
 //     of (voxel idx, position) keys in LDS, centroid of each voxel summed in
 //     position order (DESIGN.md "VoxelGrid order").
@@ -123,26 +123,30 @@ __device__ inline void mark_neighbors(int32_t* picked, const uint32_t* col, int 
     }
 }
 
-// one 64-lane block per (ring, stream); ring = ring0 + blockIdx.x
-__global__ void __launch_bounds__(64) k_fa_extract(DevView v, int ring0) {
-    const int s = blockIdx.y;
-    const int ring = ring0 + blockIdx.x;
+// ---------------------------------------------------------------- extractFeatures (FA:680-784)
+// Sector bounds of ring [rs, re] (FA:693-696).
+__device__ inline int sec_sp(int rs, int re, int j) { return (rs * (6 - j) + re * j) / 6; }
+__device__ inline int sec_ep(int rs, int re, int j) { return (rs * (5 - j) + re * (j + 1)) / 6 - 1; }
+
+// The restatement on global memory, for ring 0 (its sector 0 starts at the
+// stale cloudSmoothness[4] entry, whose index can point anywhere, Q5 — which is
+// why ring 0 runs alone, first) and for rings too long to stage.  Lanes 0..5
+// sort the six sectors with the libstdc++ introsort restatement (Q4/Q6), lane 0
+// picks.  Every thread of the block must call it.
+__device__ void extract_ring_global(const DevView& v, int s, int ring) {
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const size_t base = (size_t)s * v.H;
     const int S = v.st[s].seg_count;
     const int* se = v.ring_se + (size_t)s * R * 2;
     const int rs = se[2 * ring], re = se[2 * ring + 1];
     Smooth* sm = v.smooth + base;
-    const int lane = threadIdx.x;
-    // sector sorts (FA:693-699), lanes 0..5
-    if (lane < 6) {
-        int j = lane;
-        int sp = (rs * (6 - j) + re * j) / 6;
-        int ep = (rs * (5 - j) + re * (j + 1)) / 6 - 1;
+    const int tid = threadIdx.x;
+    if (tid < 6) {
+        const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
         if (sp < ep) slo_sort::std_sort(sm + sp, ep - sp, SmoothLess());
     }
     __syncthreads();
-    if (lane != 0) return;
+    if (tid != 0) return;
     int32_t* picked = v.picked + base;
     int32_t* lab = v.clabel + base;
     const float* curv = v.curv + base;
@@ -156,12 +160,11 @@ __global__ void __launch_bounds__(64) k_fa_extract(DevView v, int ring0) {
     float4* o_lf = v.r_lf_scan + rr * C;
     int n_sharp = 0, n_lsharp = 0, n_flat = 0, n_lf = 0;
     for (int j = 0; j < 6; j++) {
-        int sp = (rs * (6 - j) + re * j) / 6;
-        int ep = (rs * (5 - j) + re * (j + 1)) / 6 - 1;
+        const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
         if (sp >= ep) continue;
         int largestPickedNum = 0;
         for (int k = ep; k >= sp; k--) {
-            int ind = sm[k].ind;
+            const int ind = sm[k].ind;
             if (ind >= S) continue;
             if (picked[ind] == 0 && curv[ind] > v.cfg.edge_threshold && gflag[ind] == 0) {
                 largestPickedNum++;
@@ -181,7 +184,7 @@ __global__ void __launch_bounds__(64) k_fa_extract(DevView v, int ring0) {
         }
         int smallestPickedNum = 0;
         for (int k = sp; k <= ep; k++) {
-            int ind = sm[k].ind;
+            const int ind = sm[k].ind;
             if (ind >= S) continue;
             if (picked[ind] == 0 && curv[ind] < v.cfg.surf_threshold && gflag[ind] == 1) {
                 lab[ind] = -1;
@@ -198,6 +201,247 @@ __global__ void __launch_bounds__(64) k_fa_extract(DevView v, int ring0) {
     int* rc = v.ring_cnt + rr * 4;
     rc[0] = n_sharp; rc[1] = n_lsharp; rc[2] = n_flat;
     v.r_lf_n[rr] = n_lf;
+}
+
+__global__ void __launch_bounds__(256) k_fa_extract_ring0(DevView v) { extract_ring_global(v, blockIdx.y, 0); }
+
+// Rank sort of one sector by one wave: rank = number of smaller values, so
+// equal ranks mean equal values; *tie is raised (and the sector left as it
+// was) when any two values are equal.  NE = ceil(n / 64) elements per lane.
+template <int NE>
+__device__ inline void rank_sort_wave(Smooth* a, int n, int lane, int* tie_flag) {
+    Smooth mine[NE];
+    int rank[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        rank[e] = 0;
+        mine[e] = lane + 64 * e < n ? a[lane + 64 * e] : Smooth{__builtin_nanf(""), -1};
+    }
+    bool tie = false;
+#pragma unroll 4
+    for (int t = 0; t < n; ++t) {
+        const float y = a[t].value;   // one broadcast LDS read
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            rank[e] += y < mine[e].value;
+            tie |= (y == mine[e].value) & (t != lane + 64 * e);
+        }
+    }
+    const bool any_tie = __any(tie);
+    if (!any_tie) {
+        // every lane has read everything (the t loop) before anyone writes:
+        // the wave executes the reads above in order, then this barrier-free
+        // scatter; a wave-level fence orders LDS reads before the writes
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < NE; ++e)
+            if (lane + 64 * e < n) a[rank[e]] = mine[e];
+    } else if (lane == 0) {
+        *tie_flag = 1;
+    }
+}
+
+// Rings 1..R-1, one 256-thread workgroup per (ring, stream), ring = 1 + blockIdx.x.
+//
+// A ring's sorts, picks and neighbour marks only touch the ring's own points
+// [rs-5, re+5): its sectors' smoothness entries are this scan's (positions
+// in [5, S-5), ind = position) and marks stop at +-5.  So the window is staged
+// in LDS in compact form (smoothness entries; picked, label, ground flag as
+// bytes; curvature; column as 16 bits), worked on there with plain LDS
+// accesses, and written back; concurrent rings never share a word.
+//
+// Sector sorts (std::sort on [sp, ep), Q4/Q6): the sorted order is unique
+// when a sector has no equal curvatures, so a wave rank-sorts each sector;
+// only a sector holding a tie is sorted by one lane with the exact libstdc++
+// introsort restatement (slo_introsort.h), whose order of equal keys is the
+// reference's.
+//
+// Picks (FA:701-766): eligibility that picks cannot change (curvature,
+// ground flag) is evaluated by all lanes and compacted into per-sector
+// candidate lists in visiting order; one lane then walks only those, testing
+// picked[] and marking neighbours, and records the picked indices; all lanes
+// gather the points afterwards.  The less-flat collection (label <= 0,
+// FA:768-776) runs after all six sectors' picks with a wave ballot: a sector's
+// picks only label that sector's own points, so the result equals the
+// reference's per-sector interleaving.
+#define SLO_RING_STAGE 2080
+
+__global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
+    const int s = blockIdx.y;
+    const int ring = 1 + blockIdx.x;
+    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const size_t base = (size_t)s * v.H;
+    const int S = v.st[s].seg_count;
+    const int* se = v.ring_se + (size_t)s * R * 2;
+    const int rs = se[2 * ring], re = se[2 * ring + 1];
+    const int lo = max(0, rs - 5), hi = min(v.H, re + 5);
+    if (!(hi > lo && hi - lo <= SLO_RING_STAGE)) {   // uniform per block
+        extract_ring_global(v, s, ring);
+        return;
+    }
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    Smooth* sm = v.smooth + base;
+    int32_t* picked = v.picked + base;
+    int32_t* lab = v.clabel + base;
+    const float4* fp = v.fpts + base;
+
+    __shared__ Smooth lsm[SLO_RING_STAGE];
+    __shared__ float lcv[SLO_RING_STAGE];
+    __shared__ uint16_t lcol[SLO_RING_STAGE];
+    __shared__ int8_t lpk[SLO_RING_STAGE], llab[SLO_RING_STAGE];
+    __shared__ uint8_t lgf[SLO_RING_STAGE];
+    __shared__ int16_t l_sh[SLO_RING_STAGE], l_fl[SLO_RING_STAGE];
+    __shared__ int n_sh[6], n_fl[6], s_tie[6], s_cnt[3];
+    __shared__ int p_sh[12], p_ls[120], p_fl[24];
+    for (int k = tid; k < hi - lo; k += blockDim.x) {
+        const size_t g = base + lo + k;
+        lsm[k] = sm[lo + k]; lpk[k] = (int8_t)v.picked[g]; llab[k] = (int8_t)v.clabel[g];
+        lcv[k] = v.curv[g]; lcol[k] = (uint16_t)v.seg_col[g]; lgf[k] = v.seg_ground[g];
+    }
+    if (tid < 6) s_tie[tid] = 0;
+    __syncthreads();
+
+    // ---- sector sorts: two rounds of (up to) four sectors, one wave each
+    for (int r0 = 0; r0 < 6; r0 += 4) {
+        const int j = r0 + wave;
+        if (j < 6) {
+            const int sp = sec_sp(rs, re, j), n = sec_ep(rs, re, j) - sp;
+            Smooth* a = &lsm[sp - lo];
+            switch ((n + 63) >> 6) {
+                case 0: break;
+                case 1: if (n > 1) rank_sort_wave<1>(a, n, lane, &s_tie[j]); break;
+                case 2: rank_sort_wave<2>(a, n, lane, &s_tie[j]); break;
+                case 3: rank_sort_wave<3>(a, n, lane, &s_tie[j]); break;
+                case 4: rank_sort_wave<4>(a, n, lane, &s_tie[j]); break;
+                case 5: rank_sort_wave<5>(a, n, lane, &s_tie[j]); break;
+                case 6: rank_sort_wave<6>(a, n, lane, &s_tie[j]); break;
+                default: if (lane == 0) s_tie[j] = 1; break;
+            }
+        }
+    }
+    __syncthreads();
+    if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
+        const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
+        slo_sort::std_sort(&lsm[sp - lo], ep - sp, SmoothLess());
+    }
+    __syncthreads();
+
+    // ---- candidate lists (window offsets), sharp in visiting order ep..sp,
+    // flat sp..ep
+    for (int r0 = 0; r0 < 6; r0 += 4) {
+        const int j = r0 + wave;
+        if (j >= 6) continue;
+        const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+        int ns = 0, nf = 0;
+        if (sp < ep)
+            for (int kb = 0; kb <= ep - sp; kb += 64) {
+                const int ks = ep - kb - lane, kf = sp + kb + lane;
+                bool es = false, ef = false;
+                if (ks >= sp) {
+                    const int ind = lsm[ks - lo].ind;
+                    es = ind < S && lcv[ind - lo] > v.cfg.edge_threshold && lgf[ind - lo] == 0;
+                }
+                if (kf <= ep) {
+                    const int ind = lsm[kf - lo].ind;
+                    ef = ind < S && lcv[ind - lo] < v.cfg.surf_threshold && lgf[ind - lo] == 1;
+                }
+                const unsigned long long ms = __ballot(es), mf = __ballot(ef);
+                const unsigned long long below = (1ull << lane) - 1;
+                if (es) l_sh[sp - lo + ns + __popcll(ms & below)] = (int16_t)(ks - lo);
+                if (ef) l_fl[sp - lo + nf + __popcll(mf & below)] = (int16_t)(kf - lo);
+                ns += __popcll(ms);
+                nf += __popcll(mf);
+            }
+        if (lane == 0) { n_sh[j] = ns; n_fl[j] = nf; }
+    }
+    __syncthreads();
+
+    // ---- greedy picks, one lane, LDS only
+    if (tid == 0) {
+        auto mark = [&](int ind) __attribute__((always_inline)) {   // FA:719-731 / 752-764
+            auto colw = [&](int i) __attribute__((always_inline)) { return i < 0 ? 0u : (uint32_t)lcol[i - lo]; };
+            for (int l = 1; l <= 5; l++) {
+                if (abs((int)(colw(ind + l) - colw(ind + l - 1))) > 10) break;
+                lpk[ind + l - lo] = 1;
+            }
+            for (int l = -1; l >= -5; l--) {
+                if (abs((int)(colw(ind + l) - colw(ind + l + 1))) > 10) break;
+                if (ind + l >= 0) lpk[ind + l - lo] = 1;
+            }
+        };
+        int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+        for (int j = 0; j < 6; j++) {
+            const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+            if (sp >= ep) continue;
+            int largestPickedNum = 0;
+            for (int c = 0; c < n_sh[j]; ++c) {
+                const int ind = lsm[l_sh[sp - lo + c]].ind;
+                if (lpk[ind - lo] == 0) {
+                    largestPickedNum++;
+                    if (largestPickedNum <= 2) {
+                        llab[ind - lo] = 2;
+                        p_sh[n_sharp++] = ind;
+                        p_ls[n_lsharp++] = ind;
+                    } else if (largestPickedNum <= 20) {
+                        llab[ind - lo] = 1;
+                        p_ls[n_lsharp++] = ind;
+                    } else {
+                        break;
+                    }
+                    lpk[ind - lo] = 1;
+                    mark(ind);
+                }
+            }
+            int smallestPickedNum = 0;
+            for (int c = 0; c < n_fl[j]; ++c) {
+                const int ind = lsm[l_fl[sp - lo + c]].ind;
+                if (lpk[ind - lo] == 0) {
+                    llab[ind - lo] = -1;
+                    p_fl[n_flat++] = ind;
+                    smallestPickedNum++;
+                    if (smallestPickedNum >= 4) break;
+                    lpk[ind - lo] = 1;
+                    mark(ind);
+                }
+            }
+        }
+        s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat;
+    }
+    __syncthreads();
+    const size_t rr = (size_t)s * R + ring;
+    if (tid < s_cnt[0]) v.r_sharp[rr * 12 + tid] = fp[p_sh[tid]];
+    if (tid < s_cnt[1]) v.r_less_sharp[rr * 120 + tid] = fp[p_ls[tid]];
+    if (tid < s_cnt[2]) v.r_flat[rr * 24 + tid] = fp[p_fl[tid]];
+    // ---- surfPointsLessFlatScan (wave 0); sectors with sp >= ep are skipped,
+    // as the reference's `continue`
+    if (wave == 0) {
+        float4* o_lf = v.r_lf_scan + rr * C;
+        int n_lf = 0;
+        for (int kb = rs; kb < re; kb += 64) {
+            const int k = kb + lane;
+            bool take = false;
+            if (k < re) {
+                for (int j = 0; j < 6; ++j) {
+                    const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+                    if (k >= sp && k <= ep) { take = sp < ep; break; }
+                }
+                take = take && llab[k - lo] <= 0;
+            }
+            const unsigned long long m = __ballot(take);
+            const int pos = n_lf + __popcll(m & ((1ull << lane) - 1));
+            if (take && pos < C) o_lf[pos] = fp[k];
+            n_lf += __popcll(m);
+        }
+        if (lane == 0) {
+            int* rc = v.ring_cnt + rr * 4;
+            rc[0] = s_cnt[0]; rc[1] = s_cnt[1]; rc[2] = s_cnt[2];
+            v.r_lf_n[rr] = min(n_lf, C);
+        }
+    }
+    for (int k = tid; k < hi - lo; k += blockDim.x) {
+        sm[lo + k] = lsm[k]; picked[lo + k] = lpk[k]; lab[lo + k] = llab[k];
+    }
 }
 
 // ---------------------------------------------------------------- per-ring VoxelGrid(0.2)
@@ -363,8 +607,8 @@ int fa_features_run(slo_ctx* ctx) {
     dim3 gh((v.H + T - 1) / T, S);
     SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "fa_extract_ring0", k_fa_extract, dim3(1, S), dim3(64), 0, v, 0);
-    if (R > 1) SLO_LAUNCH(ctx, "fa_extract", k_fa_extract, dim3(R - 1, S), dim3(64), 0, v, 1);
+    SLO_LAUNCH(ctx, "fa_extract_ring0", k_fa_extract_ring0, dim3(1, S), dim3(256), 0, v);
+    if (R > 1) SLO_LAUNCH(ctx, "fa_extract", k_fa_extract, dim3(R - 1, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());

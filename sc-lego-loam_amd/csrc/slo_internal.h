@@ -65,6 +65,7 @@ struct StreamState {
     double det_min_dist;
     int32_t flags;
     int32_t err;
+    unsigned long long dbg[8];            // diagnostic counters (slo_get "dbg"), not part of the algorithm
 };
 
 // Spatial hash grid over one [S][es] cloud (built by grid_build): cell edge

@@ -33,7 +33,7 @@ _DT = {"range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": 
        "fa_iters": np.int32, "mapped": np.float32, "n_keyframes": np.int32, "flags": np.int32,
        "keyposes": np.float32, "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64,
        "detect": np.int32, "detect_f": np.float64, "mo_iters": np.int32, "tobe_mapped": np.float32,
-       "err": np.int32}
+       "err": np.int32, "dbg": np.uint64}
 
 
 class SloError(RuntimeError):
