@@ -169,6 +169,9 @@ struct DevView {
     double* sc_sect;     // [S][KFMAX][NS]
 };
 
+#ifndef SLO_DIAG
+#define SLO_DIAG 0              // 1: kernels add phase cycle counts to StreamState::dbg
+#endif
 #define SLO_MO_BLOCKS 64
 #define SLO_MO_PART 55          // 27 double-double sums (21 AtA + 6 AtB) + correspondence count
 #define SLO_RECORD_FLOATS 40
@@ -201,29 +204,90 @@ __device__ inline void xcd_stream_chunk(int b, int NB, int& s, int& chunk) {
 // Visit every grid point of stream s in the cells at Chebyshev ring r around
 // cell (cx, cy, cz): f(point) for points of exactly those cells (buckets are
 // shared by hash collisions, so membership is re-checked).
+//
+// The walk is latency-bound (hash -> bucket (offset, count) -> entries), so
+// it is batched for memory-level parallelism: the ring's cells go in groups
+// of GRING_BATCH whose bucket words are all loaded before any is used, and the
+// group's entries are then visited as one flattened list, GRING_UNROLL
+// independent loads at a time.  Visiting order does not matter to the callers
+// (their results are order-independent: exact distances, ties by index).
+#define GRING_BATCH 8
+#define GRING_UNROLL 4
+__device__ inline void grid_ring_cell(int r, int c, int& dx, int& dy, int& dz) {
+    // c-th cell of Chebyshev ring r (r >= 1): the two full z-faces, then the
+    // y-faces of the inner z-slices, then the x-edges of what remains
+    const int w = 2 * r + 1, face = w * w;
+    if (c < 2 * face) {
+        dz = c < face ? -r : r;
+        const int q = c % face;
+        dy = q / w - r; dx = q % w - r;
+        return;
+    }
+    c -= 2 * face;
+    const int inner = 2 * r - 1;             // z-slices strictly inside
+    if (c < 2 * w * inner) {
+        dy = c < w * inner ? -r : r;
+        const int q = c % (w * inner);
+        dz = q / w - r + 1; dx = q % w - r;
+        return;
+    }
+    c -= 2 * w * inner;                      // remaining: x = +-r, |y| < r, |z| < r
+    dx = c < inner * inner ? -r : r;
+    const int q = c % (inner * inner);
+    dz = q / inner - r + 1; dy = q % inner - r + 1;
+}
+
 template <class F>
 __device__ inline void grid_ring(const GridView& g, int s, int cx, int cy, int cz, int r, F&& f) {
     const size_t gb = (size_t)s * g.T;
     const int base = g.off[gb];
     const float4* E = g.ent + (size_t)s * g.es;
-    for (int dz = -r; dz <= r; ++dz)
-        for (int dy = -r; dy <= r; ++dy) {
-            const bool edge = (dz == -r || dz == r || dy == -r || dy == r);
-            const int step = (edge || r == 0) ? 1 : 2 * r;
-            for (int dx = -r; dx <= r; dx += step) {
-                const int tx = cx + dx, ty = cy + dy, tz = cz + dz;
-                const unsigned int b = grid_hash(tx, ty, tz, g.T);
-                const int m = g.cnt[gb + b];
-                if (m == 0) continue;
-                const float4* e = E + (g.off[gb + b] - base);
-                for (int k = 0; k < m; ++k) {
-                    const float4 p = e[k];
-                    if (grid_cell(p.x, g.inv) != tx || grid_cell(p.y, g.inv) != ty || grid_cell(p.z, g.inv) != tz)
-                        continue;
-                    f(p);
-                }
+    const int ncell = r == 0 ? 1 : (2 * r + 1) * (2 * r + 1) * (2 * r + 1) - (2 * r - 1) * (2 * r - 1) * (2 * r - 1);
+    for (int c0 = 0; c0 < ncell; c0 += GRING_BATCH) {
+        int tx[GRING_BATCH], ty[GRING_BATCH], tz[GRING_BATCH], st[GRING_BATCH], pre[GRING_BATCH + 1];
+#pragma unroll
+        for (int k = 0; k < GRING_BATCH; ++k) {
+            int dx = 0, dy = 0, dz = 0;
+            if (r > 0 && c0 + k < ncell) grid_ring_cell(r, c0 + k, dx, dy, dz);
+            tx[k] = cx + dx; ty[k] = cy + dy; tz[k] = cz + dz;
+        }
+        int m[GRING_BATCH];
+#pragma unroll
+        for (int k = 0; k < GRING_BATCH; ++k) {   // independent bucket loads
+            const bool live = c0 + k < ncell;
+            const unsigned int b = grid_hash(tx[k], ty[k], tz[k], g.T);
+            m[k] = live ? g.cnt[gb + b] : 0;
+            st[k] = live ? g.off[gb + b] - base : 0;
+        }
+        pre[0] = 0;
+#pragma unroll
+        for (int k = 0; k < GRING_BATCH; ++k) pre[k + 1] = pre[k] + m[k];
+        const int tot = pre[GRING_BATCH];
+        for (int t0 = 0; t0 < tot; t0 += GRING_UNROLL) {
+            float4 p[GRING_UNROLL];
+            int ckx[GRING_UNROLL], cky[GRING_UNROLL], ckz[GRING_UNROLL];
+#pragma unroll
+            for (int u = 0; u < GRING_UNROLL; ++u) {   // independent entry loads
+                const int t = t0 + u;
+                // the cell of flattened entry t: the last q with pre[q] <= t
+                // (selects, not indexing: the small arrays stay in registers)
+                int sk = st[0], pk = 0, ax = tx[0], ay = ty[0], az = tz[0];
+#pragma unroll
+                for (int q = 1; q < GRING_BATCH; ++q)
+                    if (t >= pre[q]) { sk = st[q]; pk = pre[q]; ax = tx[q]; ay = ty[q]; az = tz[q]; }
+                ckx[u] = ax; cky[u] = ay; ckz[u] = az;
+                p[u] = t < tot ? E[sk + (t - pk)] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < GRING_UNROLL; ++u) {
+                if (t0 + u >= tot) break;
+                if (grid_cell(p[u].x, g.inv) != ckx[u] || grid_cell(p[u].y, g.inv) != cky[u] ||
+                    grid_cell(p[u].z, g.inv) != ckz[u])
+                    continue;
+                f(p[u]);
             }
         }
+    }
 }
 
 struct VgParams;

@@ -26,8 +26,12 @@ namespace slo_la {
 
 // Householder QR least squares, A (m x n, row-major, m <= 8, n <= 6), b (m).
 // On success b[0..n) holds x; returns 0 if a diagonal of R is below eps
-// (the caller then zero-fills x, as cv::solve does).
-SLO_LA_HD int qr_solve(float* A, int m, int n, float* b) {
+// (the caller then zero-fills x, as cv::solve does).  Sizes are template
+// parameters so every loop unrolls and the small arrays live in registers
+// (on the GPU a runtime-sized local array goes to scratch memory).
+template <int M, int N>
+SLO_LA_HD int qr_solve_t(float* A, float* b) {
+    constexpr int m = M, n = N;
     float vl[8], hf[8];
     const float eps = FLT_EPSILON * 10;
     for (int l = 0; l < n; l++) {
@@ -65,20 +69,32 @@ SLO_LA_HD int qr_solve(float* A, int m, int n, float* b) {
 }
 
 // x = solve(A, b) as cv::solve(DECOMP_QR) returns it (zeros on failure)
-SLO_LA_HD void solve_qr(const float* Ain, const float* bin, int m, int n, float* x) {
-    float A[48], b[8];
-    for (int i = 0; i < m * n; ++i) A[i] = Ain[i];
-    for (int i = 0; i < m; ++i) b[i] = bin[i];
-    if (!qr_solve(A, m, n, b)) {
-        for (int i = 0; i < n; ++i) x[i] = 0.0f;
+template <int M, int N>
+SLO_LA_HD void solve_qr_t(const float* Ain, const float* bin, float* x) {
+    float A[M * N], b[M];
+#pragma unroll
+    for (int i = 0; i < M * N; ++i) A[i] = Ain[i];
+#pragma unroll
+    for (int i = 0; i < M; ++i) b[i] = bin[i];
+    if (!qr_solve_t<M, N>(A, b)) {
+        for (int i = 0; i < N; ++i) x[i] = 0.0f;
         return;
     }
-    for (int i = 0; i < n; ++i) x[i] = b[i];
+    for (int i = 0; i < N; ++i) x[i] = b[i];
+}
+// the shapes the path uses: 3x3 (FA), 5x3 (MO plane fit), 6x6 (MO)
+SLO_LA_HD void solve_qr(const float* A, const float* b, int m, int n, float* x) {
+    if (m == 3 && n == 3) solve_qr_t<3, 3>(A, b, x);
+    else if (m == 5 && n == 3) solve_qr_t<5, 3>(A, b, x);
+    else solve_qr_t<6, 6>(A, b, x);
 }
 
 // Jacobi eigen-decomposition of a symmetric n x n (n <= 6)
-SLO_LA_HD void eigen_sym(const float* S, int n, float* W, float* V) {
-    float A[36];
+template <int N>
+SLO_LA_HD void eigen_sym_t(const float* S, float* W, float* V) {
+    constexpr int n = N;
+    float A[N * N];
+#pragma unroll
     for (int i = 0; i < n * n; ++i) A[i] = S[i];
     const float eps = FLT_EPSILON;
     int indR[6], indC[6];
@@ -146,6 +162,10 @@ SLO_LA_HD void eigen_sym(const float* S, int n, float* W, float* V) {
             for (i = 0; i < n; i++) { float a = V[n * m + i]; V[n * m + i] = V[n * k + i]; V[n * k + i] = a; }
         }
     }
+}
+SLO_LA_HD void eigen_sym(const float* S, int n, float* W, float* V) {
+    if (n == 3) eigen_sym_t<3>(S, W, V);
+    else eigen_sym_t<6>(S, W, V);
 }
 
 SLO_LA_HD void inv(const float* S, int n, float* D) {

@@ -157,139 +157,148 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
 // one XCD's L2, and each takes a contiguous run of the (voxel-ordered, hence
 // spatially coherent) queries, so the map cells a workgroup walks are mostly
 // the ones its neighbours just pulled in.
+//
+// Per round of 256 queries every thread computes its query's Jacobian row
+// (matA row, matB entry; MO:1432-1441) into LDS — a zero row when the query is
+// rejected — and the 27 products of the normal equations are then summed from
+// LDS in double-double by 216 threads (27 terms x 8 slices of 32 rows) and
+// folded into per-term totals.  The query phase so keeps no accumulators in
+// registers, which is what bounds its occupancy.
+__device__ __constant__ int8_t kMoTermI[27] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 2, 2, 2, 2, 3, 3, 3, 4, 4, 5,
+                                               0, 1, 2, 3, 4, 5};
+__device__ __constant__ int8_t kMoTermJ[27] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5,
+                                               6, 6, 6, 6, 6, 6};
+
+__device__ inline bool mo_row(const DevView& v, int s, const StreamState& st, int q, float* row) {
+    const float* t = st.transformTobeMapped;
+    using slo_libm::sinf_;
+    using slo_libm::cosf_;
+    const float cRoll = cosf_(t[0]), sRoll = sinf_(t[0]), cPitch = cosf_(t[1]), sPitch = sinf_(t[1]);
+    const float cYaw = cosf_(t[2]), sYaw = sinf_(t[2]);
+    const float tX = t[3], tY = t[4], tZ = t[5];
+    const float srx = sRoll, crx = cRoll, sry = sPitch, cry = cPitch, srz = sYaw, crz = cYaw;
+    const int nc = st.n_corner_ds;
+    const bool corner = q < nc;
+    const float4 po4 = corner ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
+    const P4 po{po4.x, po4.y, po4.z, po4.w};
+    // pointAssociateToMap (MO:534-548)
+    const float x1 = cYaw * po.x - sYaw * po.y, y1 = sYaw * po.x + cYaw * po.y, z1 = po.z;
+    const float x2 = x1, y2 = cRoll * y1 - sRoll * z1, z2 = sRoll * y1 + cRoll * z1;
+    const P4 sel{cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, po.w};
+    int ind[5];
+    float dis[5];
+    const int n = corner ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
+    if (n < 5 || !(dis[4] < 1.0)) return false;
+    float cfx, cfy, cfz, cfw;
+    if (corner) {   // cornerOptimization (MO:1265-1346)
+        const float4* mc = v.map_c_ds + (size_t)s * v.cap_mc;
+        float cx = 0, cy = 0, cz = 0;
+        for (int j = 0; j < 5; j++) { float4 m = mc[ind[j]]; cx += m.x; cy += m.y; cz += m.z; }
+        cx /= 5; cy /= 5; cz /= 5;
+        float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
+        for (int j = 0; j < 5; j++) {
+            float4 m = mc[ind[j]];
+            float ax = m.x - cx, ay = m.y - cy, az = m.z - cz;
+            a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
+            a22 += ay * ay; a23 += ay * az;
+            a33 += az * az;
+        }
+        a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
+        float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33}, D1[3], V1[9];
+        slo_la::eigen_sym(A1, 3, D1, V1);
+        if (!(D1[0] > 3 * D1[1])) return false;
+        const float x0 = sel.x, y0 = sel.y, z0 = sel.z;
+        const float xa = (float)(cx + 0.1 * V1[0]), ya = (float)(cy + 0.1 * V1[1]), za = (float)(cz + 0.1 * V1[2]);
+        const float xb = (float)(cx - 0.1 * V1[0]), yb = (float)(cy - 0.1 * V1[1]), zb = (float)(cz - 0.1 * V1[2]);
+        const float m1 = (x0 - xa) * (y0 - yb) - (x0 - xb) * (y0 - ya);
+        const float m2 = (x0 - xa) * (z0 - zb) - (x0 - xb) * (z0 - za);
+        const float m3 = (y0 - ya) * (z0 - zb) - (y0 - yb) * (z0 - za);
+        const float a012 = sqrtf(m1 * m1 + m2 * m2 + m3 * m3);
+        const float l12 = sqrtf((xa - xb) * (xa - xb) + (ya - yb) * (ya - yb) + (za - zb) * (za - zb));
+        const float la = ((ya - yb) * m1 + (za - zb) * m2) / a012 / l12;
+        const float lb = -((xa - xb) * m1 - (za - zb) * m3) / a012 / l12;
+        const float lc = -((xa - xb) * m2 + (ya - yb) * m3) / a012 / l12;
+        const float ld2 = a012 / l12;
+        const float sw = (float)(1 - 0.9 * fabsf(ld2));
+        cfx = sw * la; cfy = sw * lb; cfz = sw * lc; cfw = sw * ld2;
+        if (!(sw > 0.1)) return false;
+    } else {        // surfOptimization (MO:1348-1399)
+        const float4* ms = v.map_s_ds + (size_t)s * v.cap_ms;
+        float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3];
+        for (int j = 0; j < 5; j++) { float4 m = ms[ind[j]]; A0[j * 3] = m.x; A0[j * 3 + 1] = m.y; A0[j * 3 + 2] = m.z; }
+        slo_la::solve_qr(A0, B0, 5, 3, X0);
+        float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
+        const float ps = sqrtf(pa * pa + pb * pb + pc * pc);
+        pa /= ps; pb /= ps; pc /= ps; pd /= ps;
+        for (int j = 0; j < 5; j++) {
+            float4 m = ms[ind[j]];
+            if (fabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) return false;
+        }
+        const float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
+        const float sw = (float)(1 - 0.9 * fabsf(pd2) / sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
+        cfx = sw * pa; cfy = sw * pb; cfz = sw * pc; cfw = sw * pd2;
+        if (!(sw > 0.1)) return false;
+    }
+    // LMOptimization rows (MO:1418-1441)
+    const P4& p = po;
+    row[0] = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * cfx +
+             (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * cfy +
+             (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * cfz;
+    row[1] = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * cfx +
+             ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * cfz;
+    row[2] = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * cfx +
+             (crx * crz * p.x - crx * srz * p.y) * cfy +
+             ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * cfz;
+    row[3] = cfx; row[4] = cfy; row[5] = cfz;
+    row[6] = -cfw;
+    return true;
+}
+
 __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
     int s, chunk;
     xcd_stream_chunk(blockIdx.x, SLO_MO_BLOCKS, s, chunk);
     if (s >= v.S) return;
     const StreamState& st = v.st[s];
-    slo_dd::DD acc[27];
-    for (int k = 0; k < 27; ++k) acc[k] = slo_dd::zero();
+    const int tid = threadIdx.x;
+    __shared__ float rows[256][8];
+    __shared__ int shn[4];
+    const int term = tid >> 3, slice = tid & 7;   // 216 reducing threads: 27 terms x 8 slices
+    const int ti = term < 27 ? kMoTermI[term] : 0, tj = term < 27 ? kMoTermJ[term] : 0;
+    slo_dd::DD tot = slo_dd::zero();   // per-term total (valid in slice 0)
     int nsel = 0;
     const bool live = st.mo_ran && st.map_ok && !st.mo_converged;
     if (live) {
-        const float* t = st.transformTobeMapped;
-        using slo_libm::sinf_;
-        using slo_libm::cosf_;
-        const float cRoll = cosf_(t[0]), sRoll = sinf_(t[0]), cPitch = cosf_(t[1]), sPitch = sinf_(t[1]);
-        const float cYaw = cosf_(t[2]), sYaw = sinf_(t[2]);
-        const float tX = t[3], tY = t[4], tZ = t[5];
-        const float srx = sRoll, crx = cRoll, sry = sPitch, cry = cPitch, srz = sYaw, crz = cYaw;
-        const int nc = st.n_corner_ds, nsq = st.n_surf_total_ds;
-        const float4* mc = v.map_c_ds + (size_t)s * v.cap_mc;
-        const float4* ms = v.map_s_ds + (size_t)s * v.cap_ms;
-        const int nq = nc + nsq, per = (nq + SLO_MO_BLOCKS - 1) / SLO_MO_BLOCKS;
+        const int nq = st.n_corner_ds + st.n_surf_total_ds, per = (nq + SLO_MO_BLOCKS - 1) / SLO_MO_BLOCKS;
         const int q0 = chunk * per, q1 = min(nq, q0 + per);
-        for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
-            const bool corner = q < nc;
-            float4 po4 = corner ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
-            P4 po{po4.x, po4.y, po4.z, po4.w};
-            // pointAssociateToMap (MO:534-548)
-            float x1 = cYaw * po.x - sYaw * po.y, y1 = sYaw * po.x + cYaw * po.y, z1 = po.z;
-            float x2 = x1, y2 = cRoll * y1 - sRoll * z1, z2 = sRoll * y1 + cRoll * z1;
-            P4 sel{cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, po.w};
-            int ind[5]; float dis[5];
-            int n = corner ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
-            if (n < 5 || !(dis[4] < 1.0)) continue;
-            float cfx, cfy, cfz, cfw;
-            bool ok = false;
-            if (corner) {
-                float cx = 0, cy = 0, cz = 0;
-                for (int j = 0; j < 5; j++) { float4 m = mc[ind[j]]; cx += m.x; cy += m.y; cz += m.z; }
-                cx /= 5; cy /= 5; cz /= 5;
-                float a11 = 0, a12 = 0, a13 = 0, a22 = 0, a23 = 0, a33 = 0;
-                for (int j = 0; j < 5; j++) {
-                    float4 m = mc[ind[j]];
-                    float ax = m.x - cx, ay = m.y - cy, az = m.z - cz;
-                    a11 += ax * ax; a12 += ax * ay; a13 += ax * az;
-                    a22 += ay * ay; a23 += ay * az;
-                    a33 += az * az;
+        for (int qb = q0; qb < q1; qb += 256) {   // uniform trip count
+            float row[7] = {0, 0, 0, 0, 0, 0, 0};
+            const int q = qb + tid;
+            if (q < q1 && mo_row(v, s, st, q, row)) ++nsel;
+            else for (int k = 0; k < 7; ++k) row[k] = 0.0f;   // rejected: contributes exact zeros
+            for (int k = 0; k < 7; ++k) rows[tid][k] = row[k];
+            __syncthreads();
+            if (term < 27) {
+                slo_dd::DD acc = slo_dd::zero();
+                for (int r = slice * 32; r < slice * 32 + 32; ++r)
+                    slo_dd::add(acc, (double)rows[r][ti] * (double)rows[r][tj]);
+                for (int o = 4; o > 0; o >>= 1) {   // the 8 slices of a term are 8 adjacent lanes
+                    slo_dd::DD y{__shfl_xor(acc.hi, o, 64), __shfl_xor(acc.lo, o, 64)};
+                    slo_dd::merge(acc, y);
                 }
-                a11 /= 5; a12 /= 5; a13 /= 5; a22 /= 5; a23 /= 5; a33 /= 5;
-                float A1[9] = {a11, a12, a13, a12, a22, a23, a13, a23, a33}, D1[3], V1[9];
-                slo_la::eigen_sym(A1, 3, D1, V1);
-                if (D1[0] > 3 * D1[1]) {
-                    float x0 = sel.x, y0 = sel.y, z0 = sel.z;
-                    float x1 = (float)(cx + 0.1 * V1[0]), y1 = (float)(cy + 0.1 * V1[1]), z1 = (float)(cz + 0.1 * V1[2]);
-                    float x2 = (float)(cx - 0.1 * V1[0]), y2 = (float)(cy - 0.1 * V1[1]), z2 = (float)(cz - 0.1 * V1[2]);
-                    float m1 = (x0 - x1) * (y0 - y2) - (x0 - x2) * (y0 - y1);
-                    float m2 = (x0 - x1) * (z0 - z2) - (x0 - x2) * (z0 - z1);
-                    float m3 = (y0 - y1) * (z0 - z2) - (y0 - y2) * (z0 - z1);
-                    float a012 = sqrtf(m1 * m1 + m2 * m2 + m3 * m3);
-                    float l12 = sqrtf((x1 - x2) * (x1 - x2) + (y1 - y2) * (y1 - y2) + (z1 - z2) * (z1 - z2));
-                    float la = ((y1 - y2) * m1 + (z1 - z2) * m2) / a012 / l12;
-                    float lb = -((x1 - x2) * m1 - (z1 - z2) * m3) / a012 / l12;
-                    float lc = -((x1 - x2) * m2 + (y1 - y2) * m3) / a012 / l12;
-                    float ld2 = a012 / l12;
-                    float sw = (float)(1 - 0.9 * fabsf(ld2));
-                    cfx = sw * la; cfy = sw * lb; cfz = sw * lc; cfw = sw * ld2;
-                    ok = sw > 0.1;
-                }
-            } else {
-                float A0[15], B0[5] = {-1, -1, -1, -1, -1}, X0[3];
-                for (int j = 0; j < 5; j++) { float4 m = ms[ind[j]]; A0[j * 3] = m.x; A0[j * 3 + 1] = m.y; A0[j * 3 + 2] = m.z; }
-                slo_la::solve_qr(A0, B0, 5, 3, X0);
-                float pa = X0[0], pb = X0[1], pc = X0[2], pd = 1;
-                float ps = sqrtf(pa * pa + pb * pb + pc * pc);
-                pa /= ps; pb /= ps; pc /= ps; pd /= ps;
-                bool planeValid = true;
-                for (int j = 0; j < 5; j++) {
-                    float4 m = ms[ind[j]];
-                    if (fabsf(pa * m.x + pb * m.y + pc * m.z + pd) > 0.2) { planeValid = false; break; }
-                }
-                if (planeValid) {
-                    float pd2 = pa * sel.x + pb * sel.y + pc * sel.z + pd;
-                    float sw = (float)(1 - 0.9 * fabsf(pd2) / sqrtf(sqrtf(sel.x * sel.x + sel.y * sel.y + sel.z * sel.z)));
-                    cfx = sw * pa; cfy = sw * pb; cfz = sw * pc; cfw = sw * pd2;
-                    ok = sw > 0.1;
-                }
+                slo_dd::merge(tot, acc);
             }
-            if (!ok) continue;
-            const P4& p = po;
-            float arx = (crx * sry * srz * p.x + crx * crz * sry * p.y - srx * sry * p.z) * cfx +
-                        (-srx * srz * p.x - crz * srx * p.y - crx * p.z) * cfy +
-                        (crx * cry * srz * p.x + crx * cry * crz * p.y - cry * srx * p.z) * cfz;
-            float ary = ((cry * srx * srz - crz * sry) * p.x + (sry * srz + cry * crz * srx) * p.y + crx * cry * p.z) * cfx +
-                        ((-cry * crz - srx * sry * srz) * p.x + (cry * srz - crz * srx * sry) * p.y - crx * sry * p.z) * cfz;
-            float arz = ((crz * srx * sry - cry * srz) * p.x + (-cry * crz - srx * sry * srz) * p.y) * cfx +
-                        (crx * crz * p.x - crx * srz * p.y) * cfy +
-                        ((sry * srz + cry * crz * srx) * p.x + (crz * sry - cry * srx * srz) * p.y) * cfz;
-            const double a[6] = {arx, ary, arz, cfx, cfy, cfz};
-            const double b = -cfw;
-            int k = 0;
-            for (int i = 0; i < 6; ++i)
-                for (int j = i; j < 6; ++j) slo_dd::add(acc[k++], a[i] * a[j]);
-            for (int i = 0; i < 6; ++i) slo_dd::add(acc[21 + i], a[i] * b);
-            ++nsel;
+            __syncthreads();
         }
     }
-    // block reduction of the double-double partial sums (order-independent
-    // after the final rounding, slo_ddsum.h)
-    __shared__ slo_dd::DD sh[4][27];
-    __shared__ int shn[4];
-    for (int o = 32; o > 0; o >>= 1) {
-        for (int k = 0; k < 27; ++k) {
-            slo_dd::DD y{__shfl_xor(acc[k].hi, o, 64), __shfl_xor(acc[k].lo, o, 64)};
-            slo_dd::merge(acc[k], y);
-        }
-        nsel += __shfl_xor(nsel, o, 64);
-    }
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        for (int k = 0; k < 27; ++k) sh[w][k] = acc[k];
-        shn[w] = nsel;
-    }
+    for (int o = 32; o > 0; o >>= 1) nsel += __shfl_xor(nsel, o, 64);
+    if ((tid & 63) == 0) shn[tid >> 6] = nsel;
     __syncthreads();
     double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + chunk) * SLO_MO_PART;
-    if (threadIdx.x < 27) {
-        slo_dd::DD r = sh[0][threadIdx.x];
-        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) slo_dd::merge(r, sh[ww][threadIdx.x]);
-        part[2 * threadIdx.x] = r.hi;
-        part[2 * threadIdx.x + 1] = r.lo;
-    } else if (threadIdx.x == 27) {
-        int n = shn[0];
-        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) n += shn[ww];
-        part[54] = (double)n;
+    if (term < 27 && slice == 0) {
+        part[2 * term] = tot.hi;
+        part[2 * term + 1] = tot.lo;
     }
+    if (tid == 0) part[54] = (double)(shn[0] + shn[1] + shn[2] + shn[3]);
 }
 
 // LMOptimization tail (MO:1445-1498) for one stream
