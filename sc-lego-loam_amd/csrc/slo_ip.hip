@@ -57,15 +57,22 @@ __global__ void k_ip_init(DevView v) {
     v.fl[2 * s + 1] = -1;
 }
 
+// A workgroup takes IP_PTS_PER_WG consecutive points (thread t: points t,
+// t+256, ...).  Points arrive in firing order — all rings of one azimuth, then
+// the next — so the workgroup's owner atomics keep hitting the same few
+// cache lines (one per ring over ~IP_PTS_PER_WG/R columns) while they are
+// resident in L2, instead of touching every line once per point.
+#define IP_PTS_PER_WG 2048
 __global__ void k_ip_project(DevView v) {
     const int s = blockIdx.y;
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const int n = v.npts[s];
     int fmin = INT_MAX, fmax = -1;
-    if (i < n) {
+    for (int k = 0; k < IP_PTS_PER_WG / 256; ++k) {
+        const int i = blockIdx.x * IP_PTS_PER_WG + k * 256 + threadIdx.x;
+        if (i >= n) break;
         float4 p = v.pts[(size_t)s * v.P + i];
         if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-            fmin = i; fmax = i;
+            fmin = min(fmin, i); fmax = max(fmax, i);
             int row, col; float rg;
             if (project_point(v.cfg, p, row, col, rg))
                 atomicMax(&v.owner[(size_t)s * v.H + row * v.cfg.horizon_scan + col], i);
@@ -175,21 +182,40 @@ __global__ void k_cc_union(DevView v) {
     }
 }
 
+// Component size and row set (seed excluded, Q3).  Large components put
+// thousands of pixels on one root, so the lanes of a wave that share a root
+// are combined first (one atomic per distinct root per wave).
 __global__ void k_cc_stats(DevView v) {
     const int s = blockIdx.y;
     const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= v.H) return;
     const size_t base = (size_t)s * v.H;
     int* par = v.parent + base;
-    if (par[p] < 0) return;
-    int r = p;
-    int y = par[r];
-    while (y != r) { r = y; y = par[r]; }
-    par[p] = r;
-    atomicAdd(&v.csize[base + r], 1);
-    if (p != r) {
-        const int row = p / v.cfg.horizon_scan;
-        atomicOr(&v.crows[2 * (base + r) + (row >> 6)], 1ull << (row & 63));
+    int r = -1;
+    unsigned long long rows0 = 0, rows1 = 0;
+    if (p < v.H && par[p] >= 0) {
+        r = p;
+        int y = par[r];
+        while (y != r) { r = y; y = par[r]; }
+        par[p] = r;
+        if (p != r) {
+            const int row = p / v.cfg.horizon_scan;
+            (row >> 6 ? rows1 : rows0) = 1ull << (row & 63);
+        }
+    }
+    unsigned long long pending = __ballot(r >= 0);
+    while (pending) {
+        const int leader = __ffsll((long long)pending) - 1;
+        const int lr = __shfl(r, leader, 64);
+        const bool mine = r == lr;
+        const unsigned long long grp = __ballot(mine);
+        unsigned long long a = mine ? rows0 : 0ull, b = mine ? rows1 : 0ull;
+        for (int o = 32; o > 0; o >>= 1) { a |= __shfl_xor(a, o, 64); b |= __shfl_xor(b, o, 64); }
+        if ((int)(threadIdx.x & 63) == leader) {
+            atomicAdd(&v.csize[base + lr], __popcll(grp));
+            if (a) atomicOr(&v.crows[2 * (base + lr)], a);
+            if (b) atomicOr(&v.crows[2 * (base + lr) + 1], b);
+        }
+        pending &= ~grp;
     }
 }
 
@@ -330,7 +356,7 @@ int ip_run(slo_ctx* ctx) {
     SLO_CHECK(hipMemsetAsync(v.owner, 0xff, sizeof(int32_t) * (size_t)S * v.H, ctx->stream));
     SLO_LAUNCH(ctx, "ip_init", k_ip_init, dim3((S + 63) / 64), dim3(64), 0, v);
     const int T = 256;
-    dim3 gp((v.P + T - 1) / T, S), gh((v.H + T - 1) / T, S), gr(v.cfg.n_scan, S);
+    dim3 gp((v.P + IP_PTS_PER_WG - 1) / IP_PTS_PER_WG, S), gh((v.H + T - 1) / T, S), gr(v.cfg.n_scan, S);
     SLO_LAUNCH(ctx, "ip_project", k_ip_project, gp, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_image", k_ip_image, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_cc_union", k_cc_union, gh, dim3(T), 0, v);
