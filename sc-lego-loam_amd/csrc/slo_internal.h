@@ -160,6 +160,8 @@ struct DevView {
     float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
     float4* cur_st_ds;   // [S][cap_st]
     double* mo_part;     // [S][MO_BLOCKS][SLO_MO_PART] partial A^T A / A^T b (double-double) + count
+    int cap_q;           // mapping queries per stream: cap_less_sharp + cap_st
+    int32_t* mo_nn;      // [S][cap_q][5] 5-NN map indices of each query (-1: rejected)
     // hash grids: odometry "kd-tree" clouds (corner / surf) and the DS maps
     GridView g_oc, g_os, g_mc, g_ms;
     // ---- Scan Context history (Scancontext.h:99-106)
@@ -184,9 +186,13 @@ struct DevView {
 #define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
 #define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud
 
+// Locality-preserving bucket of cell (x, y, z): x-adjacent cells get adjacent
+// buckets, so a ring walk reads each row of cells' bucket words from one cache
+// line and their entries (stored in bucket order) as one contiguous run.
+// Distinct cells can share a bucket (the index wraps mod T); walkers re-check
+// cell membership, so collisions cost time, never correctness.
 __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
-    return (((unsigned int)x * 73856093u) ^ ((unsigned int)y * 19349663u) ^ ((unsigned int)z * 83492791u)) &
-           (unsigned int)(T - 1);
+    return ((unsigned int)x + (unsigned int)y * 1031u + (unsigned int)z * 620531u) & (unsigned int)(T - 1);
 }
 __host__ __device__ inline int grid_cell(float x, float inv) { return (int)floorf(x * inv); }
 
@@ -211,7 +217,7 @@ __device__ inline void xcd_stream_chunk(int b, int NB, int& s, int& chunk) {
 // group's entries are then visited as one flattened list, GRING_UNROLL
 // independent loads at a time.  Visiting order does not matter to the callers
 // (their results are order-independent: exact distances, ties by index).
-#define GRING_BATCH 8
+#define GRING_BATCH 4
 #define GRING_UNROLL 4
 __device__ inline void grid_ring_cell(int r, int c, int& dx, int& dy, int& dz) {
     // c-th cell of Chebyshev ring r (r >= 1): the two full z-faces, then the

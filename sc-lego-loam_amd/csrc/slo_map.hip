@@ -134,17 +134,27 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
     const int cx = grid_cell(q.x, g.inv), cy = grid_cell(q.y, g.inv), cz = grid_cell(q.z, g.inv);
     const int rmax = (int)ceilf(g.inv);
     int n = 0;
+    // sorted top-5 by (distance, index); empty slots are (+inf, INT_MAX).
+    // Insertion is unrolled with constant indices so the lists stay in
+    // registers (a data-dependent index would put them in scratch memory).
+#pragma unroll
+    for (int k = 0; k < 5; ++k) { od[k] = __builtin_huge_valf(); oi[k] = INT_MAX; }
+    auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
     for (int r = 0; r <= rmax; ++r) {
         grid_ring(g, s, cx, cy, cz, r, [&](const float4& p) {
             const float d = sqd(q, p.x, p.y, p.z);
             const int idx = __float_as_int(p.w);
-            if (n == 5 && (d > od[4] || (d == od[4] && idx > oi[4]))) return;
-            int pos = n < 5 ? n : 4;
-            while (pos > 0 && (od[pos - 1] > d || (od[pos - 1] == d && oi[pos - 1] > idx))) {
-                od[pos] = od[pos - 1]; oi[pos] = oi[pos - 1]; --pos;
+            if (!less(d, idx, od[4], oi[4])) return;
+            bool placed = false;
+#pragma unroll
+            for (int k = 4; k >= 1; --k) {
+                if (!placed) {
+                    if (less(d, idx, od[k - 1], oi[k - 1])) { od[k] = od[k - 1]; oi[k] = oi[k - 1]; }
+                    else { od[k] = d; oi[k] = idx; placed = true; }
+                }
             }
-            od[pos] = d; oi[pos] = idx;
-            if (n < 5) ++n;
+            if (!placed) { od[0] = d; oi[0] = idx; }
+            n = min(n + 1, 5);
         });
         const float reach = (float)r * g.cell;
         if (r >= 1 && n == 5 && od[4] < reach * reach) break;
@@ -169,26 +179,66 @@ __device__ __constant__ int8_t kMoTermI[27] = {0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 
 __device__ __constant__ int8_t kMoTermJ[27] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 2, 3, 4, 5, 3, 4, 5, 4, 5, 5,
                                                6, 6, 6, 6, 6, 6};
 
-__device__ inline bool mo_row(const DevView& v, int s, const StreamState& st, int q, float* row) {
+// query q of stream s (corner queries first, then surf+outlier) and its
+// map-frame position (pointAssociateToMap, MO:534-548)
+struct MoTrig {
+    float srx, crx, sry, cry, srz, crz, tX, tY, tZ;
+};
+__device__ inline MoTrig mo_trig(const StreamState& st) {
     const float* t = st.transformTobeMapped;
-    using slo_libm::sinf_;
-    using slo_libm::cosf_;
-    const float cRoll = cosf_(t[0]), sRoll = sinf_(t[0]), cPitch = cosf_(t[1]), sPitch = sinf_(t[1]);
-    const float cYaw = cosf_(t[2]), sYaw = sinf_(t[2]);
-    const float tX = t[3], tY = t[4], tZ = t[5];
-    const float srx = sRoll, crx = cRoll, sry = sPitch, cry = cPitch, srz = sYaw, crz = cYaw;
+    MoTrig g;
+    g.crx = slo_libm::cosf_(t[0]); g.srx = slo_libm::sinf_(t[0]);
+    g.cry = slo_libm::cosf_(t[1]); g.sry = slo_libm::sinf_(t[1]);
+    g.crz = slo_libm::cosf_(t[2]); g.srz = slo_libm::sinf_(t[2]);
+    g.tX = t[3]; g.tY = t[4]; g.tZ = t[5];
+    return g;
+}
+__device__ inline P4 mo_query(const DevView& v, int s, const StreamState& st, int q, const MoTrig& g, P4& po) {
     const int nc = st.n_corner_ds;
-    const bool corner = q < nc;
-    const float4 po4 = corner ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
-    const P4 po{po4.x, po4.y, po4.z, po4.w};
-    // pointAssociateToMap (MO:534-548)
+    const float4 po4 = q < nc ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
+    po = P4{po4.x, po4.y, po4.z, po4.w};
+    const float cRoll = g.crx, sRoll = g.srx, cPitch = g.cry, sPitch = g.sry, cYaw = g.crz, sYaw = g.srz;
     const float x1 = cYaw * po.x - sYaw * po.y, y1 = sYaw * po.x + cYaw * po.y, z1 = po.z;
     const float x2 = x1, y2 = cRoll * y1 - sRoll * z1, z2 = sRoll * y1 + cRoll * z1;
-    const P4 sel{cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, po.w};
+    return P4{cPitch * x2 + sPitch * z2 + g.tX, y2 + g.tY, -sPitch * x2 + cPitch * z2 + g.tZ, po.w};
+}
+
+// The 5-NN of every query, one thread per query, into mo_nn (index -1 in the
+// first slot = rejected: fewer than 5 within 1 m).  A kernel of its own so its
+// few registers give full occupancy to the latency-bound grid walk.
+__global__ void __launch_bounds__(256) k_mo_knn(DevView v) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, SLO_MO_BLOCKS, s, chunk);
+    if (s >= v.S) return;
+    const StreamState& st = v.st[s];
+    if (!(st.mo_ran && st.map_ok && !st.mo_converged)) return;
+    const MoTrig g = mo_trig(st);
+    const int nc = st.n_corner_ds, nq = nc + st.n_surf_total_ds, per = (nq + SLO_MO_BLOCKS - 1) / SLO_MO_BLOCKS;
+    const int q0 = chunk * per, q1 = min(nq, q0 + per);
+    int32_t* nn = v.mo_nn + (size_t)s * v.cap_q * 5;
+    for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
+        P4 po;
+        const P4 sel = mo_query(v, s, st, q, g, po);
+        int ind[5];
+        float dis[5];
+        const int n = q < nc ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
+        const bool ok = n == 5 && dis[4] < 1.0;   // MO:1281 / 1364
+#pragma unroll
+        for (int k = 0; k < 5; ++k) nn[(size_t)q * 5 + k] = ok ? ind[k] : -1;
+    }
+}
+
+__device__ inline bool mo_row(const DevView& v, int s, const StreamState& st, int q, float* row) {
+    const MoTrig g = mo_trig(st);
+    const float srx = g.srx, crx = g.crx, sry = g.sry, cry = g.cry, srz = g.srz, crz = g.crz;
+    const bool corner = q < st.n_corner_ds;
+    P4 po;
+    const P4 sel = mo_query(v, s, st, q, g, po);
+    const int32_t* nn = v.mo_nn + ((size_t)s * v.cap_q + q) * 5;
     int ind[5];
-    float dis[5];
-    const int n = corner ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
-    if (n < 5 || !(dis[4] < 1.0)) return false;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) ind[k] = nn[k];
+    if (ind[0] < 0) return false;
     float cfx, cfy, cfz, cfw;
     if (corner) {   // cornerOptimization (MO:1265-1346)
         const float4* mc = v.map_c_ds + (size_t)s * v.cap_mc;
@@ -273,7 +323,13 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
         for (int qb = q0; qb < q1; qb += 256) {   // uniform trip count
             float row[7] = {0, 0, 0, 0, 0, 0, 0};
             const int q = qb + tid;
+#if SLO_DIAG
+            const unsigned long long t_row = clock64();
+#endif
             if (q < q1 && mo_row(v, s, st, q, row)) ++nsel;
+#if SLO_DIAG
+            if ((threadIdx.x & 63) == 0) atomicAdd(&v.st[s].dbg[1], clock64() - t_row);   // wave time per round
+#endif
             else for (int k = 0; k < 7; ++k) row[k] = 0.0f;   // rejected: contributes exact zeros
             for (int k = 0; k < 7; ++k) rows[tid][k] = row[k];
             __syncthreads();
@@ -551,6 +607,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
     if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
     for (int it = 0; it < 10; ++it) {
+        SLO_LAUNCH(ctx, "mo_knn", k_mo_knn, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_solve", k_mo_solve, dim3(S), dim3(64), 0, v, it);
     }
