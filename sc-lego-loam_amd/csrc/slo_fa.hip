@@ -11,10 +11,10 @@
 //     values persisted from earlier scans (Appendix A Q5).
 //   extractFeatures (FA:680-784): rings are independent except through the
 //     stale cloudSmoothness[4] entry of ring 0 (Q5), so ring 0 runs first and
-//     rings 1..R-1 then run in parallel, one workgroup each, staged in LDS
-//     (k_fa_extract: wave rank sorts with the exact libstdc++ introsort
-//     restatement for sectors holding ties, Q4/Q6; the greedy picks are
-//     sequential per ring as in the reference).
+//     rings 1..R-1 then run in parallel, staged in LDS (k_fa_sort: wave
+//     bitonic sorts, with the exact libstdc++ introsort restatement for
+//     sectors holding ties, Q4/Q6; k_fa_pick: the greedy picks, sequential
+//     per ring as in the reference).
 //   per-ring VoxelGrid(0.2) (FA:778-782): one block per ring, bitonic sort
 //     of (voxel idx, position) keys in LDS, centroid of each voxel summed in
 //     position order (DESIGN.md "VoxelGrid order").
@@ -208,100 +208,140 @@ __global__ void __launch_bounds__(256) k_fa_extract_ring0(DevView v) { extract_r
 // Rank sort of one sector by one wave: rank = number of smaller values, so
 // equal ranks mean equal values; *tie is raised (and the sector left as it
 // was) when any two values are equal.  NE = ceil(n / 64) elements per lane.
+// One wave sorts one sector of n <= 64*NE entries in registers: the key is
+// (order-preserving curvature bits << 32 | point index), so keys are unique
+// and the bitonic network's result is the sorted order; padding keys are
+// all-ones.  If two curvatures are equal the result is NOT written (the
+// caller then runs the exact introsort restatement on the untouched sector):
+// without ties a sort's result is unique, so it equals libstdc++'s.
+__device__ inline unsigned int f2ord_fa(float f) {
+    const unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float ord2f_fa(unsigned int o) {
+    return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
+}
+
 template <int NE>
-__device__ inline void rank_sort_wave(Smooth* a, int n, int lane, int* tie_flag) {
-    Smooth mine[NE];
-    int rank[NE];
+__device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_flag) {
+    unsigned long long k[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
-        rank[e] = 0;
-        mine[e] = lane + 64 * e < n ? a[lane + 64 * e] : Smooth{__builtin_nanf(""), -1};
-    }
-    bool tie = false;
-#pragma unroll 4
-    for (int t = 0; t < n; ++t) {
-        const float y = a[t].value;   // one broadcast LDS read
-#pragma unroll
-        for (int e = 0; e < NE; ++e) {
-            rank[e] += y < mine[e].value;
-            tie |= (y == mine[e].value) & (t != lane + 64 * e);
+        const int i = e * 64 + lane;
+        k[e] = ~0ull;
+        if (i < n) {
+            const Smooth x = a[i];
+            k[e] = ((unsigned long long)f2ord_fa(x.value) << 32) | (unsigned int)x.ind;
         }
+    }
+    constexpr int N = 64 * NE;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {   // partner in the same lane
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    if (e & es) continue;
+                    const int p = e * 64 + lane;
+                    const bool up = (p & size) == 0;
+                    const unsigned long long x = k[e], y = k[e | es];
+                    const bool sw = up ? (x > y) : (x < y);
+                    k[e] = sw ? y : x;
+                    k[e | es] = sw ? x : y;
+                }
+            } else {              // partner in lane ^ stride
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const int p = e * 64 + lane;
+                    const unsigned long long y = __shfl_xor(k[e], stride, 64);
+                    const bool up = (p & size) == 0;
+                    const bool lower = (lane & stride) == 0;
+                    // the lower position keeps the min when ascending
+                    const bool take_min = (up == lower);
+                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+            }
+        }
+    }
+    // ties: equal curvature bits in adjacent positions
+    bool tie = false;
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int p = e * 64 + lane;
+        const unsigned long long up1 = __shfl_up(k[e], 1, 64);                      // lane - 1
+        const unsigned long long wrap = e > 0 ? __shfl(k[e > 0 ? e - 1 : 0], 63, 64) : ~0ull;   // all lanes
+        const unsigned long long prev = lane == 0 ? wrap : up1;
+        if (p > 0 && p < n && (prev >> 32) == (k[e] >> 32)) tie = true;
     }
     const bool any_tie = __any(tie);
     if (!any_tie) {
-        // every lane has read everything (the t loop) before anyone writes:
-        // the wave executes the reads above in order, then this barrier-free
-        // scatter; a wave-level fence orders LDS reads before the writes
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
 #pragma unroll
-        for (int e = 0; e < NE; ++e)
-            if (lane + 64 * e < n) a[rank[e]] = mine[e];
+        for (int e = 0; e < NE; ++e) {
+            const int p = e * 64 + lane;
+            if (p < n) a[p] = Smooth{ord2f_fa((unsigned int)(k[e] >> 32)), (int)(unsigned int)k[e]};
+        }
     } else if (lane == 0) {
         *tie_flag = 1;
     }
 }
 
-// Rings 1..R-1, one 256-thread workgroup per (ring, stream), ring = 1 + blockIdx.x.
+// Rings 1..R-1 (ring = 1 + blockIdx.x), in two launches.
 //
 // A ring's sorts, picks and neighbour marks only touch the ring's own points
 // [rs-5, re+5): its sectors' smoothness entries are this scan's (positions
-// in [5, S-5), ind = position) and marks stop at +-5.  So the window is staged
-// in LDS in compact form (smoothness entries; picked, label, ground flag as
-// bytes; curvature; column as 16 bits), worked on there with plain LDS
-// accesses, and written back; concurrent rings never share a word.
+// in [5, S-5), ind = position) and marks stop at +-5.  Both kernels stage that
+// window in LDS in compact form, work on it with plain LDS accesses and write
+// it back; concurrent rings never share a word.  A ring whose window exceeds
+// SLO_RING_STAGE takes the global-memory restatement (extract_ring_global)
+// inside k_fa_pick.
 //
-// Sector sorts (std::sort on [sp, ep), Q4/Q6): the sorted order is unique
-// when a sector has no equal curvatures, so a wave rank-sorts each sector;
-// only a sector holding a tie is sorted by one lane with the exact libstdc++
-// introsort restatement (slo_introsort.h), whose order of equal keys is the
-// reference's.
+// k_fa_sort (256 threads): the six sector sorts (std::sort on [sp, ep),
+// Q4/Q6).  Without equal curvatures a sort's result is unique, so a wave
+// bitonic-sorts each sector in registers; only a sector holding a tie is
+// sorted by one lane with the exact libstdc++ introsort restatement
+// (slo_introsort.h), whose order of equal keys is the reference's.  Then the
+// pick eligibility that picks cannot change (curvature, ground flag) is
+// evaluated by all lanes and compacted into per-sector candidate lists in
+// visiting order (sharp ep..sp, flat sp..ep), stored for k_fa_pick.
 //
-// Picks (FA:701-766): eligibility that picks cannot change (curvature,
-// ground flag) is evaluated by all lanes and compacted into per-sector
-// candidate lists in visiting order; one lane then walks only those, testing
-// picked[] and marking neighbours, and records the picked indices; all lanes
-// gather the points afterwards.  The less-flat collection (label <= 0,
-// FA:768-776) runs after all six sectors' picks with a wave ballot: a sector's
-// picks only label that sector's own points, so the result equals the
-// reference's per-sector interleaving.
+// k_fa_pick (one wave): the greedy picks (FA:701-766) walk only those lists,
+// testing picked[] and marking neighbours, on one lane — a small LDS footprint
+// so many rings' serial walks share each CU — then all lanes gather the
+// points and collect the less-flat points (label <= 0, FA:768-776) with a
+// wave ballot: a sector's picks only label that sector's own points, so
+// collecting after all six sectors equals the reference's interleaving.
 #define SLO_RING_STAGE 2080
 
-__global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
+__device__ inline bool ring_window(const DevView& v, int s, int ring, int& rs, int& re, int& lo, int& hi) {
+    const int* se = v.ring_se + (size_t)s * v.cfg.n_scan * 2;
+    rs = se[2 * ring]; re = se[2 * ring + 1];
+    lo = max(0, rs - 5); hi = min(v.H, re + 5);
+    return hi > lo && hi - lo <= SLO_RING_STAGE;
+}
+
+__global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int s = blockIdx.y;
     const int ring = 1 + blockIdx.x;
-    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    int rs, re, lo, hi;
+    if (!ring_window(v, s, ring, rs, re, lo, hi)) return;   // uniform: k_fa_pick handles it
+    const int R = v.cfg.n_scan;
     const size_t base = (size_t)s * v.H;
     const int S = v.st[s].seg_count;
-    const int* se = v.ring_se + (size_t)s * R * 2;
-    const int rs = se[2 * ring], re = se[2 * ring + 1];
-    const int lo = max(0, rs - 5), hi = min(v.H, re + 5);
-    if (!(hi > lo && hi - lo <= SLO_RING_STAGE)) {   // uniform per block
-        extract_ring_global(v, s, ring);
-        return;
-    }
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Smooth* sm = v.smooth + base;
-    int32_t* picked = v.picked + base;
-    int32_t* lab = v.clabel + base;
-    const float4* fp = v.fpts + base;
-
     __shared__ Smooth lsm[SLO_RING_STAGE];
     __shared__ float lcv[SLO_RING_STAGE];
-    __shared__ uint16_t lcol[SLO_RING_STAGE];
-    __shared__ int8_t lpk[SLO_RING_STAGE], llab[SLO_RING_STAGE];
     __shared__ uint8_t lgf[SLO_RING_STAGE];
-    __shared__ int16_t l_sh[SLO_RING_STAGE], l_fl[SLO_RING_STAGE];
-    __shared__ int n_sh[6], n_fl[6], s_tie[6], s_cnt[3];
-    __shared__ int p_sh[12], p_ls[120], p_fl[24];
+    __shared__ int s_tie[6];
     for (int k = tid; k < hi - lo; k += blockDim.x) {
-        const size_t g = base + lo + k;
-        lsm[k] = sm[lo + k]; lpk[k] = (int8_t)v.picked[g]; llab[k] = (int8_t)v.clabel[g];
-        lcv[k] = v.curv[g]; lcol[k] = (uint16_t)v.seg_col[g]; lgf[k] = v.seg_ground[g];
+        lsm[k] = sm[lo + k];
+        lcv[k] = v.curv[base + lo + k];
+        lgf[k] = v.seg_ground[base + lo + k];
     }
     if (tid < 6) s_tie[tid] = 0;
     __syncthreads();
-
     // ---- sector sorts: two rounds of (up to) four sectors, one wave each
     for (int r0 = 0; r0 < 6; r0 += 4) {
         const int j = r0 + wave;
@@ -310,12 +350,10 @@ __global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
             Smooth* a = &lsm[sp - lo];
             switch ((n + 63) >> 6) {
                 case 0: break;
-                case 1: if (n > 1) rank_sort_wave<1>(a, n, lane, &s_tie[j]); break;
-                case 2: rank_sort_wave<2>(a, n, lane, &s_tie[j]); break;
-                case 3: rank_sort_wave<3>(a, n, lane, &s_tie[j]); break;
-                case 4: rank_sort_wave<4>(a, n, lane, &s_tie[j]); break;
-                case 5: rank_sort_wave<5>(a, n, lane, &s_tie[j]); break;
-                case 6: rank_sort_wave<6>(a, n, lane, &s_tie[j]); break;
+                case 1: if (n > 1) bitonic_sort_wave<1>(a, n, lane, &s_tie[j]); break;
+                case 2: bitonic_sort_wave<2>(a, n, lane, &s_tie[j]); break;
+                case 3: case 4: bitonic_sort_wave<4>(a, n, lane, &s_tie[j]); break;
+                case 5: case 6: case 7: case 8: bitonic_sort_wave<8>(a, n, lane, &s_tie[j]); break;
                 default: if (lane == 0) s_tie[j] = 1; break;
             }
         }
@@ -326,9 +364,10 @@ __global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
         slo_sort::std_sort(&lsm[sp - lo], ep - sp, SmoothLess());
     }
     __syncthreads();
-
-    // ---- candidate lists (window offsets), sharp in visiting order ep..sp,
-    // flat sp..ep
+    // ---- candidate lists: point indices as window offsets, in visiting order
+    int16_t* l_sh = v.ex_list + (size_t)s * v.H * 2;
+    int16_t* l_fl = l_sh + v.H;
+    int* cnt = v.ex_cnt + ((size_t)s * R + ring) * 12;
     for (int r0 = 0; r0 < 6; r0 += 4) {
         const int j = r0 + wave;
         if (j >= 6) continue;
@@ -338,45 +377,93 @@ __global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
             for (int kb = 0; kb <= ep - sp; kb += 64) {
                 const int ks = ep - kb - lane, kf = sp + kb + lane;
                 bool es = false, ef = false;
+                int is = 0, iff = 0;
                 if (ks >= sp) {
-                    const int ind = lsm[ks - lo].ind;
-                    es = ind < S && lcv[ind - lo] > v.cfg.edge_threshold && lgf[ind - lo] == 0;
+                    is = lsm[ks - lo].ind;
+                    es = is < S && lcv[is - lo] > v.cfg.edge_threshold && lgf[is - lo] == 0;
                 }
                 if (kf <= ep) {
-                    const int ind = lsm[kf - lo].ind;
-                    ef = ind < S && lcv[ind - lo] < v.cfg.surf_threshold && lgf[ind - lo] == 1;
+                    iff = lsm[kf - lo].ind;
+                    ef = iff < S && lcv[iff - lo] < v.cfg.surf_threshold && lgf[iff - lo] == 1;
                 }
                 const unsigned long long ms = __ballot(es), mf = __ballot(ef);
                 const unsigned long long below = (1ull << lane) - 1;
-                if (es) l_sh[sp - lo + ns + __popcll(ms & below)] = (int16_t)(ks - lo);
-                if (ef) l_fl[sp - lo + nf + __popcll(mf & below)] = (int16_t)(kf - lo);
+                if (es) l_sh[sp + ns + __popcll(ms & below)] = (int16_t)(is - lo);
+                if (ef) l_fl[sp + nf + __popcll(mf & below)] = (int16_t)(iff - lo);
                 ns += __popcll(ms);
                 nf += __popcll(mf);
             }
-        if (lane == 0) { n_sh[j] = ns; n_fl[j] = nf; }
+        if (lane == 0) { cnt[2 * j] = ns; cnt[2 * j + 1] = nf; }
+    }
+    for (int k = tid; k < hi - lo; k += blockDim.x) sm[lo + k] = lsm[k];
+}
+
+__global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
+    const int s = blockIdx.y;
+    const int ring = 1 + blockIdx.x;
+    int rs, re, lo, hi;
+    if (!ring_window(v, s, ring, rs, re, lo, hi)) {   // uniform per block
+        extract_ring_global(v, s, ring);
+        return;
+    }
+    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const size_t base = (size_t)s * v.H;
+    const int lane = threadIdx.x;
+    int32_t* picked = v.picked + base;
+    int32_t* lab = v.clabel + base;
+    const float4* fp = v.fpts + base;
+    __shared__ uint16_t lcol[SLO_RING_STAGE];
+    __shared__ int8_t lpk[SLO_RING_STAGE], llab[SLO_RING_STAGE];
+    __shared__ int16_t l_sh[SLO_RING_STAGE], l_fl[SLO_RING_STAGE];
+    __shared__ int s_cnt[3];
+    __shared__ int p_sh[12], p_ls[120], p_fl[24];
+    const int16_t* g_sh = v.ex_list + (size_t)s * v.H * 2;
+    const int16_t* g_fl = g_sh + v.H;
+    const int* cnt = v.ex_cnt + ((size_t)s * R + ring) * 12;
+    for (int k = lane; k < hi - lo; k += 64) {
+        lpk[k] = (int8_t)picked[lo + k];
+        llab[k] = (int8_t)lab[lo + k];
+        lcol[k] = (uint16_t)v.seg_col[base + lo + k];
+    }
+    for (int j = 0; j < 6; ++j) {   // lists sit at their sector's positions
+        const int sp = sec_sp(rs, re, j);
+        const int ns = cnt[2 * j], nf = cnt[2 * j + 1];
+        if (sec_ep(rs, re, j) <= sp) continue;
+        for (int c = lane; c < ns; c += 64) l_sh[sp - lo + c] = g_sh[sp + c];
+        for (int c = lane; c < nf; c += 64) l_fl[sp - lo + c] = g_fl[sp + c];
     }
     __syncthreads();
-
-    // ---- greedy picks, one lane, LDS only
-    if (tid == 0) {
+    if (lane == 0) {
         auto mark = [&](int ind) __attribute__((always_inline)) {   // FA:719-731 / 752-764
-            auto colw = [&](int i) __attribute__((always_inline)) { return i < 0 ? 0u : (uint32_t)lcol[i - lo]; };
-            for (int l = 1; l <= 5; l++) {
-                if (abs((int)(colw(ind + l) - colw(ind + l - 1))) > 10) break;
-                lpk[ind + l - lo] = 1;
+            // the 11 columns around ind, loaded together (colInd[-1] -> 0, Q5),
+            // then the two break-at-gap walks on registers
+            int c[11];
+#pragma unroll
+            for (int k = 0; k < 11; ++k) {
+                const int i = ind - 5 + k;
+                c[k] = i < 0 ? 0 : (int)lcol[max(i, lo) - lo];
             }
-            for (int l = -1; l >= -5; l--) {
-                if (abs((int)(colw(ind + l) - colw(ind + l + 1))) > 10) break;
-                if (ind + l >= 0) lpk[ind + l - lo] = 1;
+            bool go = true;
+#pragma unroll
+            for (int l = 1; l <= 5; l++) {
+                go = go && abs(c[5 + l] - c[4 + l]) <= 10;
+                if (go) lpk[ind + l - lo] = 1;
+            }
+            go = true;
+#pragma unroll
+            for (int l = 1; l <= 5; l++) {
+                go = go && abs(c[5 - l] - c[6 - l]) <= 10;
+                if (go && ind - l >= 0) lpk[ind - l - lo] = 1;
             }
         };
         int n_sharp = 0, n_lsharp = 0, n_flat = 0;
         for (int j = 0; j < 6; j++) {
             const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
             if (sp >= ep) continue;
+            const int ns = cnt[2 * j], nf = cnt[2 * j + 1];
             int largestPickedNum = 0;
-            for (int c = 0; c < n_sh[j]; ++c) {
-                const int ind = lsm[l_sh[sp - lo + c]].ind;
+            for (int c = 0; c < ns; ++c) {
+                const int ind = lo + l_sh[sp - lo + c];
                 if (lpk[ind - lo] == 0) {
                     largestPickedNum++;
                     if (largestPickedNum <= 2) {
@@ -394,8 +481,8 @@ __global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
                 }
             }
             int smallestPickedNum = 0;
-            for (int c = 0; c < n_fl[j]; ++c) {
-                const int ind = lsm[l_fl[sp - lo + c]].ind;
+            for (int c = 0; c < nf; ++c) {
+                const int ind = lo + l_fl[sp - lo + c];
                 if (lpk[ind - lo] == 0) {
                     llab[ind - lo] = -1;
                     p_fl[n_flat++] = ind;
@@ -410,37 +497,36 @@ __global__ void __launch_bounds__(256) k_fa_extract(DevView v) {
     }
     __syncthreads();
     const size_t rr = (size_t)s * R + ring;
-    if (tid < s_cnt[0]) v.r_sharp[rr * 12 + tid] = fp[p_sh[tid]];
-    if (tid < s_cnt[1]) v.r_less_sharp[rr * 120 + tid] = fp[p_ls[tid]];
-    if (tid < s_cnt[2]) v.r_flat[rr * 24 + tid] = fp[p_fl[tid]];
-    // ---- surfPointsLessFlatScan (wave 0); sectors with sp >= ep are skipped,
-    // as the reference's `continue`
-    if (wave == 0) {
-        float4* o_lf = v.r_lf_scan + rr * C;
-        int n_lf = 0;
-        for (int kb = rs; kb < re; kb += 64) {
-            const int k = kb + lane;
-            bool take = false;
-            if (k < re) {
-                for (int j = 0; j < 6; ++j) {
-                    const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
-                    if (k >= sp && k <= ep) { take = sp < ep; break; }
-                }
-                take = take && llab[k - lo] <= 0;
+    for (int t = lane; t < s_cnt[0]; t += 64) v.r_sharp[rr * 12 + t] = fp[p_sh[t]];
+    for (int t = lane; t < s_cnt[1]; t += 64) v.r_less_sharp[rr * 120 + t] = fp[p_ls[t]];
+    for (int t = lane; t < s_cnt[2]; t += 64) v.r_flat[rr * 24 + t] = fp[p_fl[t]];
+    // ---- surfPointsLessFlatScan; sectors with sp >= ep are skipped, as the
+    // reference's `continue`
+    float4* o_lf = v.r_lf_scan + rr * C;
+    int n_lf = 0;
+    for (int kb = rs; kb < re; kb += 64) {
+        const int k = kb + lane;
+        bool take = false;
+        if (k < re) {
+            for (int j = 0; j < 6; ++j) {
+                const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+                if (k >= sp && k <= ep) { take = sp < ep; break; }
             }
-            const unsigned long long m = __ballot(take);
-            const int pos = n_lf + __popcll(m & ((1ull << lane) - 1));
-            if (take && pos < C) o_lf[pos] = fp[k];
-            n_lf += __popcll(m);
+            take = take && llab[k - lo] <= 0;
         }
-        if (lane == 0) {
-            int* rc = v.ring_cnt + rr * 4;
-            rc[0] = s_cnt[0]; rc[1] = s_cnt[1]; rc[2] = s_cnt[2];
-            v.r_lf_n[rr] = min(n_lf, C);
-        }
+        const unsigned long long m = __ballot(take);
+        const int pos = n_lf + __popcll(m & ((1ull << lane) - 1));
+        if (take && pos < C) o_lf[pos] = fp[k];
+        n_lf += __popcll(m);
     }
-    for (int k = tid; k < hi - lo; k += blockDim.x) {
-        sm[lo + k] = lsm[k]; picked[lo + k] = lpk[k]; lab[lo + k] = llab[k];
+    if (lane == 0) {
+        int* rc = v.ring_cnt + rr * 4;
+        rc[0] = s_cnt[0]; rc[1] = s_cnt[1]; rc[2] = s_cnt[2];
+        v.r_lf_n[rr] = min(n_lf, C);
+    }
+    for (int k = lane; k < hi - lo; k += 64) {
+        picked[lo + k] = lpk[k];
+        lab[lo + k] = llab[k];
     }
 }
 
@@ -608,7 +694,10 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_extract_ring0", k_fa_extract_ring0, dim3(1, S), dim3(256), 0, v);
-    if (R > 1) SLO_LAUNCH(ctx, "fa_extract", k_fa_extract, dim3(R - 1, S), dim3(256), 0, v);
+    if (R > 1) {
+        SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R - 1, S), dim3(256), 0, v);
+        SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R - 1, S), dim3(64), 0, v);
+    }
     SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());

@@ -135,6 +135,8 @@ struct DevView {
     float4* kd_corner;   // [S][cap_less_sharp]  copy the "tree" searches (setInputCloud copies)
     float4* kd_surf;     // [S][cap_less_flat]
     int32_t* roff_cur;   // [S][2][R+1] first index of each ring in less_sharp / less_flat
+    int16_t* ex_list;    // [S][2][H] per-sector pick candidates (sharp, flat), window offsets
+    int32_t* ex_cnt;     // [S][R][6][2] candidate counts
     int32_t* roff_last;  // [S][2][R+1] the same for corner_last / surf_last
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2

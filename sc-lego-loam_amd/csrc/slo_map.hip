@@ -326,11 +326,12 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
 #if SLO_DIAG
             const unsigned long long t_row = clock64();
 #endif
-            if (q < q1 && mo_row(v, s, st, q, row)) ++nsel;
+            const bool okrow = q < q1 && mo_row(v, s, st, q, row);
+            if (okrow) ++nsel;
+            else for (int k = 0; k < 7; ++k) row[k] = 0.0f;   // rejected: contributes exact zeros
 #if SLO_DIAG
             if ((threadIdx.x & 63) == 0) atomicAdd(&v.st[s].dbg[1], clock64() - t_row);   // wave time per round
 #endif
-            else for (int k = 0; k < 7; ++k) row[k] = 0.0f;   // rejected: contributes exact zeros
             for (int k = 0; k < 7; ++k) rows[tid][k] = row[k];
             __syncthreads();
             if (term < 27) {
