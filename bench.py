@@ -70,8 +70,6 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
         return steps * S * P * (16 + 4)
     if name == "ip_image":        # owner + point in; range, full cloud, ground, label, CC init out
         return steps * S * H * (4 + 16 + 4 + 16 + 1 + 4 + 8)
-    if name == "fa_extract":      # curvature, smoothness, picked, label, points per segmented point
-        return steps * int(c["seg_pts"].sum()) * (4 + 8 + 4 + 4 + 16)
     srch = lambda it: (it + 4) // 5  # noqa: E731  search iterations actually run
     if name == "fa_search_surf":  # per search: queries + 3 indices, the target cloud once
         return steps * int((srch(c["fa_iters"][:, 0]) * (c["flat"] * 28 + c["surf_last"] * 16)).sum())
@@ -81,9 +79,16 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
         return steps * int((c["fa_iters"][:, 0] * c["flat"] * (16 + 12 + 48)).sum())
     if name == "fa_iter_corner":
         return steps * int((c["fa_iters"][:, 1] * c["sharp"] * (16 + 8 + 32)).sum())
-    if name == "mo_corr":         # per iteration: query + 5 neighbours (96 B) + the maps once
-        per = (c["corner_ds"] + c["surf_total_ds"]) * 96 + (c["map_corner_ds"] + c["map_surf_ds"]) * 16
+    if name == "mo_corr":         # per iteration: query + 5 neighbour indices + 5 neighbours
+        per = (c["corner_ds"] + c["surf_total_ds"]) * (16 + 20 + 80)
         return map_steps * int((c["mo_iters"] * per).sum())
+    if name == "mo_knn":          # per iteration: query + 5 neighbour indices out, the map clouds once
+        per = (c["corner_ds"] + c["surf_total_ds"]) * (16 + 20) + (c["map_corner_ds"] + c["map_surf_ds"]) * 16
+        return map_steps * int((c["mo_iters"] * per).sum())
+    if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
+        return steps * int(c["seg_pts"].sum()) * (8 + 8 + 4 + 1 + 2)
+    if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
+        return steps * int(c["seg_pts"].sum()) * (4 + 4 + 4 + 4 + 4 + 2 + 16)
     return None
 
 
@@ -159,7 +164,7 @@ def main():
     errs = sum(int(ctx.get(s, "err")[0]) != 0 for s in range(S))
 
     # ---- instrumented pass: per-kernel HIP-event times on the context stream
-    roof, kt = None, {}
+    roof, kt, workload, gbs = None, {}, None, {}
     if a.profile_steps > 0:
         ctx.timing(True)
         ctx.timing_reset()
@@ -172,11 +177,16 @@ def main():
         kt = ctx.timing_read()
         ctx.timing(False)
         counts = stream_counts(ctx, S)
+        workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1}
         total_ms = sum(v[0] for v in kt.values())
         name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
         avg_s = ms / 1e3 / max(1, n)
         b = algo_bytes(name, counts, cfg, S, a.profile_steps, map_steps)
         ach = b / n / avg_s / 1e9 if b is not None else None
+        for kn, (kms, kcalls) in kt.items():
+            kb = algo_bytes(kn, counts, cfg, S, a.profile_steps, map_steps)
+            if kb is not None and kms > 0:
+                gbs[kn] = round(kb / (kms / 1e3) / 1e9, 1)
         roof = {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
                 "traffic": None, "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
@@ -213,6 +223,7 @@ def main():
             "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
             "stream_errors": errs,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
+            "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
             "setup_seconds": round(t_gen, 1),
         }
         print(json.dumps(out), flush=True)

@@ -78,8 +78,10 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         cfg->sc_num_candidates > SLO_SC_MAX_K || cfg->sc_num_ring < 1 || cfg->sc_num_ring > 64 ||
         cfg->sc_num_sector < 1 || cfg->sc_num_sector > SLO_SC_MAX_SECTOR ||
         cfg->sc_num_ring * cfg->sc_num_sector > SLO_SC_MAX_CELLS || cfg->surrounding_keyframe_search_num < 1 ||
-        cfg->surrounding_keyframe_search_num + 2 > 64 || cfg->sc_tree_making_period < 1)
-        return SLO_E_ARG;
+        cfg->surrounding_keyframe_search_num + 2 > 64 || cfg->sc_tree_making_period < 1 ||
+        !(cfg->nearest_feature_search_sq_dist >= 0.0f) ||
+        std::ceil(std::sqrt(cfg->nearest_feature_search_sq_dist) / SLO_ODO_SURF_CELL) > SLO_ODO_SURF_R)
+        return SLO_E_ARG;   // the odometry surf search box (SLO_ODO_SURF_R cells) must cover the gate
     slo_ctx* ctx = new slo_ctx();
     ctx->cfg = *cfg;
     ctx->dev = hip_device;
@@ -208,7 +210,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // in 1 m cells; the sparse corner cloud is searched by brute force.
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << 19, v.cap_ms, 0.5f) ||
-        slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat, 1.0f)) {
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 16, v.cap_less_flat, SLO_ODO_SURF_CELL)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }

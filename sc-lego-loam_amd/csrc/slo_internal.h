@@ -179,6 +179,8 @@ struct DevView {
 #define SLO_MO_BLOCKS 64
 #define SLO_MO_PART 55          // 27 double-double sums (21 AtA + 6 AtB) + correspondence count
 #define SLO_RECORD_FLOATS 40
+#define SLO_ODO_SURF_CELL 1.0f  // odometry surf grid cell (m, power of two)
+#define SLO_ODO_SURF_R 5        // its search box radius in cells: covers sqrt(nearest_feature_search_sq_dist)
 #define SLO_KFMAX 4096          // keyframe pose / Scan Context history capacity per stream
 #define SLO_SC_MAX_K 64         // NUM_CANDIDATES_FROM_TREE limit (C5 uses 50)
 #define SLO_SC_MAX_SECTOR 64
@@ -209,91 +211,94 @@ __device__ inline void xcd_stream_chunk(int b, int NB, int& s, int& chunk) {
     chunk = k % NB;
 }
 
-// Visit every grid point of stream s in the cells at Chebyshev ring r around
-// cell (cx, cy, cz): f(point) for points of exactly those cells (buckets are
-// shared by hash collisions, so membership is re-checked).
+// Ball queries on a hash grid.  The x coefficient of grid_hash is 1, so the
+// cells of one x-row (fixed y, z) occupy consecutive buckets, and the bucket
+// offsets are an exclusive prefix sum over [S][T + 1] buckets: a row's cells
+// [xa, xb] are ONE contiguous entry range [off[h(xa)], off[h(xb) + 1]) (two
+// when the buckets wrap at T).  A ball query therefore walks rows, not cells:
+// two offset loads and a run of entries per row.
 //
-// The walk is latency-bound (hash -> bucket (offset, count) -> entries), so
-// it is batched for memory-level parallelism: the ring's cells go in groups
-// of GRING_BATCH whose bucket words are all loaded before any is used, and the
-// group's entries are then visited as one flattened list, GRING_UNROLL
-// independent loads at a time.  Visiting order does not matter to the callers
-// (their results are order-independent: exact distances, ties by index).
-#define GRING_BATCH 4
-#define GRING_UNROLL 4
-__device__ inline void grid_ring_cell(int r, int c, int& dx, int& dy, int& dz) {
-    // c-th cell of Chebyshev ring r (r >= 1): the two full z-faces, then the
-    // y-faces of the inner z-slices, then the x-edges of what remains
-    const int w = 2 * r + 1, face = w * w;
-    if (c < 2 * face) {
-        dz = c < face ? -r : r;
-        const int q = c % face;
-        dy = q / w - r; dx = q % w - r;
-        return;
+// Rows of the (2R+1)^2 box around the query's cell are visited nearest first
+// (GridRows: by gap = max(|dy|-1,0)^2 + max(|dz|-1,0)^2, then dy^2 + dz^2).
+// With the caller's current bound b on the squared distance (it tightens as
+// points are accepted):
+//   * gap * cell^2 > b ends the walk: every later row is at least that far
+//     (computed distances are monotone in the coordinate differences, and
+//     these bounds are exact in float);
+//   * a row whose exact float lower bound ((0 + ey^2) + ez^2) exceeds b is
+//     skipped;
+//   * within a row only the x cells that can still hold a point within b are
+//     taken (with a safety margin: over-inclusion only costs a test).
+// Buckets are shared by hash collisions, so cell membership is re-checked
+// (each point is then visited at most once).  Callers' results are
+// order-independent (exact distances, ties by index).
+template <int R>
+struct GridRows {
+    static constexpr int N = (2 * R + 1) * (2 * R + 1);
+    int8_t dy[N], dz[N];
+    uint8_t gap[N];
+    constexpr GridRows() : dy(), dz(), gap() {
+        int k = 0, key[N] = {};
+        for (int a = -R; a <= R; ++a)
+            for (int b = -R; b <= R; ++b) {
+                const int ga = a < 0 ? -a - 1 : (a > 0 ? a - 1 : 0), gb = b < 0 ? -b - 1 : (b > 0 ? b - 1 : 0);
+                dy[k] = (int8_t)a; dz[k] = (int8_t)b; gap[k] = (uint8_t)(ga * ga + gb * gb);
+                key[k] = gap[k] * 1024 + a * a + b * b;
+                ++k;
+            }
+        for (int i = 1; i < N; ++i)   // insertion sort by key (stable)
+            for (int j = i; j > 0 && key[j - 1] > key[j]; --j) {
+                int t = key[j]; key[j] = key[j - 1]; key[j - 1] = t;
+                int8_t u = dy[j]; dy[j] = dy[j - 1]; dy[j - 1] = u;
+                u = dz[j]; dz[j] = dz[j - 1]; dz[j - 1] = u;
+                uint8_t w = gap[j]; gap[j] = gap[j - 1]; gap[j - 1] = w;
+            }
     }
-    c -= 2 * face;
-    const int inner = 2 * r - 1;             // z-slices strictly inside
-    if (c < 2 * w * inner) {
-        dy = c < w * inner ? -r : r;
-        const int q = c % (w * inner);
-        dz = q / w - r + 1; dx = q % w - r;
-        return;
-    }
-    c -= 2 * w * inner;                      // remaining: x = +-r, |y| < r, |z| < r
-    dx = c < inner * inner ? -r : r;
-    const int q = c % (inner * inner);
-    dz = q / inner - r + 1; dy = q % inner - r + 1;
-}
+};
+template <int R>
+__constant__ GridRows<R> kGridRows = GridRows<R>();
 
-template <class F>
-__device__ inline void grid_ring(const GridView& g, int s, int cx, int cy, int cz, int r, F&& f) {
-    const size_t gb = (size_t)s * g.T;
+#define GBALL_UNROLL 4
+template <int R, class B, class F>
+__device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
+    const float inv = g.inv, cell = g.cell, c2 = cell * cell;
+    const int cx = grid_cell(qx, inv), cy = grid_cell(qy, inv), cz = grid_cell(qz, inv);
+    const size_t gb = (size_t)s * (g.T + 1);
     const int base = g.off[gb];
     const float4* E = g.ent + (size_t)s * g.es;
-    const int ncell = r == 0 ? 1 : (2 * r + 1) * (2 * r + 1) * (2 * r + 1) - (2 * r - 1) * (2 * r - 1) * (2 * r - 1);
-    for (int c0 = 0; c0 < ncell; c0 += GRING_BATCH) {
-        int tx[GRING_BATCH], ty[GRING_BATCH], tz[GRING_BATCH], st[GRING_BATCH], pre[GRING_BATCH + 1];
+    for (int k = 0; k < GridRows<R>::N; ++k) {
+        const float b = bound();
+        if ((float)kGridRows<R>.gap[k] * c2 > b) break;
+        const int dy = kGridRows<R>.dy[k], dz = kGridRows<R>.dz[k];
+        const int yy = cy + dy, zz = cz + dz;
+        const float ey = dy > 0 ? (float)yy * cell - qy : (dy < 0 ? qy - (float)(yy + 1) * cell : 0.0f);
+        const float ez = dz > 0 ? (float)zz * cell - qz : (dz < 0 ? qz - (float)(zz + 1) * cell : 0.0f);
+        float lb = ey * ey;
+        lb += ez * ez;
+        if (lb > b) continue;
+        const float rx = sqrtf((b - lb) * 1.0001f + 1e-5f * b) + 1e-3f;
+        const int xa = max(cx - R, grid_cell(qx - rx, inv)), xb = min(cx + R, grid_cell(qx + rx, inv));
+        const int h = (int)grid_hash(xa, yy, zz, g.T), len = xb - xa + 1;
+        const int h2 = min(h + len, g.T);
+        int e0 = g.off[gb + h] - base, e1 = g.off[gb + h2] - base;
+        const int w1 = h + len - h2;   // buckets wrapped to the table start
+        const int f1 = w1 > 0 ? g.off[gb + w1] - base : 0;
+        for (int pass = 0; pass < 2; ++pass) {
+            for (int e = e0; e < e1; e += GBALL_UNROLL) {
+                float4 p[GBALL_UNROLL];
 #pragma unroll
-        for (int k = 0; k < GRING_BATCH; ++k) {
-            int dx = 0, dy = 0, dz = 0;
-            if (r > 0 && c0 + k < ncell) grid_ring_cell(r, c0 + k, dx, dy, dz);
-            tx[k] = cx + dx; ty[k] = cy + dy; tz[k] = cz + dz;
-        }
-        int m[GRING_BATCH];
+                for (int u = 0; u < GBALL_UNROLL; ++u)
+                    p[u] = e + u < e1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int k = 0; k < GRING_BATCH; ++k) {   // independent bucket loads
-            const bool live = c0 + k < ncell;
-            const unsigned int b = grid_hash(tx[k], ty[k], tz[k], g.T);
-            m[k] = live ? g.cnt[gb + b] : 0;
-            st[k] = live ? g.off[gb + b] - base : 0;
-        }
-        pre[0] = 0;
-#pragma unroll
-        for (int k = 0; k < GRING_BATCH; ++k) pre[k + 1] = pre[k] + m[k];
-        const int tot = pre[GRING_BATCH];
-        for (int t0 = 0; t0 < tot; t0 += GRING_UNROLL) {
-            float4 p[GRING_UNROLL];
-            int ckx[GRING_UNROLL], cky[GRING_UNROLL], ckz[GRING_UNROLL];
-#pragma unroll
-            for (int u = 0; u < GRING_UNROLL; ++u) {   // independent entry loads
-                const int t = t0 + u;
-                // the cell of flattened entry t: the last q with pre[q] <= t
-                // (selects, not indexing: the small arrays stay in registers)
-                int sk = st[0], pk = 0, ax = tx[0], ay = ty[0], az = tz[0];
-#pragma unroll
-                for (int q = 1; q < GRING_BATCH; ++q)
-                    if (t >= pre[q]) { sk = st[q]; pk = pre[q]; ax = tx[q]; ay = ty[q]; az = tz[q]; }
-                ckx[u] = ax; cky[u] = ay; ckz[u] = az;
-                p[u] = t < tot ? E[sk + (t - pk)] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int u = 0; u < GBALL_UNROLL; ++u) {
+                    if (e + u >= e1) break;
+                    const int px = grid_cell(p[u].x, inv);
+                    if (grid_cell(p[u].y, inv) != yy || grid_cell(p[u].z, inv) != zz || px < xa || px > xb) continue;
+                    f(p[u]);
+                }
             }
-#pragma unroll
-            for (int u = 0; u < GRING_UNROLL; ++u) {
-                if (t0 + u >= tot) break;
-                if (grid_cell(p[u].x, g.inv) != ckx[u] || grid_cell(p[u].y, g.inv) != cky[u] ||
-                    grid_cell(p[u].z, g.inv) != ckz[u])
-                    continue;
-                f(p[u]);
-            }
+            if (w1 <= 0) break;
+            e0 = 0; e1 = f1;
         }
     }
 }

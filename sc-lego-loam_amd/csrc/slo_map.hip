@@ -130,35 +130,37 @@ __device__ inline float sqd(const P4& q, float x, float y, float z) {
 // 1364).  Rings of cells grow outward; after ring r every unseen point is at
 // least r*cell away, so the search stops as soon as the 5th distance is below
 // (r*cell)^2, and it never needs rings beyond ceil(1 m / cell).
+// The 5 nearest map points of q whose squared distance is below 1 (ties ->
+// lowest index), n = how many were found (<= 5).  The residuals only use a
+// 5-NN whose 5th squared distance is < 1 (MO:1281 / 1364): when the true
+// 5-NN has that, these are the same five points; when it has not, n < 5 or
+// od[4] == 1 and the query is rejected either way.  So the search is a ball
+// of squared radius 1 — R = 2 cells of 0.5 m — whose bound is the current 5th
+// distance.
 __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float* od) {
-    const int cx = grid_cell(q.x, g.inv), cy = grid_cell(q.y, g.inv), cz = grid_cell(q.z, g.inv);
-    const int rmax = (int)ceilf(g.inv);
-    int n = 0;
-    // sorted top-5 by (distance, index); empty slots are (+inf, INT_MAX).
+    // sorted top-5 by (distance, index); empty slots are (1, INT_MAX).
     // Insertion is unrolled with constant indices so the lists stay in
     // registers (a data-dependent index would put them in scratch memory).
 #pragma unroll
-    for (int k = 0; k < 5; ++k) { od[k] = __builtin_huge_valf(); oi[k] = INT_MAX; }
+    for (int k = 0; k < 5; ++k) { od[k] = 1.0f; oi[k] = INT_MAX; }
+    if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return 0;
     auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
-    for (int r = 0; r <= rmax; ++r) {
-        grid_ring(g, s, cx, cy, cz, r, [&](const float4& p) {
-            const float d = sqd(q, p.x, p.y, p.z);
-            const int idx = __float_as_int(p.w);
-            if (!less(d, idx, od[4], oi[4])) return;
-            bool placed = false;
+    int n = 0;
+    grid_ball<2>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
+        const float d = sqd(q, p.x, p.y, p.z);
+        const int idx = __float_as_int(p.w);
+        if (!less(d, idx, od[4], oi[4])) return;
+        bool placed = false;
 #pragma unroll
-            for (int k = 4; k >= 1; --k) {
-                if (!placed) {
-                    if (less(d, idx, od[k - 1], oi[k - 1])) { od[k] = od[k - 1]; oi[k] = oi[k - 1]; }
-                    else { od[k] = d; oi[k] = idx; placed = true; }
-                }
+        for (int k = 4; k >= 1; --k) {
+            if (!placed) {
+                if (less(d, idx, od[k - 1], oi[k - 1])) { od[k] = od[k - 1]; oi[k] = oi[k - 1]; }
+                else { od[k] = d; oi[k] = idx; placed = true; }
             }
-            if (!placed) { od[0] = d; oi[0] = idx; }
-            n = min(n + 1, 5);
-        });
-        const float reach = (float)r * g.cell;
-        if (r >= 1 && n == 5 && od[4] < reach * reach) break;
-    }
+        }
+        if (!placed) { od[0] = d; oi[0] = idx; }
+        n = min(n + 1, 5);
+    });
     return n;
 }
 

@@ -47,19 +47,18 @@ __device__ inline float sqdist_flann(const P4& q, const float4& p) {  // ((0+d0^
 // fails it anyway, as it would after the reference's exact FLANN search.
 // Ties -> lowest index.
 __device__ inline void nn1_grid(const GridView& g, int s, float gate, const P4& q, int& bi, float& bd) {
-    bi = -1; bd = FLT_MAX;
-    if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return;
-    const int cx = grid_cell(q.x, g.inv), cy = grid_cell(q.y, g.inv), cz = grid_cell(q.z, g.inv);
-    const int rmax = (int)ceilf(sqrtf(gate) * g.inv);
-    for (int r = 0; r <= rmax; ++r) {
-        grid_ring(g, s, cx, cy, cz, r, [&](const float4& p) {
+    // the nearest point if its squared distance is <= gate (ties -> lowest
+    // index); the caller keeps it only when < gate (FA:1009), so the search
+    // is a ball of the gate's radius (R cells) bounded by the best so far
+    constexpr int R = SLO_ODO_SURF_R;
+    bi = INT_MAX; bd = gate;
+    if (isfinite(q.x) && isfinite(q.y) && isfinite(q.z))
+        grid_ball<R>(g, s, q.x, q.y, q.z, [&]() { return bd; }, [&](const float4& p) {
             const float d = sqdist_flann(q, p);
             const int idx = __float_as_int(p.w);
             if (d < bd || (d == bd && idx < bi)) { bd = d; bi = idx; }
         });
-        const float reach = (float)r * g.cell;
-        if (r >= 1 && bd < reach * reach) break;
-    }
+    if (bi == INT_MAX) { bi = -1; bd = FLT_MAX; }
 }
 
 // block-wide double-double sum of NV terms + one int (slo_ddsum.h); result

@@ -11,10 +11,10 @@
 // Non-finite points are skipped (the raw cloud is not dense, MO:1236); the
 // int32 overflow guard returns the input unchanged, as PCL does.
 //
-// Hash grid: 1 m cells, counting sort of the map points into hashed buckets.
-// The mapping residuals only use a 5-NN whose 5th distance is < 1 m
-// (MO:1273, 1355); every such neighbour lies in the 27 cells around the
-// query's cell, so searching those cells is exact (ties -> lowest index).
+// Hash grid: power-of-two cells, counting sort of the points into hashed
+// buckets [S][T + 1] (the last bucket of each stream stays empty, so a run of
+// consecutive buckets ends at off[h + 1]); queried by grid_ball
+// (slo_internal.h).
 #include "slo_internal.h"
 #include <hipcub/hipcub.hpp>
 #include <float.h>
@@ -224,7 +224,7 @@ __global__ void k_grid_count(const float4* pts, size_t stride, const int32_t* n,
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const float4 p = pts[(size_t)s * stride + i];
         const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
-        atomicAdd(&cnt[(size_t)s * T + b], 1);
+        atomicAdd(&cnt[(size_t)s * (T + 1) + b], 1);
     }
 }
 
@@ -232,11 +232,11 @@ __global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* 
                                const int32_t* off, int32_t* cur, float4* ent, size_t ent_stride) {
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
-    const int base = off[(size_t)s * T];
+    const int base = off[(size_t)s * (T + 1)];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const float4 p = pts[(size_t)s * stride + i];
         const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
-        const int pos = off[(size_t)s * T + b] - base + atomicAdd(&cur[(size_t)s * T + b], 1);
+        const int pos = off[(size_t)s * (T + 1) + b] - base + atomicAdd(&cur[(size_t)s * (T + 1) + b], 1);
         ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
     }
 }
@@ -244,12 +244,13 @@ __global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* 
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride) {
     const int S = ctx->S;
     const float inv = 1.0f / g.cell;
-    SLO_CHECK(hipMemsetAsync(g.cnt, 0, sizeof(int32_t) * (size_t)S * g.T, ctx->stream));
-    SLO_CHECK(hipMemsetAsync(g.cur, 0, sizeof(int32_t) * (size_t)S * g.T, ctx->stream));
+    const size_t nb = (size_t)S * (g.T + 1);   // [S][T + 1]: a zero bucket ends each stream
+    SLO_CHECK(hipMemsetAsync(g.cnt, 0, sizeof(int32_t) * nb, ctx->stream));
+    SLO_CHECK(hipMemsetAsync(g.cur, 0, sizeof(int32_t) * nb, ctx->stream));
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
     SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
     size_t tb = g.temp_bytes;
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)((size_t)S * g.T), ctx->stream));
+    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)nb, ctx->stream));
     SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
                g.off, g.cur, g.ent, g.ent_stride);
     SLO_CHECK(hipGetLastError());
@@ -267,12 +268,13 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) 
     g.T = T;
     g.cell = cell;
     g.ent_stride = ent_stride;
-    SLO_CHECK(hipMalloc(&g.cnt, sizeof(int32_t) * (size_t)S * T));
-    SLO_CHECK(hipMalloc(&g.cur, sizeof(int32_t) * (size_t)S * T));
-    SLO_CHECK(hipMalloc(&g.off, sizeof(int32_t) * (size_t)S * T));
+    const size_t nb = (size_t)S * (T + 1);
+    SLO_CHECK(hipMalloc(&g.cnt, sizeof(int32_t) * nb));
+    SLO_CHECK(hipMalloc(&g.cur, sizeof(int32_t) * nb));
+    SLO_CHECK(hipMalloc(&g.off, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.ent, sizeof(float4) * (size_t)S * ent_stride));
     size_t tb = 0;
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g.cnt, g.off, (int)((size_t)S * T), ctx->stream));
+    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g.cnt, g.off, (int)nb, ctx->stream));
     g.temp_bytes = tb;
     SLO_CHECK(hipMalloc(&g.temp, tb));
     return 0;
