@@ -58,14 +58,16 @@ __global__ void k_ip_init(DevView v) {
 }
 
 // A workgroup takes IP_PTS_PER_WG consecutive points (thread t: points t,
-// t+256, ...).  Points arrive in firing order — all rings of one azimuth, then
-// the next — so the workgroup's owner atomics keep hitting the same few
-// cache lines (one per ring over ~IP_PTS_PER_WG/R columns) while they are
-// resident in L2, instead of touching every line once per point.
+// t+256, ...).  The owner image is column-major ([S][C][R]): points arrive in
+// firing order — all rings of one azimuth, then the next — so a wave's 64
+// owner atomics land in one or two 128-byte lines of one column.  Device-scope
+// atomics are executed beyond the XCD's L2 (they must be coherent across
+// XCDs), so what they cost is the number of line requests, not of lanes.
 #define IP_PTS_PER_WG 2048
 __global__ void k_ip_project(DevView v) {
     const int s = blockIdx.y;
     const int n = v.npts[s];
+    const int R = v.cfg.n_scan;
     int fmin = INT_MAX, fmax = -1;
     for (int k = 0; k < IP_PTS_PER_WG / 256; ++k) {
         const int i = blockIdx.x * IP_PTS_PER_WG + k * 256 + threadIdx.x;
@@ -75,7 +77,7 @@ __global__ void k_ip_project(DevView v) {
             fmin = min(fmin, i); fmax = max(fmax, i);
             int row, col; float rg;
             if (project_point(v.cfg, p, row, col, rg))
-                atomicMax(&v.owner[(size_t)s * v.H + row * v.cfg.horizon_scan + col], i);
+                atomicMax(&v.owner[(size_t)s * v.H + (size_t)col * R + row], i);
         }
     }
     fmin = wave_min(fmin); fmax = wave_max(fmax);
@@ -85,56 +87,43 @@ __global__ void k_ip_project(DevView v) {
     }
 }
 
-// pair test of rows (i, i+1) at column j: -1 invalid, 1 ground, 0 not ground
-__device__ inline int ground_pair(const DevView& v, int s, int i, int j) {
-    const int C = v.cfg.horizon_scan;
-    int lo = v.owner[(size_t)s * v.H + i * C + j];
-    int up = v.owner[(size_t)s * v.H + (i + 1) * C + j];
-    if (lo < 0 || up < 0) return -1;
-    float4 a = v.pts[(size_t)s * v.P + lo], b = v.pts[(size_t)s * v.P + up];
-    float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
-    float angle = (float)((double)(slo_libm::atan2f_(dz, sqrtf(dx * dx + dy * dy)) * 180) / M_PI);
-    return fabsf(angle - v.cfg.sensor_mount_angle) <= 10 ? 1 : 0;
+// ---------------------------------------------------------------- image tiles
+// k_ip_tile, k_cc_stats: one workgroup per tile of all R rows x TC columns
+// (IP_TILE_PX pixels, local index l = i * TC + jj, row-major like the global
+// pixel index p = i * C + j, so local and global orders agree).
+#define IP_TILE_PX 4096
+#define IP_TILE_MAXC 256
+#define IP_LROOT (1 << 30)   // csize flag: the pixel is a tile-local root (k_ip_tile)
+__host__ __device__ inline int ip_tile_cols(int R) { return min(IP_TILE_MAXC, max(1, IP_TILE_PX / R)); }
+
+// edge predicate of labelComponents (IP:411-423)
+__device__ inline bool seg_edge(const slo_config& c, float r1, float r2, bool horizontal) {
+    float d1 = fmaxf(r1, r2), d2 = fminf(r1, r2);
+    float sa = horizontal ? c.sin_alpha_x : c.sin_alpha_y;
+    float ca = horizontal ? c.cos_alpha_x : c.cos_alpha_y;
+    float angle = slo_libm::atan2f_(d2 * sa, (d1 - d2 * ca));
+    return angle > c.segment_theta;
 }
 
-__global__ void k_ip_image(DevView v) {
-    const int s = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= v.H) return;
-    const int C = v.cfg.horizon_scan;
-    const int i = p / C, j = p - i * C;
-    const size_t o = (size_t)s * v.H + p;
-    int own = v.owner[o];
-    float rg = FLT_MAX;
-    float4 f;
-    if (own >= 0) {
-        float4 q = v.pts[(size_t)s * v.P + own];
-        rg = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
-        f = make_float4(q.x, q.y, q.z, (float)((double)(float)i + (double)(float)j / 10000.0));
-    } else {
-        float qn = __builtin_nanf("");
-        f = make_float4(qn, qn, qn, -1.0f);
-    }
-    v.range[o] = rg;
-    v.full[o] = f;
-    // Q15: final groundMat value of row i
-    int g = 0;
-    const int gsi = v.cfg.ground_scan_ind;
-    if (i <= gsi) {
-        int pi_ = (i < gsi) ? ground_pair(v, s, i, j) : 0;
-        int pm = (i >= 1 && i - 1 < gsi) ? ground_pair(v, s, i - 1, j) : 0;
-        if (i < gsi && pi_ == -1) g = -1;
-        else if (pi_ == 1 || pm == 1) g = 1;
-    }
-    v.ground[o] = (int8_t)g;
-    int lab = (g == 1 || rg == FLT_MAX) ? -1 : 0;
-    v.label[o] = lab;
-    v.parent[o] = lab == 0 ? p : -1;
-    v.csize[o] = 0;
-    v.crows[2 * o] = 0ull;
-    v.crows[2 * o + 1] = 0ull;
+// Union-find that always links the larger root under the smaller, so a root
+// is its component's smallest index.  In LDS (one tile) and in HBM (global
+// pixel indices; device-scope atomics).
+__device__ inline int lds_find(int* par, int x) {
+    int y = __hip_atomic_load(&par[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    while (y != x) { x = y; y = __hip_atomic_load(&par[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); }
+    return x;
 }
-
+__device__ inline void lds_unite(int* par, int a, int b) {
+    while (true) {
+        a = lds_find(par, a);
+        b = lds_find(par, b);
+        if (a == b) return;
+        if (a < b) { int t = a; a = b; b = t; }
+        int old = atomicCAS(&par[a], a, b);
+        if (old == a) return;
+        a = old;
+    }
+}
 __device__ inline int ld_parent(int* a, int x) {
     return __hip_atomic_load(&a[x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -155,87 +144,211 @@ __device__ inline void unite(int* par, int a, int b) {
     }
 }
 
-// edge predicate of labelComponents (IP:411-423)
-__device__ inline bool seg_edge(const slo_config& c, float r1, float r2, bool horizontal) {
-    float d1 = fmaxf(r1, r2), d2 = fminf(r1, r2);
-    float sa = horizontal ? c.sin_alpha_x : c.sin_alpha_y;
-    float ca = horizontal ? c.cos_alpha_x : c.cos_alpha_y;
-    float angle = slo_libm::atan2f_(d2 * sa, (d1 - d2 * ca));
-    return angle > c.segment_theta;
-}
-
-__global__ void k_cc_union(DevView v) {
-    const int s = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= v.H) return;
-    const int C = v.cfg.horizon_scan, R = v.cfg.n_scan;
+// Per tile: the owner columns are transposed through LDS; then per pixel the
+// range, the full-cloud point, the final groundMat value (Q15; each row pair
+// (i, i+1) is tested once, IP:268-300) and the label seed; then the
+// components inside the tile by LDS union-find over the edges of
+// labelComponents (IP:396-423) whose both ends are in the tile.  parent[]
+// gets the global index of each pixel's tile-local root; the edges across
+// tile boundaries (and the column wrap, IP:403-406) are k_cc_merge's.
+__global__ void __launch_bounds__(256) k_ip_tile(DevView v) {
+    const int s = blockIdx.y, R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const int TC = ip_tile_cols(R), c0 = blockIdx.x * TC, nc = min(TC, C - c0), npx = R * TC;
     const size_t base = (size_t)s * v.H;
-    if (v.label[base + p] != 0) return;
-    const int i = p / C, j = p - i * C;
-    int* par = v.parent + base;
-    const float rp = v.range[base + p];
-    int q = i * C + (j + 1 == C ? 0 : j + 1);  // right neighbour (column wrap, IP:403-406)
-    if (v.label[base + q] == 0 && seg_edge(v.cfg, rp, v.range[base + q], true)) unite(par, p, q);
-    if (i + 1 < R) {
-        q = p + C;                              // next row
-        if (v.label[base + q] == 0 && seg_edge(v.cfg, rp, v.range[base + q], false)) unite(par, p, q);
+    const float4* pts = v.pts + (size_t)s * v.P;
+    const int gsi = v.cfg.ground_scan_ind, tid = threadIdx.x;
+    __shared__ int l_a[IP_TILE_PX];   // owner, then the union-find parents
+    __shared__ float l_rg[IP_TILE_PX];
+    __shared__ int8_t l_lab[IP_TILE_PX], l_pair[IP_TILE_PX];
+    __shared__ double l_q[IP_TILE_MAXC];
+    for (int k = tid; k < R * nc; k += 256) {
+        const int jj = k / R, i = k - jj * R;
+        l_a[i * TC + jj] = v.owner[base + (size_t)(c0 + jj) * R + i];
+    }
+    for (int jj = tid; jj < nc; jj += 256) l_q[jj] = (double)(float)(c0 + jj) / 10000.0;
+    __syncthreads();
+    const int npair = min(gsi, R - 1) * nc;
+    for (int k = tid; k < npair; k += 256) {
+        const int i = k / nc, jj = k - i * nc;
+        const int lo = l_a[i * TC + jj], up = l_a[(i + 1) * TC + jj];
+        int g = -1;
+        if (lo >= 0 && up >= 0) {
+            const float4 a = pts[lo], b = pts[up];
+            const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
+            const float angle = (float)((double)(slo_libm::atan2f_(dz, sqrtf(dx * dx + dy * dy)) * 180) / M_PI);
+            g = fabsf(angle - v.cfg.sensor_mount_angle) <= 10 ? 1 : 0;
+        }
+        l_pair[i * TC + jj] = (int8_t)g;
+    }
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) {
+        const int i = l / TC, jj = l - i * TC;
+        if (jj >= nc) { l_lab[l] = -1; continue; }
+        const size_t o = base + (size_t)i * C + c0 + jj;
+        const int own = l_a[l];
+        float rg = FLT_MAX;
+        float4 f;
+        if (own >= 0) {
+            const float4 q = pts[own];
+            rg = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z);
+            f = make_float4(q.x, q.y, q.z, (float)((double)(float)i + l_q[jj]));
+        } else {
+            const float qn = __builtin_nanf("");
+            f = make_float4(qn, qn, qn, -1.0f);
+        }
+        v.range[o] = rg;
+        v.full[o] = f;
+        int g = 0;   // Q15: final groundMat value of row i
+        if (i <= gsi) {
+            const int pi_ = (i < gsi && i + 1 < R) ? l_pair[l] : 0;
+            const int pm = (i >= 1 && i - 1 < gsi) ? l_pair[l - TC] : 0;
+            if (i < gsi && pi_ == -1) g = -1;
+            else if (pi_ == 1 || pm == 1) g = 1;
+        }
+        v.ground[o] = (int8_t)g;
+        const int lab = (g == 1 || rg == FLT_MAX) ? -1 : 0;
+        v.label[o] = lab;
+        v.crows[2 * o] = 0ull;
+        v.crows[2 * o + 1] = 0ull;
+        l_lab[l] = (int8_t)lab;
+        l_rg[l] = rg;
+    }
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) l_a[l] = l_lab[l] == 0 ? l : -1;
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) {
+        if (l_lab[l] != 0) continue;
+        const int i = l / TC, jj = l - i * TC;
+        if (jj + 1 < nc && l_lab[l + 1] == 0 && seg_edge(v.cfg, l_rg[l], l_rg[l + 1], true)) lds_unite(l_a, l, l + 1);
+        if (i + 1 < R && l_lab[l + TC] == 0 && seg_edge(v.cfg, l_rg[l], l_rg[l + TC], false))
+            lds_unite(l_a, l, l + TC);
+    }
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) {
+        const int i = l / TC, jj = l - i * TC;
+        if (jj >= nc) continue;
+        const int p = i * C + c0 + jj;
+        int g = -1;
+        if (l_lab[l] == 0) {
+            const int r = lds_find(l_a, l), ri = r / TC;
+            g = ri * C + c0 + (r - ri * TC);
+        }
+        v.parent[base + p] = g;
+        v.csize[base + p] = g == p ? IP_LROOT : 0;
     }
 }
 
-// Component size and row set (seed excluded, Q3).  Large components put
-// thousands of pixels on one root, so the lanes of a wave that share a root
-// are combined first (one atomic per distinct root per wave).
-__global__ void k_cc_stats(DevView v) {
-    const int s = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+// the horizontal edges between tiles (and the wrap C-1 -> 0), one thread per
+// (tile, row)
+__global__ void k_cc_merge(DevView v, int ntiles) {
+    const int s = blockIdx.y, R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= ntiles * R) return;
+    const int TC = ip_tile_cols(R), t = k / R, i = k - t * R;
+    const int j = min(C, (t + 1) * TC) - 1, jn = j + 1 == C ? 0 : j + 1;
+    const size_t base = (size_t)s * v.H;
+    const int p = i * C + j, q = i * C + jn;
+    if (v.label[base + p] == 0 && v.label[base + q] == 0 &&
+        seg_edge(v.cfg, v.range[base + p], v.range[base + q], true))
+        unite(v.parent + base, p, q);
+}
+
+// Component size and row set (seed excluded, Q3), per tile: the pixels are
+// counted per tile-local root in LDS, and each local root then adds its
+// totals to its component root with one set of atomics; it also stores that
+// root as its own parent, so every pixel's root is parent[parent[p]].
+// (k_cc_merge only relinks roots, so a non-root pixel's parent is still its
+// tile-local root; local roots are flagged in csize.)
+#define IP_STAT_SLOTS 512
+#define IP_NOT_CAND 0xfffd
+#define IP_NOT_ROOT 0xfffe
+#define IP_OVERFLOW 0xffff
+__global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
+    const int s = blockIdx.y, R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const int TC = ip_tile_cols(R), c0 = blockIdx.x * TC, nc = min(TC, C - c0), npx = R * TC;
     const size_t base = (size_t)s * v.H;
     int* par = v.parent + base;
-    int r = -1;
-    unsigned long long rows0 = 0, rows1 = 0;
-    if (p < v.H && par[p] >= 0) {
-        r = p;
-        int y = par[r];
-        while (y != r) { r = y; y = par[r]; }
-        par[p] = r;
-        if (p != r) {
-            const int row = p / v.cfg.horizon_scan;
-            (row >> 6 ? rows1 : rows0) = 1ull << (row & 63);
+    const int tid = threadIdx.x;
+    __shared__ uint16_t l_slot[IP_TILE_PX];
+    __shared__ int l_cnt[IP_STAT_SLOTS], l_fr[IP_STAT_SLOTS], l_lr[IP_STAT_SLOTS];
+    __shared__ unsigned long long l_rows[IP_STAT_SLOTS][2];
+    __shared__ int n_slots;
+    if (tid == 0) n_slots = 0;
+    for (int k = tid; k < IP_STAT_SLOTS; k += 256) { l_cnt[k] = 0; l_rows[k][0] = 0ull; l_rows[k][1] = 0ull; }
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) {
+        const int i = l / TC, jj = l - i * TC;
+        if (jj >= nc) continue;
+        const int p = i * C + c0 + jj;
+        uint16_t code = IP_NOT_CAND;
+        if (par[p] >= 0) {
+            code = IP_NOT_ROOT;
+            if (v.csize[base + p] & IP_LROOT) {
+                const int fr = find_root(par, p);
+                const int k = atomicAdd(&n_slots, 1);
+                code = IP_OVERFLOW;
+                if (k < IP_STAT_SLOTS) { code = (uint16_t)k; l_fr[k] = fr; l_lr[k] = p; }
+            }
+        }
+        l_slot[l] = code;
+    }
+    __syncthreads();
+    for (int l = tid; l < npx; l += 256) {
+        const int i = l / TC, jj = l - i * TC;
+        if (jj >= nc) continue;
+        const int code = l_slot[l];
+        if (code == IP_NOT_CAND) continue;
+        const int p = i * C + c0 + jj;
+        int lr = l;
+        if (code == IP_NOT_ROOT) {
+            const int g = par[p], gi = g / C;
+            lr = gi * TC + (g - gi * C - c0);
+        }
+        const int k = l_slot[lr];
+        const unsigned long long bit = 1ull << (i & 63);
+        if (k != IP_OVERFLOW) {
+            atomicAdd(&l_cnt[k], 1);
+            if (p != l_fr[k]) atomicOr(&l_rows[k][i >> 6], bit);
+        } else {
+            const int fr = find_root(par, lr == l ? p : par[p]);
+            atomicAdd(&v.csize[base + fr], 1);
+            if (p != fr) atomicOr(&v.crows[2 * (base + fr) + (i >> 6)], bit);
         }
     }
-    unsigned long long pending = __ballot(r >= 0);
-    while (pending) {
-        const int leader = __ffsll((long long)pending) - 1;
-        const int lr = __shfl(r, leader, 64);
-        const bool mine = r == lr;
-        const unsigned long long grp = __ballot(mine);
-        unsigned long long a = mine ? rows0 : 0ull, b = mine ? rows1 : 0ull;
-        for (int o = 32; o > 0; o >>= 1) { a |= __shfl_xor(a, o, 64); b |= __shfl_xor(b, o, 64); }
-        if ((int)(threadIdx.x & 63) == leader) {
-            atomicAdd(&v.csize[base + lr], __popcll(grp));
-            if (a) atomicOr(&v.crows[2 * (base + lr)], a);
-            if (b) atomicOr(&v.crows[2 * (base + lr) + 1], b);
-        }
-        pending &= ~grp;
+    __syncthreads();
+    const int ns = min(n_slots, IP_STAT_SLOTS);
+    for (int k = tid; k < ns; k += 256) {
+        const int fr = l_fr[k];
+        atomicAdd(&v.csize[base + fr], l_cnt[k]);
+        if (l_rows[k][0]) atomicOr(&v.crows[2 * (base + fr)], l_rows[k][0]);
+        if (l_rows[k][1]) atomicOr(&v.crows[2 * (base + fr) + 1], l_rows[k][1]);
+    }
+    __syncthreads();
+    // compress: the local roots point at their component roots (every find
+    // of this workgroup has finished; other workgroups only follow parent
+    // links, which this keeps valid)
+    for (int k = tid; k < ns; k += 256) par[l_lr[k]] = l_fr[k];
+    for (int l = tid; l < npx; l += 256) {
+        const int i = l / TC, jj = l - i * TC;
+        if (jj >= nc || l_slot[l] != IP_OVERFLOW) continue;
+        const int p = i * C + c0 + jj;
+        par[p] = find_root(par, p);
     }
 }
 
-__global__ void k_cc_label(DevView v) {
-    const int s = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= v.H) return;
-    const size_t base = (size_t)s * v.H;
-    int r = v.parent[base + p];
-    if (r < 0) return;
-    int size = v.csize[base + r];
+// final label of a label-0 pixel (IP:425-460): feasible segments keep a
+// positive label (the reference numbers them by seed order; the number is
+// only used by the visualisation cloud IP:363), the rest 999999
+__device__ inline int final_label(const DevView& v, size_t base, size_t o) {
+    const int r = v.parent[base + v.parent[o]];
+    const int size = v.csize[base + r] & (IP_LROOT - 1);
     bool feasible = false;
     if (size >= 30) feasible = true;
     else if (size >= v.cfg.segment_valid_point_num) {
-        int lines = __popcll(v.crows[2 * (base + r)]) + __popcll(v.crows[2 * (base + r) + 1]);
+        const int lines = __popcll(v.crows[2 * (base + r)]) + __popcll(v.crows[2 * (base + r) + 1]);
         if (lines >= v.cfg.segment_valid_line_num) feasible = true;
     }
-    // feasible segments keep a positive label (the reference numbers them by
-    // seed order; the number is only used by the visualisation cloud IP:363)
-    v.label[base + p] = feasible ? r + 1 : 999999;
+    return feasible ? r + 1 : 999999;
 }
 
 __device__ inline void pixel_kind(const DevView& v, size_t base, int i, int j, bool& kept, bool& outl) {
@@ -253,16 +366,19 @@ __device__ inline void pixel_kind(const DevView& v, size_t base, int i, int j, b
     }
 }
 
-// block = 256 threads per (row, stream): per-row kept / outlier counts
+// block = 256 threads per (row, stream): final labels, then per-row kept /
+// outlier counts
 __global__ void k_ip_rowcount(DevView v) {
     const int s = blockIdx.y, i = blockIdx.x;
     const int C = v.cfg.horizon_scan;
     const size_t base = (size_t)s * v.H;
     int kc = 0, oc = 0;
     for (int j = threadIdx.x; j < C; j += blockDim.x) {
-        bool k, o;
-        pixel_kind(v, base, i, j, k, o);
-        kc += k; oc += o;
+        const size_t o = base + (size_t)i * C + j;
+        if (v.label[o] == 0) v.label[o] = final_label(v, base, o);
+        bool k, ou;
+        pixel_kind(v, base, i, j, k, ou);
+        kc += k; oc += ou;
     }
     for (int o = 32; o > 0; o >>= 1) { kc += __shfl_xor(kc, o, 64); oc += __shfl_xor(oc, o, 64); }
     __shared__ int sk[16], so[16];
@@ -285,13 +401,28 @@ __global__ void k_ip_compact(DevView v) {
     const int* rc = v.rowcnt + (size_t)s * R * 2;
     __shared__ int s_off[2], s_tot[2];
     __shared__ int sc_k[256], sc_o[256];
-    if (threadIdx.x == 0) {
+    __shared__ int s_red[4][4];
+    {   // rows before i and all rows, kept / outlier
         int a = 0, b = 0, ta = 0, tb = 0;
-        for (int r = 0; r < R; ++r) {
-            if (r < i) { a += rc[2 * r]; b += rc[2 * r + 1]; }
-            ta += rc[2 * r]; tb += rc[2 * r + 1];
+        for (int r = threadIdx.x; r < R; r += blockDim.x) {
+            const int x = rc[2 * r], y = rc[2 * r + 1];
+            ta += x; tb += y;
+            if (r < i) { a += x; b += y; }
         }
-        s_off[0] = a; s_off[1] = b; s_tot[0] = ta; s_tot[1] = tb;
+        for (int o = 32; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o, 64); b += __shfl_xor(b, o, 64);
+            ta += __shfl_xor(ta, o, 64); tb += __shfl_xor(tb, o, 64);
+        }
+        if ((threadIdx.x & 63) == 0) {
+            const int w = threadIdx.x >> 6;
+            s_red[w][0] = a; s_red[w][1] = b; s_red[w][2] = ta; s_red[w][3] = tb;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+                for (int c = 0; c < 4; ++c) s_red[0][c] += s_red[w][c];
+            s_off[0] = s_red[0][0]; s_off[1] = s_red[0][1]; s_tot[0] = s_red[0][2]; s_tot[1] = s_red[0][3];
+        }
     }
     const int T = blockDim.x;
     const int chunk = (C + T - 1) / T;
@@ -356,12 +487,12 @@ int ip_run(slo_ctx* ctx) {
     SLO_CHECK(hipMemsetAsync(v.owner, 0xff, sizeof(int32_t) * (size_t)S * v.H, ctx->stream));
     SLO_LAUNCH(ctx, "ip_init", k_ip_init, dim3((S + 63) / 64), dim3(64), 0, v);
     const int T = 256;
-    dim3 gp((v.P + IP_PTS_PER_WG - 1) / IP_PTS_PER_WG, S), gh((v.H + T - 1) / T, S), gr(v.cfg.n_scan, S);
+    dim3 gp((v.P + IP_PTS_PER_WG - 1) / IP_PTS_PER_WG, S), gr(v.cfg.n_scan, S);
     SLO_LAUNCH(ctx, "ip_project", k_ip_project, gp, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "ip_image", k_ip_image, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "ip_cc_union", k_cc_union, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "ip_cc_label", k_cc_label, gh, dim3(T), 0, v);
+    const int ntiles = (v.cfg.horizon_scan + ip_tile_cols(v.cfg.n_scan) - 1) / ip_tile_cols(v.cfg.n_scan);
+    SLO_LAUNCH(ctx, "ip_tile", k_ip_tile, dim3(ntiles, S), dim3(T), 0, v);
+    SLO_LAUNCH(ctx, "ip_cc_merge", k_cc_merge, dim3((ntiles * v.cfg.n_scan + T - 1) / T, S), dim3(T), 0, v, ntiles);
+    SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_rowcount", k_ip_rowcount, gr, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_compact", k_ip_compact, gr, dim3(T), 0, v);
     SLO_CHECK(hipGetLastError());
