@@ -306,16 +306,18 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
 struct VgParams;
 struct MapWs {  // VoxelGrid workspace
     size_t items = 0;
-    unsigned long long *keys = nullptr, *keys2 = nullptr;
+    void *keys = nullptr, *keys2 = nullptr;   // 32- or 64-bit sort keys (8 B per item allocated)
     unsigned int *vals = nullptr, *vals2 = nullptr;
     int *flags = nullptr, *rank = nullptr;
+    int *starts = nullptr, *ends = nullptr, *longv = nullptr;   // per voxel; long-voxel list
+    int32_t* meta = nullptr;     // [total, max cell count, long-voxel count]
+    int32_t* h_meta = nullptr;   // pinned copy
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int32_t* off = nullptr;
     unsigned int* bounds = nullptr;
     VgParams* prm = nullptr;
     int32_t* errflag = nullptr;
-    int32_t* h_total = nullptr;
 };
 struct HashGrid {
     int T = 0;

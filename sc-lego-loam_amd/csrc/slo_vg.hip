@@ -29,23 +29,39 @@ __device__ inline float ord2f(unsigned int u) {
     return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
 }
 
-__global__ void k_vg_prefix(const int32_t* n, int n_stride, const int32_t* active, int S, int32_t* off,
-                            unsigned int* bounds) {
-    // one thread: stream offsets (tiny S); bounds init
-    if (threadIdx.x == 0 && blockIdx.x == 0) {
-        int a = 0;
-        for (int s = 0; s < S; ++s) {
-            off[s] = a;
-            a += (active == nullptr || active[s]) ? n[(size_t)s * n_stride] : 0;
+// stream offsets of the concatenated input (block scan), bounds init, and the
+// meta words [total, max cell count, long-voxel count]
+__global__ void __launch_bounds__(1024) k_vg_prefix(const int32_t* n, int n_stride, int S, int32_t* off,
+                                                    unsigned int* bounds, int32_t* meta) {
+    __shared__ int wsum[16];
+    __shared__ int carry;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (tid == 0) carry = 0;
+    __syncthreads();
+    for (int b0 = 0; b0 < S; b0 += 1024) {
+        const int s = b0 + tid;
+        const int x = s < S ? n[(size_t)s * n_stride] : 0;
+        int incl = x;   // inclusive wave scan
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
         }
-        off[S] = a;
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        int before = carry;
+        for (int k = 0; k < w; ++k) before += wsum[k];
+        if (s < S) off[s] = before + incl - x;
+        __syncthreads();
+        if (tid == 1023) carry = before + incl;
+        __syncthreads();
     }
-    for (int s = threadIdx.x; s < S; s += blockDim.x) {
+    if (tid == 0) { off[S] = carry; meta[0] = carry; meta[1] = 0; meta[2] = 0; }
+    for (int s = tid; s < S; s += 1024)
         for (int k = 0; k < 3; ++k) { bounds[6 * s + k] = 0xffffffffu; bounds[6 * s + 3 + k] = 0u; }
-    }
 }
 
-__global__ void k_vg_bounds(const float4* in, size_t in_stride, const int32_t* off, unsigned int* bounds) {
+__global__ void __launch_bounds__(256) k_vg_bounds(const float4* in, size_t in_stride, const int32_t* off,
+                                                   unsigned int* bounds) {
     const int s = blockIdx.y;
     const int n = off[s + 1] - off[s];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
@@ -60,22 +76,33 @@ __global__ void k_vg_bounds(const float4* in, size_t in_stride, const int32_t* o
             mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], o, 64));
             mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], o, 64));
         }
+    __shared__ unsigned int red[4][6];
+    const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
-        for (int k = 0; k < 3; ++k) {
-            atomicMin(&bounds[6 * s + k], mn[k]);
-            atomicMax(&bounds[6 * s + 3 + k], mx[k]);
-        }
+        for (int k = 0; k < 3; ++k) { red[w][k] = mn[k]; red[w][3 + k] = mx[k]; }
+    __syncthreads();
+    if (threadIdx.x < 6) {   // one atomic per component per workgroup
+        const int k = threadIdx.x;
+        unsigned int r = red[0][k];
+        for (int ww = 1; ww < (int)(blockDim.x >> 6); ++ww) r = k < 3 ? min(r, red[ww][k]) : max(r, red[ww][k]);
+        if (k < 3) { if (r != 0xffffffffu) atomicMin(&bounds[6 * s + k], r); }
+        else if (r != 0u) atomicMax(&bounds[6 * s + k], r);
+    }
 }
 
+// voxel-index parameters (PCL applyFilter) and the largest cell count over
+// the streams (meta[1]), which sizes the sort keys
 struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; };
 
-__global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
+__global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm,
+                            int32_t* meta) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     VgParams p;
     p.inv = 1.0f / leaf;
     p.overflow = 0;
-    if (off[s + 1] - off[s] == 0 || bounds[6 * s] == 0xffffffffu) {
+    const int n = off[s + 1] - off[s];
+    if (n == 0 || bounds[6 * s] == 0xffffffffu) {
         p.minb[0] = p.minb[1] = p.minb[2] = 0; p.mul1 = p.mul2 = 0;
         prm[s] = p;
         return;
@@ -86,64 +113,141 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
               dz = (long long)((mx[2] - mn[2]) * p.inv) + 1;
     if (dx * dy * dz > 2147483647LL) p.overflow = 1;
     for (int k = 0; k < 3; ++k) p.minb[k] = (int)floorf(mn[k] * p.inv);
-    int maxbx = (int)floorf(mx[0] * p.inv), maxby = (int)floorf(mx[1] * p.inv);
-    int divx = maxbx - p.minb[0] + 1, divy = maxby - p.minb[1] + 1;
+    int maxbx = (int)floorf(mx[0] * p.inv), maxby = (int)floorf(mx[1] * p.inv), maxbz = (int)floorf(mx[2] * p.inv);
+    int divx = maxbx - p.minb[0] + 1, divy = maxby - p.minb[1] + 1, divz = maxbz - p.minb[2] + 1;
     p.mul1 = divx;
     p.mul2 = divx * divy;
     prm[s] = p;
+    // indices are < divx*divy*divz (or < n: the overflow keys are positions)
+    const long long cells = p.overflow ? (long long)n : (long long)divx * divy * divz;
+    atomicMax(&meta[1], (int)min(cells, 2147483647LL));
 }
 
-__global__ void k_vg_keys(const float4* in, size_t in_stride, const int32_t* off, const VgParams* prm,
-                          unsigned long long* keys, unsigned int* vals) {
+// keys: (stream << vbits) | voxel index; non-finite points get the all-ones
+// index, which sorts after every voxel of the stream and is never a voxel
+template <class K>
+__global__ void k_vg_keys(const float4* in, size_t in_stride, const int32_t* off, const VgParams* prm, int vbits,
+                          K* keys, unsigned int* vals) {
     const int s = blockIdx.y;
     const int base = off[s], n = off[s + 1] - base;
     const VgParams p = prm[s];
+    const K hi = (K)s << vbits, none = ((K)1 << vbits) - 1;
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         float4 q = in[(size_t)s * in_stride + i];
-        unsigned long long k;
+        K k;
         if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) {
-            // sorts after every voxel of stream s, keeping the stream's segment contiguous
-            k = ((unsigned long long)s << 32) | 0xffffffffull;
+            k = hi | none;
         } else if (p.overflow) {
-            k = ((unsigned long long)s << 32) | (unsigned int)i;
+            k = hi | (K)(unsigned int)i;
         } else {
             int ijk0 = (int)(floorf(q.x * p.inv) - (float)p.minb[0]);
             int ijk1 = (int)(floorf(q.y * p.inv) - (float)p.minb[1]);
             int ijk2 = (int)(floorf(q.z * p.inv) - (float)p.minb[2]);
-            unsigned int idx = (unsigned int)(ijk0 + ijk1 * p.mul1 + ijk2 * p.mul2);
-            k = ((unsigned long long)s << 32) | idx;
+            k = hi | (K)(unsigned int)(ijk0 + ijk1 * p.mul1 + ijk2 * p.mul2);
         }
         keys[base + i] = k;
         vals[base + i] = (unsigned int)i;
     }
 }
 
-__global__ void k_vg_heads(const unsigned long long* keys, int total, int* flags) {
+template <class K>
+__global__ void k_vg_heads(const K* keys, int total, int vbits, int* flags) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > total) return;
     if (j == total) { flags[j] = 0; return; }
-    unsigned long long k = keys[j];
-    flags[j] = ((unsigned int)k != 0xffffffffu) && (j == 0 || k != keys[j - 1]);
+    const K k = keys[j], none = ((K)1 << vbits) - 1;
+    flags[j] = (k & none) != none && (j == 0 || k != keys[j - 1]);
 }
 
-__global__ void k_vg_centroid(const float4* in, size_t in_stride, const unsigned long long* keys,
-                              const unsigned int* vals, const int* rank, const int32_t* off, int total,
-                              float4* out, size_t out_stride, int out_cap) {
+// voxel r = rank of its first item: its item range [starts[r], ends[r])
+template <class K>
+__global__ void k_vg_runs(const K* keys, const int* rank, int total, int vbits, int* starts, int* ends) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= total) return;
-    const unsigned long long k = keys[j];
-    if ((unsigned int)k == 0xffffffffu || (j > 0 && keys[j - 1] == k)) return;
-    const int s = (int)(k >> 32);
-    const int r = rank[j] - rank[off[s]];
-    float sx = 0, sy = 0, sz = 0, si = 0;
-    int e = j;
-    while (e < total && keys[e] == k) {
-        float4 p = in[(size_t)s * in_stride + vals[e]];
-        sx += p.x; sy += p.y; sz += p.z; si += p.w;
-        ++e;
+    const K k = keys[j], none = ((K)1 << vbits) - 1;
+    if ((k & none) == none) return;
+    const bool head = j == 0 || keys[j - 1] != k;
+    const int r = head ? rank[j] : rank[j] - 1;   // rank = heads strictly before j
+    if (head) starts[r] = j;
+    if (j + 1 == total || keys[j + 1] != k) ends[r] = j + 1;
+}
+
+// Centroid of one voxel: the points are summed in input order (the sort is
+// stable), one float chain per component as PCL's CentroidPoint.  Voxels of
+// up to VG_SHORT points: one thread each, loads issued 4 at a time ahead of
+// the chain.  Longer ones are listed for k_vg_long.
+#define VG_SHORT 32
+struct VgOut { float4* out; size_t stride; int cap; };
+
+__device__ inline void vg_store(const VgOut& o, const int* rank, const int32_t* off, int s, int r, float sx, float sy,
+                                float sz, float si, int cnt) {
+    const int pos = r - rank[off[s]];
+    const float c = (float)cnt;
+    if (pos < o.cap) o.out[(size_t)s * o.stride + pos] = make_float4(sx / c, sy / c, sz / c, si / c);
+}
+
+template <class K>
+__global__ void k_vg_centroid(const float4* in, size_t in_stride, const K* keys, const unsigned int* vals,
+                              const int* rank, const int32_t* off, int total, int vbits, const int* starts,
+                              const int* ends, int32_t* meta, int* longv, VgOut o) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= rank[total]) return;
+    const int a = starts[r], e = ends[r];
+    if (e - a > VG_SHORT) {
+        longv[atomicAdd(&meta[2], 1)] = r;
+        return;
     }
-    float c = (float)(e - j);
-    if (r < out_cap) out[(size_t)s * out_stride + r] = make_float4(sx / c, sy / c, sz / c, si / c);
+    const int s = (int)(keys[a] >> vbits);
+    const float4* src = in + (size_t)s * in_stride;
+    float sx = 0, sy = 0, sz = 0, si = 0;
+    for (int j = a; j < e; j += 4) {
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = j + u < e ? src[vals[j + u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (j + u < e) { sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w; }
+    }
+    vg_store(o, rank, off, s, r, sx, sy, sz, si, e - a);
+}
+
+// Long voxels, one wave each (persistent grid over the list): the wave
+// stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
+// intensity chains over them in order.
+template <class K>
+__global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_stride, const K* keys,
+                                                 const unsigned int* vals, const int* rank, const int32_t* off,
+                                                 int vbits, const int* starts, const int* ends, const int32_t* meta,
+                                                 const int* longv, VgOut o) {
+    __shared__ float4 buf[4][256];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int nlong = meta[2];
+    float4* b = buf[w];
+    for (int t = blockIdx.x * 4 + w; t < nlong; t += gridDim.x * 4) {
+        const int r = longv[t], a = starts[r], e = ends[r];
+        const int s = (int)(keys[a] >> vbits);
+        const float4* src = in + (size_t)s * in_stride;
+        float acc = 0.0f;
+        for (int c0 = a; c0 < e; c0 += 256) {
+            const int m = min(256, e - c0);
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int k = u * 64 + lane;
+                if (k < m) b[k] = src[vals[c0 + k]];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
+            __builtin_amdgcn_wave_barrier();
+            if (lane < 4) {
+                const float* f = reinterpret_cast<const float*>(b) + lane;
+                for (int k = 0; k < m; ++k) acc += f[4 * k];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
+            __builtin_amdgcn_wave_barrier();
+        }
+        const float sx = __shfl(acc, 0, 64), sy = __shfl(acc, 1, 64), sz = __shfl(acc, 2, 64),
+                    si = __shfl(acc, 3, 64);
+        if (lane == 0) vg_store(o, rank, off, s, r, sx, sy, sz, si, e - a);
+    }
 }
 
 __global__ void k_vg_count(const int* rank, const int32_t* off, int S, int32_t* nout, int nout_stride, int out_cap,
@@ -158,8 +262,8 @@ __global__ void k_vg_count(const int* rank, const int32_t* off, int S, int32_t* 
 static int ensure_ws(slo_ctx* ctx, size_t items) {
     MapWs& w = ctx->mws;
     if (items <= w.items) return 0;
-    if (w.keys) { hipFree(w.keys); hipFree(w.keys2); hipFree(w.vals); hipFree(w.vals2); hipFree(w.flags); hipFree(w.rank); }
-    if (w.temp) hipFree(w.temp);
+    void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.starts, w.ends, w.longv, w.temp};
+    for (void* p : old) if (p) hipFree(p);
     w.items = items;
     SLO_CHECK(hipMalloc(&w.keys, 8 * items));
     SLO_CHECK(hipMalloc(&w.keys2, 8 * items));
@@ -167,12 +271,47 @@ static int ensure_ws(slo_ctx* ctx, size_t items) {
     SLO_CHECK(hipMalloc(&w.vals2, 4 * items));
     SLO_CHECK(hipMalloc(&w.flags, 4 * (items + 1)));
     SLO_CHECK(hipMalloc(&w.rank, 4 * (items + 1)));
-    size_t t1 = 0, t2 = 0;
-    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, w.keys, w.keys2, w.vals, w.vals2, (int)items, 0, 64,
+    SLO_CHECK(hipMalloc(&w.starts, 4 * items));
+    SLO_CHECK(hipMalloc(&w.ends, 4 * items));
+    SLO_CHECK(hipMalloc(&w.longv, 4 * items));
+    size_t t1 = 0, t2 = 0, t3 = 0;
+    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long*)w.keys,
+                                                 (unsigned long long*)w.keys2, w.vals, w.vals2, (int)items, 0, 64,
                                                  ctx->stream));
+    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t3, (unsigned int*)w.keys, (unsigned int*)w.keys2, w.vals,
+                                                 w.vals2, (int)items, 0, 32, ctx->stream));
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, w.flags, w.rank, (int)items + 1, ctx->stream));
-    w.temp_bytes = std::max(t1, t2);
+    w.temp_bytes = std::max(std::max(t1, t2), t3);
     SLO_CHECK(hipMalloc(&w.temp, w.temp_bytes));
+    return 0;
+}
+
+template <class K>
+static int vg_sorted(slo_ctx* ctx, const float4* in, size_t in_stride, int total, int vbits, int sbits,
+                     const VgOut& o) {
+    MapWs& w = ctx->mws;
+    const int S = ctx->S, T = 256;
+    const int bx = std::max(1, std::min(64, (int)((in_stride + T - 1) / T)));
+    K* keys = (K*)w.keys;
+    K* keys2 = (K*)w.keys2;
+    SLO_LAUNCH(ctx, "vg_keys", k_vg_keys<K>, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.prm, vbits, keys,
+               w.vals);
+    size_t tb = w.temp_bytes;
+    hipEvent_t ev = nullptr;
+    if (ctx->timing) timing_begin(ctx, "vg_sort", &ev);
+    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys, keys2, w.vals, w.vals2, total, 0, vbits + sbits,
+                                                 ctx->stream));
+    if (ctx->timing) timing_end(ctx, "vg_sort", ev);
+    const int gi = (total + T - 1) / T;
+    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits,
+               w.flags);
+    tb = w.temp_bytes;
+    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.flags, w.rank, total + 1, ctx->stream));
+    SLO_LAUNCH(ctx, "vg_runs", k_vg_runs<K>, dim3(gi), dim3(T), 0, keys2, w.rank, total, vbits, w.starts, w.ends);
+    SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid<K>, dim3(gi), dim3(T), 0, in, in_stride, keys2, w.vals2, w.rank,
+               w.off, total, vbits, w.starts, w.ends, w.meta, w.longv, o);
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long<K>, dim3(std::min(1024, gi)), dim3(T), 0, in, in_stride, keys2, w.vals2,
+               w.rank, w.off, vbits, w.starts, w.ends, w.meta, w.longv, o);
     return 0;
 }
 
@@ -180,35 +319,30 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
     MapWs& w = ctx->mws;
     const int S = ctx->S;
-    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(256), 0, d_n, n_stride, (const int32_t*)nullptr, S,
-               w.off, w.bounds);
-    SLO_CHECK(hipMemcpyAsync(w.h_total, w.off + S, sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SLO_CHECK(hipStreamSynchronize(ctx->stream));
-    const int total = *w.h_total;
-    if (int r = ensure_ws(ctx, (size_t)total + 1)) return r;
     const int T = 256;
     const int bx = std::max(1, std::min(64, (int)((in_stride + T - 1) / T)));
+    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, d_n, n_stride, S, w.off, w.bounds, w.meta);
     SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.bounds);
-    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
+    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm,
+               w.meta);
+    // one host round trip per filter: the item count and the key width
+    SLO_CHECK(hipMemcpyAsync(w.h_meta, w.meta, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    const int total = w.h_meta[0];
+    int vbits = 1;   // every index < 2^vbits - 1 (the all-ones index marks non-finite points)
+    while (vbits < 32 && (1LL << vbits) <= (long long)w.h_meta[1]) ++vbits;
+    if (w.h_meta[1] >= (1 << 30)) vbits = 32;   // int index arithmetic may wrap, as in PCL
+    int sbits = 0;
+    while ((1 << sbits) < S) ++sbits;
+    if (int r = ensure_ws(ctx, (size_t)total + 1)) return r;
     if (total > 0) {
-        SLO_LAUNCH(ctx, "vg_keys", k_vg_keys, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.prm, w.keys, w.vals);
-        int sbits = 1;
-        while ((1 << sbits) < S) ++sbits;
-        size_t tb = w.temp_bytes;
-        hipEvent_t ev = nullptr;
-        if (ctx->timing) timing_begin(ctx, "vg_sort", &ev);
-        SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.keys, w.keys2, w.vals, w.vals2, total, 0,
-                                                     32 + sbits + 1, ctx->stream));
-        if (ctx->timing) timing_end(ctx, "vg_sort", ev);
+        const VgOut o{out, out_stride, out_cap};
+        const int r = vbits + sbits <= 32 && vbits < 32 ? vg_sorted<unsigned int>(ctx, in, in_stride, total, vbits, sbits, o)
+                                          : vg_sorted<unsigned long long>(ctx, in, in_stride, total, vbits, sbits, o);
+        if (r) return r;
+    } else {
+        SLO_CHECK(hipMemsetAsync(w.rank, 0, sizeof(int), ctx->stream));
     }
-    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, dim3((total + 1 + T - 1) / T), dim3(T), 0, w.keys2, total, w.flags);
-    {
-        size_t tb = w.temp_bytes;
-        SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.flags, w.rank, total + 1, ctx->stream));
-    }
-    if (total > 0)
-        SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid, dim3((total + T - 1) / T), dim3(T), 0, in, in_stride, w.keys2,
-                   w.vals2, w.rank, w.off, total, out, out_stride, out_cap);
     SLO_LAUNCH(ctx, "vg_count", k_vg_count, dim3((S + 63) / 64), dim3(64), 0, w.rank, w.off, S, d_nout, nout_stride,
                out_cap, w.errflag);
     (void)tag;
@@ -309,15 +443,17 @@ int vg_alloc(slo_ctx* ctx) {
     SLO_CHECK(hipMalloc(&w.prm, sizeof(VgParams) * S));
     SLO_CHECK(hipMalloc(&w.errflag, sizeof(int32_t)));
     SLO_CHECK(hipMemset(w.errflag, 0, sizeof(int32_t)));
-    SLO_CHECK(hipHostMalloc((void**)&w.h_total, sizeof(int32_t)));
+    SLO_CHECK(hipMalloc(&w.meta, 4 * sizeof(int32_t)));
+    SLO_CHECK(hipHostMalloc((void**)&w.h_meta, 4 * sizeof(int32_t)));
     return 0;
 }
 
 void vg_free(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
-    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.temp, w.off, w.bounds, w.prm, w.errflag};
+    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.starts, w.ends, w.longv,
+                  w.temp, w.off, w.bounds, w.prm, w.errflag, w.meta};
     for (void* p : ps) if (p) hipFree(p);
-    if (w.h_total) hipHostFree(w.h_total);
+    if (w.h_meta) hipHostFree(w.h_meta);
     w = MapWs();
 }
 
