@@ -259,7 +259,7 @@ template <int R>
 __constant__ GridRows<R> kGridRows = GridRows<R>();
 
 #define GBALL_UNROLL 4
-template <int R, class B, class F>
+template <int R, int U = GBALL_UNROLL, class B, class F>
 __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
     const float inv = g.inv, cell = g.cell, c2 = cell * cell;
     const int cx = grid_cell(qx, inv), cy = grid_cell(qy, inv), cz = grid_cell(qz, inv);
@@ -284,13 +284,13 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
         const int w1 = h + len - h2;   // buckets wrapped to the table start
         const int f1 = w1 > 0 ? g.off[gb + w1] - base : 0;
         for (int pass = 0; pass < 2; ++pass) {
-            for (int e = e0; e < e1; e += GBALL_UNROLL) {
-                float4 p[GBALL_UNROLL];
+            for (int e = e0; e < e1; e += U) {
+                float4 p[U];
 #pragma unroll
-                for (int u = 0; u < GBALL_UNROLL; ++u)
+                for (int u = 0; u < U; ++u)
                     p[u] = e + u < e1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-                for (int u = 0; u < GBALL_UNROLL; ++u) {
+                for (int u = 0; u < U; ++u) {
                     if (e + u >= e1) break;
                     const int px = grid_cell(p[u].x, inv);
                     if (grid_cell(p[u].y, inv) != yy || grid_cell(p[u].z, inv) != zz || px < xa || px > xb) continue;

@@ -208,8 +208,6 @@ __global__ void __launch_bounds__(256) k_ip_tile(DevView v) {
         v.ground[o] = (int8_t)g;
         const int lab = (g == 1 || rg == FLT_MAX) ? -1 : 0;
         v.label[o] = lab;
-        v.crows[2 * o] = 0ull;
-        v.crows[2 * o + 1] = 0ull;
         l_lab[l] = (int8_t)lab;
         l_rg[l] = rg;
     }
@@ -234,7 +232,8 @@ __global__ void __launch_bounds__(256) k_ip_tile(DevView v) {
             g = ri * C + c0 + (r - ri * TC);
         }
         v.parent[base + p] = g;
-        v.csize[base + p] = g == p ? IP_LROOT : 0;
+        v.csize[base + p] = g == p ? IP_LROOT : 0;   // sizes and row sets are only kept at roots
+        if (g == p) { v.crows[2 * (base + p)] = 0ull; v.crows[2 * (base + p) + 1] = 0ull; }
     }
 }
 
@@ -392,15 +391,15 @@ __global__ void k_ip_rowcount(DevView v) {
     }
 }
 
-// block = 256 threads per (row, stream); thread t owns a contiguous chunk of
-// the row so a block scan keeps row-major order.
-__global__ void k_ip_compact(DevView v) {
+// block = 256 threads per (row, stream): the row's kept and outlier pixels
+// are appended in row-major order (cloudSegmentation, IP:319-355) after the
+// rows before it.
+__global__ void __launch_bounds__(256) k_ip_compact(DevView v) {
     const int s = blockIdx.y, i = blockIdx.x;
     const int C = v.cfg.horizon_scan, R = v.cfg.n_scan;
     const size_t base = (size_t)s * v.H;
     const int* rc = v.rowcnt + (size_t)s * R * 2;
     __shared__ int s_off[2], s_tot[2];
-    __shared__ int sc_k[256], sc_o[256];
     __shared__ int s_red[4][4];
     {   // rows before i and all rows, kept / outlier
         int a = 0, b = 0, ta = 0, tb = 0;
@@ -424,38 +423,37 @@ __global__ void k_ip_compact(DevView v) {
             s_off[0] = s_red[0][0]; s_off[1] = s_red[0][1]; s_tot[0] = s_red[0][2]; s_tot[1] = s_red[0][3];
         }
     }
-    const int T = blockDim.x;
-    const int chunk = (C + T - 1) / T;
-    const int j0 = threadIdx.x * chunk, j1 = min(C, j0 + chunk);
-    int kc = 0, oc = 0;
-    for (int j = j0; j < j1; ++j) { bool k, o; pixel_kind(v, base, i, j, k, o); kc += k; oc += o; }
-    sc_k[threadIdx.x] = kc; sc_o[threadIdx.x] = oc;
+    // one pixel per thread per pass, in row order; positions by wave ballots
+    // and a 4-wave scan
+    __shared__ int s_wt[2][4];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long below = (1ull << lane) - 1;
     __syncthreads();
-    // inclusive scan (Hillis-Steele) over 256 entries
-    for (int d = 1; d < T; d <<= 1) {
-        int a = threadIdx.x >= d ? sc_k[threadIdx.x - d] : 0;
-        int b = threadIdx.x >= d ? sc_o[threadIdx.x - d] : 0;
+    int wk = s_off[0], wo = s_off[1];
+    for (int j0 = 0; j0 < C; j0 += 256) {
+        const int j = j0 + (int)threadIdx.x;
+        bool k = false, o = false;
+        if (j < C) pixel_kind(v, base, i, j, k, o);
+        const unsigned long long mk = __ballot(k), mo = __ballot(o);
+        if (lane == 0) { s_wt[0][w] = __popcll(mk); s_wt[1][w] = __popcll(mo); }
         __syncthreads();
-        sc_k[threadIdx.x] += a; sc_o[threadIdx.x] += b;
-        __syncthreads();
-    }
-    int wk = s_off[0] + sc_k[threadIdx.x] - kc;
-    int wo = s_off[1] + sc_o[threadIdx.x] - oc;
-    for (int j = j0; j < j1; ++j) {
-        bool k, o;
-        pixel_kind(v, base, i, j, k, o);
-        const size_t px = base + i * C + j;
+        int pk = 0, po = 0, tk = 0, to = 0;
+        for (int ww = 0; ww < 4; ++ww) {
+            if (ww < w) { pk += s_wt[0][ww]; po += s_wt[1][ww]; }
+            tk += s_wt[0][ww]; to += s_wt[1][ww];
+        }
+        const size_t px = base + (size_t)i * C + j;
         if (k) {
-            const size_t d = base + wk;
+            const size_t d = base + wk + pk + __popcll(mk & below);
             v.seg[d] = v.full[px];
             v.seg_ground[d] = v.ground[px] == 1;
             v.seg_col[d] = (uint32_t)j;
             v.seg_range[d] = v.range[px];
-            ++wk;
         } else if (o) {
-            v.outlier[base + wo] = v.full[px];
-            ++wo;
+            v.outlier[base + wo + po + __popcll(mo & below)] = v.full[px];
         }
+        wk += tk; wo += to;
+        __syncthreads();
     }
     if (threadIdx.x == 0) {
         int* se = v.ring_se + (size_t)s * R * 2;

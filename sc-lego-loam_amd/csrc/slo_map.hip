@@ -137,6 +137,9 @@ __device__ inline float sqd(const P4& q, float x, float y, float z) {
 // od[4] == 1 and the query is rejected either way.  So the search is a ball
 // of squared radius 1 — R = 2 cells of 0.5 m — whose bound is the current 5th
 // distance.
+#ifndef SLO_KNN_UNROLL
+#define SLO_KNN_UNROLL 2   // entry loads in flight per walk step: 4 costs occupancy (110 VGPRs -> 4 waves)
+#endif
 __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float* od) {
     // sorted top-5 by (distance, index); empty slots are (1, INT_MAX).
     // Insertion is unrolled with constant indices so the lists stay in
@@ -146,7 +149,7 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
     if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return 0;
     auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
     int n = 0;
-    grid_ball<2>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
+    grid_ball<2, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
         const float d = sqd(q, p.x, p.y, p.z);
         const int idx = __float_as_int(p.w);
         if (!less(d, idx, od[4], oi[4])) return;
