@@ -9,7 +9,7 @@ import os
 import subprocess
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))   # sc-lego-loam_amd/
-LIB_PATH = os.path.join(_PKG, "libslo.so")
+LIB_PATH = os.environ.get("SLO_LIB") or os.path.join(_PKG, "libslo.so")   # SLO_LIB: an experiment build
 _LIB = None
 
 
