@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
     ap.add_argument("--cpu-scans", type=int, default=40, help="scans per CPU thread in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
+    ap.add_argument("--traffic-from", default=None,
+                    help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
     return ap.parse_args()
 
 
@@ -90,6 +92,22 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
     if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
         return steps * int(c["seg_pts"].sum()) * (4 + 4 + 4 + 4 + 4 + 2 + 16)
     return None
+
+
+def pmc_traffic(path, kernel):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, MI355X_MICROARCH.md), or None."""
+    import glob
+    import json
+    if path is None:
+        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
+        path = cands[-1] if cands else None
+    if path is None or not os.path.exists(path):
+        return None, None
+    k = json.load(open(path))["kernels"].get(kernel)
+    if not k or not k.get("hbm_bytes_per_launch"):
+        return None, None
+    return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
 
 
 def main():
@@ -187,9 +205,10 @@ def main():
             kb = algo_bytes(kn, counts, cfg, S, a.profile_steps, map_steps)
             if kb is not None and kms > 0:
                 gbs[kn] = round(kb / (kms / 1e3) / 1e9, 1)
+        traffic, tsrc = pmc_traffic(a.traffic_from, name)
         roof = {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
-                "traffic": None, "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
+                "traffic": traffic, "traffic_source": tsrc, "kernel": name, "avg_launch_us": round(avg_s * 1e6, 2),
                 "bytes_per_launch": int(b / n) if b is not None else None,
                 "share_of_device_time": round(ms / total_ms, 4)}
 
