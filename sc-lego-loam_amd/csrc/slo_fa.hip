@@ -307,8 +307,8 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
 // visiting order (sharp ep..sp, flat sp..ep), stored for k_fa_pick.
 //
 // k_fa_pick (one wave): the greedy picks (FA:701-766) walk only those lists,
-// testing picked[] and marking neighbours, on one lane — a small LDS footprint
-// so many rings' serial walks share each CU — then all lanes gather the
+// 64 candidates per round, one pick per round (see the loop) — a small LDS
+// footprint so many rings share each CU — then all lanes gather the
 // points and collect the less-flat points (label <= 0, FA:768-776) with a
 // wave ballot: a sector's picks only label that sector's own points, so
 // collecting after all six sectors equals the reference's interleaving.
@@ -414,8 +414,6 @@ __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
     const float4* fp = v.fpts + base;
     __shared__ uint16_t lcol[SLO_RING_STAGE];
     __shared__ int8_t lpk[SLO_RING_STAGE], llab[SLO_RING_STAGE];
-    __shared__ int16_t l_sh[SLO_RING_STAGE], l_fl[SLO_RING_STAGE];
-    __shared__ int s_cnt[3];
     __shared__ int p_sh[12], p_ls[120], p_fl[24];
     const int16_t* g_sh = v.ex_list + (size_t)s * v.H * 2;
     const int16_t* g_fl = g_sh + v.H;
@@ -425,77 +423,71 @@ __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
         llab[k] = (int8_t)lab[lo + k];
         lcol[k] = (uint16_t)v.seg_col[base + lo + k];
     }
-    for (int j = 0; j < 6; ++j) {   // lists sit at their sector's positions
-        const int sp = sec_sp(rs, re, j);
-        const int ns = cnt[2 * j], nf = cnt[2 * j + 1];
-        if (sec_ep(rs, re, j) <= sp) continue;
-        for (int c = lane; c < ns; c += 64) l_sh[sp - lo + c] = g_sh[sp + c];
-        for (int c = lane; c < nf; c += 64) l_fl[sp - lo + c] = g_fl[sp + c];
-    }
     __syncthreads();
-    if (lane == 0) {
-        auto mark = [&](int ind) __attribute__((always_inline)) {   // FA:719-731 / 752-764
-            // the 11 columns around ind, loaded together (colInd[-1] -> 0, Q5),
-            // then the two break-at-gap walks on registers
-            int c[11];
-#pragma unroll
-            for (int k = 0; k < 11; ++k) {
-                const int i = ind - 5 + k;
-                c[k] = i < 0 ? 0 : (int)lcol[max(i, lo) - lo];
-            }
-            bool go = true;
-#pragma unroll
-            for (int l = 1; l <= 5; l++) {
-                go = go && abs(c[5 + l] - c[4 + l]) <= 10;
-                if (go) lpk[ind + l - lo] = 1;
-            }
-            go = true;
-#pragma unroll
-            for (int l = 1; l <= 5; l++) {
-                go = go && abs(c[5 - l] - c[6 - l]) <= 10;
-                if (go && ind - l >= 0) lpk[ind - l - lo] = 1;
-            }
-        };
-        int n_sharp = 0, n_lsharp = 0, n_flat = 0;
-        for (int j = 0; j < 6; j++) {
-            const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
-            if (sp >= ep) continue;
-            const int ns = cnt[2 * j], nf = cnt[2 * j + 1];
-            int largestPickedNum = 0;
-            for (int c = 0; c < ns; ++c) {
-                const int ind = lo + l_sh[sp - lo + c];
-                if (lpk[ind - lo] == 0) {
-                    largestPickedNum++;
-                    if (largestPickedNum <= 2) {
-                        llab[ind - lo] = 2;
-                        p_sh[n_sharp++] = ind;
-                        p_ls[n_lsharp++] = ind;
-                    } else if (largestPickedNum <= 20) {
-                        llab[ind - lo] = 1;
-                        p_ls[n_lsharp++] = ind;
+    // FA:719-731 / 752-764 on lanes 1..10: lanes 1..5 test the column gaps
+    // forward, 6..10 backward; a neighbour is marked when every gap up to it
+    // passes (the reference's walk breaks at the first failing gap).
+    // colInd[-1] reads 0 (Q5).
+    auto mark = [&](int ind) __attribute__((always_inline)) {
+        auto col = [&](int i) __attribute__((always_inline)) { return i < 0 ? 0 : (int)lcol[max(i, lo) - lo]; };
+        const int l = lane <= 5 ? lane : lane - 5;
+        const bool fwd = lane >= 1 && lane <= 5, bwd = lane >= 6 && lane <= 10;
+        const int tgt = fwd ? ind + l : ind - l;
+        bool ok = false;
+        if (fwd) ok = abs(col(ind + l) - col(ind + l - 1)) <= 10;
+        else if (bwd) ok = abs(col(ind - l) - col(ind - l + 1)) <= 10;
+        const unsigned long long m = __ballot(ok);
+        const unsigned int need = (1u << l) - 1;
+        if (fwd && (((unsigned int)(m >> 1) & need) == need)) lpk[tgt - lo] = 1;
+        if (bwd && (((unsigned int)(m >> 6) & need) == need) && tgt >= 0) lpk[tgt - lo] = 1;
+    };
+    // Greedy picks (FA:701-766), one wave per ring.  The candidates of a list
+    // are taken 64 at a time; each round the first one still unpicked is the
+    // one the serial walk picks next (every earlier one is already marked, and
+    // marks only accumulate), so the rounds = picks, not candidates.
+    int n_sharp = 0, n_lsharp = 0, n_flat = 0;
+    for (int j = 0; j < 6; j++) {
+        const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+        if (sp >= ep) continue;
+        for (int phase = 0; phase < 2; ++phase) {   // sharp, then flat
+            const int n = cnt[2 * j + phase];
+            const int16_t* list = (phase == 0 ? g_sh : g_fl) + sp;
+            int npk = 0;
+            bool done = false;
+            for (int c0 = 0; c0 < n && !done; c0 += 64) {
+                const int myind = c0 + lane < n ? lo + list[c0 + lane] : -1;
+                int cur = 0;
+                while (true) {
+                    const bool ok = lane >= cur && myind >= 0 && lpk[myind - lo] == 0;
+                    const unsigned long long m = __ballot(ok);
+                    if (!m) break;
+                    const int f = __ffsll((long long)m) - 1;
+                    const int ind = __shfl(myind, f, 64);
+                    cur = f + 1;
+                    ++npk;
+                    if (phase == 0) {
+                        if (npk > 20) { done = true; break; }
+                        if (lane == 0) {
+                            llab[ind - lo] = npk <= 2 ? 2 : 1;
+                            if (npk <= 2) p_sh[n_sharp] = ind;
+                            p_ls[n_lsharp] = ind;
+                        }
+                        n_sharp += npk <= 2;
+                        ++n_lsharp;
                     } else {
-                        break;
+                        if (lane == 0) { llab[ind - lo] = -1; p_fl[n_flat] = ind; }
+                        ++n_flat;
+                        if (npk >= 4) { done = true; break; }
                     }
-                    lpk[ind - lo] = 1;
+                    if (lane == 0) lpk[ind - lo] = 1;
                     mark(ind);
-                }
-            }
-            int smallestPickedNum = 0;
-            for (int c = 0; c < nf; ++c) {
-                const int ind = lo + l_fl[sp - lo + c];
-                if (lpk[ind - lo] == 0) {
-                    llab[ind - lo] = -1;
-                    p_fl[n_flat++] = ind;
-                    smallestPickedNum++;
-                    if (smallestPickedNum >= 4) break;
-                    lpk[ind - lo] = 1;
-                    mark(ind);
+                    __syncthreads();   // one wave: orders this round's LDS writes before the next reads
                 }
             }
         }
-        s_cnt[0] = n_sharp; s_cnt[1] = n_lsharp; s_cnt[2] = n_flat;
     }
     __syncthreads();
+    const int s_cnt[3] = {n_sharp, n_lsharp, n_flat};
     const size_t rr = (size_t)s * R + ring;
     for (int t = lane; t < s_cnt[0]; t += 64) v.r_sharp[rr * 12 + t] = fp[p_sh[t]];
     for (int t = lane; t < s_cnt[1]; t += 64) v.r_less_sharp[rr * 120 + t] = fp[p_ls[t]];
