@@ -222,8 +222,17 @@ __device__ inline float ord2f_fa(unsigned int o) {
     return __uint_as_float((o & 0x80000000u) ? (o & 0x7fffffffu) : ~o);
 }
 
-template <int NE>
-__device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_flag) {
+// Sorts a[0, n) of one sector by curvature in registers.  Keys are
+// (curvature, not-a-candidate, index): equal curvatures are std::sort's only
+// freedom, and their order is observable only through the pick lists, i.e.
+// between two candidates of the same list (cand(ind): the point is in the
+// sector's sharp or flat list — for one curvature value all candidates are in
+// the same list).  So candidates come first inside a group of equal
+// curvatures, and when a group holds two of them the sector is flagged for
+// the exact introsort; otherwise the result is written back (its order of
+// non-candidates inside a group is never read).
+template <int NE, class Cand>
+__device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_flag, Cand&& cand) {
     unsigned long long k[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
@@ -231,7 +240,8 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
         k[e] = ~0ull;
         if (i < n) {
             const Smooth x = a[i];
-            k[e] = ((unsigned long long)f2ord_fa(x.value) << 32) | (unsigned int)x.ind;
+            k[e] = ((unsigned long long)f2ord_fa(x.value) << 32) | (cand(x.ind) ? 0u : 0x80000000u) |
+                   (unsigned int)x.ind;
         }
     }
     constexpr int N = 64 * NE;
@@ -265,7 +275,7 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
             }
         }
     }
-    // ties: equal curvature bits in adjacent positions
+    // ties that matter: two candidates of equal curvature, adjacent
     bool tie = false;
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
@@ -273,14 +283,15 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
         const unsigned long long up1 = __shfl_up(k[e], 1, 64);                      // lane - 1
         const unsigned long long wrap = e > 0 ? __shfl(k[e > 0 ? e - 1 : 0], 63, 64) : ~0ull;   // all lanes
         const unsigned long long prev = lane == 0 ? wrap : up1;
-        if (p > 0 && p < n && (prev >> 32) == (k[e] >> 32)) tie = true;
+        if (p > 0 && p < n && (prev >> 32) == (k[e] >> 32) && !(prev & 0x80000000ull) && !(k[e] & 0x80000000ull))
+            tie = true;
     }
     const bool any_tie = __any(tie);
     if (!any_tie) {
 #pragma unroll
         for (int e = 0; e < NE; ++e) {
             const int p = e * 64 + lane;
-            if (p < n) a[p] = Smooth{ord2f_fa((unsigned int)(k[e] >> 32)), (int)(unsigned int)k[e]};
+            if (p < n) a[p] = Smooth{ord2f_fa((unsigned int)(k[e] >> 32)), (int)((unsigned int)k[e] & 0x7fffffffu)};
         }
     } else if (lane == 0) {
         *tie_flag = 1;
@@ -318,7 +329,9 @@ __device__ inline bool ring_window(const DevView& v, int s, int ring, int& rs, i
     const int* se = v.ring_se + (size_t)s * v.cfg.n_scan * 2;
     rs = se[2 * ring]; re = se[2 * ring + 1];
     lo = max(0, rs - 5); hi = min(v.H, re + 5);
-    return hi > lo && hi - lo <= SLO_RING_STAGE;
+    // rs >= 5: every sorted entry is this scan's (ring 0 empty would put the
+    // stale entry 4 here, Q5)
+    return rs >= 5 && hi > lo && hi - lo <= SLO_RING_STAGE;
 }
 
 __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
@@ -335,6 +348,12 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     __shared__ float lcv[SLO_RING_STAGE];
     __shared__ uint8_t lgf[SLO_RING_STAGE];
     __shared__ int s_tie[6];
+#if SLO_DIAG
+    unsigned long long t_d = clock64();
+#define SORT_STAMP(k) if (tid == 0) { const unsigned long long t_n = clock64(); atomicAdd(&v.st[s].dbg[k], t_n - t_d); t_d = t_n; }
+#else
+#define SORT_STAMP(k)
+#endif
     for (int k = tid; k < hi - lo; k += blockDim.x) {
         lsm[k] = sm[lo + k];
         lcv[k] = v.curv[base + lo + k];
@@ -342,28 +361,37 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     }
     if (tid < 6) s_tie[tid] = 0;
     __syncthreads();
+    SORT_STAMP(0)
     // ---- sector sorts: two rounds of (up to) four sectors, one wave each
     for (int r0 = 0; r0 < 6; r0 += 4) {
         const int j = r0 + wave;
         if (j < 6) {
             const int sp = sec_sp(rs, re, j), n = sec_ep(rs, re, j) - sp;
             Smooth* a = &lsm[sp - lo];
+            // the list predicates of the candidate pass below (FA:704-705, 737-738)
+            auto cand = [&](int ind) __attribute__((always_inline)) {
+                const float c = lcv[ind - lo];
+                const int g = lgf[ind - lo];
+                return ind < S && ((c > v.cfg.edge_threshold && g == 0) || (c < v.cfg.surf_threshold && g == 1));
+            };
             switch ((n + 63) >> 6) {
                 case 0: break;
-                case 1: if (n > 1) bitonic_sort_wave<1>(a, n, lane, &s_tie[j]); break;
-                case 2: bitonic_sort_wave<2>(a, n, lane, &s_tie[j]); break;
-                case 3: case 4: bitonic_sort_wave<4>(a, n, lane, &s_tie[j]); break;
-                case 5: case 6: case 7: case 8: bitonic_sort_wave<8>(a, n, lane, &s_tie[j]); break;
+                case 1: if (n > 1) bitonic_sort_wave<1>(a, n, lane, &s_tie[j], cand); break;
+                case 2: bitonic_sort_wave<2>(a, n, lane, &s_tie[j], cand); break;
+                case 3: case 4: bitonic_sort_wave<4>(a, n, lane, &s_tie[j], cand); break;
+                case 5: case 6: case 7: case 8: bitonic_sort_wave<8>(a, n, lane, &s_tie[j], cand); break;
                 default: if (lane == 0) s_tie[j] = 1; break;
             }
         }
     }
     __syncthreads();
+    SORT_STAMP(1)
     if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
         const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
         slo_sort::std_sort(&lsm[sp - lo], ep - sp, SmoothLess());
     }
     __syncthreads();
+    SORT_STAMP(2)
     // ---- candidate lists: point indices as window offsets, in visiting order
     int16_t* l_sh = v.ex_list + (size_t)s * v.H * 2;
     int16_t* l_fl = l_sh + v.H;
@@ -395,7 +423,13 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
             }
         if (lane == 0) { cnt[2 * j] = ns; cnt[2 * j + 1] = nf; }
     }
+    SORT_STAMP(3)
     for (int k = tid; k < hi - lo; k += blockDim.x) sm[lo + k] = lsm[k];
+#if SLO_DIAG
+    if (tid < 6 && s_tie[tid]) atomicAdd(&v.st[s].dbg[5], 1ull);
+#endif
+    SORT_STAMP(4)
+#undef SORT_STAMP
 }
 
 __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {

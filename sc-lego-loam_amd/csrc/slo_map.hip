@@ -335,7 +335,7 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
             if (okrow) ++nsel;
             else for (int k = 0; k < 7; ++k) row[k] = 0.0f;   // rejected: contributes exact zeros
 #if SLO_DIAG
-            if ((threadIdx.x & 63) == 0) atomicAdd(&v.st[s].dbg[1], clock64() - t_row);   // wave time per round
+            if ((threadIdx.x & 63) == 0) atomicAdd(&v.st[s].dbg[7], clock64() - t_row);   // wave time per round
 #endif
             for (int k = 0; k < 7; ++k) rows[tid][k] = row[k];
             __syncthreads();

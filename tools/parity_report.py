@@ -16,7 +16,7 @@ import numpy as np  # noqa: E402
 
 import oracle_py as O  # noqa: E402
 import slo_amd  # noqa: E402
-from parity_util import mismatch, seg_class  # noqa: E402
+from parity_util import canon_smooth, mismatch, seg_class  # noqa: E402
 
 FRONT = ["range", "ground", "seg_pts", "seg_ground", "seg_col", "seg_range", "ring_start", "ring_end", "orient",
          "outlier", "fa_seg_pts", "sharp", "flat", "corner_last", "surf_last"]
@@ -59,8 +59,14 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                     row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
                 row["label_class"] = int((seg_class(ctx.get(s, "label")) != seg_class(ors[s].get("label"))).sum())
                 S = len(ors[s].get("seg_pts"))
-                for name in ("curvature", "picked", "cloud_label", "smooth_ind"):
+                for name in ("curvature", "picked", "cloud_label"):
                     row[name] = mismatch(ctx.get(s, name)[:S], ors[s].get(name)[:S])
+                cfg_o = O.preset(preset_id)
+                cv, sg = ors[s].get("curvature"), ors[s].get("seg_ground")
+                rso, reo = ors[s].get("ring_start"), ors[s].get("ring_end")
+                cs = [canon_smooth(x[:S], cv, sg, rso, reo, cfg_o.edge_threshold, cfg_o.surf_threshold)
+                      for x in (ctx.get(s, "smooth_ind"), ors[s].get("smooth_ind"))]
+                row["smooth_ind"] = mismatch(cs[0], cs[1])
             row["odom"] = posediff(ctx.get(s, "transform_sum"), ors[s].get("transform_sum"))
             worst["odom"] = max(worst["odom"], row["odom"])
             if fl_o & 2:
