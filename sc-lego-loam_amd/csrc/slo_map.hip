@@ -364,19 +364,32 @@ __global__ void __launch_bounds__(256) k_mo_corr(DevView v) {
 }
 
 // LMOptimization tail (MO:1445-1498) for one stream
-__global__ void k_mo_solve(DevView v, int iterCount) {
+__global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
-    if (threadIdx.x != 0) return;
     if (!(st.mo_ran && st.map_ok && !st.mo_converged)) return;
-    slo_dd::DD acc[27];
-    for (int k = 0; k < 27; ++k) acc[k] = slo_dd::zero();
-    int nsel = 0;
-    for (int b = 0; b < SLO_MO_BLOCKS; ++b) {
-        const double* part = v.mo_part + ((size_t)s * SLO_MO_BLOCKS + b) * SLO_MO_PART;
-        for (int k = 0; k < 27; ++k) slo_dd::merge(acc[k], slo_dd::DD{part[2 * k], part[2 * k + 1]});
-        nsel += (int)part[54];
+    // the workgroups' partial sums: lane k < 27 folds term k, lane 27 the
+    // correspondence count (double-double: the fold order does not change the
+    // rounded result, slo_ddsum.h)
+    __shared__ slo_dd::DD s_acc[27];
+    __shared__ int s_nsel;
+    const int lane = threadIdx.x;
+    if (lane < 27) {
+        slo_dd::DD a = slo_dd::zero();
+        const double* part = v.mo_part + (size_t)s * SLO_MO_BLOCKS * SLO_MO_PART + 2 * lane;
+#pragma unroll 8
+        for (int b = 0; b < SLO_MO_BLOCKS; ++b)
+            slo_dd::merge(a, slo_dd::DD{part[(size_t)b * SLO_MO_PART], part[(size_t)b * SLO_MO_PART + 1]});
+        s_acc[lane] = a;
+    } else if (lane == 27) {
+        int n = 0;
+        for (int b = 0; b < SLO_MO_BLOCKS; ++b) n += (int)v.mo_part[((size_t)s * SLO_MO_BLOCKS + b) * SLO_MO_PART + 54];
+        s_nsel = n;
     }
+    __syncthreads();
+    if (lane != 0) return;
+    const slo_dd::DD* acc = s_acc;
+    const int nsel = s_nsel;
     st.mo_iters = iterCount + 1;
     st.n_sel = nsel;
     if (nsel < 50) return;  // LMOptimization returns false, loop continues
