@@ -27,6 +27,9 @@ import json
 import os
 import sys
 import time
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sc-lego-loam_amd"))
@@ -40,13 +43,17 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--streams", type=int, default=192, help="streams per GPU")
+    ap.add_argument("--streams", type=int, default=256, help="streams per GPU")
+    ap.add_argument("--groups", type=int, default=2,
+                    help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
     ap.add_argument("--preset", default="hdl64_1800")
     ap.add_argument("--config-id", type=int, default=3)
     ap.add_argument("--history", type=int, default=60, help="seeded Scan Context history per stream")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
     ap.add_argument("--cpu-scans", type=int, default=40, help="scans per CPU thread in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
     ap.add_argument("--traffic-from", default=None,
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
     return ap.parse_args()
@@ -99,9 +106,11 @@ def pmc_traffic(path, kernel):
     (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, MI355X_MICROARCH.md), or None."""
     import glob
     import json
-    if path is None:
-        cands = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json")))
-        path = cands[-1] if cands else None
+    if path is None:   # the latest round's profile: profiles/rNN/
+        import re
+        cands = [(int(m.group(1)), p) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json"))
+                 for m in [re.search(r"profiles/r(\d+)/summary\.json$", p)] if m]
+        path = max(cands)[1] if cands else None
     if path is None or not os.path.exists(path):
         return None, None
     k = json.load(open(path))["kernels"].get(kernel)
@@ -119,7 +128,8 @@ def main():
 
     rank, world, local = sdist.env_rank()
     torch.cuda.set_device(local)
-    if world > 1:
+    gather = world > 1 or a.force_gather
+    if gather:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = slo_amd.preset(a.preset)
     pid = slo_amd.PRESETS[a.preset]
@@ -141,60 +151,91 @@ def main():
         dev[k0:k0 + nk].copy_(torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, k0, nk, P, gthreads)))
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
 
-    ctx = slo_amd.Context(cfg, local, S)
-    rec_n = ctx.L.slo_record_floats()
+    groups = sdist.group_slices(S, a.groups)
+    ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
+    rec_n = ctxs[0].L.slo_record_floats()
     rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if world > 1 else None
-    ext = torch.cuda.ExternalStream(ctx.stream_handle)
+    gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
+    exts = [torch.cuda.ExternalStream(c.stream_handle) for c in ctxs]
+    pool = ThreadPoolExecutor(max_workers=len(ctxs)) if len(ctxs) > 1 else None
+
+    def each(fn):
+        """fn(g, ctx, offset, count) for every group, concurrently (ctypes drops the GIL)"""
+        if pool is None:
+            fn(0, ctxs[0], *groups[0])
+            return
+        for f in [pool.submit(fn, g, c, *groups[g]) for g, c in enumerate(ctxs)]:
+            f.result()
 
     # seed Scan Context history (makeAndSaveScancontextAndKeys) in chunks
     for h0 in range(-a.history, 0, 4):
         nh = min(4, -h0)
         hist = torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, h0, nh, P, gthreads)).cuda(local)
         for h in range(nh):
-            ctx.batch_sc_make(hist[h].data_ptr(), cnt.data_ptr())
-        ctx.synchronize()
+            each(lambda g, c, o, n: c.batch_sc_make(hist[h, o].data_ptr(), cnt[o].data_ptr()))
+        each(lambda g, c, o, n: c.synchronize())
         del hist
     t_gen = time.time() - t_gen
 
+    def sync_all():
+        each(lambda g, c, o, n: c.synchronize())
+
     def step(k):
-        ctx.batch_process(dev[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
-        if world > 1:
-            ctx.pack_records(rec.data_ptr())
-            with torch.cuda.stream(ext):
+        each(lambda g, c, o, n: c.batch_process(dev[k, o].data_ptr(), cnt[o].data_ptr(), 0.1 * k))
+        if gather:   # records of every group, then one all-gather after all of them
+            evs = []
+            for g, c in enumerate(ctxs):
+                c.pack_records(rec[groups[g][0]].data_ptr())
+                ev = torch.cuda.Event()
+                ev.record(exts[g])
+                evs.append(ev)
+            for ev in evs[1:]:
+                exts[0].wait_event(ev)
+            with torch.cuda.stream(exts[0]):
                 sdist.gather_records(rec, gathered)
+                done = torch.cuda.Event()
+                done.record(exts[0])
+            for e in exts[1:]:
+                e.wait_event(done)   # next step's records overwrite rec
 
     for k in range(a.warmup):
         step(k)
-    ctx.synchronize()
+    sync_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for k in range(a.warmup, a.warmup + a.steps):
         step(k)
-    ctx.synchronize()
+    sync_all()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
     value = S * a.steps * world / el
-    errs = sum(int(ctx.get(s, "err")[0]) != 0 for s in range(S))
+    errs = sum(int(c.get(s, "err")[0]) != 0 for c in ctxs for s in range(c.n_streams))
 
-    # ---- instrumented pass: per-kernel HIP-event times on the context stream
+    # ---- instrumented pass: per-kernel HIP-event times on each context's
+    # stream, groups run one after the other so the events time each kernel alone
     roof, kt, workload, gbs = None, {}, None, {}
     if a.profile_steps > 0:
-        ctx.timing(True)
-        ctx.timing_reset()
+        for c in ctxs:
+            c.timing(True)
+            c.timing_reset()
         k0 = a.warmup + a.steps
         map_steps = 0
         for k in range(k0, k0 + a.profile_steps):
-            step(k)
-            ctx.synchronize()
-            map_steps += int(int(ctx.get(0, "flags")[0]) & 2 != 0)
-        kt = ctx.timing_read()
-        ctx.timing(False)
-        counts = stream_counts(ctx, S)
+            for g, c in enumerate(ctxs):
+                c.batch_process(dev[k, groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(), 0.1 * k)
+                c.synchronize()
+            map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
+        for c in ctxs:
+            for kn, (kms, kcalls) in c.timing_read().items():
+                m0, c0 = kt.get(kn, (0.0, 0))
+                kt[kn] = (m0 + kms, c0 + kcalls)
+            c.timing(False)
+        parts = [stream_counts(c, c.n_streams) for c in ctxs]
+        counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1}
         total_ms = sum(v[0] for v in kt.values())
         name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
@@ -235,7 +276,8 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10",
-                       "preset": a.preset, "streams_per_gpu": S, "scans_per_step": S * world,
+                       "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": len(ctxs),
+                       "scans_per_step": S * world,
                        "sc_history_seed": a.history, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,
             "cpu_baseline": cpu,
@@ -246,8 +288,11 @@ def main():
             "setup_seconds": round(t_gen, 1),
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
-    if world > 1:
+    for c in ctxs:
+        c.close()
+    if pool is not None:
+        pool.shutdown()
+    if gather:
         dist.destroy_process_group()
 
 

@@ -27,6 +27,22 @@ def stream_shard(rank, world, streams_per_rank):
     return rank * streams_per_rank, streams_per_rank
 
 
+def group_slices(streams_per_rank, groups):
+    """Split a rank's streams into `groups` contiguous (offset, count) slices,
+    one per context.  Each context runs on its own HIP stream and host thread,
+    so one group's latency-bound phases and host round trips (the VoxelGrid
+    size read) overlap the other's kernels."""
+    if groups <= 0 or streams_per_rank < groups:
+        raise ValueError("bad groups")
+    base, extra = divmod(streams_per_rank, groups)
+    out, o = [], 0
+    for g in range(groups):
+        n = base + (1 if g < extra else 0)
+        out.append((o, n))
+        o += n
+    return out
+
+
 def gather_records(rec, out=None):
     """All-gather the [S, F] per-stream records of every rank into
     [world*S, F], rank-major (= global stream order)."""

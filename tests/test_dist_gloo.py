@@ -64,3 +64,15 @@ def test_stream_shard_bounds():
     assert sdist.stream_shard(3, 8, 64) == (192, 64)
     with pytest.raises(ValueError):
         sdist.stream_shard(8, 8, 64)
+
+
+def test_group_slices_cover_the_rank():
+    from slo_amd.dist import group_slices
+    for S, G in [(256, 2), (192, 1), (7, 3), (5, 5)]:
+        sl = group_slices(S, G)
+        assert len(sl) == G
+        assert sl[0][0] == 0 and sum(n for _, n in sl) == S
+        assert all(sl[i][0] + sl[i][1] == sl[i + 1][0] for i in range(G - 1))
+        assert max(n for _, n in sl) - min(n for _, n in sl) <= 1
+    with pytest.raises(ValueError):
+        group_slices(2, 3)
