@@ -127,7 +127,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.clabel, S * H);
     c.add(&v.smooth, S * H);
     c.add(&v.ex_list, 2 * S * H);
-    c.add(&v.ex_cnt, 12 * S * R);
+    c.add(&v.ex_cnt, SLO_EX_CNT * S * R);
     c.add(&v.ring_cnt, 4 * S * R);
     c.add(&v.r_sharp, S * R * 12);
     c.add(&v.r_less_sharp, S * R * 120);

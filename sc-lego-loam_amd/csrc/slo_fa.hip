@@ -10,8 +10,9 @@
 //     of the reference is kept.  Positions outside [5, S-5) keep the stale
 //     values persisted from earlier scans (Appendix A Q5).
 //   extractFeatures (FA:680-784): rings are independent except through the
-//     stale cloudSmoothness[4] entry of ring 0 (Q5), so ring 0 runs first and
-//     rings 1..R-1 then run in parallel, staged in LDS (k_fa_sort: wave
+//     stale cloudSmoothness[4] entry of ring 0 (Q5); when that entry points
+//     outside ring 0, ring 0 runs first (k_fa_extract_stale), and the rings
+//     run in parallel, staged in LDS (k_fa_sort: wave
 //     bitonic sorts, with the exact libstdc++ introsort restatement for
 //     sectors holding ties, Q4/Q6; k_fa_pick: the greedy picks, sequential
 //     per ring as in the reference).
@@ -203,17 +204,47 @@ __device__ void extract_ring_global(const DevView& v, int s, int ring) {
     v.r_lf_n[rr] = n_lf;
 }
 
-__global__ void __launch_bounds__(256) k_fa_extract_ring0(DevView v) { extract_ring_global(v, blockIdx.y, 0); }
+#define SLO_RING_STAGE 2080
 
-// Rank sort of one sector by one wave: rank = number of smaller values, so
-// equal ranks mean equal values; *tie is raised (and the sector left as it
-// was) when any two values are equal.  NE = ceil(n / 64) elements per lane.
-// One wave sorts one sector of n <= 64*NE entries in registers: the key is
-// (order-preserving curvature bits << 32 | point index), so keys are unique
-// and the bitonic network's result is the sorted order; padding keys are
-// all-ones.  If two curvatures are equal the result is NOT written (the
-// caller then runs the exact introsort restatement on the untouched sector):
-// without ties a sort's result is unique, so it equals libstdc++'s.
+// A ring's sorts, picks and marks stay inside its window [rs-5, re+5) when
+// every entry of its sectors is one of its own points.  That holds for every
+// ring with rs >= 5 (entries at positions >= 5 are this scan's, ind =
+// position), and for the ring holding the stale cloudSmoothness[4] entry (the
+// first ring with points, rs = 4, Q5) when that entry's index is one of the
+// ring's own points — the usual case: it was left there by the previous
+// scan's sort of the same ring.  Such rings run in parallel in LDS (k_fa_sort,
+// k_fa_pick) if the window fits SLO_RING_STAGE.
+__device__ inline bool ring_window(const DevView& v, int s, int ring, int& rs, int& re, int& lo, int& hi) {
+    const int* se = v.ring_se + (size_t)s * v.cfg.n_scan * 2;
+    rs = se[2 * ring]; re = se[2 * ring + 1];
+    lo = max(0, rs - 5); hi = min(v.H, re + 5);
+    if (!(hi > lo && hi - lo <= SLO_RING_STAGE)) return false;
+    if (rs >= 5) return true;
+    // its marks (+-5) must stay in the window too; below position 0 they are
+    // dropped (lo == 0 for the first ring).  The entry is usually {0, 0}: the
+    // zero-initialised array's entry 4 sorts first forever (curvature 0).
+    const int i4 = v.smooth[(size_t)s * v.H + 4].ind;
+    return i4 >= 0 && (i4 - 5 >= lo || lo == 0) && i4 + 5 < hi && i4 < v.st[s].seg_count;
+}
+
+// The rings whose sectors may start at the stale entry 4 (rs < 5: the empty
+// leading rings and the first ring with points), in ring order with the
+// global-memory restatement — unless ring_window keeps the stale ring local,
+// then k_fa_sort / k_fa_pick take it with the others.  Runs before them: a
+// stale index can point into any ring.
+__global__ void __launch_bounds__(256) k_fa_extract_stale(DevView v) {
+    const int s = blockIdx.y, R = v.cfg.n_scan;
+    const int* se = v.ring_se + (size_t)s * R * 2;
+    for (int ring = 0; ring < R && se[2 * ring] < 5; ++ring) {
+        int rs, re, lo, hi;
+        if (ring_window(v, s, ring, rs, re, lo, hi)) break;
+        extract_ring_global(v, s, ring);
+        __syncthreads();
+    }
+}
+
+// One wave sorts one sector of n <= 64*NE entries in registers (bitonic
+// network over unique keys; padding keys are all-ones).
 __device__ inline unsigned int f2ord_fa(float f) {
     const unsigned int u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -230,9 +261,11 @@ __device__ inline float ord2f_fa(unsigned int o) {
 // the same list).  So candidates come first inside a group of equal
 // curvatures, and when a group holds two of them the sector is flagged for
 // the exact introsort; otherwise the result is written back (its order of
-// non-candidates inside a group is never read).
+// non-candidates inside a group is never read) — except the
+// first entry of the sector that starts at position 4 (first_exact): it
+// becomes the next scan's stale entry (Q5), so a tie for it falls back too.
 template <int NE, class Cand>
-__device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_flag, Cand&& cand) {
+__device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_flag, Cand&& cand, bool first_exact) {
     unsigned long long k[NE];
 #pragma unroll
     for (int e = 0; e < NE; ++e) {
@@ -283,7 +316,8 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
         const unsigned long long up1 = __shfl_up(k[e], 1, 64);                      // lane - 1
         const unsigned long long wrap = e > 0 ? __shfl(k[e > 0 ? e - 1 : 0], 63, 64) : ~0ull;   // all lanes
         const unsigned long long prev = lane == 0 ? wrap : up1;
-        if (p > 0 && p < n && (prev >> 32) == (k[e] >> 32) && !(prev & 0x80000000ull) && !(k[e] & 0x80000000ull))
+        if (p > 0 && p < n && (prev >> 32) == (k[e] >> 32) &&
+            ((!(prev & 0x80000000ull) && !(k[e] & 0x80000000ull)) || (first_exact && p == 1)))
             tie = true;
     }
     const bool any_tie = __any(tie);
@@ -298,15 +332,12 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
     }
 }
 
-// Rings 1..R-1 (ring = 1 + blockIdx.x), in two launches.
-//
-// A ring's sorts, picks and neighbour marks only touch the ring's own points
-// [rs-5, re+5): its sectors' smoothness entries are this scan's (positions
-// in [5, S-5), ind = position) and marks stop at +-5.  Both kernels stage that
-// window in LDS in compact form, work on it with plain LDS accesses and write
-// it back; concurrent rings never share a word.  A ring whose window exceeds
-// SLO_RING_STAGE takes the global-memory restatement (extract_ring_global)
-// inside k_fa_pick.
+// The rings ring_window keeps local (ring = blockIdx.x), in two launches.
+// Both kernels stage the ring's window in LDS in compact form, work on it
+// with plain LDS accesses and write it back; concurrent rings never share a
+// word.  The other rings are the stale ones k_fa_extract_stale has done and
+// rings whose window exceeds SLO_RING_STAGE, which take the global-memory
+// restatement (extract_ring_global) inside k_fa_pick.
 //
 // k_fa_sort (256 threads): the six sector sorts (std::sort on [sp, ep),
 // Q4/Q6).  Without equal curvatures a sort's result is unique, so a wave
@@ -323,23 +354,18 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
 // points and collect the less-flat points (label <= 0, FA:768-776) with a
 // wave ballot: a sector's picks only label that sector's own points, so
 // collecting after all six sectors equals the reference's interleaving.
-#define SLO_RING_STAGE 2080
-
-__device__ inline bool ring_window(const DevView& v, int s, int ring, int& rs, int& re, int& lo, int& hi) {
-    const int* se = v.ring_se + (size_t)s * v.cfg.n_scan * 2;
-    rs = se[2 * ring]; re = se[2 * ring + 1];
-    lo = max(0, rs - 5); hi = min(v.H, re + 5);
-    // rs >= 5: every sorted entry is this scan's (ring 0 empty would put the
-    // stale entry 4 here, Q5)
-    return rs >= 5 && hi > lo && hi - lo <= SLO_RING_STAGE;
-}
 
 __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int s = blockIdx.y;
-    const int ring = 1 + blockIdx.x;
-    int rs, re, lo, hi;
-    if (!ring_window(v, s, ring, rs, re, lo, hi)) return;   // uniform: k_fa_pick handles it
+    const int ring = blockIdx.x;
     const int R = v.cfg.n_scan;
+    int rs, re, lo, hi;
+    const bool local = ring_window(v, s, ring, rs, re, lo, hi);
+    // the decision for k_fa_pick (which must not re-evaluate it: this kernel
+    // rewrites the stale entry 4)
+    int* cnt = v.ex_cnt + ((size_t)s * R + ring) * SLO_EX_CNT;
+    if (threadIdx.x == 0) cnt[12] = local;
+    if (!local) return;   // uniform
     const size_t base = (size_t)s * v.H;
     const int S = v.st[s].seg_count;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -376,10 +402,10 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
             };
             switch ((n + 63) >> 6) {
                 case 0: break;
-                case 1: if (n > 1) bitonic_sort_wave<1>(a, n, lane, &s_tie[j], cand); break;
-                case 2: bitonic_sort_wave<2>(a, n, lane, &s_tie[j], cand); break;
-                case 3: case 4: bitonic_sort_wave<4>(a, n, lane, &s_tie[j], cand); break;
-                case 5: case 6: case 7: case 8: bitonic_sort_wave<8>(a, n, lane, &s_tie[j], cand); break;
+                case 1: if (n > 1) bitonic_sort_wave<1>(a, n, lane, &s_tie[j], cand, sp < 5); break;
+                case 2: bitonic_sort_wave<2>(a, n, lane, &s_tie[j], cand, sp < 5); break;
+                case 3: case 4: bitonic_sort_wave<4>(a, n, lane, &s_tie[j], cand, sp < 5); break;
+                case 5: case 6: case 7: case 8: bitonic_sort_wave<8>(a, n, lane, &s_tie[j], cand, sp < 5); break;
                 default: if (lane == 0) s_tie[j] = 1; break;
             }
         }
@@ -395,7 +421,6 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     // ---- candidate lists: point indices as window offsets, in visiting order
     int16_t* l_sh = v.ex_list + (size_t)s * v.H * 2;
     int16_t* l_fl = l_sh + v.H;
-    int* cnt = v.ex_cnt + ((size_t)s * R + ring) * 12;
     for (int r0 = 0; r0 < 6; r0 += 4) {
         const int j = r0 + wave;
         if (j >= 6) continue;
@@ -434,13 +459,15 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
 
 __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
     const int s = blockIdx.y;
-    const int ring = 1 + blockIdx.x;
+    const int ring = blockIdx.x;
+    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const int* cnt = v.ex_cnt + ((size_t)s * R + ring) * SLO_EX_CNT;
     int rs, re, lo, hi;
-    if (!ring_window(v, s, ring, rs, re, lo, hi)) {   // uniform per block
-        extract_ring_global(v, s, ring);
+    ring_window(v, s, ring, rs, re, lo, hi);   // bounds only; the decision is k_fa_sort's
+    if (!cnt[12]) {   // uniform per block
+        if (rs >= 5) extract_ring_global(v, s, ring);   // too long to stage (rs < 5: done, k_fa_extract_stale)
         return;
     }
-    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const size_t base = (size_t)s * v.H;
     const int lane = threadIdx.x;
     int32_t* picked = v.picked + base;
@@ -451,7 +478,6 @@ __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
     __shared__ int p_sh[12], p_ls[120], p_fl[24];
     const int16_t* g_sh = v.ex_list + (size_t)s * v.H * 2;
     const int16_t* g_fl = g_sh + v.H;
-    const int* cnt = v.ex_cnt + ((size_t)s * R + ring) * 12;
     for (int k = lane; k < hi - lo; k += 64) {
         lpk[k] = (int8_t)picked[lo + k];
         llab[k] = (int8_t)lab[lo + k];
@@ -719,11 +745,9 @@ int fa_features_run(slo_ctx* ctx) {
     dim3 gh((v.H + T - 1) / T, S);
     SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "fa_extract_ring0", k_fa_extract_ring0, dim3(1, S), dim3(256), 0, v);
-    if (R > 1) {
-        SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R - 1, S), dim3(256), 0, v);
-        SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R - 1, S), dim3(64), 0, v);
-    }
+    SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());

@@ -136,7 +136,7 @@ struct DevView {
     float4* kd_surf;     // [S][cap_less_flat]
     int32_t* roff_cur;   // [S][2][R+1] first index of each ring in less_sharp / less_flat
     int16_t* ex_list;    // [S][2][H] per-sector pick candidates (sharp, flat), window offsets
-    int32_t* ex_cnt;     // [S][R][6][2] candidate counts
+    int32_t* ex_cnt;     // [S][R][SLO_EX_CNT]: per sector (sharp, flat) candidate counts, [12] = staged in LDS
     int32_t* roff_last;  // [S][2][R+1] the same for corner_last / surf_last
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
@@ -181,6 +181,7 @@ struct DevView {
 #define SLO_RECORD_FLOATS 40
 #define SLO_ODO_SURF_CELL 1.0f  // odometry surf grid cell (m, power of two)
 #define SLO_ODO_SURF_R 5        // its search box radius in cells: covers sqrt(nearest_feature_search_sq_dist)
+#define SLO_EX_CNT 16
 #define SLO_KFMAX 4096          // keyframe pose / Scan Context history capacity per stream
 #define SLO_SC_MAX_K 64         // NUM_CANDIDATES_FROM_TREE limit (C5 uses 50)
 #define SLO_SC_MAX_SECTOR 64

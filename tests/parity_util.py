@@ -44,19 +44,20 @@ def make_scans(preset_id, config_id, n_streams, n_scans, oracle_mod):
 
 def canon_smooth(smooth_ind, curv, seg_ground, ring_start, ring_end, edge_th, surf_th):
     """cloudSmoothness indices with the one freedom the pipeline cannot observe
-    removed: inside a group of equal curvatures of a sector of rings >= 1,
-    only the order of the pick candidates is read (FA:704-705, 737-738: one
-    list per curvature value), so non-candidates are put last in index order
-    and candidates keep their relative order.  Ring 0 (whose sector 0 starts at
-    the stale entry 4, Q5) and every position outside the sorted ranges are
-    compared as they are."""
+    removed: inside a group of equal curvatures of a sector, only the order of
+    the pick candidates is read (FA:704-705, 737-738: one list per curvature
+    value), so non-candidates are put last in index order and candidates keep
+    their relative order.  Positions below 5 (the stale entry 4 that the next
+    scan reads, Q5) and every position outside the sorted ranges are compared
+    as they are."""
     out = np.array(smooth_ind, np.int64, copy=True)
     S = len(seg_ground)
-    for r in range(1, len(ring_start)):
+    for r in range(len(ring_start)):
         a, b = int(ring_start[r]), int(ring_end[r])
         for j in range(6):
             sp, ep = (a * (6 - j) + b * j) // 6, (a * (5 - j) + b * (j + 1)) // 6 - 1
-            if sp >= ep or sp < 5:
+            sp = max(sp, 5)
+            if sp >= ep:
                 continue
             inds = out[sp:ep]
             ok = inds < S
