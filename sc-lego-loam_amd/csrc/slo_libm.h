@@ -272,6 +272,39 @@ SLO_HD float cosf_(float y) {
     return (y - y) / (y - y);
 }
 
+// sinf_ and cosf_ of one argument with one range reduction (the same
+// expressions as the two functions above, so the same bits)
+SLO_HD void sincosf_(float y, float* sp, float* cp) {
+    const float pio4 = 0x1.921FB6p-1f;
+    double x = y;
+    int n;
+    if (abstop12_(y) < abstop12_(pio4)) {
+        double s = x * x;
+        if (abstop12_(y) < abstop12_(0x1p-12f)) { *sp = y; *cp = 1.0f; return; }
+        *sp = sincosf_poly_(x, s, sincos_table(0), 0);
+        *cp = sincosf_poly_(x, s, sincos_table(0), 1);
+        return;
+    } else if (abstop12_(y) < abstop12_(120.0f)) {
+        x = reduce_fast_(x, sincos_table(0), &n);
+        double s = ((n & 3) == 0 || (n & 3) == 3) ? 1.0 : -1.0;
+        const sincos_tab p = sincos_table((n & 2) ? 1 : 0);
+        *sp = sincosf_poly_(x * s, x * x, p, n);
+        *cp = sincosf_poly_(x * s, x * x, p, n ^ 1);
+        return;
+    } else if (abstop12_(y) < abstop12_(__builtin_inff())) {
+        uint32_t xi = f2u(y);
+        int sign = xi >> 31;
+        x = reduce_large_(xi, &n);
+        int q = (n + sign) & 3;
+        double s = (q == 0 || q == 3) ? 1.0 : -1.0;
+        const sincos_tab p = sincos_table(((n + sign) & 2) ? 1 : 0);
+        *sp = sincosf_poly_(x * s, x * x, p, n);
+        *cp = sincosf_poly_(x * s, x * x, p, n ^ 1);
+        return;
+    }
+    *sp = *cp = (y - y) / (y - y);
+}
+
 // ---------------------------------------------------------------- asinf
 // glibc sysdeps/ieee754/flt-32/e_asinf.c (fdlibm float port with the
 // single-precision polynomial R(x^2)).

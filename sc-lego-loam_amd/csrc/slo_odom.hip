@@ -416,44 +416,55 @@ __global__ void __launch_bounds__(256) k_fa_iter(DevView v, int iter0) {
 }
 
 // integrateTransformation (FA:1697-1725) + publishCloudsLast (FA:1759-1788)
-__global__ void __launch_bounds__(256) k_fa_odo_finish(DevView v) {
-    const int s = blockIdx.x;
-    StreamState& st = v.st[s];
+// TransformToEnd (FA:885-953) of the less-sharp / less-flat clouds into the
+// next *Last buffers, and into the "trees" when they are rebuilt
+// (setInputCloud copies, only when both clouds are big enough): chip-wide,
+// SLO_TOEND_BLOCKS workgroups per stream (XCD-aware), sin/cos of the frame
+// rotation once per workgroup.
+#define SLO_TOEND_BLOCKS 16
+__global__ void __launch_bounds__(256) k_fa_to_end(DevView v) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, SLO_TOEND_BLOCKS, s, chunk);
+    if (s >= v.S) return;
+    const StreamState& st = v.st[s];
     if (st.odo_phase == 3) return;
-    const int tid = threadIdx.x, T = blockDim.x;
-    __shared__ float tc[6];
-    if (tid == 0) {
-        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-        slo_pose::integrate(st.transformSum, tc);
-    }
+    __shared__ float tc[6], tct[6];
+    if (threadIdx.x < 6) tc[threadIdx.x] = st.transformCur[threadIdx.x];
+    __syncthreads();
+    if (threadIdx.x == 0) slo_pose::tc_trig(tc, tct);
     __syncthreads();
     const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
+    const bool rebuild = nLS > 10 && nLF > 100;
     const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
     const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
     float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
     float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
-    // TransformToEnd into the next *Last buffers; the "trees" are rebuilt
-    // (setInputCloud copies) only when both clouds are big enough
-    const bool rebuild = nLS > 10 && nLF > 100;
     float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
     float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
-    for (int i = tid; i < nLS; i += T) {
-        const P4 q = slo_pose::transform_to_end(ld4(lsharp, i), tc);
+    for (int i = chunk * blockDim.x + threadIdx.x; i < nLS + nLF; i += SLO_TOEND_BLOCKS * blockDim.x) {
+        const bool corner = i < nLS;
+        const int k = corner ? i : i - nLS;
+        const P4 q = slo_pose::transform_to_end(ld4(corner ? lsharp : lflat, k), tc, tct);
         const float4 o = make_float4(q.x, q.y, q.z, q.w);
-        cnext[i] = o;
-        if (rebuild) kdc[i] = o;
+        (corner ? cnext : snext)[k] = o;
+        if (rebuild) (corner ? kdc : kds)[k] = o;
     }
-    for (int i = tid; i < nLF; i += T) {
-        const P4 q = slo_pose::transform_to_end(ld4(lflat, i), tc);
-        const float4 o = make_float4(q.x, q.y, q.z, q.w);
-        snext[i] = o;
-        if (rebuild) kds[i] = o;
-    }
+}
+
+// integrate (FA:1697-1725) and the *Last / tree bookkeeping, per stream
+__global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    if (st.odo_phase == 3) return;
     copy_ring_offsets(v, s);
-    if (tid == 0) {
+    if (threadIdx.x == 0) {
+        float tc[6];
+        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+        slo_pose::integrate(st.transformSum, tc);
+        const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;
-        if (rebuild) { st.kdCornerNum = nLS; st.kdSurfNum = nLF; }
+        if (nLS > 10 && nLF > 100) { st.kdCornerNum = nLS; st.kdSurfNum = nLF; }
     }
 }
 
@@ -472,7 +483,8 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
-    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v);
     SLO_CHECK(hipGetLastError());
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);

@@ -31,23 +31,28 @@ SLO_P_HD P4 transform_to_start(P4 pi, const float* tc) {
     float s = 10 * (pi.w - (float)(int)pi.w);
     float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
     float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
-    float x1 = cosf_(rz) * (pi.x - tx) + sinf_(rz) * (pi.y - ty);
-    float y1 = -sinf_(rz) * (pi.x - tx) + cosf_(rz) * (pi.y - ty);
+    float srx, crx, sry, cry, srz, crz;   // sin/cos pairs share one range reduction
+    slo_libm::sincosf_(rx, &srx, &crx);
+    slo_libm::sincosf_(ry, &sry, &cry);
+    slo_libm::sincosf_(rz, &srz, &crz);
+    float x1 = crz * (pi.x - tx) + srz * (pi.y - ty);
+    float y1 = -srz * (pi.x - tx) + crz * (pi.y - ty);
     float z1 = (pi.z - tz);
     float x2 = x1;
-    float y2 = cosf_(rx) * y1 + sinf_(rx) * z1;
-    float z2 = -sinf_(rx) * y1 + cosf_(rx) * z1;
+    float y2 = crx * y1 + srx * z1;
+    float z2 = -srx * y1 + crx * z1;
     P4 o;
-    o.x = cosf_(ry) * x2 - sinf_(ry) * z2;
+    o.x = cry * x2 - sry * z2;
     o.y = y2;
-    o.z = sinf_(ry) * x2 + cosf_(ry) * z2;
+    o.z = sry * x2 + cry * z2;
     o.w = pi.w;
     return o;
 }
 
 // imu quantities are the reference's values without an IMU: start angles 0
 // (so cos=1, sin=0 after updateImuRollPitchYawStartSinCos), shifts 0, last 0
-SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
+// tct = sin/cos of tc[0..2]: {srx, crx, sry, cry, srz, crz} (sincosf_)
+SLO_P_HD P4 transform_to_end(P4 pi, const float* tc, const float* tct) {
     const float cosImuRollStart = cosf_(0.0f), cosImuPitchStart = cosf_(0.0f), cosImuYawStart = cosf_(0.0f);
     const float sinImuRollStart = sinf_(0.0f), sinImuPitchStart = sinf_(0.0f), sinImuYawStart = sinf_(0.0f);
     const float imuShiftFromStartX = 0, imuShiftFromStartY = 0, imuShiftFromStartZ = 0;
@@ -55,25 +60,29 @@ SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
     float s = 10 * (pi.w - (float)(int)pi.w);
     float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
     float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
-    float x1 = cosf_(rz) * (pi.x - tx) + sinf_(rz) * (pi.y - ty);
-    float y1 = -sinf_(rz) * (pi.x - tx) + cosf_(rz) * (pi.y - ty);
+    float srx, crx, sry, cry, srz, crz;   // sin/cos pairs share one range reduction
+    slo_libm::sincosf_(rx, &srx, &crx);
+    slo_libm::sincosf_(ry, &sry, &cry);
+    slo_libm::sincosf_(rz, &srz, &crz);
+    float x1 = crz * (pi.x - tx) + srz * (pi.y - ty);
+    float y1 = -srz * (pi.x - tx) + crz * (pi.y - ty);
     float z1 = (pi.z - tz);
     float x2 = x1;
-    float y2 = cosf_(rx) * y1 + sinf_(rx) * z1;
-    float z2 = -sinf_(rx) * y1 + cosf_(rx) * z1;
-    float x3 = cosf_(ry) * x2 - sinf_(ry) * z2;
+    float y2 = crx * y1 + srx * z1;
+    float z2 = -srx * y1 + crx * z1;
+    float x3 = cry * x2 - sry * z2;
     float y3 = y2;
-    float z3 = sinf_(ry) * x2 + cosf_(ry) * z2;
-    rx = tc[0]; ry = tc[1]; rz = tc[2];
+    float z3 = sry * x2 + cry * z2;
     tx = tc[3]; ty = tc[4]; tz = tc[5];
-    float x4 = cosf_(ry) * x3 + sinf_(ry) * z3;
+    srx = tct[0]; crx = tct[1]; sry = tct[2]; cry = tct[3]; srz = tct[4]; crz = tct[5];
+    float x4 = cry * x3 + sry * z3;
     float y4 = y3;
-    float z4 = -sinf_(ry) * x3 + cosf_(ry) * z3;
+    float z4 = -sry * x3 + cry * z3;
     float x5 = x4;
-    float y5 = cosf_(rx) * y4 - sinf_(rx) * z4;
-    float z5 = sinf_(rx) * y4 + cosf_(rx) * z4;
-    float x6 = cosf_(rz) * x5 - sinf_(rz) * y5 + tx;
-    float y6 = sinf_(rz) * x5 + cosf_(rz) * y5 + ty;
+    float y5 = crx * y4 - srx * z4;
+    float z5 = srx * y4 + crx * z4;
+    float x6 = crz * x5 - srz * y5 + tx;
+    float y6 = srz * x5 + crz * y5 + ty;
     float z6 = z5 + tz;
     float x7 = cosImuRollStart * (x6 - imuShiftFromStartX) - sinImuRollStart * (y6 - imuShiftFromStartY);
     float y7 = sinImuRollStart * (x6 - imuShiftFromStartX) + cosImuRollStart * (y6 - imuShiftFromStartY);
@@ -96,6 +105,18 @@ SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
     o.z = z11;
     o.w = (float)(int)pi.w;
     return o;
+}
+
+SLO_P_HD void tc_trig(const float* tc, float* tct) {
+    slo_libm::sincosf_(tc[0], &tct[0], &tct[1]);
+    slo_libm::sincosf_(tc[1], &tct[2], &tct[3]);
+    slo_libm::sincosf_(tc[2], &tct[4], &tct[5]);
+}
+
+SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
+    float tct[6];
+    tc_trig(tc, tct);
+    return transform_to_end(pi, tc, tct);
 }
 
 SLO_P_HD void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz, float alx,

@@ -100,3 +100,12 @@ def test_voxel_grid_stable_and_sorted_orders_agree_as_sets():
     a, b = outs
     assert len(a) == len(b) > 1000
     np.testing.assert_allclose(a, b, rtol=0, atol=2e-5)
+
+
+def test_gpu_sincos_matches_sinf_cosf(tmp_path):
+    # the fused sin/cos of the GPU pose transforms == its sinf/cosf == glibc
+    exe = tmp_path / "sincos_check"
+    src = os.path.join(HERE, "cpp", "sincos_check.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-mfma", "-o", str(exe), src], check=True)
+    bad, cases = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
+    assert cases > 700000 and bad == 0
