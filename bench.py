@@ -47,6 +47,9 @@ def parse():
     ap.add_argument("--groups", type=int, default=2,
                     help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
     ap.add_argument("--preset", default="hdl64_1800")
+    ap.add_argument("--keyframe-cap", type=int, default=32768,
+                    help="slo_config.keyframe_cloud_cap: points per keyframe surf/outlier cloud (0 = worst case); "
+                         "an overflow sets the stream's error bit, reported as stream_errors")
     ap.add_argument("--config-id", type=int, default=3)
     ap.add_argument("--history", type=int, default=60, help="seeded Scan Context history per stream")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
@@ -132,6 +135,7 @@ def main():
     if gather:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = slo_amd.preset(a.preset)
+    cfg.keyframe_cloud_cap = a.keyframe_cap
     pid = slo_amd.PRESETS[a.preset]
     P = cfg.max_points
     S = a.streams

@@ -70,6 +70,13 @@ typedef struct slo_config {
     int32_t skip_frame_num;
     /* capacity: maximum points per input scan */
     int32_t max_points;
+    /* capacity: points of one keyframe's surf / outlier cloud kept for the
+       local map (mapOptmization.cpp:1580-1594); 0 = the worst case (R*C /
+       R*ceil(C/5), never clipped).  A keyframe cloud larger than a non-zero
+       cap is clipped and sets SLO_ERR_MAP_CAPACITY in the stream's error
+       bits, so a run that stays exact reports no error.  Host-side only: the
+       CPU restatement ignores it. */
+    int32_t keyframe_cloud_cap;
 } slo_config;
 
 /* preset ids */
@@ -165,6 +172,7 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->sc_atan_float = 1;
     c->skip_frame_num = 1;
     c->max_points = R * C;
+    c->keyframe_cloud_cap = 0;
     return 0;
 }
 #endif

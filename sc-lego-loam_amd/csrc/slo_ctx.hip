@@ -74,7 +74,7 @@ void* slo_stream(slo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** out) {
     if (!cfg || !out || n_streams <= 0 || cfg->n_scan <= 0 || cfg->n_scan > 128 || cfg->horizon_scan <= 0 ||
-        cfg->horizon_scan > 4096 || cfg->max_points <= 0 || cfg->sc_num_candidates < 1 ||
+        cfg->horizon_scan > 4096 || cfg->max_points <= 0 || cfg->keyframe_cloud_cap < 0 || cfg->sc_num_candidates < 1 ||
         cfg->sc_num_candidates > SLO_SC_MAX_K || cfg->sc_num_ring < 1 || cfg->sc_num_ring > 64 ||
         cfg->sc_num_sector < 1 || cfg->sc_num_sector > SLO_SC_MAX_SECTOR ||
         cfg->sc_num_ring * cfg->sc_num_sector > SLO_SC_MAX_CELLS || cfg->surrounding_keyframe_search_num < 1 ||
@@ -147,6 +147,10 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.kd_surf, S * v.cap_less_flat);
     c.add(&v.roff_cur, S * 2 * (R + 1));
     c.add(&v.roff_last, S * 2 * (R + 1));
+    c.add(&v.sx_surf_last, S * v.cap_less_flat);
+    c.add(&v.sx_surf_next, S * v.cap_less_flat);
+    c.add(&v.sx_kd_corner, S * v.cap_less_sharp);
+    c.add(&v.sharp_perm, S * v.cap_sharp);
     c.add(&v.ind_surf, S * v.cap_flat * 3);
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
@@ -162,13 +166,16 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     v.cap_ks = (int)H;
     v.cap_ko = R * ((C + 4) / 5);
     v.cap_mc = NKF * v.cap_kc;
-    v.cap_ms = NKF * (v.cap_ks + v.cap_ko);
+    const int kcap = cfg->keyframe_cloud_cap;
+    v.cap_kfs = kcap > 0 ? std::min(v.cap_ks, kcap) : v.cap_ks;
+    v.cap_kfo = kcap > 0 ? std::min(v.cap_ko, kcap) : v.cap_ko;
+    v.cap_ms = NKF * (v.cap_kfs + v.cap_kfo);
     v.cap_st = (int)H + v.cap_ko;
     const size_t NRS = (size_t)cfg->sc_num_ring * cfg->sc_num_sector;
     c.add(&v.outl_cam, S * H);
     c.add(&v.kf_corner, S * v.KFR * v.cap_kc);
-    c.add(&v.kf_surf, S * v.KFR * v.cap_ks);
-    c.add(&v.kf_outl, S * v.KFR * v.cap_ko);
+    c.add(&v.kf_surf, S * v.KFR * v.cap_kfs);
+    c.add(&v.kf_outl, S * v.KFR * v.cap_kfo);
     c.add(&v.kf_n, S * v.KFR * 3);
     c.add(&v.kf_pose, S * v.KFMAX * 6);
     c.add(&v.map_c, S * v.cap_mc);

@@ -138,6 +138,12 @@ struct DevView {
     int16_t* ex_list;    // [S][2][H] per-sector pick candidates (sharp, flat), window offsets
     int32_t* ex_cnt;     // [S][R][SLO_EX_CNT]: per sector (sharp, flat) candidate counts, [12] = staged in LDS
     int32_t* roff_last;  // [S][2][R+1] the same for corner_last / surf_last
+    // x-sorted surf clouds (k_fa_sx_rings): each ring's segment of surf_last
+    // / surf_next sorted by x, w = the point's index in the cloud (int bits)
+    float4* sx_surf_last;    // [S][cap_less_flat]
+    float4* sx_surf_next;    // [S][cap_less_flat]
+    float4* sx_kd_corner;    // [S][cap_less_sharp] the corner "tree" cloud sorted by x (w = index)
+    int32_t* sharp_perm;     // [S][cap_sharp] sharp points in x order (query grouping)
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
     StreamState* st;     // [S]
@@ -145,6 +151,7 @@ struct DevView {
     int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
     int KFMAX;           // keyframe pose / Scan Context history capacity
     int cap_kc, cap_ks, cap_ko, cap_mc, cap_ms, cap_st;
+    int cap_kfs, cap_kfo;  // keyframe surf / outlier cloud slots (cfg.keyframe_cloud_cap)
     float4* outl_cam;    // [S][H]          outlier cloud, camera frame (adjustOutlierCloud)
     float4* kf_corner;   // [S][KFR][cap_kc] keyframe clouds, world frame
     float4* kf_surf;     // [S][KFR][cap_ks]
@@ -259,6 +266,11 @@ struct GridRows {
 template <int R>
 __constant__ GridRows<R> kGridRows = GridRows<R>();
 
+//
+// Probe: the query's own cell is visited first, on its own (one bucket), so
+// the walk starts with the bound its points give instead of the caller's
+// initial radius; the row walk then skips that cell (each point is still
+// visited once).
 #define GBALL_UNROLL 4
 template <int R, int U = GBALL_UNROLL, class B, class F>
 __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
@@ -267,6 +279,22 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
     const size_t gb = (size_t)s * (g.T + 1);
     const int base = g.off[gb];
     const float4* E = g.ent + (size_t)s * g.es;
+    static_assert(GridRows<R>().dy[0] == 0 && GridRows<R>().dz[0] == 0, "row 0 is the probed cell's row");
+    {
+        const int h0 = (int)grid_hash(cx, cy, cz, g.T);
+        const int p0 = g.off[gb + h0] - base, p1 = g.off[gb + h0 + 1] - base;
+        for (int e = p0; e < p1; e += U) {
+            float4 p[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) p[u] = e + u < p1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                if (e + u >= p1) break;
+                if (grid_cell(p[u].x, inv) != cx || grid_cell(p[u].y, inv) != cy || grid_cell(p[u].z, inv) != cz) continue;
+                f(p[u]);
+            }
+        }
+    }
     for (int k = 0; k < GridRows<R>::N; ++k) {
         const float b = bound();
         if ((float)kGridRows<R>.gap[k] * c2 > b) break;
@@ -294,7 +322,8 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
                 for (int u = 0; u < U; ++u) {
                     if (e + u >= e1) break;
                     const int px = grid_cell(p[u].x, inv);
-                    if (grid_cell(p[u].y, inv) != yy || grid_cell(p[u].z, inv) != zz || px < xa || px > xb) continue;
+                    if (grid_cell(p[u].y, inv) != yy || grid_cell(p[u].z, inv) != zz || px < xa || px > xb ||
+                        (k == 0 && px == cx)) continue;   // k == 0: the probed cell's row (dy = dz = 0)
                     f(p[u]);
                 }
             }

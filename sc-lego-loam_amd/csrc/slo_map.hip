@@ -97,9 +97,9 @@ __global__ void k_mo_assemble(DevView v) {
     for (int i = threadIdx.x; i < kn[0]; i += blockDim.x)
         if (oc + i < v.cap_mc) v.map_c[(size_t)s * v.cap_mc + oc + i] = v.kf_corner[ks * v.cap_kc + i];
     for (int i = threadIdx.x; i < kn[1]; i += blockDim.x)
-        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = v.kf_surf[ks * v.cap_ks + i];
+        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = v.kf_surf[ks * v.cap_kfs + i];
     for (int i = threadIdx.x; i < kn[2]; i += blockDim.x)
-        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = v.kf_outl[ks * v.cap_ko + i];
+        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = v.kf_outl[ks * v.cap_kfo + i];
 }
 
 __global__ void k_mo_concat(DevView v) {
@@ -516,10 +516,10 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
     const float ctYaw = cosf_(pose[5]), stYaw = sinf_(pose[5]);
     const int slot = kfid % v.KFR;
     const size_t ks = (size_t)s * v.KFR + slot;
-    const int n3[3] = {min(st.n_corner_ds, v.cap_kc), min(st.n_surf_ds, v.cap_ks), min(st.n_outl_ds, v.cap_ko)};
+    const int n3[3] = {min(st.n_corner_ds, v.cap_kc), min(st.n_surf_ds, v.cap_kfs), min(st.n_outl_ds, v.cap_kfo)};
     const float4* src[3] = {v.cur_c_ds + (size_t)s * v.cap_less_sharp, v.cur_s_ds + (size_t)s * v.H,
                             v.cur_o_ds + (size_t)s * v.cap_ko};
-    float4* dst[3] = {v.kf_corner + ks * v.cap_kc, v.kf_surf + ks * v.cap_ks, v.kf_outl + ks * v.cap_ko};
+    float4* dst[3] = {v.kf_corner + ks * v.cap_kc, v.kf_surf + ks * v.cap_kfs, v.kf_outl + ks * v.cap_kfo};
     for (int c = 0; c < 3; ++c)
         for (int i = threadIdx.x; i < n3[c]; i += blockDim.x) {
             float4 p = src[c][i];

@@ -127,7 +127,7 @@ __device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int it
 // ---------------------------------------------------------------- launch structure
 // The 25 + 25 Gauss-Newton iterations of a stream are sequential, the streams
 // independent.  Each phase (surf, then corner) runs as 5 rounds of
-//   k_fa_search<PH>  one thread per query, S x ceil(cap/256) workgroups: the
+//   k_fa_search_*   one thread (surf) / 4 waves (corner) per query: the
 //                    correspondence search of iteration 5b (findCorresponding*
 //                    runs when iterCount % 5 == 0, FA:1157 / 1046) — the
 //                    expensive part, spread over the whole chip;
@@ -140,6 +140,31 @@ __device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int it
 __device__ inline void copy_ring_offsets(const DevView& v, int s) {
     const int n = 2 * (v.cfg.n_scan + 1);
     for (int k = threadIdx.x; k < n; k += blockDim.x) v.roff_last[(size_t)s * n + k] = v.roff_cur[(size_t)s * n + k];
+}
+
+#define SLO_PERM_MAX 2048   // >= cap_sharp = 12 R (R <= 128)
+__device__ inline uint64_t sx_key(float x, int idx) {
+    uint32_t u = __float_as_uint(x);
+    u = (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+    return ((uint64_t)u << 32) | (uint32_t)idx;
+}
+
+// sorts key[0..n) ascending in LDS (np = next power of two >= n, padded with ~0)
+__device__ inline void lds_bitonic(uint64_t* key, int n, int np) {
+    const int tid = threadIdx.x, T = blockDim.x;
+    for (int i = n + tid; i < np; i += T) key[i] = ~0ull;
+    __syncthreads();
+    for (int k = 2; k <= np; k <<= 1)
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < np; i += T) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const uint64_t x = key[i], y = key[l];
+                    if ((x > y) == ((i & k) == 0)) { key[i] = y; key[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
 }
 
 __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan) {
@@ -169,114 +194,415 @@ __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan)
         st.iters_surf = st.iters_corner = 0;
         st.odo_phase = (st.cornerLastNum < 10 || st.surfLastNum < 100) ? 2 : 0;
     }
+    // the sharp points in x order: k_fa_search_corner groups its queries by
+    // it (a grouping only; results do not depend on it)
+    __shared__ uint64_t key[SLO_PERM_MAX];
+    const int ns = st.n_sharp;
+    const float4* sp = v.sharp + (size_t)s * v.cap_sharp;
+    for (int i = tid; i < ns; i += T) key[i] = sx_key(sp[i].x, i);
+    int np = 1;
+    while (np < ns) np <<= 1;
+    lds_bitonic(key, ns, np);
+    for (int i = tid; i < ns; i += T) v.sharp_perm[(size_t)s * v.cap_sharp + i] = (int)(uint32_t)key[i];
 }
 
-// min of sq3_ref over a[j0..j1) visited upward / downward with the
-// reference's strict '<' (so ties keep the first index met)
-__device__ inline void walk_up(const float4* a, int j0, int j1, const P4& q, float& m, int& mi) {
-#pragma unroll 4
-    for (int j = j0; j < j1; ++j) {
-        const float d = sq3_ref(a[j], q);
-        if (d < m) { m = d; mi = j; }
+// ---------------------------------------------------------------- x-sorted clouds
+// The correspondence searches are nearest-point queries over (a) the whole
+// corner "tree" cloud and (b) single rings of the *Last clouds restricted to
+// index ranges (the reference's ring-ordered walks).  Both run as sweeps over
+// an x-sorted copy: start at the query's x (binary search) and walk outward in
+// both directions until fl((p.x - q.x)^2) exceeds the current bound.  The
+// distance expressions add non-negative squares to that first term, and float
+// subtraction / squaring are monotone, so every point the sweep stops before
+// is strictly farther than the bound: the result (with its tie rule) equals
+// the exhaustive walk's.
+// one wave per (stream, ring), four rings per workgroup: the ring's segment
+// of the cloud becoming surf_last sorted by x — a bitonic network over the
+// segment's 64 * NE (x, index) keys held in registers (lane-local stages in
+// registers, cross-lane stages by shuffles), NE chosen per ring
+template <int NE>
+__device__ inline void sx_sort_wave(const float4* in, float4* out, int a, int n, int lane) {
+    unsigned long long k[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int i = e * 64 + lane;
+        k[e] = i < n ? sx_key(in[a + i].x, a + i) : ~0ull;
     }
-}
-__device__ inline void walk_down(const float4* a, int j0, int j1, const P4& q, float& m, int& mi) {
-#pragma unroll 4
-    for (int j = j1 - 1; j >= j0; --j) {
-        const float d = sq3_ref(a[j], q);
-        if (d < m) { m = d; mi = j; }
+    constexpr int N = 64 * NE;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {   // partner in the same lane
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    if (e & es) continue;
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const unsigned long long x = k[e], y = k[e | es];
+                    const bool sw = up ? (x > y) : (x < y);
+                    k[e] = sw ? y : x;
+                    k[e | es] = sw ? x : y;
+                }
+            } else {              // partner in lane ^ stride
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const unsigned long long y = __shfl_xor(k[e], stride, 64);
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const bool take_min = up == ((lane & stride) == 0);
+                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int i = e * 64 + lane;
+        if (i < n) {
+            const int idx = (int)(uint32_t)k[e];
+            const float4 p = in[idx];
+            out[a + i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
+        }
     }
 }
 
-// findCorrespondingSurfFeatures (FA:1155-1268) / ...CornerFeatures
-// (FA:1044-1153) for one query: exact 1-NN in the tree cloud, then the
-// ring-ordered walk for the 2nd (and 3rd) points within +-2.5 rings.
-//
-// The *Last clouds are concatenated ring by ring, so the reference's walk —
-// step away from `closest` until the ring leaves [cscan-2, cscan+2], sorting
-// each point into "same/lower ring" or "other ring" by its ring — is exactly a
-// min over four index ranges cut at the ring boundaries (roff_last), in the
-// same visiting order: forward over [closest+1, ...) bounded by Q7's
-// min(query count, cloud size), then backward from closest-1.
-//
-// 1-NN: surf (dense, ~10^4-10^5 points) through the 1 m hash grid; corner
-// (sparse, <= 120 R points) by brute force, the cloud streamed through LDS in
-// 256-point tiles shared by the workgroup's 256 queries (lowest index wins
-// ties: strict '<' in index order).
-template <int PH>
-__global__ void __launch_bounds__(256) k_fa_search(DevView v, int nb) {
+#define SLO_SX_RING_MAX 4096   // >= horizon_scan limit (slo_create): a ring holds <= C points
+__global__ void __launch_bounds__(256) k_fa_sx_rings(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    const int R = v.cfg.n_scan;
+    const int lane = threadIdx.x & 63, r = chunk * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
+    const int a = rf[r], n = rf[r + 1] - a;
+    if (n <= 0) return;
+    const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
+    float4* out = v.sx_surf_next + (size_t)s * v.cap_less_flat;
+    if (n <= 64) sx_sort_wave<1>(in, out, a, n, lane);
+    else if (n <= 128) sx_sort_wave<2>(in, out, a, n, lane);
+    else if (n <= 256) sx_sort_wave<4>(in, out, a, n, lane);
+    else if (n <= 512) sx_sort_wave<8>(in, out, a, n, lane);
+    // longer rings: k_fa_sx_long
+}
+
+// rings of more than 512 points (one workgroup each, bitonic sort in LDS)
+__global__ void __launch_bounds__(256) k_fa_sx_long(DevView v, int nb) {
+    int s, r;
+    xcd_stream_chunk(blockIdx.x, nb, s, r);
+    if (s >= v.S) return;
+    const int R = v.cfg.n_scan;
+    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
+    const int a = rf[r], n = rf[r + 1] - a;
+    if (n <= 512) return;
+    const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
+    float4* out = v.sx_surf_next + (size_t)s * v.cap_less_flat;
+    __shared__ uint64_t key[SLO_SX_RING_MAX];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sx_key(in[a + i].x, a + i);
+    int np = 1;
+    while (np < n) np <<= 1;
+    lds_bitonic(key, n, np);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int idx = (int)(uint32_t)key[i];
+        const float4 p = in[idx];
+        out[a + i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
+    }
+}
+
+// one workgroup per stream: the corner "tree" cloud sorted by x, whenever the
+// tree is (re)built (checkSystemInitialization, or publishCloudsLast with
+// enough points, FA:1779-1786)
+template <int NP>
+__global__ void __launch_bounds__(1024) k_fa_sx_kd(DevView v) {
+    const int s = blockIdx.x;
+    const StreamState& st = v.st[s];
+    if (!(st.odo_phase == 3 || (st.n_less_sharp > 10 && st.n_less_flat > 100))) return;
+    const int n = st.kdCornerNum;
+    const float4* in = v.kd_corner + (size_t)s * v.cap_less_sharp;
+    float4* out = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
+    __shared__ uint64_t key[NP];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sx_key(in[i].x, i);
+    int np = 1;
+    while (np < n) np <<= 1;
+    lds_bitonic(key, n, np);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int idx = (int)(uint32_t)key[i];
+        const float4 p = in[idx];
+        out[i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
+    }
+}
+
+// first position in a[lo, hi) whose x is >= qx
+__device__ inline int sx_lower(const float4* a, int lo, int hi, float qx) {
+    while (lo < hi) {
+        const int m = (lo + hi) >> 1;
+        if (a[m].x < qx) lo = m + 1; else hi = m;
+    }
+    return lo;
+}
+
+// sweep a[lo, hi) outward from position j0 (4 loads in flight); visit(p) for
+// every point until fl((p.x - qx)^2) > bound()
+template <class B, class F>
+__device__ inline void sx_sweep(const float4* a, int lo, int hi, int j0, float qx, B&& bound, F&& visit) {
+    for (int j = j0; j < hi; j += 4) {
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = a[min(j + u, hi - 1)];
+        bool stop = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (stop || j + u >= hi) { stop = true; continue; }
+            const float dx = p[u].x - qx;
+            if (dx * dx > bound()) { stop = true; continue; }
+            visit(p[u]);
+        }
+        if (stop) break;
+    }
+    for (int j = j0 - 1; j >= lo; j -= 4) {
+        float4 p[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) p[u] = a[max(j - u, lo)];
+        bool stop = false;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (stop || j - u < lo) { stop = true; continue; }
+            const float dx = p[u].x - qx;
+            if (dx * dx > bound()) { stop = true; continue; }
+            visit(p[u]);
+        }
+        if (stop) break;
+    }
+}
+
+// The reference's 2nd / 3rd point walks (FA:1058-1099, 1169-1225) keep, per
+// target, the strict minimum of sq3_ref first over a forward index range
+// (ties -> lowest index), then over a backward range (replaced only by a
+// strictly smaller distance; ties -> the first met going down = highest
+// index), starting from the gate (strict).  As one total order: the smallest
+// (d, class, t) with class 0 / t = idx forward, class 1 / t = -idx backward,
+// and the gate itself (d = gate, class -1) never beaten by a tie.
+struct WalkBest {
+    float d; int cls, t;
+    __device__ void init(float gate) { d = gate; cls = -1; t = 0; }
+    __device__ void offer(float dd, int c, int tt) {
+        if (dd < d || (dd == d && (c < cls || (c == cls && tt < t)))) { d = dd; cls = c; t = tt; }
+    }
+    __device__ int index() const { return cls < 0 ? -1 : (cls == 0 ? t : -t); }
+};
+
+// sweep ring r of the x-sorted cloud `sx` (segment [rf[r], rf[r+1])),
+// classifying each point by its index: [f0, f1) forward, [b0, b1) backward
+__device__ inline void ring_walk(const float4* sx, const int32_t* rf, int R, int r, const P4& q,
+                                 int f0, int f1, int b0, int b1, WalkBest& wb) {
+    if (r < 0 || r >= R) return;
+    const int lo = rf[r], hi = rf[r + 1];
+    if (lo >= hi || (max(f0, lo) >= min(f1, hi) && max(b0, lo) >= min(b1, hi))) return;
+    const int j0 = sx_lower(sx, lo, hi, q.x);
+    sx_sweep(sx, lo, hi, j0, q.x, [&]() { return wb.d; }, [&](const float4& p) {
+        const int idx = __float_as_int(p.w);
+        const bool fw = idx >= f0 && idx < f1, bw = idx >= b0 && idx < b1;
+        if (!fw && !bw) return;
+        wb.offer(sq3_ref(p, q), fw ? 0 : 1, fw ? idx : -idx);
+    });
+}
+
+// the same over ring r of the unsorted cloud, in index order (short rings)
+__device__ inline void ring_walk_linear(const float4* a, const int32_t* rf, int R, int r, const P4& q,
+                                        int f0, int f1, int b0, int b1, WalkBest& wb) {
+    if (r < 0 || r >= R) return;
+    const int lo = rf[r], hi = rf[r + 1];
+    for (int pass = 0; pass < 2; ++pass) {
+        const int j0 = max(lo, pass == 0 ? f0 : b0), j1 = min(hi, pass == 0 ? f1 : b1);
+#pragma unroll 4
+        for (int j = j0; j < j1; ++j) wb.offer(sq3_ref(a[j], q), pass, pass == 0 ? j : -j);
+    }
+}
+
+#ifndef SLO_SURF_LINEAR
+#define SLO_SURF_LINEAR 0   // 1: surf walks in index order over surf_last (no x-sorted rings)
+#endif
+#ifndef SLO_DIAG_ODO
+#define SLO_DIAG_ODO 0   // 1: k_fa_search_* add per-wave phase cycles to StreamState::dbg[0..3]
+#endif
+#if SLO_DIAG_ODO
+#define ODO_STAMP(k) do { const unsigned long long t_n = clock64(); \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&v.st[s].dbg[k], t_n - t_d); t_d = t_n; } while (0)
+#else
+#define ODO_STAMP(k) do {} while (0)
+#endif
+
+// The *Last clouds are concatenated ring by ring, so the reference's walk for
+// the 2nd / 3rd points — step away from `closest` until the ring leaves
+// [cscan-2, cscan+2], sorting each point into "same/lower ring" or "other
+// ring" by its ring — is a minimum over index ranges cut at the ring
+// boundaries (roff_last) with the visiting order's tie rule (WalkBest):
+// forward over [closest+1, ...) bounded by Q7's min(query count, cloud
+// size), then backward from closest-1.
+
+// findCorrespondingSurfFeatures (FA:1155-1268), one thread per query: exact
+// 1-NN in the tree cloud through the 1 m hash grid, then the walks for the
+// 2nd / 3rd points as x-sweeps over the rings of the x-sorted surf_last.
+__global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
     int s, chunk;
     xcd_stream_chunk(blockIdx.x, nb, s, chunk);
     if (s >= v.S) return;
     const StreamState& st = v.st[s];
-    if (st.odo_phase != PH) return;
+    if (st.odo_phase != 0) return;
     const int i = chunk * blockDim.x + threadIdx.x;
-    const int nq = PH == 0 ? st.n_flat : st.n_sharp;
-    if (chunk * (int)blockDim.x >= nq) return;   // whole workgroup idle (uniform)
+    const int nq = st.n_flat;
+    if (chunk * (int)blockDim.x >= nq) return;   // uniform
+#if SLO_DIAG_ODO
+    unsigned long long t_d = clock64();
+#endif
     const bool active = i < nq;
     const float gate = v.cfg.nearest_feature_search_sq_dist;
     const int R = v.cfg.n_scan;
     float tc[6];
     for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-    const float4* qp = PH == 0 ? v.flat + (size_t)s * v.cap_flat : v.sharp + (size_t)s * v.cap_sharp;
-    const P4 sel = slo_pose::transform_to_start(ld4(qp, active ? i : 0), tc);
-    const int32_t* rf = v.roff_last + ((size_t)s * 2 + (PH == 0 ? 1 : 0)) * (R + 1);
+    const P4 sel = slo_pose::transform_to_start(ld4(v.flat + (size_t)s * v.cap_flat, active ? i : 0), tc);
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + 1) * (R + 1);
     auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
-    int ci; float cd;
-    if (PH == 0) {
-        nn1_grid(v.g_os, s, gate, sel, ci, cd);
-    } else {
-        __shared__ float4 tile[256];
-        const float4* kd = v.kd_corner + (size_t)s * v.cap_less_sharp;
-        const int n = st.kdCornerNum;
-        ci = -1; cd = FLT_MAX;
-        const bool fin = isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z);
-        for (int t0 = 0; t0 < n; t0 += 256) {
-            __syncthreads();
-            if (t0 + (int)threadIdx.x < n) tile[threadIdx.x] = kd[t0 + threadIdx.x];
-            __syncthreads();
-            const int m = min(256, n - t0);
-            if (active && fin)
-                for (int k = 0; k < m; ++k) {
-                    const float d = sqdist_flann(sel, tile[k]);
-                    if (d < cd) { cd = d; ci = t0 + k; }
-                }
-        }
+    int ci = -1; float cd = FLT_MAX;
+    if (active) nn1_grid(v.g_os, s, gate, sel, ci, cd);
+    ODO_STAMP(0);
+    const float4* sx = v.sx_surf_last + (size_t)s * v.cap_less_flat;
+    const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
+    const int surfLastNum = st.surfLastNum;
+    int closest = -1, i2 = -1, i3 = -1;
+    if (active && cd < gate && ci >= 0 && ci < surfLastNum) {
+        closest = ci;
+        const int cscan = (int)slast[closest].w;
+        const int lim = min(nq, surfLastNum);                        // Q7: bounded by the flat count
+        const int e0 = ring_first(cscan + 1), e2 = ring_first(cscan + 3);
+        const int b0 = ring_first(cscan), b2 = ring_first(cscan - 2);
+        WalkBest w2, w3;
+        w2.init(gate); w3.init(gate);
+#if SLO_SURF_LINEAR
+#define SURF_WALK(...) ring_walk_linear(slast, __VA_ARGS__)
+#else
+#define SURF_WALK(...) ring_walk(sx, __VA_ARGS__)
+#endif
+        SURF_WALK(rf, R, cscan, sel, closest + 1, min(e0, lim), b0, closest, w2);   // ring == cscan
+        const int f0 = max(closest + 1, e0), f1 = min(e2, lim), bb1 = min(b0, closest);
+        for (int r = cscan - 2; r <= cscan + 2; ++r)                              // other rings
+            if (r != cscan) SURF_WALK(rf, R, r, sel, f0, f1, b2, bb1, w3);
+#undef SURF_WALK
+        i2 = w2.index(); i3 = w3.index();
     }
+    ODO_STAMP(1);
     if (!active) return;
-    if (PH == 0) {
-        const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
-        const int surfLastNum = st.surfLastNum;
-        int closest = -1, i2 = -1, i3 = -1;
-        if (cd < gate && ci >= 0 && ci < surfLastNum) {
-            closest = ci;
-            const int cscan = (int)slast[closest].w;
-            const int lim = min(nq, surfLastNum);                        // Q7: bounded by the flat count
-            const int e0 = ring_first(cscan + 1), e2 = ring_first(cscan + 3);
-            const int b0 = ring_first(cscan), b2 = ring_first(cscan - 2);
-            float m2 = gate, m3 = gate;
-            walk_up(slast, closest + 1, min(e0, lim), sel, m2, i2);         // ring == cscan
-            walk_up(slast, max(closest + 1, e0), min(e2, lim), sel, m3, i3); // cscan < ring <= cscan+2
-            walk_down(slast, b0, closest, sel, m2, i2);                      // ring == cscan
-            walk_down(slast, b2, min(b0, closest), sel, m3, i3);             // cscan-2 <= ring < cscan
-        }
-        int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
-        ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
-    } else {
-        const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
-        const int cornerLastNum = st.cornerLastNum;
-        int closest = -1, i2 = -1;
-        if (cd < gate && ci >= 0 && ci < cornerLastNum) {
-            closest = ci;
-            const int cscan = (int)clast[closest].w;
-            const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
-            float m2 = gate;
-            walk_up(clast, max(closest + 1, ring_first(cscan + 1)), min(ring_first(cscan + 3), lim), sel, m2, i2);
-            walk_down(clast, ring_first(cscan - 2), min(ring_first(cscan), closest), sel, m2, i2);
-        }
-        int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
-        indc[2 * i] = closest; indc[2 * i + 1] = i2;
+    int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
+    ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
+}
+
+// findCorrespondingCornerFeatures (FA:1044-1153): one workgroup = 64 queries
+// (consecutive in x order, sharp_perm) x 4 waves.  1-NN by brute force over
+// the x-window of the x-sorted tree cloud that can hold a point within the
+// gate of any of the 64 queries (a wider margin than float rounding needs;
+// every point outside it is farther than the gate, where the reference
+// rejects the neighbour anyway), streamed through LDS: wave w takes a quarter
+// of each 256-point tile, every lane keeps four independent minimum chains,
+// and the 16 partial minima of a query merge by (distance, index) — the
+// result of the reference's exact nearest neighbour with ties to the lowest
+// index.  Then the 2nd point: wave w walks ring cscan + {-2, -1, +1, +2}[w]
+// and the four WalkBests merge in LDS.
+__global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    const StreamState& st = v.st[s];
+    if (st.odo_phase != 1) return;
+    const int nq = st.n_sharp;
+    if (chunk * 64 >= nq) return;   // uniform
+#if SLO_DIAG_ODO
+    unsigned long long t_d = clock64();
+#endif
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int pos = chunk * 64 + lane;
+    const bool active = pos < nq;
+    const int i = active ? v.sharp_perm[(size_t)s * v.cap_sharp + pos] : 0;
+    const float gate = v.cfg.nearest_feature_search_sq_dist;
+    const int R = v.cfg.n_scan;
+    float tc[6];
+    for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    const P4 sel = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
+    const bool fin = active && isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z);
+    // the workgroup's x-window (every wave computes the same one)
+    float xmin = fin ? sel.x : FLT_MAX, xmax = fin ? sel.x : -FLT_MAX;
+    for (int o = 32; o > 0; o >>= 1) {
+        xmin = fminf(xmin, __shfl_xor(xmin, o, 64));
+        xmax = fmaxf(xmax, __shfl_xor(xmax, o, 64));
     }
+    const float4* kx = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
+    const int n = st.kdCornerNum;
+    int lo = 0, hi = 0;
+    if (xmin <= xmax) {
+        const float rr = sqrtf(gate) * 1.001f + 1e-3f + 1e-5f * fmaxf(fabsf(xmin), fabsf(xmax));
+        lo = sx_lower(kx, 0, n, xmin - rr);
+        hi = sx_lower(kx, lo, n, xmax + rr);
+    }
+    __shared__ float4 tile[256];
+    __shared__ float s_d[4][64];
+    __shared__ int s_i[4][64], s_c[4][64];
+    float cd[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+    int ci[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+    auto take = [&](int c, const float4& p) {
+        const float d = sqdist_flann(sel, p);
+        const int idx = __float_as_int(p.w);
+        if (d < cd[c] || (d == cd[c] && idx < ci[c])) { cd[c] = d; ci[c] = idx; }
+    };
+    for (int t0 = lo; t0 < hi; t0 += 256) {
+        __syncthreads();
+        if (t0 + tid < hi) tile[tid] = kx[t0 + tid];
+        __syncthreads();
+        const int m = min(256, hi - t0) - w * 64;   // this wave's share of the tile: [w*64, w*64 + m)
+        if (fin && m > 0) {
+            if (m >= 64) {
+#pragma unroll 4
+                for (int j = 0; j < 64; j += 4)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) take(c, tile[w * 64 + j + c]);
+            } else {
+                for (int j = 0; j < m; ++j) take(j & 3, tile[w * 64 + j]);
+            }
+        }
+    }
+    for (int c = 1; c < 4; ++c)
+        if (cd[c] < cd[0] || (cd[c] == cd[0] && ci[c] < ci[0])) { cd[0] = cd[c]; ci[0] = ci[c]; }
+    s_d[w][lane] = cd[0]; s_i[w][lane] = ci[0];
+    __syncthreads();
+    float bd = s_d[0][lane];
+    int bi = s_i[0][lane];
+    for (int k = 1; k < 4; ++k) {
+        const float d = s_d[k][lane];
+        const int x = s_i[k][lane];
+        if (d < bd || (d == bd && x < bi)) { bd = d; bi = x; }
+    }
+    ODO_STAMP(2);
+    const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + 0) * (R + 1);
+    auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
+    const int cornerLastNum = st.cornerLastNum;
+    const bool found = fin && bi != INT_MAX && bd < gate && bi < cornerLastNum;
+    WalkBest wb;
+    wb.init(gate);
+    if (found) {
+        const int cscan = (int)clast[bi].w;
+        const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
+        const int f0 = max(bi + 1, ring_first(cscan + 1)), f1 = min(ring_first(cscan + 3), lim);
+        const int b0 = ring_first(cscan - 2), b1 = min(ring_first(cscan), bi);
+        const int r = cscan + (w < 2 ? w - 2 : w - 1);
+        ring_walk_linear(clast, rf, R, r, sel, f0, f1, b0, b1, wb);
+    }
+    __syncthreads();   // s_d / s_i reads above are done
+    s_d[w][lane] = wb.d; s_c[w][lane] = wb.cls; s_i[w][lane] = wb.t;
+    __syncthreads();
+    ODO_STAMP(3);
+    if (w != 0 || !active) return;
+    for (int k = 1; k < 4; ++k) wb.offer(s_d[k][lane], s_c[k][lane], s_i[k][lane]);
+    int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
+    indc[2 * i] = found ? bi : -1; indc[2 * i + 1] = found ? wb.index() : -1;
 }
 
 // iterations iter0 .. iter0+4 of calculateTransformationSurf (FA:1270-1377)
@@ -473,24 +799,35 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
     if (!first_scan) {
-        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 255) / 256;
+        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 63) / 64;
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search<0>, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
+            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
             SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
         }
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search<1>, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
+            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
     SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v);
+    const int R = v.cfg.n_scan;
+    if (!SLO_SURF_LINEAR)
+    {
+        SLO_LAUNCH(ctx, "fa_sx_rings", k_fa_sx_rings, dim3(xcd_grid(S, (R + 3) / 4)), dim3(256), 0, v, (R + 3) / 4);
+        if (v.cfg.horizon_scan > 512)
+            SLO_LAUNCH(ctx, "fa_sx_long", k_fa_sx_long, dim3(xcd_grid(S, R)), dim3(256), 0, v, R);
+    }
+    if (v.cap_less_sharp <= 4096) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<4096>, dim3(S), dim3(1024), 0, v);
+    else if (v.cap_less_sharp <= 8192) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<8192>, dim3(S), dim3(1024), 0, v);
+    else SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<16384>, dim3(S), dim3(1024), 0, v);
     SLO_CHECK(hipGetLastError());
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);
     std::swap(ctx->v.surf_last, ctx->v.surf_next);
+    std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
     // setInputCloud: hash grid over the (possibly unchanged) surf tree cloud
-    // (the corner tree is searched by brute force, k_fa_search<1>)
+    // (the corner tree by a windowed brute force over its x-sorted copy, k_fa_sx_kd)
     const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
     return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
 }

@@ -38,6 +38,7 @@ class SloConfig(ctypes.Structure):
         ("sc_num_candidates", ctypes.c_int32), ("sc_search_ratio", ctypes.c_double),
         ("sc_dist_thres", ctypes.c_double), ("sc_tree_making_period", ctypes.c_int32),
         ("sc_atan_float", ctypes.c_int32), ("skip_frame_num", ctypes.c_int32), ("max_points", ctypes.c_int32),
+        ("keyframe_cloud_cap", ctypes.c_int32),
     ]
 
 
