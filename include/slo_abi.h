@@ -114,6 +114,37 @@ int slo_sc_make_and_save(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
  * (used to seed the Scan Context history, e.g. from a previous session) */
 int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
 
+/* ---------------------------------------------------------------- loop-closure verification
+ * mapOptmization.cpp:841-1110 (detectLoopClosure + performLoopClosure, minus
+ * the GTSAM factors).  Needs cfg.loop_verify = 1 and
+ * cfg.loop_archive_points > 0 at slo_create (the keyframe archive).  One
+ * record per candidate, [0] = radius search (RS), [1] = Scan Context (SC). */
+typedef struct slo_loop_result {
+    int32_t id;          /* candidate keyframe, -1 none */
+    int32_t ran;         /* ICP ran (only when an SC candidate exists, MO:925-927) */
+    int32_t converged;   /* icp.hasConverged() */
+    int32_t accepted;    /* converged && fitness <= historyKeyframeFitnessScore (MO:1020 / 1071) */
+    int32_t iters;       /* ICP iterations */
+    int32_t n_src, n_tgt;  /* source cloud / downsampled submap sizes */
+    int32_t pad;
+    double fitness;      /* icp.getFitnessScore() */
+    float T[16];         /* icp.getFinalTransformation(), row-major */
+    float xyzrpy[6];     /* pcl::getTranslationAndEulerAngles(T): x, y, z, roll, pitch, yaw */
+} slo_loop_result;
+
+/* RS + SC verification for every stream whose SC detect ran this scan
+ * (slo_batch_process calls it when cfg.loop_verify is set); results via
+ * slo_get(.., "loop") */
+int slo_batch_loop_closure(slo_ctx* ctx);
+/* the same for stream 0 after slo_sc_detect; out[0] = RS, out[1] = SC */
+int slo_loop_closure(slo_ctx* ctx, slo_loop_result* out);
+/* pcl::IterativeClosestPoint::align + getFitnessScore (MO:1006-1016) on given
+ * device clouds, one pair per stream: d_src [n_streams][src_stride] float4,
+ * d_nsrc int32 [n_streams], d_tgt [n_streams][tgt_stride], d_ntgt; counts
+ * must fit loop_archive_points.  Writes n_streams records to host h_out. */
+int slo_icp_align_batch(slo_ctx* ctx, const void* d_src, size_t src_stride, const int32_t* d_nsrc, const void* d_tgt,
+                        size_t tgt_stride, const int32_t* d_ntgt, slo_loop_result* h_out);
+
 /* ---------------------------------------------------------------- multi-GPU records
  * Pack one fixed-size record per stream (odometry pose, mapped pose,
  * keyframe count, loop result, newest ring key) into device memory d_out
@@ -129,7 +160,7 @@ int slo_record_floats(void);
  * "picked", "cloud_label", "smooth_ind", "sharp", "less_sharp", "flat",
  * "less_flat", "corner_last", "surf_last", "transform_sum", "transform_cur",
  * "fa_iters", "mapped", "n_keyframes", "keyposes", "sc_desc", "ring_key",
- * "sector_key", "detect", "detect_f", "flags". */
+ * "sector_key", "detect", "detect_f", "flags", "loop" (2 x slo_loop_result), "key_times". */
 int slo_get(slo_ctx* ctx, int stream, const char* name, void* dst, size_t cap_bytes);
 
 /* per-kernel timing (HIP events around every launch when enabled) */

@@ -10,6 +10,7 @@
 // The raw cloud handed to mapping is the scan being mapped (Q16).
 #include "oracle_fa.h"
 #include "oracle_mo.h"
+#include "oracle_lc.h"
 #include <thread>
 #include <chrono>
 #include <atomic>
@@ -25,6 +26,7 @@ struct OracleStream {
     MapOptimization mo;
     SCManager::DetectResult det{};
     bool det_valid = false;
+    LoopResult loop[2];      // RS, SC verification of the last detect (cfg.loop_verify)
     int scan_index = 0;
     explicit OracleStream(const slo_config& c) : cfg(c), ip(c), fa(c), mo(c) {}
 
@@ -43,6 +45,10 @@ struct OracleStream {
                 det = mo.sc.detectLoopClosureID();
                 det_valid = true;
                 flags |= 8;
+                if (cfg.loop_verify) {
+                    perform_loop_closure(cfg, mo, det.loop_id, t, loop, mo.stable_voxel);
+                    if (loop[1].ran) flags |= 16;
+                }
             }
         }
         scan_index++;
@@ -147,6 +153,11 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
         for (int i = 0; i < s->det.n_cand; ++i) v.push_back(s->det.cand[i]);
         return cp(v.data(), (int)v.size(), 4);
     }
+    if (name == "loop") {   // 2 x LoopResult (RS, SC) of the last detect
+        if (!s->det_valid || !s->cfg.loop_verify) return 0;
+        return cp(s->loop, 2, (int)sizeof(LoopResult));
+    }
+    if (name == "key_times") return cp(s->mo.keyTimes.data(), (int)s->mo.keyTimes.size(), 8);
     if (name == "detect_f") {
         if (!s->det_valid) return 0;
         double v[2] = {(double)s->det.yaw, s->det.min_dist};
@@ -154,6 +165,28 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
     }
     return -1;
 }
+
+// ---- loop-closure unit entry points (oracle_lc.h)
+// icp.align + getFitnessScore of src (n x XYZI) onto tgt (m x XYZI)
+void oracle_icp_align(const slo_config* cfg, const float* src, int n, const float* tgt, int m, LoopResult* out) {
+    Cloud a(n), b(m);
+    if (n) memcpy(a.data(), src, 16 * (size_t)n);
+    if (m) memcpy(b.data(), tgt, 16 * (size_t)m);
+    *out = LoopResult();
+    out->id = 0;
+    icp_align(*cfg, a, b, *out);
+}
+// pcl::umeyama of the pairs (src[i], dst[i]) (one ICP increment); returns 0 on success
+int oracle_umeyama(const float* src, const float* dst, int n, float* T) {
+    IcpSums a;
+    for (int i = 0; i < n; ++i) {
+        Pt p{src[4 * i], src[4 * i + 1], src[4 * i + 2], 0}, q{dst[4 * i], dst[4 * i + 1], dst[4 * i + 2], 0};
+        a.add(p, q, 0.0f);
+    }
+    return umeyama_from_sums(a, T) ? 0 : -1;
+}
+// JacobiSVD<Matrix3d> of a row-major 3x3
+int oracle_svd3(const double* A, double* U, double* S, double* V) { return jacobi_svd3(A, U, S, V) ? 0 : -1; }
 
 // ---- SC unit entry points (pure functions over given descriptors)
 double oracle_sc_distance(const slo_config* cfg, const double* sc1, const double* sc2, int* shift) {

@@ -28,6 +28,8 @@ struct MapOptimization {
     float transformTobeMapped[6] = {0}, transformBefMapped[6] = {0}, transformAftMapped[6] = {0};
     std::vector<Cloud> cornerCloudKeyFrames, surfCloudKeyFrames, outlierCloudKeyFrames;
     std::vector<Pose6> keyPoses;  // cloudKeyPoses6D (3D = x,y,z)
+    std::vector<double> keyTimes; // cloudKeyPoses6D[i].time (MO:1609: timeLaserOdometry)
+    double timeLaserOdometry = 0;
     std::deque<Cloud> recentCorner, recentSurf, recentOutlier;
     int latestFrameID = 0;
     Pt previousRobotPosPoint{0, 0, 0, 0}, currentRobotPosPoint{0, 0, 0, 0};
@@ -380,6 +382,7 @@ struct MapOptimization {
         }
         Pose6 p6{est[3], est[4], est[5], est[0], est[1], est[2]};
         keyPoses.push_back(p6);
+        keyTimes.push_back(timeLaserOdometry);
         if (keyPoses.size() > 1) {
             float e[6];
             memcpy(e, est, sizeof(e));
@@ -399,6 +402,7 @@ struct MapOptimization {
         ran = false;
         saved_keyframe = false;
         for (int i = 0; i < 6; ++i) transformSum[i] = odomSum[i];
+        timeLaserOdometry = t;
         if (!(t - timeLastProcessing >= cfg.mapping_process_interval)) return false;
         timeLastProcessing = t;
         laserCloudCornerLast = corner;

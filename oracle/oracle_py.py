@@ -40,6 +40,12 @@ class SloConfig(ctypes.Structure):
         ("sc_dist_thres", ctypes.c_double), ("sc_tree_making_period", ctypes.c_int32),
         ("sc_atan_float", ctypes.c_int32), ("skip_frame_num", ctypes.c_int32), ("max_points", ctypes.c_int32),
         ("keyframe_cloud_cap", ctypes.c_int32),
+        ("loop_verify", ctypes.c_int32), ("loop_archive_points", ctypes.c_int32),
+        ("history_keyframe_search_radius", ctypes.c_float), ("history_keyframe_search_num", ctypes.c_int32),
+        ("history_keyframe_fitness_score", ctypes.c_float), ("leaf_history", ctypes.c_float),
+        ("loop_time_gap", ctypes.c_double), ("icp_max_iterations", ctypes.c_int32),
+        ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
+        ("icp_fitness_epsilon", ctypes.c_double),
     ]
 
 
@@ -82,6 +88,10 @@ def lib():
         L.oracle_sc_session_detect.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_sc_knn.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                     ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_icp_align.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_int, ctypes.c_void_p]
+        L.oracle_umeyama.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
         _LIB = L
     return _LIB
 
@@ -107,10 +117,49 @@ _DTYPES = {
     "transform_sum": np.float32, "transform_cur": np.float32, "fa_iters": np.int32, "mapped": np.float32,
     "tobe_mapped": np.float32, "mo_iters": np.int32, "n_keyframes": np.int32, "keyposes": np.float32,
     "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64, "detect": np.int32,
-    "detect_f": np.float64,
+    "detect_f": np.float64, "key_times": np.float64,
 }
+# LoopResult (oracle/oracle_lc.h == slo_loop_result in include/slo_abi.h): [RS, SC]
+LOOP_DTYPE = np.dtype([("id", "<i4"), ("ran", "<i4"), ("converged", "<i4"), ("accepted", "<i4"), ("iters", "<i4"),
+                       ("n_src", "<i4"), ("n_tgt", "<i4"), ("pad", "<i4"), ("fitness", "<f8"),
+                       ("T", "<f4", (16,)), ("xyzrpy", "<f4", (6,))])
+assert LOOP_DTYPE.itemsize == 128
+_DTYPES["loop"] = LOOP_DTYPE
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
            "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"}
+
+
+def voxel_grid(pts, leaf, stable=False):
+    """PCL VoxelGrid (oracle_common.h); NaN rows are dropped first (VoxelGrid skips them)"""
+    pts = np.ascontiguousarray(pts, np.float32).reshape(-1, 4)
+    pts = np.ascontiguousarray(pts[np.isfinite(pts[:, :3]).all(axis=1)])
+    out = np.empty((max(len(pts), 1), 4), np.float32)
+    n = lib().oracle_voxel_grid(pts.ctypes.data, len(pts), float(leaf), int(stable), out.ctypes.data, len(out))
+    return out[:n].copy()
+
+
+def icp_align(cfg, src, tgt):
+    """pcl::IterativeClosestPoint::align + getFitnessScore (oracle_lc.h) -> LOOP_DTYPE record"""
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 4)
+    tgt = np.ascontiguousarray(tgt, np.float32).reshape(-1, 4)
+    out = np.zeros(1, LOOP_DTYPE)
+    lib().oracle_icp_align(ctypes.byref(cfg), src.ctypes.data, len(src), tgt.ctypes.data, len(tgt), out.ctypes.data)
+    return out[0]
+
+
+def umeyama(src, dst):
+    src = np.ascontiguousarray(src, np.float32).reshape(-1, 4)
+    dst = np.ascontiguousarray(dst, np.float32).reshape(-1, 4)
+    T = np.zeros(16, np.float32)
+    rc = lib().oracle_umeyama(src.ctypes.data, dst.ctypes.data, len(src), T.ctypes.data)
+    return T.reshape(4, 4) if rc == 0 else None
+
+
+def svd3(A):
+    A = np.ascontiguousarray(A, np.float64).reshape(3, 3)
+    U, S, V = np.zeros((3, 3)), np.zeros(3), np.zeros((3, 3))
+    rc = lib().oracle_svd3(A.ctypes.data, U.ctypes.data, S.ctypes.data, V.ctypes.data)
+    return (U, S, V) if rc == 0 else None
 
 
 class SCSession:

@@ -77,6 +77,26 @@ typedef struct slo_config {
        bits, so a run that stays exact reports no error.  Host-side only: the
        CPU restatement ignores it. */
     int32_t keyframe_cloud_cap;
+    /* loop-closure verification (performLoopClosure, mapOptmization.cpp:
+       964-1110, with detectLoopClosure 841-962): after every SC detect that
+       reports a loop, the radius-search (RS) and Scan Context (SC) candidate
+       submaps are assembled and each is aligned by ICP.  0 = off (the
+       reference's loop thread, ICP and GTSAM factors are then not run). */
+    int32_t loop_verify;
+    /* capacity: points per stream of the keyframe archive (corner + surf DS
+       clouds of every keyframe, body frame: cornerCloudKeyFrames /
+       surfCloudKeyFrames, MO:1587-1594) the submaps are built from; required
+       (> 0) when loop_verify is set */
+    int32_t loop_archive_points;
+    float history_keyframe_search_radius;   /* 20.0 m (utility.h:137) */
+    int32_t history_keyframe_search_num;    /* 25 (utility.h:138): submap = keyframes id-25..id+25 */
+    float history_keyframe_fitness_score;   /* 1.5 (utility.h:139) */
+    float leaf_history;                     /* 0.3 (downSizeFilterHistoryKeyFrames, MO:268) */
+    double loop_time_gap;                   /* 30.0 s (MO:866) */
+    int32_t icp_max_iterations;             /* 100 (MO:1008 / 1059) */
+    double icp_max_corr_dist;               /* 100 (MO:1007 / 1058) */
+    double icp_transformation_epsilon;      /* 1e-6 (MO:1009 / 1060) */
+    double icp_fitness_epsilon;             /* 1e-6 (MO:1010 / 1061) */
 } slo_config;
 
 /* preset ids */
@@ -173,6 +193,17 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->skip_frame_num = 1;
     c->max_points = R * C;
     c->keyframe_cloud_cap = 0;
+    c->loop_verify = 0;
+    c->loop_archive_points = 0;
+    c->history_keyframe_search_radius = (float)20.0;
+    c->history_keyframe_search_num = 25;
+    c->history_keyframe_fitness_score = (float)1.5;
+    c->leaf_history = (float)0.3;
+    c->loop_time_gap = 30.0;
+    c->icp_max_iterations = 100;
+    c->icp_max_corr_dist = 100.0;
+    c->icp_transformation_epsilon = 1e-6;
+    c->icp_fitness_epsilon = 1e-6;
     return 0;
 }
 #endif

@@ -74,7 +74,10 @@ void* slo_stream(slo_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 
 int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** out) {
     if (!cfg || !out || n_streams <= 0 || cfg->n_scan <= 0 || cfg->n_scan > 128 || cfg->horizon_scan <= 0 ||
-        cfg->horizon_scan > 4096 || cfg->max_points <= 0 || cfg->keyframe_cloud_cap < 0 || cfg->sc_num_candidates < 1 ||
+        cfg->horizon_scan > 4096 || cfg->max_points <= 0 || cfg->keyframe_cloud_cap < 0 ||
+        (cfg->loop_verify && (cfg->loop_archive_points <= 0 || cfg->history_keyframe_search_num < 0 ||
+                              cfg->history_keyframe_search_num > SLO_LC_MAX_N || cfg->icp_max_iterations < 1 ||
+                              !(cfg->leaf_history > 0) || !(cfg->icp_max_corr_dist >= 0))) || cfg->sc_num_candidates < 1 ||
         cfg->sc_num_candidates > SLO_SC_MAX_K || cfg->sc_num_ring < 1 || cfg->sc_num_ring > 64 ||
         cfg->sc_num_sector < 1 || cfg->sc_num_sector > SLO_SC_MAX_SECTOR ||
         cfg->sc_num_ring * cfg->sc_num_sector > SLO_SC_MAX_CELLS || cfg->surrounding_keyframe_search_num < 1 ||
@@ -221,6 +224,10 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
+    if (cfg->loop_verify && slo::lc_alloc(ctx)) {
+        slo_destroy(ctx);
+        return SLO_E_HIP;
+    }
     v.g_os = slo::grid_view(ctx->grid_os);
     v.g_mc = slo::grid_view(ctx->grid_c);
     v.g_ms = slo::grid_view(ctx->grid_s);
@@ -238,6 +245,7 @@ void slo_destroy(slo_ctx* ctx) {
     slo::grid_free(ctx->grid_s);
     slo::grid_free(ctx->grid_oc);
     slo::grid_free(ctx->grid_os);
+    slo::lc_free(ctx);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->h_st) hipHostFree(ctx->h_st);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
@@ -307,7 +315,9 @@ int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t
     if (!ctx->fa_published) return SLO_OK;
     if (!(t_scan - ctx->t_last_processing >= ctx->cfg.mapping_process_interval)) return SLO_OK;
     ctx->t_last_processing = t_scan;
-    return slo::map_run(ctx, (const float4*)d_points, d_counts);
+    int r = slo::map_run(ctx, (const float4*)d_points, d_counts);
+    if (r) return r;
+    return slo::lc_archive_run(ctx, t_scan);   // keyframe archive for loop verification (cfg.loop_verify)
 }
 
 int slo_batch_sc_detect(slo_ctx* ctx) {
@@ -323,7 +333,38 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     if (r) return r;
     r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
     if (r) return r;
-    return slo_batch_sc_detect(ctx);
+    r = slo_batch_sc_detect(ctx);
+    if (r || !ctx->cfg.loop_verify) return r;
+    return slo_batch_loop_closure(ctx);
+}
+
+int slo_batch_loop_closure(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    if (!ctx->cfg.loop_verify) { ctx->err = "loop verification needs cfg.loop_verify"; return SLO_E_STATE; }
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::lc_run(ctx);
+}
+
+int slo_loop_closure(slo_ctx* ctx, slo_loop_result* out) {
+    if (!ctx || !out) return SLO_E_ARG;
+    int r = slo_batch_loop_closure(ctx);
+    if (r) return r;
+    SLO_CHECK(hipMemcpyAsync(out, ctx->lc.res, 2 * sizeof(slo_loop_result), hipMemcpyDeviceToHost, ctx->stream));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
+}
+
+int slo_icp_align_batch(slo_ctx* ctx, const void* d_src, size_t src_stride, const int32_t* d_nsrc, const void* d_tgt,
+                        size_t tgt_stride, const int32_t* d_ntgt, slo_loop_result* h_out) {
+    if (!ctx || !d_src || !d_nsrc || !d_tgt || !d_ntgt || !h_out) return SLO_E_ARG;
+    if (!ctx->cfg.loop_verify) { ctx->err = "ICP needs cfg.loop_verify (its buffers)"; return SLO_E_STATE; }
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = slo::lc_icp_run(ctx, (const float4*)d_src, src_stride, d_nsrc, (const float4*)d_tgt, tgt_stride, d_ntgt);
+    if (r) return r;
+    SLO_CHECK(hipMemcpy2DAsync(h_out, sizeof(slo_loop_result), ctx->lc.res + 1, 2 * sizeof(slo_loop_result),
+                               sizeof(slo_loop_result), ctx->S, hipMemcpyDeviceToHost, ctx->stream));
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
 }
 
 // ---------------------------------------------------------------- readback
@@ -410,6 +451,12 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     } else if (name == "detect_f") {
         if (!st.det_valid) { count = 0; esz = 8; }
         else { double d[2] = {(double)st.det_yaw, st.det_min_dist}; tmp.resize(16); memcpy(tmp.data(), d, 16); count = 2; esz = 8; }
+    } else if (name == "loop") {   // RS, SC verification of this scan's detect
+        if (ctx->cfg.loop_verify && st.det_valid) dev(ctx->lc.res + 2 * s, 2, sizeof(slo_loop_result));
+        else { count = 0; esz = sizeof(slo_loop_result); }
+    } else if (name == "key_times") {
+        if (ctx->cfg.loop_verify) dev(ctx->lc.ktime + s * v.KFMAX, std::min(st.n_keyframes, v.KFMAX), 8);
+        else { count = 0; esz = 8; }
     }
     else return SLO_E_ARG;
     const size_t bytes = std::min(cap_bytes, count * esz);

@@ -333,6 +333,42 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
     }
 }
 
+// ---- loop-closure verification (slo_lc.hip; mapOptmization.cpp:841-1110)
+#define SLO_LC_MAX_N 64                      // historyKeyframeSearchNum limit
+#define SLO_LC_SEG (2 * SLO_LC_MAX_N + 1)    // submap keyframes id-N .. id+N
+// per stream; the int32 counts come first (vg_run / grid_build read them at
+// an int32 stride of sizeof(LcState) / 4)
+struct LcState {
+    int32_t used;                  // archive points in use
+    int32_t rs_id, sc_id, latest;  // candidates of the last select; newest keyframe
+    int32_t n_src_raw, n_src, n_raw, n_tgt;   // source before / after the intensity filter; submap raw / DS
+    int32_t active, iter, converged, pass;
+    int32_t nseg, src_off, pad0, pad1;
+    int32_t seg_off[SLO_LC_SEG + 1];          // submap prefix: keyframe seg k -> [seg_off[k], seg_off[k+1])
+    int32_t seg_src[SLO_LC_SEG];              // its archive offset
+    float seg_trig[SLO_LC_SEG][9];            // cos/sin roll, pitch, yaw + x, y, z of its pose
+    float src_trig[9];                        // the source's pose (RS: newest keyframe, SC: the candidate)
+    float T[16], Ti[16];                      // final transformation, last increment (row-major)
+    double prev_mse;
+};
+struct LcView {
+    int A;             // archive / submap capacity per stream (cfg.loop_archive_points)
+    int cap_src;       // source capacity per stream
+    float4* kfa;       // [S][A] keyframe archive: per keyframe corner DS then surf DS, body frame
+    int32_t* kmeta;    // [S][KFMAX][3] archive offset, n corner, n surf
+    double* ktime;     // [S][KFMAX] cloudKeyPoses6D.time
+    float4* src;       // [S][cap_src] ICP source (input_)
+    float4* src_t;     // [S][cap_src] input_transformed
+    int32_t* corr_j;   // [S][cap_src] nearest target index (-1: none / rejected)
+    float* corr_d;     // [S][cap_src] its squared distance
+    float4* raw;       // [S][A] submap before VoxelGrid
+    float4* tgt;       // [S][A] submap after VoxelGrid (ICP target)
+    LcState* st;       // [S]
+    slo_loop_result* res;   // [S][2] RS, SC
+    int32_t* n_active; // live ICP jobs
+    GridView g;        // hash grid over tgt
+};
+
 struct VgParams;
 struct MapWs {  // VoxelGrid workspace
     size_t items = 0;
@@ -392,6 +428,10 @@ struct slo_ctx {
     slo::MapWs mws;
     slo::HashGrid grid_c, grid_s, grid_oc, grid_os;
     bool map_ready = false;
+    // loop-closure verification (cfg.loop_verify)
+    slo::LcView lc{};
+    slo::HashGrid grid_lc;
+    int32_t* h_lc_active = nullptr;     // pinned copy of lc.n_active
 };
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -414,6 +454,12 @@ int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n
 int sc_detect_run(slo_ctx* ctx);
 int sc_detect_run_one(slo_ctx* ctx);
 int pack_records_run(slo_ctx* ctx, float* d_out);
+int lc_alloc(slo_ctx* ctx);
+void lc_free(slo_ctx* ctx);
+int lc_archive_run(slo_ctx* ctx, double t_scan);
+int lc_run(slo_ctx* ctx);
+int lc_icp_run(slo_ctx* ctx, const float4* src, size_t src_stride, const int32_t* nsrc, const float4* tgt,
+               size_t tgt_stride, const int32_t* ntgt);
 }  // namespace slo
 
 #define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \

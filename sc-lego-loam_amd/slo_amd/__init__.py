@@ -33,7 +33,13 @@ _DT = {"range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": 
        "fa_iters": np.int32, "mapped": np.float32, "n_keyframes": np.int32, "flags": np.int32,
        "keyposes": np.float32, "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64,
        "detect": np.int32, "detect_f": np.float64, "mo_iters": np.int32, "tobe_mapped": np.float32,
-       "err": np.int32, "dbg": np.uint64}
+       "err": np.int32, "dbg": np.uint64, "key_times": np.float64}
+# slo_loop_result (include/slo_abi.h), one per candidate: [RS, SC]
+LOOP_DTYPE = np.dtype([("id", "<i4"), ("ran", "<i4"), ("converged", "<i4"), ("accepted", "<i4"), ("iters", "<i4"),
+                       ("n_src", "<i4"), ("n_tgt", "<i4"), ("pad", "<i4"), ("fitness", "<f8"),
+                       ("T", "<f4", (16,)), ("xyzrpy", "<f4", (6,))])
+assert LOOP_DTYPE.itemsize == 128
+_DT["loop"] = LOOP_DTYPE
 
 
 class SloError(RuntimeError):
@@ -110,6 +116,24 @@ class Context:
 
     def batch_sc_make(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_sc_make(self.h, d_pts, d_cnt), "slo_batch_sc_make")
+
+    def batch_loop_closure(self):
+        """RS + SC loop verification (MO:841-1110) for every stream whose SC detect ran."""
+        self._ok(self.L.slo_batch_loop_closure(self.h), "slo_batch_loop_closure")
+
+    def loop_closure(self):
+        """stream 0: -> LOOP_DTYPE[2] (RS, SC)"""
+        out = np.zeros(2, LOOP_DTYPE)
+        self._ok(self.L.slo_loop_closure(self.h, out.ctypes.data), "slo_loop_closure")
+        return out
+
+    def icp_align_batch(self, d_src, src_stride, d_nsrc, d_tgt, tgt_stride, d_ntgt):
+        """pcl::IterativeClosestPoint::align + getFitnessScore per stream on
+        device clouds -> LOOP_DTYPE[n_streams]"""
+        out = np.zeros(self.n_streams, LOOP_DTYPE)
+        self._ok(self.L.slo_icp_align_batch(self.h, d_src, int(src_stride), d_nsrc, d_tgt, int(tgt_stride), d_ntgt,
+                                            out.ctypes.data), "slo_icp_align_batch")
+        return out
 
     def pack_records(self, d_out):
         self._ok(self.L.slo_pack_records(self.h, d_out), "slo_pack_records")

@@ -39,6 +39,12 @@ class SloConfig(ctypes.Structure):
         ("sc_dist_thres", ctypes.c_double), ("sc_tree_making_period", ctypes.c_int32),
         ("sc_atan_float", ctypes.c_int32), ("skip_frame_num", ctypes.c_int32), ("max_points", ctypes.c_int32),
         ("keyframe_cloud_cap", ctypes.c_int32),
+        ("loop_verify", ctypes.c_int32), ("loop_archive_points", ctypes.c_int32),
+        ("history_keyframe_search_radius", ctypes.c_float), ("history_keyframe_search_num", ctypes.c_int32),
+        ("history_keyframe_fitness_score", ctypes.c_float), ("leaf_history", ctypes.c_float),
+        ("loop_time_gap", ctypes.c_double), ("icp_max_iterations", ctypes.c_int32),
+        ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
+        ("icp_fitness_epsilon", ctypes.c_double),
     ]
 
 
@@ -69,7 +75,7 @@ EXPORTS = [
     "slo_batch_sc_detect", "slo_batch_process", "slo_image_projection", "slo_feature_association",
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
-    "slo_gen_batch",
+    "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
 ]
 
 
@@ -120,6 +126,9 @@ def lib():
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
+    L.slo_batch_loop_closure.argtypes = [P]
+    L.slo_loop_closure.argtypes = [P, P]
+    L.slo_icp_align_batch.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_size_t, P, P]
     L.slo_sc_make_and_save.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
     L.slo_batch_sc_make.argtypes = [P, P, P]
     L.slo_pack_records.argtypes = [P, P]
