@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
-    ap.add_argument("--streams", type=int, default=256, help="streams per GPU")
+    ap.add_argument("--streams", type=int, default=512, help="streams per GPU")
     ap.add_argument("--groups", type=int, default=2,
                     help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
     ap.add_argument("--preset", default="hdl64_1800")
@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
+    ap.add_argument("--icp-jobs", type=int, default=64,
+                    help="loop-verification ICP alignments per batch in the separate ICP measurement (0 = skip)")
     ap.add_argument("--traffic-from", default=None,
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
     return ap.parse_args()
@@ -122,6 +124,68 @@ def pmc_traffic(path, kernel):
     return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
 
 
+def icp_bench(torch, slo_amd, pid, a, local, gthreads, reps=3):
+    """ICP alignments/s of slo_icp_align_batch + the lc_corr kernel's roofline."""
+    import numpy as np
+    J = a.icp_jobs
+    cfg = slo_amd.preset(a.preset)
+    cfg.loop_verify = 1
+    P = cfg.max_points
+    raw = slo_amd.gen_batch(pid, a.config_id, 0, J, 0, 1, P, gthreads)[0]   # [J][P][4]
+    fin = np.isfinite(raw[..., :3]).all(axis=2)
+    srcs, tgts = [], []
+    rng = np.random.default_rng(5)
+    for j in range(J):
+        pts = raw[j][fin[j]]
+        tgt = pts[::4]
+        src = pts[::16].copy()
+        yaw, t = rng.uniform(-0.02, 0.02), rng.uniform(-0.3, 0.3, size=3).astype(np.float32)
+        c, s_ = np.float32(np.cos(yaw)), np.float32(np.sin(yaw))
+        x, y = src[:, 0].copy(), src[:, 1].copy()
+        src[:, 0], src[:, 1], src[:, 2] = c * x - s_ * y + t[0], s_ * x + c * y + t[1], src[:, 2] + t[2]
+        srcs.append(src)
+        tgts.append(tgt)
+    ss, ts = max(len(x) for x in srcs), max(len(x) for x in tgts)
+    cfg.loop_archive_points = int(ts)
+    hs = np.zeros((J, ss, 4), np.float32)
+    ht = np.zeros((J, ts, 4), np.float32)
+    for j in range(J):
+        hs[j, :len(srcs[j])] = srcs[j]
+        ht[j, :len(tgts[j])] = tgts[j]
+    dsrc, dtgt = torch.from_numpy(hs).cuda(local), torch.from_numpy(ht).cuda(local)
+    ns = torch.tensor([len(x) for x in srcs], dtype=torch.int32, device=f"cuda:{local}")
+    nt = torch.tensor([len(x) for x in tgts], dtype=torch.int32, device=f"cuda:{local}")
+    ctx = slo_amd.Context(cfg, local, J)
+    run = lambda: ctx.icp_align_batch(dsrc.data_ptr(), ss, ns.data_ptr(), dtgt.data_ptr(), ts, nt.data_ptr())  # noqa: E731
+    res = run()   # warm-up
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        res = run()
+    el = (time.perf_counter() - t0) / reps
+    ctx.timing(True)
+    ctx.timing_reset()
+    res = run()
+    kt = ctx.timing_read()
+    ctx.timing(False)
+    ctx.close()
+    iters = res["iters"].astype(np.int64)
+    nsrc = np.array([len(x) for x in srcs], np.int64)
+    ntgt = np.array([len(x) for x in tgts], np.int64)
+    ms, n = kt.get("lc_corr", (0.0, 0))
+    # per launch: every live job reads its query and writes it back moved
+    # (16 + 16 B) plus the correspondence (8 B); the target once (16 B / point)
+    b = int(((nsrc * 40 + ntgt * 16) * iters).sum())
+    ach = b / (ms / 1e3) / 1e9 if ms > 0 else None
+    return {"metric": "ICP alignments/s (pcl::IterativeClosestPoint::align + getFitnessScore, max 100 iterations)",
+            "value": round(J / el, 2), "jobs": J, "ms_per_batch": round(el * 1e3, 3),
+            "source_points_mean": round(float(nsrc.mean()), 1), "target_points_mean": round(float(ntgt.mean()), 1),
+            "iterations_mean": round(float(iters.mean()), 2), "accepted": int(res["accepted"].sum()),
+            "roofline": {"bound": "hbm", "kernel": "lc_corr", "achieved": round(ach, 2) if ach else None,
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach else None,
+                         "avg_launch_us": round(ms / max(1, n) * 1e3, 2), "launches": int(n)},
+            "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}}
+
+
 def main():
     a = parse()
     import torch
@@ -156,7 +220,9 @@ def main():
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
 
     groups = sdist.group_slices(S, a.groups)
+    free0 = torch.cuda.mem_get_info(local)[0]
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
+    ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     rec_n = ctxs[0].L.slo_record_floats()
     rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
     gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
@@ -257,6 +323,18 @@ def main():
                 "bytes_per_launch": int(b / n) if b is not None else None,
                 "share_of_device_time": round(ms / total_ms, 4)}
 
+    # ---- loop verification (MO:964-1110), measured apart
+    # from the headline (not part of the metric): a batch of --icp-jobs ICP
+    # alignments through slo_icp_align_batch, each a 1/16-subsampled scan
+    # displaced by a loop-closure-sized drift (<= 0.3 m, 0.02 rad) onto every
+    # 4th point of the same scan (~29k points, a voxelised submap's density)
+    icp = None
+    if rank == 0 and a.icp_jobs > 0:
+        for c in ctxs:
+            c.close()
+        ctxs = []
+        icp = icp_bench(torch, slo_amd, pid, a, local, gthreads)
+
     # ---- CPU baseline (oracle = C++ restatement of the reference), rank 0, N = 1
     cpu = None
     if rank == 0 and world == 1 and a.cpu_scans > 0:
@@ -289,7 +367,8 @@ def main():
             "stream_errors": errs,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
             "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
-            "setup_seconds": round(t_gen, 1),
+            "setup_seconds": round(t_gen, 1), "context_hbm_gb": round(ctx_bytes / 2**30, 2),
+            "loop_verify_icp": icp,
         }
         print(json.dumps(out), flush=True)
     for c in ctxs:

@@ -16,7 +16,7 @@
 //   k_lc_gather    submap concatenation, each keyframe in its own pose
 //                  (MO:894-901 / 941-947), chip-wide
 //   vg_run         downSizeFilterHistoryKeyFrames (0.3 m, MO:902 / 948)
-//   grid_build     1 m hash grid over the submap (the ICP "kd-tree")
+//   grid_build     0.5 m hash grid over the submap (the ICP "kd-tree")
 //   k_lc_corr      ICP correspondences: input_transformed advanced by the
 //                  previous increment, exact 1-NN, max distance (chip-wide)
 //   k_lc_solve     one workgroup per stream: double-double correspondence
@@ -36,8 +36,8 @@
 
 namespace slo {
 
-#define SLO_LC_CELL 1.0f   // submap grid cell (m, power of two)
-#define SLO_LC_R 6         // grid walk box radius in cells; farther neighbours: exhaustive scan
+#define SLO_LC_CELL 0.5f   // submap grid cell (m, power of two): ~1-10 points of a 0.3 m voxelised submap
+#define SLO_LC_R 12        // grid walk box radius in cells (6 m); farther neighbours: exhaustive scan
 
 __device__ inline float lc_sqdist(float qx, float qy, float qz, const float4& p) {   // FLANN L2_Simple, d = q - p
     const float d0 = qx - p.x, d1 = qy - p.y, d2 = qz - p.z;
