@@ -58,6 +58,10 @@ struct StreamState {
     int32_t mo_ran, kf_saved, mo_iters, mo_converged;
     int32_t n_corner_map, n_surf_map, n_corner_ds, n_surf_total_ds, n_raw_ds;
     int32_t n_surf_ds, n_outl_ds, n_st, n_cmap_ds, n_smap_ds, n_sel, map_ok;
+    // sin/cos of transformTobeMapped (pointAssociateToMap's cRoll .. tZ),
+    // kept with the pose by mo_prepare / mo_solve (computed once per pose,
+    // not per query)
+    float mo_trig[9];
     // scan context
     int32_t sc_count, sc_tree_n, sc_counter;
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];

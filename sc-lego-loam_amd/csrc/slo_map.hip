@@ -30,6 +30,16 @@ using slo_pose::P4;
 #define ST_STRIDE ((int)(sizeof(StreamState) / sizeof(int32_t)))
 
 // ---------------------------------------------------------------- prepare
+// pointAssociateToMap's sin/cos (MO:521-532) of transformTobeMapped into st.mo_trig
+__device__ inline void mo_store_trig(StreamState& st) {
+    const float* t = st.transformTobeMapped;
+    float* o = st.mo_trig;
+    o[0] = slo_libm::sinf_(t[0]); o[1] = slo_libm::cosf_(t[0]);
+    o[2] = slo_libm::sinf_(t[1]); o[3] = slo_libm::cosf_(t[1]);
+    o[4] = slo_libm::sinf_(t[2]); o[5] = slo_libm::cosf_(t[2]);
+    o[6] = t[3]; o[7] = t[4]; o[8] = t[5];
+}
+
 __global__ void k_mo_prepare(DevView v) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
@@ -46,6 +56,7 @@ __global__ void k_mo_prepare(DevView v) {
     for (int k = 0; k < 6; ++k) st.mo_sum[k] = st.transformSum[k];  // laserOdometryHandler
     slo_pose::associate_to_map(st.mo_sum, st.transformBefMapped, st.transformAftMapped, st.transformIncre,
                                st.transformTobeMapped);
+    mo_store_trig(st);
     // extractSurroundingKeyFrames: recent keyframe deque
     const int nk = st.n_keyframes;
     const int N = v.cfg.surrounding_keyframe_search_num;
@@ -189,15 +200,14 @@ __device__ __constant__ int8_t kMoTermJ[27] = {0, 1, 2, 3, 4, 5, 1, 2, 3, 4, 5, 
 struct MoTrig {
     float srx, crx, sry, cry, srz, crz, tX, tY, tZ;
 };
-__device__ inline MoTrig mo_trig(const StreamState& st) {
-    const float* t = st.transformTobeMapped;
+// the stored sin/cos of transformTobeMapped (StreamState::mo_trig)
+__device__ inline MoTrig mo_trig_of(const float* t) {
     MoTrig g;
-    g.crx = slo_libm::cosf_(t[0]); g.srx = slo_libm::sinf_(t[0]);
-    g.cry = slo_libm::cosf_(t[1]); g.sry = slo_libm::sinf_(t[1]);
-    g.crz = slo_libm::cosf_(t[2]); g.srz = slo_libm::sinf_(t[2]);
-    g.tX = t[3]; g.tY = t[4]; g.tZ = t[5];
+    g.srx = t[0]; g.crx = t[1]; g.sry = t[2]; g.cry = t[3]; g.srz = t[4]; g.crz = t[5];
+    g.tX = t[6]; g.tY = t[7]; g.tZ = t[8];
     return g;
 }
+__device__ inline MoTrig mo_trig(const StreamState& st) { return mo_trig_of(st.mo_trig); }
 __device__ inline P4 mo_query(const DevView& v, int s, const StreamState& st, int q, const MoTrig& g, P4& po) {
     const int nc = st.n_corner_ds;
     const float4 po4 = q < nc ? v.cur_c_ds[(size_t)s * v.cap_less_sharp + q] : v.cur_st_ds[(size_t)s * v.cap_st + (q - nc)];
@@ -422,6 +432,7 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
         slo_la::mul(st.matP_mo, X2, 6, 6, 1, X);
     }
     for (int i = 0; i < 6; ++i) st.transformTobeMapped[i] += X[i];
+    mo_store_trig(st);
     double r0 = X[0] * 57.29578f, r1 = X[1] * 57.29578f, r2 = X[2] * 57.29578f;
     double t0 = X[3] * 100, t1 = X[4] * 100, t2 = X[5] * 100;
     float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);

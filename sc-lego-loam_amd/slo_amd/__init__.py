@@ -244,6 +244,14 @@ class MapOptimization(_Node):
         return {"ran": bool(v.ran), "keyframe_saved": bool(v.keyframe_saved), "n_keyframes": v.n_keyframes,
                 "transform_aft_mapped": np.array(v.transform_aft_mapped[:], np.float32)}
 
+    def performLoopClosure(self):
+        """detectLoopClosure + performLoopClosure (MO:841-1110) minus the GTSAM
+        factors, after this keyframe's SCManager.detectLoopClosureID (context
+        created with cfg.loop_verify = 1).  -> {"RS": record, "SC": record}
+        with the LOOP_DTYPE fields (id, converged, accepted, fitness, T, ...)."""
+        r = self.ctx.loop_closure()
+        return {"RS": r[0], "SC": r[1]}
+
 
 class SCManager:
     """Mirror of the public SCManager API (Scancontext.h:63-73) on stream 0 of
