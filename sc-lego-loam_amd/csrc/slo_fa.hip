@@ -610,6 +610,62 @@ __device__ inline void block_minmax(float& v0, float& v1, float& v2, float& w0, 
     __syncthreads();
 }
 
+// Bitonic sort of the 256 * NE keys key_of(0 .. 256 NE) (padding ~0) by a
+// 256-thread workgroup, result ascending in lds[0 ..): element g = w * 64 NE
+// + e * 64 + lane lives in register e of lane `lane` of wave w, so every
+// stage with a stride below 64 NE runs in registers (in-lane exchanges,
+// cross-lane shuffles) and only the strides spanning waves (at most
+// log2(4) per merge size) go through LDS with barriers.  The network is
+// fully unrolled (constant register indices).
+template <int NE, class KF>
+__device__ inline void ring_sort_regs(unsigned long long* lds, KF&& key_of) {
+    constexpr int WN = 64 * NE, N = 256 * NE;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    unsigned long long k[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) k[e] = key_of(w * WN + e * 64 + lane);
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= WN) {          // partner in another wave
+#pragma unroll
+                for (int e = 0; e < NE; ++e) lds[w * WN + e * 64 + lane] = k[e];
+                __syncthreads();
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const int g = w * WN + e * 64 + lane;
+                    const unsigned long long y = lds[g ^ stride];
+                    const bool take_min = ((g & size) == 0) == ((g & stride) == 0);
+                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+                __syncthreads();
+            } else if (stride >= 64) {   // partner in the same lane
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    if (e & es) continue;
+                    const bool up = ((w * WN + e * 64 + lane) & size) == 0;
+                    const unsigned long long x = k[e], y = k[e | es];
+                    const bool sw = up ? (x > y) : (x < y);
+                    k[e] = sw ? y : x;
+                    k[e | es] = sw ? x : y;
+                }
+            } else {                     // partner in lane ^ stride
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const unsigned long long y = __shfl_xor(k[e], stride, 64);
+                    const bool take_min = (((w * WN + e * 64 + lane) & size) == 0) == ((lane & stride) == 0);
+                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) lds[w * WN + e * 64 + lane] = k[e];
+    __syncthreads();
+}
+
 __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int s = blockIdx.y, ring = blockIdx.x;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
@@ -617,7 +673,7 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int n = v.r_lf_n[rr];
     const float4* in = v.r_lf_scan + rr * C;
     float4* out = v.r_lf_ds + rr * C;
-    __shared__ unsigned long long keys[SLO_DS_MAX];
+    extern __shared__ unsigned long long keys[];   // max(256, pow2 >= horizon_scan) keys (launch)
     __shared__ float sh[64];
     __shared__ int scan[256];
     const float leaf = v.cfg.leaf_less_flat;
@@ -644,31 +700,35 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
     const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
     const int mul1 = divx, mul2 = divx * divy;
-    int npow = 1;
-    while (npow < n) npow <<= 1;
-    for (int i = threadIdx.x; i < npow; i += blockDim.x) {
-        unsigned long long k = ~0ull;
-        if (i < n) {
-            float4 p = in[i];
-            int ijk0 = (int)(floorf(p.x * inv) - (float)minbx);
-            int ijk1 = (int)(floorf(p.y * inv) - (float)minby);
-            int ijk2 = (int)(floorf(p.z * inv) - (float)minbz);
-            unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
-            k = ((unsigned long long)idx << 32) | (unsigned int)i;
-        }
-        keys[i] = k;
-    }
-    __syncthreads();
-    for (int size = 2; size <= npow; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int t = threadIdx.x; t < npow / 2; t += blockDim.x) {
-                int lo = 2 * t - (t & (stride - 1));
-                int hi = lo + stride;
-                bool up = (lo & size) == 0;
-                unsigned long long a = keys[lo], b = keys[hi];
-                if ((a > b) == up) { keys[lo] = b; keys[hi] = a; }
+    auto key_of = [&](int i) -> unsigned long long {
+        if (i >= n) return ~0ull;
+        const float4 p = in[i];
+        const int ijk0 = (int)(floorf(p.x * inv) - (float)minbx);
+        const int ijk1 = (int)(floorf(p.y * inv) - (float)minby);
+        const int ijk2 = (int)(floorf(p.z * inv) - (float)minbz);
+        const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
+        return ((unsigned long long)idx << 32) | (unsigned int)i;
+    };
+    if (n <= 256) ring_sort_regs<1>(keys, key_of);
+    else if (n <= 512) ring_sort_regs<2>(keys, key_of);
+    else if (n <= 1024) ring_sort_regs<4>(keys, key_of);
+    else if (n <= 2048) ring_sort_regs<8>(keys, key_of);
+    else {   // rings longer than 2048 points (horizon_scan > 2048): bitonic in LDS
+        int npow = 1;
+        while (npow < n) npow <<= 1;
+        for (int i = threadIdx.x; i < npow; i += blockDim.x) keys[i] = key_of(i);
+        __syncthreads();
+        for (int size = 2; size <= npow; size <<= 1) {
+            for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                for (int t = threadIdx.x; t < npow / 2; t += blockDim.x) {
+                    int lo = 2 * t - (t & (stride - 1));
+                    int hi = lo + stride;
+                    bool up = (lo & size) == 0;
+                    unsigned long long a = keys[lo], b = keys[hi];
+                    if ((a > b) == up) { keys[lo] = b; keys[hi] = a; }
+                }
+                __syncthreads();
             }
-            __syncthreads();
         }
     }
     // voxel heads -> rank via block scan over contiguous chunks
@@ -748,7 +808,9 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
-    SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), 0, v);
+    int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
+    while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
+    SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());
     return 0;
