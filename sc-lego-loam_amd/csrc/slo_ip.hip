@@ -19,6 +19,7 @@
 // All float math matches the host bit for bit (slo_libm, -ffp-contract=off,
 // correctly rounded sqrtf/division).
 #include "slo_internal.h"
+#include "slo_fastatan.h"
 #include "slo_libm.h"
 #include <float.h>
 
@@ -33,15 +34,33 @@ __device__ inline int wave_max(int x) {
     return x;
 }
 
-// row / column of a finite point (IP:229-246); returns false if rejected
+// atan2f value -> degrees as the reference writes it: atan2(..) * 180 / M_PI
+// (float product, double quotient, narrowed to float)
+__device__ inline float ip_deg(float a) { return (float)((double)(a * 180) / M_PI); }
+// the row (IP:231-233, Q1: truncation, (-1,0) -> 0) and the unwrapped column
+// (IP:235-238) of an elevation / azimuth atan2f value; both monotone in it
+__device__ inline long long ip_row_of(const slo_config& c, float a) {
+    const float rowf = (ip_deg(a) + c.ang_bottom) / c.ang_res_y;
+    return (long long)rowf;
+}
+__device__ inline long long ip_col_of(const slo_config& c, float a) {
+    const double colD = -round(((double)ip_deg(a) - 90.0) / (double)c.ang_res_x) + (double)(c.horizon_scan / 2);
+    return (long long)colD;
+}
+
+// row / column of a finite point (IP:229-246); returns false if rejected.
+// The bins are taken at both ends of the atan2f bracket (slo_fastatan.h);
+// only when they differ is glibc's atan2f itself evaluated.
 __device__ inline bool project_point(const slo_config& c, float4 p, int& row, int& col, float& range) {
-    float verticalAngle = (float)((double)(slo_libm::atan2f_(p.z, sqrtf(p.x * p.x + p.y * p.y)) * 180) / M_PI);
-    float rowf = (verticalAngle + c.ang_bottom) / c.ang_res_y;
-    long long r = (long long)rowf;  // Q1: truncation; (-1,0) -> 0
+    const float h = sqrtf(p.x * p.x + p.y * p.y);
+    float lo, hi;
+    long long r;
+    if (!slo_fast::atan2_bracket(p.z, h, lo, hi) || (r = ip_row_of(c, lo)) != ip_row_of(c, hi))
+        r = ip_row_of(c, slo_libm::atan2f_(p.z, h));
     if (r < 0 || r >= c.n_scan) return false;
-    float horizonAngle = (float)((double)(slo_libm::atan2f_(p.x, p.y) * 180) / M_PI);
-    double colD = -round(((double)horizonAngle - 90.0) / (double)c.ang_res_x) + (double)(c.horizon_scan / 2);
-    long long cc = (long long)colD;
+    long long cc;
+    if (!slo_fast::atan2_bracket(p.x, p.y, lo, hi) || (cc = ip_col_of(c, lo)) != ip_col_of(c, hi))
+        cc = ip_col_of(c, slo_libm::atan2f_(p.x, p.y));
     if (cc >= c.horizon_scan) cc -= c.horizon_scan;
     if (cc < 0 || cc >= c.horizon_scan) return false;
     float rg = sqrtf(p.x * p.x + p.y * p.y + p.z * p.z);
@@ -96,13 +115,17 @@ __global__ void k_ip_project(DevView v) {
 #define IP_LROOT (1 << 30)   // csize flag: the pixel is a tile-local root (k_ip_tile)
 __host__ __device__ inline int ip_tile_cols(int R) { return min(IP_TILE_MAXC, max(1, IP_TILE_PX / R)); }
 
-// edge predicate of labelComponents (IP:411-423)
+// edge predicate of labelComponents (IP:411-423): atan2f(..) > segmentTheta,
+// decided at both ends of the atan2f bracket (slo_fastatan.h) when it can be
 __device__ inline bool seg_edge(const slo_config& c, float r1, float r2, bool horizontal) {
     float d1 = fmaxf(r1, r2), d2 = fminf(r1, r2);
     float sa = horizontal ? c.sin_alpha_x : c.sin_alpha_y;
     float ca = horizontal ? c.cos_alpha_x : c.cos_alpha_y;
-    float angle = slo_libm::atan2f_(d2 * sa, (d1 - d2 * ca));
-    return angle > c.segment_theta;
+    const float y = d2 * sa, x = d1 - d2 * ca;
+    float lo, hi;
+    if (slo_fast::atan2_bracket(y, x, lo, hi) && (lo > c.segment_theta) == (hi > c.segment_theta))
+        return lo > c.segment_theta;
+    return slo_libm::atan2f_(y, x) > c.segment_theta;
 }
 
 // Union-find that always links the larger root under the smaller, so a root
@@ -175,8 +198,19 @@ __global__ void __launch_bounds__(256) k_ip_tile(DevView v) {
         if (lo >= 0 && up >= 0) {
             const float4 a = pts[lo], b = pts[up];
             const float dx = b.x - a.x, dy = b.y - a.y, dz = b.z - a.z;
-            const float angle = (float)((double)(slo_libm::atan2f_(dz, sqrtf(dx * dx + dy * dy)) * 180) / M_PI);
-            g = fabsf(angle - v.cfg.sensor_mount_angle) <= 10 ? 1 : 0;
+            const float h = sqrtf(dx * dx + dy * dy);
+            // fabsf(angle - sensorMountAngle) <= 10 (IP:291) as its two
+            // monotone halves, decided at the atan2f bracket's ends if they agree
+            const float mount = v.cfg.sensor_mount_angle;
+            float lo, hi;
+            bool ok = slo_fast::atan2_bracket(dz, h, lo, hi);
+            const float ul = ip_deg(lo) - mount, uh = ip_deg(hi) - mount;
+            if (ok && (ul >= -10) == (uh >= -10) && (ul <= 10) == (uh <= 10)) {
+                g = (ul >= -10 && ul <= 10) ? 1 : 0;
+            } else {
+                const float angle = ip_deg(slo_libm::atan2f_(dz, h));
+                g = fabsf(angle - mount) <= 10 ? 1 : 0;
+            }
         }
         l_pair[i * TC + jj] = (int8_t)g;
     }

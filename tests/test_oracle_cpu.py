@@ -109,3 +109,14 @@ def test_gpu_sincos_matches_sinf_cosf(tmp_path):
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-mfma", "-o", str(exe), src], check=True)
     bad, cases = map(int, subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split())
     assert cases > 700000 and bad == 0
+
+
+def test_atan2_bracket_contains_glibc_atan2f(tmp_path):
+    # the image projection's fast path (slo_fastatan.h) decides bins at both
+    # ends of a polynomial bracket; it must contain glibc's atan2f everywhere
+    exe = tmp_path / "atan_bracket_check"
+    src = os.path.join(HERE, "cpp", "atan_bracket_check.cpp")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-o", str(exe), src], check=True)
+    bad, cases, worst = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
+    assert int(cases) > 40_000_000 and int(bad) == 0
+    assert float(worst) < 1e-6   # 2.5e-6 half-width: > 2x margin
