@@ -44,7 +44,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--streams", type=int, default=512, help="streams per GPU")
-    ap.add_argument("--groups", type=int, default=2,
+    ap.add_argument("--groups", type=int, default=3,
                     help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
     ap.add_argument("--preset", default="hdl64_1800")
     ap.add_argument("--keyframe-cap", type=int, default=32768,
