@@ -223,6 +223,7 @@ def main():
     free0 = torch.cuda.mem_get_info(local)[0]
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
     ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
+    n_ctx = len(ctxs)
     rec_n = ctxs[0].L.slo_record_floats()
     rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
     gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
@@ -358,7 +359,7 @@ def main():
             "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
             "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10",
-                       "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": len(ctxs),
+                       "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
                        "scans_per_step": S * world,
                        "sc_history_seed": a.history, "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,

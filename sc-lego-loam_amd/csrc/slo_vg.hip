@@ -375,18 +375,33 @@ __global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* 
     }
 }
 
+// cnt / cur back to zero for the next build: only the buckets the points hit
+// are non-zero, so clearing those replaces two memsets of the whole [S][T + 1]
+// arrays (grid_alloc zeroes them once)
+__global__ void k_grid_clear(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
+                             int32_t* cnt, int32_t* cur) {
+    const int s = blockIdx.y;
+    const int m = n[(size_t)s * n_stride];
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const float4 p = pts[(size_t)s * stride + i];
+        const size_t b = (size_t)s * (T + 1) + grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
+        cnt[b] = 0;
+        cur[b] = 0;
+    }
+}
+
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride) {
     const int S = ctx->S;
     const float inv = 1.0f / g.cell;
     const size_t nb = (size_t)S * (g.T + 1);   // [S][T + 1]: a zero bucket ends each stream
-    SLO_CHECK(hipMemsetAsync(g.cnt, 0, sizeof(int32_t) * nb, ctx->stream));
-    SLO_CHECK(hipMemsetAsync(g.cur, 0, sizeof(int32_t) * nb, ctx->stream));
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
     SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
     size_t tb = g.temp_bytes;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)nb, ctx->stream));
     SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
                g.off, g.cur, g.ent, g.ent_stride);
+    SLO_LAUNCH(ctx, "grid_clear", k_grid_clear, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt,
+               g.cur);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
@@ -406,6 +421,8 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) 
     SLO_CHECK(hipMalloc(&g.cnt, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.cur, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.off, sizeof(int32_t) * nb));
+    SLO_CHECK(hipMemset(g.cnt, 0, sizeof(int32_t) * nb));   // kept zero between builds (k_grid_clear)
+    SLO_CHECK(hipMemset(g.cur, 0, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.ent, sizeof(float4) * (size_t)S * ent_stride));
     size_t tb = 0;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g.cnt, g.off, (int)nb, ctx->stream));
