@@ -390,10 +390,64 @@ __global__ void k_grid_clear(const float4* pts, size_t stride, const int32_t* n,
     }
 }
 
+// Small grids (T <= SLO_GRID_LDS_T buckets): one workgroup per stream builds
+// the whole grid in LDS — bucket counts by LDS atomics, the stream's
+// exclusive scan as a block scan (written to off), then the scatter with LDS
+// rank counters — with no device-scope atomics and no global scan.
+#define SLO_GRID_LDS_T 32768
+__global__ void __launch_bounds__(1024) k_grid_build_lds(const float4* pts, size_t stride, const int32_t* n,
+                                                         int n_stride, int T, float inv, int32_t* off, float4* ent,
+                                                         size_t ent_stride) {
+    __shared__ int cnt[SLO_GRID_LDS_T];
+    __shared__ int wsum[16];
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int m = n[(size_t)s * n_stride];
+    const float4* P = pts + (size_t)s * stride;
+    int32_t* O = off + (size_t)s * (T + 1);
+    for (int k = tid; k < T; k += 1024) cnt[k] = 0;
+    __syncthreads();
+    for (int i = tid; i < m; i += 1024) {
+        const float4 p = P[i];
+        atomicAdd(&cnt[grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T)], 1);
+    }
+    __syncthreads();
+    const int per = (T + 1023) / 1024, k0 = tid * per, k1 = min(T, k0 + per);
+    int sum = 0;
+    for (int k = k0; k < k1; ++k) sum += cnt[k];
+    int incl = sum;   // block exclusive scan of the per-thread sums
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int run = incl - sum;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+    for (int k = k0; k < k1; ++k) {
+        const int c = cnt[k];
+        cnt[k] = run;   // bucket start, then the scatter's running position
+        O[k] = run;
+        run += c;
+    }
+    if (tid == 1023) O[T] = run;   // == m: the stream's closing (empty) bucket
+    __syncthreads();
+    for (int i = tid; i < m; i += 1024) {
+        const float4 p = P[i];
+        const int b = (int)grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
+        ent[(size_t)s * ent_stride + atomicAdd(&cnt[b], 1)] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+    }
+}
+
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride) {
     const int S = ctx->S;
     const float inv = 1.0f / g.cell;
     const size_t nb = (size_t)S * (g.T + 1);   // [S][T + 1]: a zero bucket ends each stream
+    if (g.T <= SLO_GRID_LDS_T) {
+        SLO_LAUNCH(ctx, "grid_build_lds", k_grid_build_lds, dim3(S), dim3(1024), 0, pts, stride, n, n_stride, g.T, inv,
+                   g.off, g.ent, g.ent_stride);
+        SLO_CHECK(hipGetLastError());
+        return 0;
+    }
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
     SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
     size_t tb = g.temp_bytes;
