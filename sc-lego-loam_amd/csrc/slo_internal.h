@@ -276,15 +276,20 @@ __constant__ GridRows<R> kGridRows = GridRows<R>();
 // initial radius; the row walk then skips that cell (each point is still
 // visited once).
 #define GBALL_UNROLL 4
+// grid_ball_rows: the same walk restricted to rows k = k0, k0 + ks, ... < k1
+// (and the probe cell only if `probe`), so several lanes can share one query
+// (each bound by its own best; correct because a point a lane skips is
+// farther than that lane's best, hence than the joint best).
 template <int R, int U = GBALL_UNROLL, class B, class F>
-__device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
+__device__ inline void grid_ball_rows(const GridView& g, int s, float qx, float qy, float qz, int k0, int k1, int ks,
+                                      bool probe, B&& bound, F&& f) {
     const float inv = g.inv, cell = g.cell, c2 = cell * cell;
     const int cx = grid_cell(qx, inv), cy = grid_cell(qy, inv), cz = grid_cell(qz, inv);
     const size_t gb = (size_t)s * (g.T + 1);
     const int base = g.off[gb];
     const float4* E = g.ent + (size_t)s * g.es;
     static_assert(GridRows<R>().dy[0] == 0 && GridRows<R>().dz[0] == 0, "row 0 is the probed cell's row");
-    {
+    if (probe) {
         const int h0 = (int)grid_hash(cx, cy, cz, g.T);
         const int p0 = g.off[gb + h0] - base, p1 = g.off[gb + h0 + 1] - base;
         for (int e = p0; e < p1; e += U) {
@@ -299,7 +304,7 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
             }
         }
     }
-    for (int k = 0; k < GridRows<R>::N; ++k) {
+    for (int k = k0; k < min(k1, GridRows<R>::N); k += ks) {
         const float b = bound();
         if ((float)kGridRows<R>.gap[k] * c2 > b) break;
         const int dy = kGridRows<R>.dy[k], dz = kGridRows<R>.dz[k];
@@ -335,6 +340,12 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
             e0 = 0; e1 = f1;
         }
     }
+}
+
+
+template <int R, int U = GBALL_UNROLL, class B, class F>
+__device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
+    grid_ball_rows<R, U>(g, s, qx, qy, qz, 0, GridRows<R>::N, 1, true, bound, f);
 }
 
 // ---- loop-closure verification (slo_lc.hip; mapOptmization.cpp:841-1110)
