@@ -524,9 +524,17 @@ __global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
     const int i = active ? v.sharp_perm[(size_t)s * v.cap_sharp + pos] : 0;
     const float gate = v.cfg.nearest_feature_search_sq_dist;
     const int R = v.cfg.n_scan;
-    float tc[6];
-    for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-    const P4 sel = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
+    // TransformToStart of the 64 queries once (wave 0), shared through LDS
+    __shared__ float4 s_sel[64];
+    if (w == 0) {
+        float tc[6];
+        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+        const P4 q = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
+        s_sel[lane] = make_float4(q.x, q.y, q.z, q.w);
+    }
+    __syncthreads();
+    const float4 sel4 = s_sel[lane];
+    const P4 sel{sel4.x, sel4.y, sel4.z, sel4.w};
     const bool fin = active && isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z);
     // the workgroup's x-window (every wave computes the same one)
     float xmin = fin ? sel.x : FLT_MAX, xmax = fin ? sel.x : -FLT_MAX;
