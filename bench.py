@@ -200,6 +200,13 @@ def main():
     torch.cuda.set_device(local)
     gather = world > 1 or a.force_gather
     if gather:
+        if "RANK" not in os.environ:   # --force-gather outside torch.distributed.run: a 1-rank group
+            import socket
+            with socket.socket() as sk:
+                sk.bind(("127.0.0.1", 0))
+                port = sk.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                              MASTER_PORT=str(port))
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = slo_amd.preset(a.preset)
     cfg.keyframe_cloud_cap = a.keyframe_cap

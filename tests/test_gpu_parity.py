@@ -53,6 +53,7 @@ def _tools_path():
     (0, 1, 3, 18),    # C1 VLP-16
     (4, 2, 2, 10),    # OS1-64 as shipped (64 x 1024)
     (2, 2, 1, 6),     # VLS-128 (C5 sensor)
+    (7, 5, 2, 10),    # C5 dense 128 x 2048 (262 k points per scan), two mapping rounds
 ])
 def test_pipeline_bit_exact(preset, config, streams, scans):
     _torch()
