@@ -287,7 +287,7 @@ static int ensure_ws(slo_ctx* ctx, size_t items) {
 }
 
 template <class K>
-static int vg_sorted(slo_ctx* ctx, const float4* in, size_t in_stride, int total, int vbits, int sbits,
+static int vg_sorted(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, int total, int vbits, int sbits,
                      const VgOut& o) {
     MapWs& w = ctx->mws;
     const int S = ctx->S, T = 256;
@@ -298,10 +298,11 @@ static int vg_sorted(slo_ctx* ctx, const float4* in, size_t in_stride, int total
                w.vals);
     size_t tb = w.temp_bytes;
     hipEvent_t ev = nullptr;
-    if (ctx->timing) timing_begin(ctx, "vg_sort", &ev);
+    const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
+    if (ctx->timing) timing_begin(ctx, sort_name.c_str(), &ev);
     SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys, keys2, w.vals, w.vals2, total, 0, vbits + sbits,
                                                  ctx->stream));
-    if (ctx->timing) timing_end(ctx, "vg_sort", ev);
+    if (ctx->timing) timing_end(ctx, sort_name.c_str(), ev);
     const int gi = (total + T - 1) / T;
     SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits,
                w.flags);
@@ -337,15 +338,14 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     if (int r = ensure_ws(ctx, (size_t)total + 1)) return r;
     if (total > 0) {
         const VgOut o{out, out_stride, out_cap};
-        const int r = vbits + sbits <= 32 && vbits < 32 ? vg_sorted<unsigned int>(ctx, in, in_stride, total, vbits, sbits, o)
-                                          : vg_sorted<unsigned long long>(ctx, in, in_stride, total, vbits, sbits, o);
+        const int r = vbits + sbits <= 32 && vbits < 32 ? vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, sbits, o)
+                                          : vg_sorted<unsigned long long>(ctx, tag, in, in_stride, total, vbits, sbits, o);
         if (r) return r;
     } else {
         SLO_CHECK(hipMemsetAsync(w.rank, 0, sizeof(int), ctx->stream));
     }
     SLO_LAUNCH(ctx, "vg_count", k_vg_count, dim3((S + 63) / 64), dim3(64), 0, w.rank, w.off, S, d_nout, nout_stride,
                out_cap, w.errflag);
-    (void)tag;
     SLO_CHECK(hipGetLastError());
     return 0;
 }
