@@ -170,6 +170,65 @@ int slo_timing_enable(slo_ctx* ctx, int enable);
 int slo_timing_read(slo_ctx* ctx, char* names_buf, size_t buf_bytes, double* total_ms, int64_t* launches, int cap);
 int slo_timing_reset(slo_ctx* ctx);
 
+/* ---------------------------------------------------------------- wire format
+ * sensor_msgs/PointCloud2 -> pcl::PointCloud<PointXYZI>, the conversion of
+ * ImageProjection::copyPointCloud (imageProjection.cpp:167,
+ * pcl::fromROSMsg).  PCL's field mapping (pcl/conversions.h FieldMapper /
+ * FieldMatches): each of x, y, z, intensity takes the FIRST message field of
+ * the same name whose datatype is FLOAT32 (7) and whose count is 1 or 0; a
+ * field with no match stays 0 (PointXYZI's constructor) — e.g. an intensity
+ * sent as UINT16 reads as 0, exactly like the reference.  Point (r, c) is at
+ * data + r * row_step + c * point_step; is_bigendian is not looked at (PCL
+ * copies bytes as they are).  NaN removal (IP:170) is part of the projection. */
+#define SLO_PF_INT8 1
+#define SLO_PF_UINT8 2
+#define SLO_PF_INT16 3
+#define SLO_PF_UINT16 4
+#define SLO_PF_INT32 5
+#define SLO_PF_UINT32 6
+#define SLO_PF_FLOAT32 7
+#define SLO_PF_FLOAT64 8
+
+typedef struct slo_pc2_field {   /* sensor_msgs/PointField */
+    const char* name;
+    uint32_t offset;
+    uint8_t datatype;
+    uint32_t count;
+} slo_pc2_field;
+
+typedef struct slo_pc2 {         /* sensor_msgs/PointCloud2 (header omitted: t_scan is passed separately) */
+    uint32_t height, width;
+    const slo_pc2_field* fields;
+    int32_t n_fields;
+    uint8_t is_bigendian;
+    uint32_t point_step, row_step;
+    const uint8_t* data;
+    size_t data_bytes;
+    uint8_t is_dense;
+} slo_pc2;
+
+/* byte offsets of x, y, z, intensity inside a point, -1 = no matching field */
+typedef struct slo_pc2_layout {
+    uint32_t point_step;
+    int32_t off_x, off_y, off_z, off_intensity;
+} slo_pc2_layout;
+
+/* the field mapping alone; SLO_E_ARG if a matched field does not fit in point_step */
+int slo_pc2_layout_of(const slo_pc2* msg, slo_pc2_layout* out);
+/* fromROSMsg into host (x,y,z,intensity) float4s; *n_out = width * height.
+ * SLO_E_CAPACITY (with *n_out set) when cap_points is too small, SLO_E_ARG
+ * when data_bytes cannot hold the last point. */
+int slo_pc2_to_xyzi(const slo_pc2* msg, float* out_xyzi, size_t cap_points, size_t* n_out);
+/* ImageProjection::cloudHandler (IP:181) taking the message itself */
+int slo_image_projection_pc2(slo_ctx* ctx, const slo_pc2* msg, slo_seg_view* out);
+/* batched, on the device: n_streams messages of one point layout, message s
+ * at d_bytes + s * msg_stride with d_dims[3 s .. 3 s + 2] = (width, height,
+ * row_step); writes the d_points / d_counts of slo_batch_image_projection.
+ * A message of more than cfg.max_points points keeps its first max_points
+ * (the context's capacity; bit 8 of slo_get(.., "err") is set).  Asynchronous. */
+int slo_batch_pc2_unpack(slo_ctx* ctx, const uint8_t* d_bytes, size_t msg_stride, const int32_t* d_dims,
+                         const slo_pc2_layout* layout, void* d_points, int32_t* d_counts);
+
 /* synthetic stream generator (sc-lego-loam_amd/csrc/slo_gen.h), host side */
 int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float* out_xyzi);
 /* n_streams x n_scans scans, layout [scan][stream][max_points][4], host threads */

@@ -201,6 +201,7 @@ struct DevView {
 #define SLO_ERR_KEYFRAMES 1     // keyframe pose history full: keyframe dropped
 #define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
 #define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud
+#define SLO_ERR_INPUT 8         // slo_batch_pc2_unpack: a message exceeded max_points
 
 // Locality-preserving bucket of cell (x, y, z): x-adjacent cells get adjacent
 // buckets, so a ring walk reads each row of cells' bucket words from one cache

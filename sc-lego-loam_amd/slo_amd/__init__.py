@@ -18,6 +18,7 @@ import numpy as np
 
 from . import _abi
 from ._abi import SloConfig, SegView, FaView, MapView
+from . import wire
 
 PRESETS = {
     "vlp16": 0, "hdl32": 1, "vls128": 2, "os1_16": 3, "os1_64": 4,
@@ -107,6 +108,13 @@ class Context:
     # batched, device pointers (int addresses)
     def batch_image_projection(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_image_projection(self.h, d_pts, d_cnt), "slo_batch_image_projection")
+
+    def batch_pc2_unpack(self, d_bytes, msg_stride, d_dims, layout, d_pts, d_cnt):
+        """slo_batch_pc2_unpack: one raw PointCloud2 payload per stream (device
+        bytes, message s at s * msg_stride, d_dims int32 [S][3] = width,
+        height, row_step) -> the d_pts / d_cnt of batch_image_projection."""
+        self._ok(self.L.slo_batch_pc2_unpack(self.h, d_bytes, msg_stride, d_dims, ctypes.byref(layout), d_pts,
+                                             d_cnt), "slo_batch_pc2_unpack")
 
     def batch_feature_association(self):
         self._ok(self.L.slo_batch_feature_association(self.h), "slo_batch_feature_association")
@@ -202,10 +210,17 @@ class ImageProjection(_Node):
     contents as numpy arrays."""
 
     def cloudHandler(self, points_xyzi):
-        pts = np.ascontiguousarray(points_xyzi, np.float32)
+        """points_xyzi: (n, 4) float32 array, or a wire.PointCloud2 message
+        (converted by pcl::fromROSMsg rules inside libslo, IP:167)."""
         v = SegView()
-        self.ctx._ok(self.ctx.L.slo_image_projection(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
-                                                     ctypes.byref(v)), "slo_image_projection")
+        if isinstance(points_xyzi, wire.PointCloud2):
+            m = wire._CMsg(points_xyzi)
+            self.ctx._ok(self.ctx.L.slo_image_projection_pc2(self.ctx.h, ctypes.byref(m.c), ctypes.byref(v)),
+                         "slo_image_projection_pc2")
+        else:
+            pts = np.ascontiguousarray(points_xyzi, np.float32)
+            self.ctx._ok(self.ctx.L.slo_image_projection(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
+                                                         ctypes.byref(v)), "slo_image_projection")
         R = self.ctx.cfg.n_scan
         return {
             "seg_pts": _arr(v.segmented, v.n_segmented, np.float32, 4),

@@ -56,6 +56,25 @@ class SegView(ctypes.Structure):
                 ("n_outlier", ctypes.c_int32), ("outlier", ctypes.c_void_p)]
 
 
+class Pc2Field(ctypes.Structure):
+    """slo_pc2_field (include/slo_abi.h) = sensor_msgs/PointField"""
+    _fields_ = [("name", ctypes.c_char_p), ("offset", ctypes.c_uint32), ("datatype", ctypes.c_uint8),
+                ("count", ctypes.c_uint32)]
+
+
+class Pc2(ctypes.Structure):
+    """slo_pc2 (include/slo_abi.h) = sensor_msgs/PointCloud2 without the header"""
+    _fields_ = [("height", ctypes.c_uint32), ("width", ctypes.c_uint32), ("fields", ctypes.POINTER(Pc2Field)),
+                ("n_fields", ctypes.c_int32), ("is_bigendian", ctypes.c_uint8), ("point_step", ctypes.c_uint32),
+                ("row_step", ctypes.c_uint32), ("data", ctypes.c_void_p), ("data_bytes", ctypes.c_size_t),
+                ("is_dense", ctypes.c_uint8)]
+
+
+class Pc2Layout(ctypes.Structure):
+    _fields_ = [("point_step", ctypes.c_uint32), ("off_x", ctypes.c_int32), ("off_y", ctypes.c_int32),
+                ("off_z", ctypes.c_int32), ("off_intensity", ctypes.c_int32)]
+
+
 class FaView(ctypes.Structure):
     _fields_ = [("n_sharp", ctypes.c_int32), ("n_less_sharp", ctypes.c_int32), ("n_flat", ctypes.c_int32),
                 ("n_less_flat", ctypes.c_int32), ("sharp", ctypes.c_void_p), ("less_sharp", ctypes.c_void_p),
@@ -76,6 +95,7 @@ EXPORTS = [
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
+    "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
 ]
 
 
@@ -132,6 +152,10 @@ def lib():
     L.slo_sc_make_and_save.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
     L.slo_batch_sc_make.argtypes = [P, P, P]
     L.slo_pack_records.argtypes = [P, P]
+    L.slo_pc2_layout_of.argtypes = [ctypes.POINTER(Pc2), ctypes.POINTER(Pc2Layout)]
+    L.slo_pc2_to_xyzi.argtypes = [ctypes.POINTER(Pc2), P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+    L.slo_image_projection_pc2.argtypes = [P, ctypes.POINTER(Pc2), ctypes.POINTER(SegView)]
+    L.slo_batch_pc2_unpack.argtypes = [P, P, ctypes.c_size_t, P, ctypes.POINTER(Pc2Layout), P, P]
     L.slo_record_floats.argtypes = []
     _LIB = L
     return L
