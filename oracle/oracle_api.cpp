@@ -187,6 +187,17 @@ int oracle_umeyama(const float* src, const float* dst, int n, float* T) {
 }
 // JacobiSVD<Matrix3d> of a row-major 3x3
 int oracle_svd3(const double* A, double* U, double* S, double* V) { return jacobi_svd3(A, U, S, V) ? 0 : -1; }
+// slo_libm_d.h elementwise: which = 0 sin, 1 cos, 2 atan2(a, b), 3 asin
+void oracle_libm_d(int which, const double* a, const double* b, double* out, int n) {
+    for (int i = 0; i < n; ++i)
+        out[i] = which == 0 ? slo_libm::sin_d(a[i]) : which == 1 ? slo_libm::cos_d(a[i])
+               : which == 2 ? slo_libm::atan2_d(a[i], b[i]) : slo_libm::asin_d(a[i]);
+}
+// the mapping node's angle round trips (oracle_tf.h): which = 0 tf hand-off, 1 keyframe estimate
+void oracle_pose_roundtrip(int which, const float* in, float* out) {
+    if (which == 0) odom_handoff(in, out);
+    else keyframe_estimate(in, out);
+}
 
 // ---- SC unit entry points (pure functions over given descriptors)
 double oracle_sc_distance(const slo_config* cfg, const double* sc1, const double* sc2, int* shift) {

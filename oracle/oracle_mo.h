@@ -15,6 +15,7 @@
 #pragma once
 
 #include "oracle_sc.h"
+#include "oracle_tf.h"
 #include <deque>
 
 namespace oracle {
@@ -373,12 +374,14 @@ struct MapOptimization {
         if (sqrtf(dx * dx + dy * dy + dz * dz) < 0.3) saveThisKeyFrame = false;
         if (!saveThisKeyFrame && !keyPoses.empty()) return;
         previousRobotPosPoint = currentRobotPosPoint;
-        const float* est;  // iSAM2 estimate of the new node == its initial value
+        // iSAM2 estimate of the new node == its initial value, read back
+        // through Rot3::RzRyRx -> pitch()/yaw()/roll() (oracle_tf.h)
+        float est[6];
         if (keyPoses.empty()) {
             for (int i = 0; i < 6; ++i) transformLast[i] = transformTobeMapped[i];
-            est = transformTobeMapped;
+            keyframe_estimate(transformTobeMapped, est);
         } else {
-            est = transformAftMapped;
+            keyframe_estimate(transformAftMapped, est);
         }
         Pose6 p6{est[3], est[4], est[5], est[0], est[1], est[2]};
         keyPoses.push_back(p6);
@@ -401,7 +404,7 @@ struct MapOptimization {
              const float* raw, int n_raw, double t) {
         ran = false;
         saved_keyframe = false;
-        for (int i = 0; i < 6; ++i) transformSum[i] = odomSum[i];
+        odom_handoff(odomSum, transformSum);   // tf quaternion round trip (FA:1728 -> MO:658-666, Q18)
         timeLaserOdometry = t;
         if (!(t - timeLastProcessing >= cfg.mapping_process_interval)) return false;
         timeLastProcessing = t;

@@ -92,6 +92,8 @@ def lib():
                                        ctypes.c_int, ctypes.c_void_p]
         L.oracle_umeyama.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
+        L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 
@@ -160,6 +162,14 @@ def svd3(A):
     U, S, V = np.zeros((3, 3)), np.zeros(3), np.zeros((3, 3))
     rc = lib().oracle_svd3(A.ctypes.data, U.ctypes.data, S.ctypes.data, V.ctypes.data)
     return (U, S, V) if rc == 0 else None
+
+
+def pose_roundtrip(t6, which):
+    """which = "odom": FA:1728 -> MO:658 tf round trip; "keyframe": Rot3 RzRyRx -> pitch/yaw/roll (MO:1588-1601)"""
+    a = np.ascontiguousarray(t6, np.float32)
+    out = np.zeros(6, np.float32)
+    lib().oracle_pose_roundtrip(0 if which == "odom" else 1, a.ctypes.data, out.ctypes.data)
+    return out
 
 
 class SCSession:

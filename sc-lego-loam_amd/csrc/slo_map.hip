@@ -53,7 +53,7 @@ __global__ void k_mo_prepare(DevView v) {
     st.kf_saved = 0;
     st.mo_iters = 0;
     st.mo_converged = 0;
-    for (int k = 0; k < 6; ++k) st.mo_sum[k] = st.transformSum[k];  // laserOdometryHandler
+    slo_pose::odom_handoff(st.transformSum, st.mo_sum);   // laserOdometryHandler, via the tf round trip
     slo_pose::associate_to_map(st.mo_sum, st.transformBefMapped, st.transformAftMapped, st.transformIncre,
                                st.transformTobeMapped);
     mo_store_trig(st);
@@ -498,10 +498,11 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
             if ((saveThis || st.n_keyframes == 0) && st.n_keyframes < v.KFMAX) {
                 st.prevPos[0] = cx; st.prevPos[1] = cy; st.prevPos[2] = cz;
                 float est[6];
-                if (st.n_keyframes == 0) {
-                    for (int i = 0; i < 6; ++i) { st.transformLast[i] = st.transformTobeMapped[i]; est[i] = st.transformTobeMapped[i]; }
+                if (st.n_keyframes == 0) {   // iSAM2 estimate = initial value, through Rot3
+                    for (int i = 0; i < 6; ++i) st.transformLast[i] = st.transformTobeMapped[i];
+                    slo_pose::keyframe_estimate(st.transformTobeMapped, est);
                 } else {
-                    for (int i = 0; i < 6; ++i) est[i] = st.transformAftMapped[i];
+                    slo_pose::keyframe_estimate(st.transformAftMapped, est);
                 }
                 pose[0] = est[3]; pose[1] = est[4]; pose[2] = est[5];
                 pose[3] = est[0]; pose[4] = est[1]; pose[5] = est[2];

@@ -8,9 +8,12 @@
 //   accumulate_rotation featureAssociation.cpp:1015-1032
 //   integrate           featureAssociation.cpp:1697-1725
 //   associate_to_map    mapOptmization.cpp:397-482
+//   odom_handoff        featureAssociation.cpp:1728-1734 -> mapOptmization.cpp:658-666
+//   keyframe_estimate   mapOptmization.cpp:1545-1556, 1588-1601
 #pragma once
 
 #include "slo_libm.h"
+#include "slo_libm_d.h"
 
 #if defined(__HIPCC__)
 #define SLO_P_HD __host__ __device__ inline
@@ -220,6 +223,96 @@ SLO_P_HD void associate_to_map(const float* sum, const float* bef, const float* 
     tbm[3] = aft[3] - (cosf_(tbm[1]) * x2 + sinf_(tbm[1]) * z2);
     tbm[4] = aft[4] - y2;
     tbm[5] = aft[5] - (-sinf_(tbm[1]) * x2 + cosf_(tbm[1]) * z2);
+}
+
+// ---------------------------------------------------------------- f64 angle round trips
+// The mapping node never sees FA's float angles directly: the odometry
+// crosses a tf quaternion (createQuaternionMsgFromRollPitchYaw -> Matrix3x3
+// getRPY) and every keyframe pose a GTSAM Rot3 (RzRyRx -> pitch/yaw/roll).
+// Both are identities inside (-pi, pi] and wrap outside, so a heading that
+// has turned past pi reaches mapping wrapped, as in the reference.  Double
+// evaluation order as in tf's LinearMath and GTSAM's Rot3M/Rot3 (RQ); the
+// double sin/cos/atan2/asin are slo_libm_d.h's, shared with the oracle, so
+// the float casts agree bit for bit even where a tiny angle exposes the last
+// double bit.
+
+// tf::Quaternion::setRPY(roll, pitch, yaw) -> (x, y, z, w)
+SLO_P_HD void tf_quat_rpy(double roll, double pitch, double yaw, double q[4]) {
+    const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
+    const double cy = slo_libm::cos_d(hy), sy = slo_libm::sin_d(hy);
+    const double cp = slo_libm::cos_d(hp), sp = slo_libm::sin_d(hp);
+    const double cr = slo_libm::cos_d(hr), sr = slo_libm::sin_d(hr);
+    q[0] = sr * cp * cy - cr * sp * sy;
+    q[1] = cr * sp * cy + sr * cp * sy;
+    q[2] = cr * cp * sy - sr * sp * cy;
+    q[3] = cr * cp * cy + sr * sp * sy;
+}
+
+// Matrix3x3(q).getRPY(roll, pitch, yaw): setRotation, then getEulerYPR solution 1
+SLO_P_HD void tf_rpy_of(const double q[4], double& roll, double& pitch, double& yaw) {
+    const double x = q[0], y = q[1], z = q[2], w = q[3];
+    const double k = 2.0 / (x * x + y * y + z * z + w * w);
+    const double xs = x * k, ys = y * k, zs = z * k;
+    const double r00 = 1.0 - (y * ys + z * zs), r01 = x * ys - w * zs, r02 = x * zs + w * ys;
+    const double r10 = x * ys + w * zs;
+    const double r20 = x * zs - w * ys, r21 = y * zs + w * xs, r22 = 1.0 - (x * xs + y * ys);
+    if (fabs(r20) >= 1.0) {   // pitch at +-90 deg
+        yaw = 0.0;
+        const double delta = slo_libm::atan2_d(r01, r02);
+        pitch = r20 > 0 ? M_PI / 2.0 : -M_PI / 2.0;
+        roll = (r20 > 0 ? pitch : -pitch) + delta;
+        return;
+    }
+    pitch = -slo_libm::asin_d(r20);
+    const double c = slo_libm::cos_d(pitch);
+    roll = slo_libm::atan2_d(r21 / c, r22 / c);
+    yaw = slo_libm::atan2_d(r10 / c, r00 / c);
+}
+
+// laserOdometryHandler's transformSum from FA's (publishOdometry's message
+// carries (-q.y, -q.z, q.x, q.w); the handler's Quaternion(o.z, -o.x, -o.y,
+// o.w) is q again)
+SLO_P_HD void odom_handoff(const float ts[6], float out[6]) {
+    double q[4], r, p, y;
+    tf_quat_rpy((double)ts[2], (double)(-ts[0]), (double)(-ts[1]), q);
+    tf_rpy_of(q, r, p, y);
+    out[0] = (float)(-p);
+    out[1] = (float)(-y);
+    out[2] = (float)r;
+    for (int i = 3; i < 6; ++i) out[i] = ts[i];
+}
+
+// row-major A * B, entries summed left to right (Eigen's 3x3 coefficient product)
+SLO_P_HD void mat3_mul(const double* A, const double* B, double* C) {
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) C[3 * i + j] = (A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j]) + A[3 * i + 2] * B[6 + j];
+}
+
+// Pose3(Rot3::RzRyRx(t[2], t[0], t[1]), ..) read back with pitch()/yaw()/roll()
+SLO_P_HD void keyframe_estimate(const float t[6], float out[6]) {
+    const double ax = (double)t[2], ay = (double)t[0], az = (double)t[1];
+    const double cx = slo_libm::cos_d(ax), sx = slo_libm::sin_d(ax);
+    const double cy = slo_libm::cos_d(ay), sy = slo_libm::sin_d(ay);
+    const double cz = slo_libm::cos_d(az), sz = slo_libm::sin_d(az);
+    const double ssx = sx * sy, csx = cx * sy;
+    const double A[9] = {cy * cz, -(cx * sz) + ssx * cz, sx * sz + csx * cz,
+                         cy * sz, cx * cz + ssx * sz,    -(sx * cz) + csx * sz,
+                         -sy,     sx * cy,               cx * cy};
+    // RQ (Rot3.cpp): peel Rx, then Ry, then Rz
+    const double rx = -slo_libm::atan2_d(-A[7], A[8]);
+    const double c1 = slo_libm::cos_d(-rx), s1 = slo_libm::sin_d(-rx);
+    const double Qx[9] = {1, 0, 0, 0, c1, -s1, 0, s1, c1};
+    double B[9], C[9];
+    mat3_mul(A, Qx, B);
+    const double ry = -slo_libm::atan2_d(B[6], B[8]);
+    const double c2 = slo_libm::cos_d(-ry), s2 = slo_libm::sin_d(-ry);
+    const double Qy[9] = {c2, 0, s2, 0, 1, 0, -s2, 0, c2};
+    mat3_mul(B, Qy, C);
+    const double rz = -slo_libm::atan2_d(-C[3], C[4]);
+    out[0] = (float)ry;
+    out[1] = (float)rz;
+    out[2] = (float)rx;
+    for (int i = 3; i < 6; ++i) out[i] = t[i];
 }
 
 }  // namespace slo_pose

@@ -21,6 +21,34 @@ def test_libm_restatement_matches_glibc():
         assert O.lib().oracle_libm_selftest(300000, seed) == 0
 
 
+def _libm_d(which, a, b=None):
+    import ctypes  # noqa: F401
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(a if b is None else b, np.float64)
+    out = np.zeros_like(a)
+    O.lib().oracle_libm_d(which, a.ctypes.data, b.ctypes.data, out.ctypes.data, len(a))
+    return out
+
+
+def test_double_libm_within_one_ulp_of_glibc():
+    # slo_libm_d.h (fdlibm sin/cos/atan2/asin, shared by the oracle and the
+    # device for the Q18 round trips) against the host glibc via Python's math
+    import math
+    rng = np.random.default_rng(3)
+    n = 40000
+    ang = np.concatenate([rng.uniform(-20, 20, n), rng.uniform(-1e-3, 1e-3, n),
+                          rng.uniform(-7, 7, n).astype(np.float32).astype(np.float64)])
+    cases = [(0, ang, None, math.sin), (1, ang, None, math.cos),
+             (3, np.concatenate([rng.uniform(-1, 1, n), rng.uniform(-1e-4, 1e-4, n)]), None, math.asin),
+             (2, rng.normal(size=n) * 10.0 ** rng.integers(-8, 3, n), rng.normal(size=n), math.atan2)]
+    for which, a, b, f in cases:
+        got = _libm_d(which, a, b)
+        want = np.array([f(*v) for v in (zip(a, b) if b is not None else ((x,) for x in a))])
+        ulp = np.abs(got.view(np.int64) - want.view(np.int64))
+        assert ulp.max() <= 1, (which, int(ulp.max()))
+        assert (ulp == 0).mean() > 0.7, which
+
+
 def test_introsort_restatement_matches_libstdcxx(tmp_path):
     exe = tmp_path / "introsort_check"
     src = os.path.join(HERE, "cpp", "introsort_check.cpp")

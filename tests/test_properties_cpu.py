@@ -135,3 +135,30 @@ def test_voxel_grid_single_point_voxels_are_fixed_points(leaf):
     out = O.voxel_grid(pts, leaf, stable=True)
     assert len(out) == len(pts)
     assert sorted(map(tuple, out.tolist())) == sorted(map(tuple, pts.tolist()))
+
+
+def _cam_rot(t):
+    """rotation of a camera-frame pose (rx, ry, rz) as the mapping node builds
+    it: Rot3::RzRyRx(rz, rx, ry) in the GTSAM axes (MO:1545)"""
+    return _rot(float(t[2]), float(t[0]), float(t[1]))
+
+
+@FAST
+@given(rx=st.floats(-1.5, 1.5), ry=st.floats(-12.0, 12.0), rz=st.floats(-3.1, 3.1),
+       which=st.sampled_from(["odom", "keyframe"]))
+def test_pose_round_trips_wrap_but_keep_the_rotation(rx, ry, rz, which):
+    # SURVEY Q18: the tf hand-off (FA:1728 -> MO:658) and the Rot3 read-back
+    # of a keyframe (MO:1588-1601) keep the float angles inside (-pi, pi]
+    # (to the last bit, except that a zero or tiny angle picks up the
+    # ~1e-16 rad residue of the f64 trig, as in the reference), and
+    # elsewhere wrap them to an equal rotation
+    t = np.array([rx, ry, rz, 1.5, -2.0, 7.25], np.float32)
+    out = O.pose_roundtrip(t, which)
+    assert out[3:].tobytes() == t[3:].tobytes()
+    assert -np.pi <= out[1] <= np.pi and -np.pi / 2 <= out[0] <= np.pi / 2
+    np.testing.assert_allclose(_cam_rot(out), _cam_rot(t), atol=2e-6)
+    if abs(float(t[1])) < 3.14159:
+        np.testing.assert_allclose(out, t, rtol=2.0 ** -23, atol=1e-15)
+    else:
+        k = np.round((float(t[1]) - float(out[1])) / (2 * np.pi))
+        assert k != 0 and abs(float(out[1]) - (float(t[1]) - 2 * np.pi * k)) < 1e-5

@@ -1,5 +1,8 @@
 set -euo pipefail
-mkdir -p gpurun_out/w20
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/w20/gpu_tests.log 2>&1 || { tail -30 gpurun_out/w20/gpu_tests.log; exit 1; }
-timeout -k 10 400 python3 bench.py --cpu-scans 0 > gpurun_out/w20/b512.json 2> gpurun_out/w20/b512.err
+D=gpurun_out/w22
+mkdir -p $D
+for g in 3 4; do
+  timeout -k 10 300 python3 bench.py --cpu-scans 0 --icp-jobs 0 --groups $g > $D/g$g.json 2> $D/g$g.err
+done
+timeout -k 10 300 python3 bench.py --cpu-scans 0 --icp-jobs 0 --groups 4 --streams 640 > $D/g4s640.json 2> $D/g4s640.err
 echo done
