@@ -169,6 +169,9 @@ int slo_timing_enable(slo_ctx* ctx, int enable);
  * launch counts; returns number of kernels */
 int slo_timing_read(slo_ctx* ctx, char* names_buf, size_t buf_bytes, double* total_ms, int64_t* launches, int cap);
 int slo_timing_reset(slo_ctx* ctx);
+/* time only the launches named `name` (NULL or "" = all); the bench times
+ * its dominant kernel this way inside the timed region */
+int slo_timing_filter(slo_ctx* ctx, const char* name);
 
 /* ---------------------------------------------------------------- wire format
  * sensor_msgs/PointCloud2 -> pcl::PointCloud<PointXYZI>, the conversion of

@@ -13,6 +13,9 @@ using slo::StreamState;
 
 namespace slo {
 
+bool timing_on(const slo_ctx* ctx, const char* name) {
+    return ctx->timing_only.empty() || ctx->timing_only == name;
+}
 void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a) {
     (void)name;
     hipEventCreate(a);
@@ -471,6 +474,11 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
 int slo_timing_enable(slo_ctx* ctx, int enable) {
     if (!ctx) return SLO_E_ARG;
     ctx->timing = enable != 0;
+    return SLO_OK;
+}
+int slo_timing_filter(slo_ctx* ctx, const char* name) {
+    if (!ctx) return SLO_E_ARG;
+    ctx->timing_only = name ? name : "";
     return SLO_OK;
 }
 int slo_timing_reset(slo_ctx* ctx) {

@@ -430,6 +430,7 @@ struct slo_ctx {
     bool fa_published = false;
     // timing
     bool timing = false;
+    std::string timing_only;            // non-empty: time only launches of this name (slo_timing_filter)
     struct KT { std::vector<hipEvent_t> ev; double total_ms = 0; int64_t n = 0; };
     std::map<std::string, KT> ktimes;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
@@ -453,6 +454,7 @@ struct slo_ctx {
 // launch helpers with optional per-kernel HIP-event timing
 namespace slo {
 void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a);
+bool timing_on(const slo_ctx* ctx, const char* name);
 void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
@@ -481,7 +483,8 @@ int lc_icp_run(slo_ctx* ctx, const float4* src, size_t src_stride, const int32_t
 #define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \
     do {                                                                              \
         hipEvent_t ev_a_ = nullptr;                                                   \
-        if ((ctx)->timing) slo::timing_begin((ctx), name, &ev_a_);                    \
+        const bool tm_ = (ctx)->timing && slo::timing_on((ctx), name);                \
+        if (tm_) slo::timing_begin((ctx), name, &ev_a_);                              \
         hipLaunchKernelGGL(kernel, grid, block, shmem, (ctx)->stream, __VA_ARGS__);   \
-        if ((ctx)->timing) slo::timing_end((ctx), name, ev_a_);                       \
+        if (tm_) slo::timing_end((ctx), name, ev_a_);                                 \
     } while (0)

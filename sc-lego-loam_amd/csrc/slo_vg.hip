@@ -299,10 +299,11 @@ static int vg_sorted(slo_ctx* ctx, const char* tag, const float4* in, size_t in_
     size_t tb = w.temp_bytes;
     hipEvent_t ev = nullptr;
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
-    if (ctx->timing) timing_begin(ctx, sort_name.c_str(), &ev);
+    const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
+    if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
     SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys, keys2, w.vals, w.vals2, total, 0, vbits + sbits,
                                                  ctx->stream));
-    if (ctx->timing) timing_end(ctx, sort_name.c_str(), ev);
+    if (tm) timing_end(ctx, sort_name.c_str(), ev);
     const int gi = (total + T - 1) / T;
     SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits,
                w.flags);

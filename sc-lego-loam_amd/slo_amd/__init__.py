@@ -170,6 +170,10 @@ class Context:
     def timing(self, enable=True):
         self._ok(self.L.slo_timing_enable(self.h, int(enable)), "slo_timing_enable")
 
+    def timing_filter(self, name=None):
+        """time only launches named `name` (None: all)"""
+        self._ok(self.L.slo_timing_filter(self.h, name.encode() if name else None), "slo_timing_filter")
+
     def timing_reset(self):
         self._ok(self.L.slo_timing_reset(self.h), "slo_timing_reset")
 

@@ -95,7 +95,7 @@ EXPORTS = [
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
-    "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
+    "slo_timing_filter", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
 ]
 
 
@@ -143,6 +143,7 @@ def lib():
     L.slo_get.argtypes = [P, ctypes.c_int, ctypes.c_char_p, P, ctypes.c_size_t]
     L.slo_timing_enable.argtypes = [P, ctypes.c_int]
     L.slo_timing_reset.argtypes = [P]
+    L.slo_timing_filter.argtypes = [P, ctypes.c_char_p]
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]

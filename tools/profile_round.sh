@@ -2,7 +2,9 @@
 # Collect the round's measurements on the GPU box (run through gpurun):
 #   1. bench.py (default config, with the CPU baseline)      -> gpurun_out/<tag>/bench.json
 #   2. rocprofv3 --kernel-trace --stats of the same bench command (minus the
-#      CPU leg, which launches no kernels; 8 timed + 4 warm-up + 4 instrumented steps)                   -> gpurun_out/<tag>/kt/
+#      CPU leg and the ICP batch; no warm-up and no instrumented pass: the
+#      trace's mo_knn launches are exactly the bench's timed ones, so the
+#      trace average checks roofline.avg_launch_us of the line in kt.log)                             -> gpurun_out/<tag>/kt/
 #   3. rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE (separate passes, no trace
 #      domains; MI355X_MICROARCH.md "rocprofv3 PMC slots")   -> gpurun_out/<tag>/pmc_*/
 # then python3 tools/pmc_summary.py gpurun_out/<tag> profiles/<tag> (here).
@@ -13,7 +15,7 @@ shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-SHORT="--cpu-scans 0 --steps 8 --warmup 4 --profile-steps 4 $*"
+SHORT="--cpu-scans 0 --steps 8 --warmup 0 --profile-steps 0 --icp-jobs 0 $*"
 echo "[profile] bench" && timeout -k 10 600 python3 bench.py "$@" > "$OUT/bench.json" 2> "$OUT/bench.err"
 tail -1 "$OUT/bench.json"
 echo "[profile] kernel trace" && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
