@@ -55,6 +55,9 @@ int slo_synchronize(slo_ctx* ctx);
  * float4 in firing order, NaN for no return; d_counts: device int32
  * [n_streams].  All batched calls are asynchronous on slo_stream(). */
 int slo_batch_image_projection(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
+/* cfg.use_cloud_ring: device uint16 [n_streams][cfg.max_points], the ring of
+ * each input point (indexed like d_points); kept for the following calls */
+int slo_batch_set_rings(slo_ctx* ctx, const uint16_t* d_rings);
 /* features (FA:1833-1839) + scan-to-scan odometry (FA:1846-1859) */
 int slo_batch_feature_association(slo_ctx* ctx);
 /* mapping step for streams whose FA published this scan and whose
@@ -101,6 +104,12 @@ typedef struct slo_map_view {
 /* pts: n points, stride_bytes apart, xyz at off_xyz (3 floats), intensity at off_i */
 int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
                          size_t off_i, slo_seg_view* out);
+/* useCloudRing (cfg.use_cloud_ring, IP:172-178, 225-226): rings[k] is the
+ * "ring" of input point k in the message's order; the reference reads it at
+ * the point's index AFTER NaN removal (laserCloudInRing->points[i]), which
+ * is the same point only for the dense clouds it accepts (IP:174-177) */
+int slo_image_projection_ring(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                              size_t off_i, const uint16_t* rings, slo_seg_view* out);
 int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out);
 /* raw_pts: the raw cloud of the scan being mapped (same layout arguments) */
 int slo_map_optimization(slo_ctx* ctx, const void* raw_pts, size_t n, size_t stride_bytes, size_t off_xyz,
@@ -210,10 +219,12 @@ typedef struct slo_pc2 {         /* sensor_msgs/PointCloud2 (header omitted: t_s
     uint8_t is_dense;
 } slo_pc2;
 
-/* byte offsets of x, y, z, intensity inside a point, -1 = no matching field */
+/* byte offsets of x, y, z, intensity (FLOAT32) and ring (UINT16, the
+ * reference's PointXYZIR, utility.h:158-169) inside a point, -1 = no match */
 typedef struct slo_pc2_layout {
     uint32_t point_step;
     int32_t off_x, off_y, off_z, off_intensity;
+    int32_t off_ring;
 } slo_pc2_layout;
 
 /* the field mapping alone; SLO_E_ARG if a matched field does not fit in point_step */
@@ -222,15 +233,19 @@ int slo_pc2_layout_of(const slo_pc2* msg, slo_pc2_layout* out);
  * SLO_E_CAPACITY (with *n_out set) when cap_points is too small, SLO_E_ARG
  * when data_bytes cannot hold the last point. */
 int slo_pc2_to_xyzi(const slo_pc2* msg, float* out_xyzi, size_t cap_points, size_t* n_out);
-/* ImageProjection::cloudHandler (IP:181) taking the message itself */
+/* ImageProjection::cloudHandler (IP:181) taking the message itself; with
+ * cfg.use_cloud_ring the rows come from the uint16 "ring" field exactly as
+ * IP:172-178 / 225-226 read them (SLO_E_ARG unless is_dense) */
 int slo_image_projection_pc2(slo_ctx* ctx, const slo_pc2* msg, slo_seg_view* out);
 /* batched, on the device: n_streams messages of one point layout, message s
  * at d_bytes + s * msg_stride with d_dims[3 s .. 3 s + 2] = (width, height,
  * row_step); writes the d_points / d_counts of slo_batch_image_projection.
  * A message of more than cfg.max_points points keeps its first max_points
- * (the context's capacity; bit 8 of slo_get(.., "err") is set).  Asynchronous. */
+ * (the context's capacity; bit 8 of slo_get(.., "err") is set).  d_rings
+ * (optional, NULL = none) receives each point's ring for slo_batch_set_rings
+ * (0 where the layout has no uint16 ring).  Asynchronous. */
 int slo_batch_pc2_unpack(slo_ctx* ctx, const uint8_t* d_bytes, size_t msg_stride, const int32_t* d_dims,
-                         const slo_pc2_layout* layout, void* d_points, int32_t* d_counts);
+                         const slo_pc2_layout* layout, void* d_points, int32_t* d_counts, uint16_t* d_rings);
 
 /* synthetic stream generator (sc-lego-loam_amd/csrc/slo_gen.h), host side */
 int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float* out_xyzi);

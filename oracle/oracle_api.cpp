@@ -70,6 +70,9 @@ void oracle_destroy(void* h) { delete (OracleStream*)h; }
 
 int oracle_step(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step(pts, n, t); }
 
+// useCloudRing input for the next scans (the message's ring field, unfiltered order)
+void oracle_set_rings(void* h, const uint16_t* rings, int n) { ((OracleStream*)h)->ip.rings.assign(rings, rings + n); }
+
 // image projection only (for front-end parity of a single scan)
 void oracle_image_projection(void* h, const float* pts, int n) { ((OracleStream*)h)->ip.cloudHandler(pts, n); }
 

@@ -61,6 +61,8 @@ struct ImageProjection {
         std::fill(fullInfoCloud.begin(), fullInfoCloud.end(), nanPoint);
     }
 
+    std::vector<uint16_t> rings;   // useCloudRing: the message's ring field, unfiltered order
+
     // IP:163-179 — removeNaNFromPointCloud keeps order; input is (x,y,z,i) x n
     void copyPointCloud(const float* pts, int n) {
         laserCloudIn.clear();
@@ -87,12 +89,20 @@ struct ImageProjection {
         size_t cloudSize = laserCloudIn.size();
         for (size_t i = 0; i < cloudSize; ++i) {
             Pt thisPoint = laserCloudIn[i];
-            float verticalAngle = (float)((double)(slo_libm::atan2f_(thisPoint.z,
-                sqrtf(thisPoint.x * thisPoint.x + thisPoint.y * thisPoint.y)) * 180) / M_PI);
-            float rowf = (verticalAngle + cfg.ang_bottom) / cfg.ang_res_y;
-            // Q1: float -> size_t; negative values in (-1, 0) truncate to 0,
-            // below -1 wrap to huge and are rejected by the range check.
-            int64_t rowIdn = (int64_t)rowf;  // truncation toward zero
+            int64_t rowIdn;
+            if (cfg.use_cloud_ring) {
+                // IP:225-226: the ring of laserCloudInRing->points[i], the
+                // UNfiltered cloud indexed by the filtered index i (the
+                // reference requires is_dense clouds, IP:174-177)
+                rowIdn = i < rings.size() ? (int64_t)rings[i] : 0;
+            } else {
+                float verticalAngle = (float)((double)(slo_libm::atan2f_(thisPoint.z,
+                    sqrtf(thisPoint.x * thisPoint.x + thisPoint.y * thisPoint.y)) * 180) / M_PI);
+                float rowf = (verticalAngle + cfg.ang_bottom) / cfg.ang_res_y;
+                // Q1: float -> size_t; negative values in (-1, 0) truncate to 0,
+                // below -1 wrap to huge and are rejected by the range check.
+                rowIdn = (int64_t)rowf;  // truncation toward zero
+            }
             if (rowIdn < 0 || rowIdn >= R) continue;
             float horizonAngle = (float)((double)(slo_libm::atan2f_(thisPoint.x, thisPoint.y) * 180) / M_PI);
             double colD = -round(((double)horizonAngle - 90.0) / (double)cfg.ang_res_x) + (double)(C / 2);

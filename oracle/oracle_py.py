@@ -46,6 +46,7 @@ class SloConfig(ctypes.Structure):
         ("loop_time_gap", ctypes.c_double), ("icp_max_iterations", ctypes.c_int32),
         ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
         ("icp_fitness_epsilon", ctypes.c_double),
+        ("use_cloud_ring", ctypes.c_int32),
     ]
 
 
@@ -92,6 +93,7 @@ def lib():
                                        ctypes.c_int, ctypes.c_void_p]
         L.oracle_umeyama.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
+        L.oracle_set_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
@@ -224,6 +226,11 @@ class OracleStream:
     def step(self, pts, t):
         pts = np.ascontiguousarray(pts, np.float32)
         return lib().oracle_step(self.h, pts.ctypes.data, len(pts), float(t))
+
+    def set_rings(self, rings):
+        """useCloudRing (cfg.use_cloud_ring): ring per input point, message order"""
+        r = np.ascontiguousarray(rings, np.uint16)
+        lib().oracle_set_rings(self.h, r.ctypes.data, len(r))
 
     def image_projection(self, pts):
         pts = np.ascontiguousarray(pts, np.float32)

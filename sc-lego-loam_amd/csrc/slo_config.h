@@ -97,6 +97,10 @@ typedef struct slo_config {
     double icp_max_corr_dist;               /* 100 (MO:1007 / 1058) */
     double icp_transformation_epsilon;      /* 1e-6 (MO:1009 / 1060) */
     double icp_fitness_epsilon;             /* 1e-6 (MO:1010 / 1061) */
+    /* useCloudRing (utility.h:64, false in the reference): the row of a point
+       is its "ring" field instead of its elevation (IP:225-226); rings come
+       from slo_batch_set_rings or the PointCloud2's uint16 "ring" field */
+    int32_t use_cloud_ring;
 } slo_config;
 
 /* preset ids */
@@ -204,6 +208,7 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->icp_max_corr_dist = 100.0;
     c->icp_transformation_epsilon = 1e-6;
     c->icp_fitness_epsilon = 1e-6;
+    c->use_cloud_ring = 0;
     return 0;
 }
 #endif

@@ -109,6 +109,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     const size_t S = n_streams, H = v.H;
     Carver c;
     c.add(&ctx->d_in, S * v.P);
+    c.add(&ctx->d_ring_in, S * v.P);
     c.add(&ctx->d_cnt, S);
     c.add(&v.owner, S * H);
     c.add(&v.fl, 2 * S);
@@ -264,8 +265,18 @@ int slo_synchronize(slo_ctx* ctx) {
     return SLO_OK;
 }
 
+int slo_batch_set_rings(slo_ctx* ctx, const uint16_t* d_rings) {
+    if (!ctx) return SLO_E_ARG;
+    ctx->v.rings = d_rings;
+    return SLO_OK;
+}
+
 int slo_batch_image_projection(slo_ctx* ctx, const void* d_points, const int32_t* d_counts) {
     if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    if (ctx->cfg.use_cloud_ring && !ctx->v.rings) {
+        ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings";
+        return SLO_E_STATE;
+    }
     SLO_CHECK(hipSetDevice(ctx->dev));
     ctx->v.pts = (const float4*)d_points;
     ctx->v.npts = d_counts;
@@ -553,14 +564,19 @@ static int single_stream(slo_ctx* ctx) {
 
 // ImageProjection::cloudHandler (IP:181-196): copyPointCloud .. cloudSegmentation;
 // *out mirrors /segmented_cloud, /segmented_cloud_info and /outlier_cloud.
-int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz, size_t off_i,
-                         slo_seg_view* out) {
+int slo_image_projection_ring(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                              size_t off_i, const uint16_t* rings, slo_seg_view* out) {
     if (!ctx || (!pts && n) || !out) return SLO_E_ARG;
+    if (ctx->cfg.use_cloud_ring && !rings && n) { ctx->err = "cfg.use_cloud_ring needs rings"; return SLO_E_ARG; }
     int r = single_stream(ctx);
     if (r) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     r = stage_points(ctx, pts, n, stride_bytes, off_xyz, off_i);
     if (r) return r;
+    if (ctx->cfg.use_cloud_ring) {
+        if (n) SLO_CHECK(hipMemcpyAsync(ctx->d_ring_in, rings, 2 * n, hipMemcpyHostToDevice, ctx->stream));
+        ctx->v.rings = ctx->d_ring_in;
+    }
     ctx->v.pts = ctx->d_in;
     ctx->v.npts = ctx->d_cnt;
     r = slo::ip_run(ctx);
@@ -586,6 +602,11 @@ int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
     out->n_outlier = st.outlier_count;
     out->outlier = (const float*)view_copy(ctx, 6, v.outlier, 16 * (size_t)st.outlier_count, &rc);
     return rc;
+}
+
+int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz, size_t off_i,
+                         slo_seg_view* out) {
+    return slo_image_projection_ring(ctx, pts, n, stride_bytes, off_xyz, off_i, nullptr, out);
 }
 
 // FeatureAssociation::runFeatureAssociation (FA:1817-1859) on the result of

@@ -96,6 +96,7 @@ struct DevView {
     // inputs
     const float4* pts;   // [S][P]
     const int32_t* npts; // [S]
+    const uint16_t* rings; // [S][P] ring per input point (cfg.use_cloud_ring), else unused
     // image projection
     int32_t* owner;      // [S][H]
     int32_t* fl;         // [S][2] first/last finite index
@@ -440,6 +441,7 @@ struct slo_ctx {
     std::vector<char> h_view[16];       // backing store of the single-scan views
     int32_t h_ring[2][128];
     float4* d_in = nullptr;   // internal input buffer [S][P]
+    uint16_t* d_ring_in = nullptr;   // internal ring buffer [S][P] (single-scan useCloudRing)
     int32_t* d_cnt = nullptr;
     // mapping workspaces
     slo::MapWs mws;

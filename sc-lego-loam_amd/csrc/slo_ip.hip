@@ -51,12 +51,17 @@ __device__ inline long long ip_col_of(const slo_config& c, float a) {
 // row / column of a finite point (IP:229-246); returns false if rejected.
 // The bins are taken at both ends of the atan2f bracket (slo_fastatan.h);
 // only when they differ is glibc's atan2f itself evaluated.
-__device__ inline bool project_point(const slo_config& c, float4 p, int& row, int& col, float& range) {
-    const float h = sqrtf(p.x * p.x + p.y * p.y);
+// ring >= 0: the row is the point's ring field (useCloudRing, IP:225-226).
+__device__ inline bool project_point(const slo_config& c, float4 p, int ring, int& row, int& col, float& range) {
     float lo, hi;
     long long r;
-    if (!slo_fast::atan2_bracket(p.z, h, lo, hi) || (r = ip_row_of(c, lo)) != ip_row_of(c, hi))
-        r = ip_row_of(c, slo_libm::atan2f_(p.z, h));
+    if (ring >= 0) {
+        r = ring;
+    } else {
+        const float h = sqrtf(p.x * p.x + p.y * p.y);
+        if (!slo_fast::atan2_bracket(p.z, h, lo, hi) || (r = ip_row_of(c, lo)) != ip_row_of(c, hi))
+            r = ip_row_of(c, slo_libm::atan2f_(p.z, h));
+    }
     if (r < 0 || r >= c.n_scan) return false;
     long long cc;
     if (!slo_fast::atan2_bracket(p.x, p.y, lo, hi) || (cc = ip_col_of(c, lo)) != ip_col_of(c, hi))
@@ -95,7 +100,8 @@ __global__ void k_ip_project(DevView v) {
         if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
             fmin = min(fmin, i); fmax = max(fmax, i);
             int row, col; float rg;
-            if (project_point(v.cfg, p, row, col, rg))
+            const int ring = v.cfg.use_cloud_ring ? (int)v.rings[(size_t)s * v.P + i] : -1;
+            if (project_point(v.cfg, p, ring, row, col, rg))
                 atomicMax(&v.owner[(size_t)s * v.H + (size_t)col * R + row], i);
         }
     }

@@ -20,17 +20,18 @@
 // costs one HBM pass instead of a host loop per stream.
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <cmath>
 #include <vector>
 #include "slo_internal.h"
 
 namespace {
 
 // FieldMatches<PointT, Tag> for a scalar float field (pcl/conversions.h)
-int match_field(const slo_pc2* m, const char* name) {
+int match_field(const slo_pc2* m, const char* name, int datatype = SLO_PF_FLOAT32) {
     for (int k = 0; k < m->n_fields; ++k) {
         const slo_pc2_field& f = m->fields[k];
         if (!f.name || strcmp(f.name, name) != 0) continue;
-        if (f.datatype == SLO_PF_FLOAT32 && (f.count == 1 || f.count == 0)) return (int)f.offset;
+        if (f.datatype == datatype && (f.count == 1 || f.count == 0)) return (int)f.offset;
     }
     return -1;
 }
@@ -42,8 +43,10 @@ int layout_of(const slo_pc2* m, slo_pc2_layout* L) {
     L->off_y = match_field(m, "y");
     L->off_z = match_field(m, "z");
     L->off_intensity = match_field(m, "intensity");
+    L->off_ring = match_field(m, "ring", SLO_PF_UINT16);   // PointXYZIR's uint16 ring (utility.h:158-169)
     for (int o : {L->off_x, L->off_y, L->off_z, L->off_intensity})
         if (o >= 0 && (uint64_t)o + 4 > m->point_step) return SLO_E_ARG;
+    if (L->off_ring >= 0 && (uint64_t)L->off_ring + 2 > m->point_step) return SLO_E_ARG;
     return SLO_OK;
 }
 
@@ -89,7 +92,8 @@ int to_xyzi(const slo_pc2* m, float* out, size_t cap, size_t* n_out) {
 __global__ void __launch_bounds__(256) k_pc2_unpack(const uint8_t* __restrict__ bytes, size_t msg_stride,
                                                     const int32_t* __restrict__ dims, slo_pc2_layout L, int P,
                                                     bool layout_aligned, float4* __restrict__ out,
-                                                    int32_t* __restrict__ counts, slo::StreamState* st) {
+                                                    int32_t* __restrict__ counts, uint16_t* __restrict__ rings,
+                                                    slo::StreamState* st) {
     const int s = blockIdx.y;
     const int w = dims[3 * s], h = dims[3 * s + 1], row_step = dims[3 * s + 2];
     const long long n_all = (long long)max(w, 0) * max(h, 0);
@@ -111,6 +115,10 @@ __global__ void __launch_bounds__(256) k_pc2_unpack(const uint8_t* __restrict__ 
         return __uint_as_float(u);
     };
     out[(size_t)s * P + i] = make_float4(rd(L.off_x), rd(L.off_y), rd(L.off_z), rd(L.off_intensity));
+    if (rings) {
+        const int o = L.off_ring;
+        rings[(size_t)s * P + i] = o < 0 ? 0 : (uint16_t)(p[o] | (p[o + 1] << 8));
+    }
 }
 
 }  // namespace
@@ -126,21 +134,42 @@ int slo_pc2_to_xyzi(const slo_pc2* msg, float* out_xyzi, size_t cap_points, size
 int slo_image_projection_pc2(slo_ctx* ctx, const slo_pc2* msg, slo_seg_view* out) {
     if (!ctx || !msg || !out) return SLO_E_ARG;
     thread_local std::vector<float> buf;
+    thread_local std::vector<uint16_t> ring_raw, ring_eff;
     const size_t n = (size_t)msg->width * msg->height;
     if (n > (size_t)ctx->cfg.max_points) { ctx->err = "too many points"; return SLO_E_CAPACITY; }
     buf.resize(4 * std::max<size_t>(n, 1));
     size_t got = 0;
     const int r = to_xyzi(msg, buf.data(), n, &got);
     if (r) { ctx->err = "malformed PointCloud2"; return r; }
-    return slo_image_projection(ctx, buf.data(), got, 16, 0, 12, out);
+    if (!ctx->cfg.use_cloud_ring) return slo_image_projection(ctx, buf.data(), got, 16, 0, 12, out);
+    // useCloudRing (IP:172-178): fromROSMsg into PointXYZIR, whose is_dense
+    // must be set (else the reference shuts down), then row = the ring of
+    // laserCloudInRing->points[i] with i the index after NaN removal
+    if (!msg->is_dense) { ctx->err = "useCloudRing needs an is_dense cloud (IP:174-177)"; return SLO_E_ARG; }
+    slo_pc2_layout L;
+    layout_of(msg, &L);
+    ring_raw.assign(std::max<size_t>(n, 1), 0);
+    ring_eff.assign(std::max<size_t>(n, 1), 0);
+    size_t i = 0;
+    for (uint32_t row = 0; row < msg->height; ++row)
+        for (uint32_t col = 0; col < msg->width; ++col, ++i)
+            if (L.off_ring >= 0)
+                memcpy(&ring_raw[i], msg->data + (size_t)row * msg->row_step + (size_t)col * msg->point_step + L.off_ring, 2);
+    size_t f = 0;   // filtered index of each finite point
+    for (size_t k = 0; k < n; ++k) {
+        const float* p = &buf[4 * k];
+        if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) ring_eff[k] = ring_raw[f++];
+    }
+    return slo_image_projection_ring(ctx, buf.data(), got, 16, 0, 12, ring_eff.data(), out);
 }
 
 int slo_batch_pc2_unpack(slo_ctx* ctx, const uint8_t* d_bytes, size_t msg_stride, const int32_t* d_dims,
-                         const slo_pc2_layout* layout, void* d_points, int32_t* d_counts) {
+                         const slo_pc2_layout* layout, void* d_points, int32_t* d_counts, uint16_t* d_rings) {
     if (!ctx || !d_bytes || !d_dims || !layout || !d_points || !d_counts) return SLO_E_ARG;
     const slo_pc2_layout L = *layout;
     for (int o : {L.off_x, L.off_y, L.off_z, L.off_intensity})
         if (o >= 0 && (uint64_t)o + 4 > L.point_step) { ctx->err = "field outside point_step"; return SLO_E_ARG; }
+    if (L.off_ring >= 0 && (uint64_t)L.off_ring + 2 > L.point_step) { ctx->err = "ring outside point_step"; return SLO_E_ARG; }
     SLO_CHECK(hipSetDevice(ctx->dev));
     const int P = ctx->cfg.max_points;
     const bool aligned = ((uintptr_t)d_bytes % 4 == 0) && msg_stride % 4 == 0 && L.point_step % 4 == 0 &&
@@ -148,7 +177,7 @@ int slo_batch_pc2_unpack(slo_ctx* ctx, const uint8_t* d_bytes, size_t msg_stride
                          (L.off_z < 0 || L.off_z % 4 == 0) && (L.off_intensity < 0 || L.off_intensity % 4 == 0);
     const dim3 grid((P + 255) / 256, ctx->S);
     k_pc2_unpack<<<grid, 256, 0, ctx->stream>>>(d_bytes, msg_stride, d_dims, L, P, aligned, (float4*)d_points,
-                                                d_counts, ctx->v.st);
+                                                d_counts, d_rings, ctx->v.st);
     SLO_CHECK(hipGetLastError());
     return SLO_OK;
 }

@@ -109,12 +109,17 @@ class Context:
     def batch_image_projection(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_image_projection(self.h, d_pts, d_cnt), "slo_batch_image_projection")
 
-    def batch_pc2_unpack(self, d_bytes, msg_stride, d_dims, layout, d_pts, d_cnt):
+    def batch_pc2_unpack(self, d_bytes, msg_stride, d_dims, layout, d_pts, d_cnt, d_rings=None):
         """slo_batch_pc2_unpack: one raw PointCloud2 payload per stream (device
         bytes, message s at s * msg_stride, d_dims int32 [S][3] = width,
-        height, row_step) -> the d_pts / d_cnt of batch_image_projection."""
+        height, row_step) -> the d_pts / d_cnt of batch_image_projection
+        (and, if given, each point's uint16 ring into d_rings)."""
         self._ok(self.L.slo_batch_pc2_unpack(self.h, d_bytes, msg_stride, d_dims, ctypes.byref(layout), d_pts,
-                                             d_cnt), "slo_batch_pc2_unpack")
+                                             d_cnt, d_rings), "slo_batch_pc2_unpack")
+
+    def batch_set_rings(self, d_rings):
+        """slo_batch_set_rings (cfg.use_cloud_ring): device uint16 [S][max_points]"""
+        self._ok(self.L.slo_batch_set_rings(self.h, d_rings), "slo_batch_set_rings")
 
     def batch_feature_association(self):
         self._ok(self.L.slo_batch_feature_association(self.h), "slo_batch_feature_association")
@@ -213,9 +218,11 @@ class ImageProjection(_Node):
     Returns the /segmented_cloud, /segmented_cloud_info and /outlier_cloud
     contents as numpy arrays."""
 
-    def cloudHandler(self, points_xyzi):
+    def cloudHandler(self, points_xyzi, rings=None):
         """points_xyzi: (n, 4) float32 array, or a wire.PointCloud2 message
-        (converted by pcl::fromROSMsg rules inside libslo, IP:167)."""
+        (converted by pcl::fromROSMsg rules inside libslo, IP:167).  rings:
+        uint16 per point for cfg.use_cloud_ring with an array input (a
+        message brings its own "ring" field)."""
         v = SegView()
         if isinstance(points_xyzi, wire.PointCloud2):
             m = wire._CMsg(points_xyzi)
@@ -223,8 +230,10 @@ class ImageProjection(_Node):
                          "slo_image_projection_pc2")
         else:
             pts = np.ascontiguousarray(points_xyzi, np.float32)
-            self.ctx._ok(self.ctx.L.slo_image_projection(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
-                                                         ctypes.byref(v)), "slo_image_projection")
+            r = None if rings is None else np.ascontiguousarray(rings, np.uint16)
+            self.ctx._ok(self.ctx.L.slo_image_projection_ring(self.ctx.h, pts.ctypes.data, len(pts), 16, 0, 12,
+                                                              None if r is None else r.ctypes.data,
+                                                              ctypes.byref(v)), "slo_image_projection_ring")
         R = self.ctx.cfg.n_scan
         return {
             "seg_pts": _arr(v.segmented, v.n_segmented, np.float32, 4),

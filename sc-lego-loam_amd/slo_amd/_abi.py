@@ -45,6 +45,7 @@ class SloConfig(ctypes.Structure):
         ("loop_time_gap", ctypes.c_double), ("icp_max_iterations", ctypes.c_int32),
         ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
         ("icp_fitness_epsilon", ctypes.c_double),
+        ("use_cloud_ring", ctypes.c_int32),
     ]
 
 
@@ -72,7 +73,7 @@ class Pc2(ctypes.Structure):
 
 class Pc2Layout(ctypes.Structure):
     _fields_ = [("point_step", ctypes.c_uint32), ("off_x", ctypes.c_int32), ("off_y", ctypes.c_int32),
-                ("off_z", ctypes.c_int32), ("off_intensity", ctypes.c_int32)]
+                ("off_z", ctypes.c_int32), ("off_intensity", ctypes.c_int32), ("off_ring", ctypes.c_int32)]
 
 
 class FaView(ctypes.Structure):
@@ -95,7 +96,7 @@ EXPORTS = [
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
-    "slo_timing_filter", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
+    "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
 ]
 
 
@@ -144,6 +145,9 @@ def lib():
     L.slo_timing_enable.argtypes = [P, ctypes.c_int]
     L.slo_timing_reset.argtypes = [P]
     L.slo_timing_filter.argtypes = [P, ctypes.c_char_p]
+    L.slo_image_projection_ring.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
+                                            P, ctypes.POINTER(SegView)]
+    L.slo_batch_set_rings.argtypes = [P, P]
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
@@ -156,7 +160,7 @@ def lib():
     L.slo_pc2_layout_of.argtypes = [ctypes.POINTER(Pc2), ctypes.POINTER(Pc2Layout)]
     L.slo_pc2_to_xyzi.argtypes = [ctypes.POINTER(Pc2), P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
     L.slo_image_projection_pc2.argtypes = [P, ctypes.POINTER(Pc2), ctypes.POINTER(SegView)]
-    L.slo_batch_pc2_unpack.argtypes = [P, P, ctypes.c_size_t, P, ctypes.POINTER(Pc2Layout), P, P]
+    L.slo_batch_pc2_unpack.argtypes = [P, P, ctypes.c_size_t, P, ctypes.POINTER(Pc2Layout), P, P, P]
     L.slo_record_floats.argtypes = []
     _LIB = L
     return L

@@ -104,3 +104,22 @@ def test_field_mapping_matches_restatement(seed, width, height, step, pad, nf):
     got = wire.fromROSMsg(msg)
     want = from_ros_msg_numpy(msg)
     assert bits(got) == bits(want)
+
+
+def test_oracle_cloud_ring_rows():
+    # useCloudRing (IP:225-226): every point's row is its ring; rings >= N_SCAN
+    # are dropped (IP:232); the ring is read at the index after NaN removal
+    cfg = O.preset(0)
+    cfg.use_cloud_ring = 1
+    R, C = cfg.n_scan, cfg.horizon_scan
+    orc = O.OracleStream(cfg, stable_voxel=True)
+    n_fin = int(np.isfinite(SCAN[:, :3]).all(axis=1).sum())
+    rings = np.full(len(SCAN), 3, np.uint16)
+    rings[n_fin // 2:] = R + 1   # the second half of the finite points: out of range
+    orc.set_rings(rings)
+    orc.image_projection(SCAN)
+    rng = orc.get("range").reshape(R, C)
+    empty = rng[0, 0]
+    assert (rng[np.arange(R) != 3] == empty).all()
+    filled = int((rng[3] != empty).sum())
+    assert 0 < filled <= n_fin // 2
