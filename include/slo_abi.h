@@ -241,7 +241,8 @@ int slo_image_projection_pc2(slo_ctx* ctx, const slo_pc2* msg, slo_seg_view* out
  * at d_bytes + s * msg_stride with d_dims[3 s .. 3 s + 2] = (width, height,
  * row_step); writes the d_points / d_counts of slo_batch_image_projection.
  * A message of more than cfg.max_points points keeps its first max_points
- * (the context's capacity; bit 8 of slo_get(.., "err") is set).  d_rings
+ * (the context's capacity; bit 8 of slo_get(.., "err") is set); one whose
+ * points would reach past msg_stride is not read (count 0, same bit).  d_rings
  * (optional, NULL = none) receives each point's ring for slo_batch_set_rings
  * (0 where the layout has no uint16 ring).  Asynchronous. */
 int slo_batch_pc2_unpack(slo_ctx* ctx, const uint8_t* d_bytes, size_t msg_stride, const int32_t* d_dims,

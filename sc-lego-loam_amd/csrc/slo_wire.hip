@@ -96,12 +96,17 @@ __global__ void __launch_bounds__(256) k_pc2_unpack(const uint8_t* __restrict__ 
                                                     slo::StreamState* st) {
     const int s = blockIdx.y;
     const int w = dims[3 * s], h = dims[3 * s + 1], row_step = dims[3 * s + 2];
-    const long long n_all = (long long)max(w, 0) * max(h, 0);
+    long long n_all = (long long)max(w, 0) * max(h, 0);
+    // a message whose points would reach past its slot (or a negative
+    // row_step) is not read at all: count 0 and the input error bit
+    const bool fits = n_all == 0 || (row_step >= 0 && (long long)(h - 1) * row_step +
+                                     (long long)(w - 1) * L.point_step + L.point_step <= (long long)msg_stride);
+    if (!fits) n_all = 0;
     const int n = (int)min(n_all, (long long)P);
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i == 0) {
         counts[s] = n;
-        if (n_all > P) atomicOr(&st[s].err, SLO_ERR_INPUT);
+        if (n_all > P || !fits) atomicOr(&st[s].err, SLO_ERR_INPUT);
     }
     if (i >= n) return;
     const bool aligned = layout_aligned && (row_step & 3) == 0;

@@ -106,5 +106,13 @@ def test_batch_unpack_clips_to_capacity_and_flags_it():
         assert cnt.tolist() == [P, 50]
         assert bits(d_pts[0].cpu().numpy()) == bits(pts[:P])
         assert int(ctx.get(0, "err")[0]) & 8 == 8 and int(ctx.get(1, "err")[0]) & 8 == 0
+        # a row_step that would read past the message slot: nothing is read
+        d_dims[1, 2] = stride
+        d_dims[1, 1] = 2
+        ctx.batch_pc2_unpack(d_raw.data_ptr(), stride, d_dims.data_ptr(), wire.layout_of(msgs[0]),
+                             d_pts.data_ptr(), d_cnt.data_ptr())
+        ctx.synchronize()
+        assert d_cnt.cpu().numpy().tolist() == [P, 0]
+        assert int(ctx.get(1, "err")[0]) & 8 == 8
     finally:
         ctx.close()
