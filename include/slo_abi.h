@@ -169,7 +169,10 @@ int slo_record_floats(void);
  * "picked", "cloud_label", "smooth_ind", "sharp", "less_sharp", "flat",
  * "less_flat", "corner_last", "surf_last", "transform_sum", "transform_cur",
  * "fa_iters", "mapped", "n_keyframes", "keyposes", "sc_desc", "ring_key",
- * "sector_key", "detect", "detect_f", "flags", "loop" (2 x slo_loop_result), "key_times". */
+ * "sector_key", "detect", "detect_f", "flags", "loop" (2 x slo_loop_result), "key_times",
+ * "integrated" (transformFusion's /integrated_to_init for this scan, 6 floats:
+ * transformFusion.cpp:186-219 on this scan's odometry and the last
+ * published mapping result). */
 int slo_get(slo_ctx* ctx, int stream, const char* name, void* dst, size_t cap_bytes);
 
 /* per-kernel timing (HIP events around every launch when enabled) */

@@ -28,6 +28,7 @@ struct OracleStream {
     bool det_valid = false;
     LoopResult loop[2];      // RS, SC verification of the last detect (cfg.loop_verify)
     int scan_index = 0;
+    float integrated[6] = {0};   // /integrated_to_init (transformFusion's transformMapped)
     explicit OracleStream(const slo_config& c) : cfg(c), ip(c), fa(c), mo(c) {}
 
     // returns bit flags: 1 = FA odometry ran, 2 = mapping ran, 4 = keyframe, 8 = detect ran
@@ -37,6 +38,14 @@ struct OracleStream {
         ip.cloudHandler(pts, n);
         fa.run(ip.segmentedCloud, ip.segMsg, ip.outlierCloud);
         if (fa.systemInitedLM && scan_index > 0) flags |= 1;
+        if (flags & 1) {
+            // TransformFusion::laserOdometryHandler (TF:186-219) on this scan's
+            // /laser_odom_to_init, with the /aft_mapped_to_init of the last
+            // mapping run (the mapping of this scan publishes after it)
+            float sum[6], incre[6];
+            odom_handoff(fa.transformSum, sum);
+            MapOptimization::associate_to_map(sum, mo.tfBef, mo.tfAft, incre, integrated);
+        }
         if (fa.published_to_mapping) {
             bool ran = mo.run(fa.laserCloudCornerLast, fa.laserCloudSurfLast, fa.outlierCloud, fa.transformSum, pts, n, t);
             if (ran) flags |= 2;
@@ -123,6 +132,7 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
     if (name == "corner_last") return copy_cloud(s->fa.laserCloudCornerLast, (float*)out, cap);
     if (name == "surf_last") return copy_cloud(s->fa.laserCloudSurfLast, (float*)out, cap);
     if (name == "transform_sum") return cp(s->fa.transformSum, 6, 4);
+    if (name == "integrated") return cp(s->integrated, 6, 4);
     if (name == "transform_cur") return cp(s->fa.transformCur, 6, 4);
     if (name == "fa_iters") { int v[2] = {s->fa.iters_surf, s->fa.iters_corner}; return cp(v, 2, 4); }
     if (name == "mapped") return cp(s->mo.transformAftMapped, 6, 4);

@@ -49,10 +49,16 @@ struct MapOptimization {
     // per-run stats
     int lm_iters = 0;
     bool ran = false, saved_keyframe = false;
+    // /aft_mapped_to_init as TransformFusion decodes it (publishTF MO:680-705 -> TF:222-241)
+    float tfAft[6] = {0}, tfBef[6] = {0};
 
     explicit MapOptimization(const slo_config& c) : cfg(c), sc(c) {}
 
-    void transformAssociateToMap() {
+    // transformAssociateToMap (MO:397-482); TransformFusion (transformFusion.cpp:94-181)
+    // evaluates the same expressions on its own copies of the three transforms
+    static void associate_to_map(const float* transformSum, const float* transformBefMapped,
+                                 const float* transformAftMapped, float* transformIncre,
+                                 float* transformTobeMapped) {
         using namespace slo_libm;
         float x1 = cosf_(transformSum[1]) * (transformBefMapped[3] - transformSum[3]) -
                    sinf_(transformSum[1]) * (transformBefMapped[5] - transformSum[5]);
@@ -121,6 +127,10 @@ struct MapOptimization {
         transformTobeMapped[3] = transformAftMapped[3] - (cosf_(transformTobeMapped[1]) * x2 + sinf_(transformTobeMapped[1]) * z2);
         transformTobeMapped[4] = transformAftMapped[4] - y2;
         transformTobeMapped[5] = transformAftMapped[5] - (-sinf_(transformTobeMapped[1]) * x2 + cosf_(transformTobeMapped[1]) * z2);
+    }
+
+    void transformAssociateToMap() {
+        associate_to_map(transformSum, transformBefMapped, transformAftMapped, transformIncre, transformTobeMapped);
     }
 
     void transformUpdate() {
@@ -423,6 +433,8 @@ struct MapOptimization {
         downsampleCurrentScan();
         scan2MapOptimization();
         saveKeyFramesAndFactor();
+        odom_handoff(transformAftMapped, tfAft);   // publishTF: quaternion round trip (orientation)
+        for (int k = 0; k < 6; ++k) tfBef[k] = transformBefMapped[k];   // twist fields, exact
         // clearCloud (MO:1640): the DS maps are kept aside for parity checks
         lastCornerMapDS.swap(laserCloudCornerFromMapDS);
         lastSurfMapDS.swap(laserCloudSurfFromMapDS);

@@ -119,6 +119,7 @@ _DTYPES = {
     "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32, "orient": np.float32,
     "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32, "smooth_ind": np.int32,
     "transform_sum": np.float32, "transform_cur": np.float32, "fa_iters": np.int32, "mapped": np.float32,
+    "integrated": np.float32,
     "tobe_mapped": np.float32, "mo_iters": np.int32, "n_keyframes": np.int32, "keyposes": np.float32,
     "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64, "detect": np.int32,
     "detect_f": np.float64, "key_times": np.float64,

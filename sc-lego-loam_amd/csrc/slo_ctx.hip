@@ -430,6 +430,7 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "corner_last") dev(v.corner_last + s * v.cap_less_sharp, st.cornerLastNum, 16);
     else if (name == "surf_last") dev(v.surf_last + s * v.cap_less_flat, st.surfLastNum, 16);
     else if (name == "transform_sum") { tmp.resize(24); memcpy(tmp.data(), st.transformSum, 24); count = 6; esz = 4; }
+    else if (name == "integrated") { tmp.resize(24); memcpy(tmp.data(), st.integrated, 24); count = 6; esz = 4; }
     else if (name == "transform_cur") { tmp.resize(24); memcpy(tmp.data(), st.transformCur, 24); count = 6; esz = 4; }
     else if (name == "fa_iters") { int32_t a[2] = {st.iters_surf, st.iters_corner}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4; }
     else if (name == "mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformAftMapped, 24); count = 6; esz = 4; }

@@ -62,6 +62,9 @@ struct StreamState {
     // kept with the pose by mo_prepare / mo_solve (computed once per pose,
     // not per query)
     float mo_trig[9];
+    // transformFusion (transformFusion.cpp): /aft_mapped_to_init as it
+    // decodes it (publishTF, MO:680-705) and its /integrated_to_init
+    float tf_aft[6], tf_bef[6], integrated[6];
     // scan context
     int32_t sc_count, sc_tree_n, sc_counter;
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];

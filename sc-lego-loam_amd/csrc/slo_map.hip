@@ -517,6 +517,9 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
                 st.kf_saved = 1;
                 save = 1;
             }
+            // publishTF (MO:680-705) as transformFusion reads it (TF:222-241)
+            slo_pose::odom_handoff(st.transformAftMapped, st.tf_aft);
+            for (int i = 0; i < 6; ++i) st.tf_bef[i] = st.transformBefMapped[i];
         }
     }
     __syncthreads();

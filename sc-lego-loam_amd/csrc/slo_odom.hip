@@ -795,6 +795,12 @@ __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
         float tc[6];
         for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
         slo_pose::integrate(st.transformSum, tc);
+        // TransformFusion::laserOdometryHandler (TF:186-219): this scan's
+        // odometry through the tf round trip, associated to the map with the
+        // last published mapping result (this scan's mapping comes after)
+        float sum[6], incre[6];
+        slo_pose::odom_handoff(st.transformSum, sum);
+        slo_pose::associate_to_map(sum, st.tf_bef, st.tf_aft, incre, st.integrated);
         const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;

@@ -30,7 +30,7 @@ _CLOUD_OUT = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "less_s
 _DT = {"range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8,
        "seg_col": np.uint32, "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32,
        "orient": np.float32, "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32,
-       "smooth_ind": np.int32, "transform_sum": np.float32, "transform_cur": np.float32,
+       "smooth_ind": np.int32, "transform_sum": np.float32, "transform_cur": np.float32, "integrated": np.float32,
        "fa_iters": np.int32, "mapped": np.float32, "n_keyframes": np.int32, "flags": np.int32,
        "keyposes": np.float32, "sc_desc": np.float64, "ring_key": np.float64, "sector_key": np.float64,
        "detect": np.int32, "detect_f": np.float64, "mo_iters": np.int32, "tobe_mapped": np.float32,

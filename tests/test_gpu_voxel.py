@@ -12,7 +12,7 @@ from parity_util import mismatch
 pytestmark = pytest.mark.gpu
 
 
-def test_grouped_key_voxel_grid_matches_oracle():
+def test_wide_streams_voxel_grid_matches_oracle():
     import torch
     assert torch.cuda.is_available(), "no HIP device"
     pid, S = 0, 64

@@ -67,6 +67,8 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 cs = [canon_smooth(x[:S], cv, sg, rso, reo, cfg_o.edge_threshold, cfg_o.surf_threshold)
                       for x in (ctx.get(s, "smooth_ind"), ors[s].get("smooth_ind"))]
                 row["smooth_ind"] = mismatch(cs[0], cs[1])
+            if fl_o & 1:   # transformFusion's /integrated_to_init for this scan
+                row["integrated"] = mismatch(ctx.get(s, "integrated"), ors[s].get("integrated"))
             row["odom"] = posediff(ctx.get(s, "transform_sum"), ors[s].get("transform_sum"))
             worst["odom"] = max(worst["odom"], row["odom"])
             if fl_o & 2:
