@@ -260,6 +260,15 @@ class FeatureAssociation(_Node):
                 "surf_last": _arr(v.less_flat, v.n_less_flat, np.float32, 4)}
 
 
+class TransformFusion(_Node):
+    """Mirror of TransformFusion (transformFusion.cpp): no callbacks to drive,
+    the device computes /integrated_to_init inside every odometry step."""
+
+    def integrated(self, stream=0):
+        """transformMapped (rx, ry, rz, tx, ty, tz) of the last scan (TF:186-219)"""
+        return self.ctx.get(stream, "integrated")
+
+
 class MapOptimization(_Node):
     """Mirror of mapOptimization::run (mapOptmization.cpp:1673-1706) minus
     GTSAM and publishing; `raw_xyzi` is the scan's raw cloud (/os1_points)."""

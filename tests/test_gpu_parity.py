@@ -109,6 +109,7 @@ def test_node_mirrors_match_oracle():
     cfg = slo_amd.preset(pid)
     ctx = slo_amd.Context(cfg, 0, 1)
     ip, fa, mo = slo_amd.ImageProjection(ctx), slo_amd.FeatureAssociation(ctx), slo_amd.MapOptimization(ctx)
+    tf = slo_amd.TransformFusion(ctx)
     orc = O.OracleStream(O.preset(pid), stable_voxel=True)
     try:
         for k in range(10):
@@ -122,6 +123,8 @@ def test_node_mirrors_match_oracle():
             for key in ("sharp", "flat", "corner_last", "surf_last"):
                 assert mismatch(f[key], orc.get(key)) == 0, (k, key)
             assert mismatch(f["transform_sum"], orc.get("transform_sum")) == 0
+            if k > 0:
+                assert mismatch(tf.integrated(), orc.get("integrated")) == 0
             m = mo.run(pts, 0.1 * k)
             assert m["ran"] == bool(fl & 2) and m["keyframe_saved"] == bool(fl & 4)
             if m["ran"]:
