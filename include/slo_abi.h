@@ -257,6 +257,28 @@ int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float
 int slo_gen_batch(int preset, int config_id, int stream0, int n_streams, int scan0, int n_scans, float* out,
                   int n_threads);
 
+/* Pose-graph back end (sc-lego-loam_amd/csrc/slo_pg.hip), host side.  Replaces
+ * mapOptimization's GTSAM iSAM2 graph: prior + odometry between factors
+ * (MO:365-368, 1541-1611), robust Cauchy loop factors (MO:985-997, 1038-1046,
+ * 1083-1091, the isam->update after them) and correctPoses (MO:1642-1664). */
+typedef struct slo_pg slo_pg;
+int slo_pg_create(slo_pg** out);
+void slo_pg_destroy(slo_pg* g);
+const char* slo_pg_last_error(slo_pg* g);
+int slo_pg_size(slo_pg* g);
+/* saveKeyFramesAndFactor's graph step: transform = transformAftMapped (transformTobeMapped
+ * for the first key frame), LeGO order rx ry rz tx ty tz; writes the updated
+ * transformAftMapped and the new cloudKeyPoses6D entry (x y z roll pitch yaw); either may be NULL */
+int slo_pg_add_keyframe(slo_pg* g, const float transform[6], float transform_out[6], float key_pose6d[6]);
+/* BetweenFactor(from_id, to_id, poseFrom.between(poseTo)), each pose given as the
+ * Pose3(Rot3::RzRyRx(v0, v1, v2), Point3(v3, v4, v5)) arguments the reference builds */
+int slo_pg_add_loop(slo_pg* g, int from_id, int to_id, const float pose_from[6], const float pose_to[6]);
+/* solve to convergence (max_iters <= 0: 100); iters_out / cost_out may be NULL */
+int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out);
+/* correctPoses: all key poses, 6 floats each; returns the count or a negative code */
+int slo_pg_get_key_poses(slo_pg* g, float* out6, int cap);
+int slo_pg_last_transform(slo_pg* g, float out[6]);
+
 #ifdef __cplusplus
 }
 #endif

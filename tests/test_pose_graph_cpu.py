@@ -1,0 +1,160 @@
+"""Pose-graph back end (csrc/slo_pg.hip) through the C ABI vs the numpy
+restatement oracle/oracle_pg.py — mapOptimization's iSAM2 graph (MO:365-368,
+985-997, 1038-1046, 1083-1091, 1541-1611) and correctPoses (MO:1642-1664).
+
+Host-only code: it runs here without a GPU.  Parity is unpinned against GTSAM
+(absent from the image, no fixtures in the reference); the oracle and the
+product solve the same graph independently.  Tolerances: outputs are float32,
+so 2e-4 m / 2e-5 rad between solver and oracle.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "sc-lego-loam_amd"))
+sys.path.insert(0, ROOT)
+
+from oracle import oracle_pg as O  # noqa: E402
+
+pg = pytest.importorskip("slo_amd.pose_graph")
+
+
+def _wrap(d, ang):
+    d = np.array(d, np.float64)
+    d[..., ang] = (d[..., ang] + np.pi) % (2 * np.pi) - np.pi
+    return np.abs(d)
+
+
+def _close_t(a, b, atol):      # LeGO transform order: angles first
+    return _wrap(np.asarray(a, np.float64) - b, slice(0, 3)).max() < atol
+
+
+def _close_k(a, b, atol):      # PointTypePose order: angles last
+    return _wrap(np.asarray(a, np.float64) - b, slice(3, 6)).max() < atol
+
+
+def _truth(n, laps=2, radius=20.0):
+    """Ground-truth key poses (GTSAM frame) on a circle driven `laps` times."""
+    out = []
+    for k in range(n):
+        a = 2 * np.pi * laps * k / n
+        T = O.pose(0.02 * np.sin(3 * a), 0.01 * np.cos(a), a + np.pi / 2,
+                   radius * np.cos(a), radius * np.sin(a), 0.5 * np.sin(2 * a))
+        out.append(T)
+    return out
+
+
+def _to_transform(T):
+    r = O.xyz(T[:3, :3])
+    return np.array([r[1], r[2], r[0], T[1, 3], T[2, 3], T[0, 3]])
+
+
+def _drifting(truth, seed, sigma=(0.002, 0.02)):
+    rng = np.random.default_rng(seed)
+    est = [truth[0]]
+    for k in range(1, len(truth)):
+        z = np.linalg.inv(truth[k - 1]) @ truth[k]
+        d = np.concatenate([rng.normal(0, sigma[0], 3), rng.normal(0, sigma[1], 3)])
+        est.append(est[-1] @ z @ O.exp(d))
+    return est
+
+
+def _build(truth, est, loops):
+    g, o = pg.PoseGraph(), O.Graph()
+    for T in est:
+        t = _to_transform(T)
+        g.add_keyframe(t)
+        o.add_keyframe(t)
+    for i, j, Z in loops:
+        a, b = np.zeros(6), O.to_rzryrx_args(Z)
+        g.add_loop(i, j, a, b)
+        o.add_loop(i, j, a, b)
+    return g, o
+
+
+def test_chain_reproduces_odometry():
+    truth = _truth(40, laps=1)
+    g = pg.PoseGraph()
+    for k, T in enumerate(truth):
+        t = _to_transform(T)
+        out, kp = g.add_keyframe(t)
+        assert _close_t(out, t, 2e-5)
+        assert _close_k(kp, O.to_key_pose6d(T), 2e-5)
+    assert len(g) == 40
+    it, cost = g.optimize()
+    assert cost < 1e-6
+    assert _close_k(g.key_poses(), np.array([O.to_key_pose6d(T) for T in truth]), 2e-5)
+
+
+def test_loops_match_oracle_and_reduce_drift():
+    n = 36
+    truth = _truth(n, laps=2)
+    est = _drifting(truth, seed=3)
+    half = n // 2
+    loops = [(k, k - half, np.linalg.inv(truth[k]) @ truth[k - half]) for k in (half + 2, n - 1)]
+    # an outlier loop: the Cauchy kernel must keep it from bending the map
+    loops.append((n - 5, 3, O.pose(0.3, -0.2, 0.5, 4.0, -3.0, 1.0)))
+    g, o = _build(truth, est, loops)
+    it, cost = g.optimize()
+    oc = o.optimize()
+    assert it >= 1 and np.isfinite(cost)
+    assert cost == pytest.approx(oc, rel=1e-4, abs=1e-6)
+    kp, ko = g.key_poses(), o.key_poses()
+    assert np.abs(kp[:, :3] - ko[:, :3]).max() < 2e-4
+    assert _wrap(kp[:, 3:] - ko[:, 3:], slice(0, 3)).max() < 2e-5
+    drift_before = np.linalg.norm(est[-1][:3, 3] - truth[-1][:3, 3])
+    kt = np.array([O.to_key_pose6d(T) for T in truth])
+    drift_after = np.linalg.norm(kp[-1, :3] - kt[-1, :3])
+    # the reference's odometry variances (1e-6 rad^2, 1e-8 m^2, MO:366) are
+    # ~1e7 times stiffer than its loop variance (0.5, MO:989): a loop only
+    # nudges the map toward truth, and the solve reproduces exactly that
+    assert drift_after < drift_before
+
+
+def test_keyframe_after_loop_continues_from_corrected_pose():
+    n = 24
+    truth = _truth(n + 1, laps=2)
+    est = _drifting(truth, seed=5)
+    g, o = _build(truth, est[:n], [(n - 1, n - 1 - (n + 1) // 2,
+                                    np.linalg.inv(truth[n - 1]) @ truth[n - 1 - (n + 1) // 2])])
+    g.optimize()
+    o.optimize()
+    t = _to_transform(est[n])   # transformAftMapped from scan-to-map, before the correction
+    out, kp = g.add_keyframe(t)
+    o.add_keyframe(t)
+    assert np.abs(kp[:3] - o.key_poses()[-1][:3]).max() < 2e-4
+    assert _close_t(out, o.last, 2e-4)
+
+
+def test_errors_are_loud():
+    g = pg.PoseGraph()
+    with pytest.raises(RuntimeError):
+        g.optimize()
+    g.add_keyframe(np.zeros(6))
+    with pytest.raises(RuntimeError, match="out of range"):
+        g.add_loop(0, 5, np.zeros(6), np.zeros(6))
+
+
+def test_long_map_converges():
+    """A KITTI-00-sized map (1500 key poses, many loops): the skyline solve
+    finishes and re-optimising is a fixed point."""
+    n = 1500
+    truth = _truth(n, laps=3, radius=150.0)
+    est = _drifting(truth, seed=11, sigma=(0.0005, 0.01))
+    third = n // 3
+    loops = [(k, k - third, np.linalg.inv(truth[k]) @ truth[k - third]) for k in range(third + 50, n, 97)]
+    g = pg.PoseGraph()
+    for T in est:
+        g.add_keyframe(_to_transform(T))
+    for i, j, Z in loops:
+        g.add_loop(i, j, np.zeros(6), O.to_rzryrx_args(Z))
+    it, cost = g.optimize()
+    kp = g.key_poses()
+    it2, cost2 = g.optimize()
+    assert cost2 <= cost * (1 + 1e-9) + 1e-12
+    assert _close_k(g.key_poses(), kp, 1e-3)
+    kt = np.array([O.to_key_pose6d(T) for T in truth])
+    assert np.linalg.norm(kp[-1, :3] - kt[-1, :3]) < np.linalg.norm(est[-1][:3, 3] - truth[-1][:3, 3])
