@@ -97,6 +97,8 @@ EXPORTS = [
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
     "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
+    # pose-graph back end (csrc/slo_pg.hip, host side)
+    "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform",
 ]
 
 
