@@ -35,6 +35,10 @@ extern "C" {
 #define SLO_E_HIP (-2)
 #define SLO_E_CAPACITY (-3)
 #define SLO_E_STATE (-4)
+/* a positive status is a result with a caveat, not an error: slo_pg_optimize
+ * stopped at max_iters before its convergence test held (the estimate is the
+ * last accepted iterate) */
+#define SLO_NOT_CONVERGED 1
 
 typedef struct slo_ctx slo_ctx;
 
@@ -273,7 +277,10 @@ int slo_pg_add_keyframe(slo_pg* g, const float transform[6], float transform_out
 /* BetweenFactor(from_id, to_id, poseFrom.between(poseTo)), each pose given as the
  * Pose3(Rot3::RzRyRx(v0, v1, v2), Point3(v3, v4, v5)) arguments the reference builds */
 int slo_pg_add_loop(slo_pg* g, int from_id, int to_id, const float pose_from[6], const float pose_to[6]);
-/* solve to convergence (max_iters <= 0: 100); iters_out / cost_out may be NULL */
+/* solve to convergence (max_iters <= 0: 100); iters_out / cost_out may be NULL.
+ * SLO_OK when the relative cost decrease fell below 1e-12 or no damping lowered
+ * the cost any more (converged to rounding); SLO_NOT_CONVERGED when max_iters
+ * ran out first */
 int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out);
 /* correctPoses: all key poses, 6 floats each; returns the count or a negative code */
 int slo_pg_get_key_poses(slo_pg* g, float* out6, int cap);

@@ -275,6 +275,34 @@ void oracle_sc_knn(const slo_config* cfg, const float* data, int n, const float*
     for (int c = 0; c < K; ++c) { idx[c] = ci[c]; dist[c] = cd[c]; }
 }
 
+// ---- slo_ddsum.h under test: sum of the exact float products a[i]*b[i]
+// mode 0 = sequential add (the oracle's loop), 1 = a pairwise merge tree of
+// per-element sums (the device reductions), 2 = 64 strided lane sums merged
+// in a butterfly (a wave's shuffle reduction); returns the rounded float
+float oracle_ddsum(const float* a, const float* b, int n, int mode) {
+    using namespace slo_dd;
+    if (mode == 0) {
+        DD s = zero();
+        for (int i = 0; i < n; ++i) add(s, (double)a[i] * (double)b[i]);
+        return to_float(s);
+    }
+    std::vector<DD> v;
+    if (mode == 1) {
+        for (int i = 0; i < n; ++i) { DD s = zero(); add(s, (double)a[i] * (double)b[i]); v.push_back(s); }
+    } else {
+        v.assign(64, zero());
+        for (int i = 0; i < n; ++i) add(v[i % 64], (double)a[i] * (double)b[i]);
+    }
+    if (v.empty()) return 0.0f;
+    while (v.size() > 1) {
+        std::vector<DD> w;
+        for (size_t i = 0; i + 1 < v.size(); i += 2) { DD s = v[i]; merge(s, v[i + 1]); w.push_back(s); }
+        if (v.size() & 1) w.push_back(v.back());
+        v.swap(w);
+    }
+    return to_float(v[0]);
+}
+
 // ---- libm self-test against the host glibc (tests/test_libm.py)
 long oracle_libm_selftest(long n, unsigned long seed) {
     uint64_t st = seed * 0x9E3779B97F4A7C15ULL + 1;

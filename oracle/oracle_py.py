@@ -95,6 +95,8 @@ def lib():
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
         L.oracle_set_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_ddsum.restype = ctypes.c_float
+        L.oracle_ddsum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.oracle_libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB

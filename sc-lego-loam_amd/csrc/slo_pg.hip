@@ -287,6 +287,21 @@ int fail(slo_pg* g, int code, const char* msg) {
     return code;
 }
 
+// the entry points promise not to throw (C callers): an allocation failure
+// inside becomes SLO_E_CAPACITY with the message kept
+template <class F>
+int guarded(slo_pg* g, const char* where, F&& f) {
+    try {
+        return f();
+    } catch (const std::bad_alloc&) {
+        try { if (g) g->err = std::string(where) + ": out of memory"; } catch (...) {}
+        return SLO_E_CAPACITY;
+    } catch (...) {
+        try { if (g) g->err = std::string(where) + ": internal error"; } catch (...) {}
+        return SLO_E_STATE;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -305,6 +320,7 @@ int slo_pg_size(slo_pg* g) { return g ? (int)g->est.size() : SLO_E_ARG; }
 
 int slo_pg_add_keyframe(slo_pg* g, const float transform[6], float transform_out[6], float key_pose6d[6]) {
     if (!g || !transform) return fail(g, SLO_E_ARG, "slo_pg_add_keyframe: null argument");
+    return guarded(g, "slo_pg_add_keyframe", [&]() -> int {
     double t[6];
     for (int k = 0; k < 6; ++k) t[k] = transform[k];
     Factor f;
@@ -337,6 +353,7 @@ int slo_pg_add_keyframe(slo_pg* g, const float transform[6], float transform_out
         key_pose6d[3] = (float)xyz[1]; key_pose6d[4] = (float)xyz[2]; key_pose6d[5] = (float)xyz[0];
     }
     return SLO_OK;
+    });
 }
 
 int slo_pg_add_loop(slo_pg* g, int from_id, int to_id, const float pose_from[6], const float pose_to[6]) {
@@ -344,6 +361,7 @@ int slo_pg_add_loop(slo_pg* g, int from_id, int to_id, const float pose_from[6],
     int n = (int)g->est.size();
     if (from_id < 0 || to_id < 0 || from_id >= n || to_id >= n || from_id == to_id)
         return fail(g, SLO_E_ARG, "slo_pg_add_loop: key pose id out of range");
+    return guarded(g, "slo_pg_add_loop", [&]() -> int {
     // Pose3(Rot3::RzRyRx(v0, v1, v2), Point3(v3, v4, v5)), as MO:1035-1037 / 1080-1082 build them
     Pose a = pose_rzryrx(pose_from[0], pose_from[1], pose_from[2], pose_from[3], pose_from[4], pose_from[5]);
     Pose b = pose_rzryrx(pose_to[0], pose_to[1], pose_to[2], pose_to[3], pose_to[4], pose_to[5]);
@@ -354,6 +372,7 @@ int slo_pg_add_loop(slo_pg* g, int from_id, int to_id, const float pose_from[6],
     f.robust = true;
     g->fac.push_back(f);
     return SLO_OK;
+    });
 }
 
 int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out) {
@@ -361,6 +380,7 @@ int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out) 
     int n = (int)g->est.size(), N = 6 * n;
     if (n == 0) return fail(g, SLO_E_STATE, "slo_pg_optimize: empty graph");
     if (max_iters <= 0) max_iters = 100;
+    return guarded(g, "slo_pg_optimize", [&]() -> int {
     // envelope: each pose's rows reach back to its lowest connected pose
     std::vector<int> lo(n);
     for (int p = 0; p < n; ++p) lo[p] = p;
@@ -385,6 +405,7 @@ int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out) 
     std::vector<Pose> trial(n);
     double cost = total_cost(g, g->est), lambda = 1e-5;
     int it = 0;
+    bool converged = false;
     for (; it < max_iters; ++it) {
         linearise(g, g->est, H, b);
         bool accepted = false;
@@ -403,12 +424,12 @@ int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out) 
                 lambda = lambda > 1e-12 ? lambda * 0.1 : lambda;
                 double old = cost;
                 cost = c;
-                if (dec <= 1e-12 * (old > 1e-300 ? old : 1e-300) || dec < 1e-18) { ++it; goto done; }
+                if (dec <= 1e-12 * (old > 1e-300 ? old : 1e-300) || dec < 1e-18) { ++it; converged = true; goto done; }
             } else {
                 lambda *= 10;
             }
         }
-        if (!accepted) break;  // no decrease at any damping: converged to rounding
+        if (!accepted) { converged = true; break; }  // no decrease at any damping: converged to rounding
     }
 done:
     // transformLast is not touched here: the reference refreshes it only in
@@ -416,7 +437,12 @@ done:
     // measured from the pre-correction pose, as in the reference
     if (iters_out) *iters_out = it;
     if (cost_out) *cost_out = cost;
+    if (!converged) {
+        g->err = "slo_pg_optimize: max_iters reached before convergence";
+        return SLO_NOT_CONVERGED;
+    }
     return SLO_OK;
+    });
 }
 
 // correctPoses (MO:1642-1664): cloudKeyPoses6D for every key pose, PointTypePose order x y z roll pitch yaw

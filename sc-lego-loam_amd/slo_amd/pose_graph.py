@@ -77,8 +77,11 @@ class PoseGraph:
         self._check(self._L.slo_pg_add_loop(self._g, int(from_id), int(to_id), ap, bp))
 
     def optimize(self, max_iters=100):
+        """(iterations, final cost); ``self.converged`` is False when max_iters ran out first"""
         it, cost = ctypes.c_int(), ctypes.c_double()
-        self._check(self._L.slo_pg_optimize(self._g, int(max_iters), ctypes.byref(it), ctypes.byref(cost)))
+        rc = self._L.slo_pg_optimize(self._g, int(max_iters), ctypes.byref(it), ctypes.byref(cost))
+        self._check(rc)
+        self.converged = rc == 0
         return it.value, cost.value
 
     def key_poses(self):

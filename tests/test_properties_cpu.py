@@ -7,7 +7,7 @@ import ctypes
 
 import numpy as np
 import pytest
-from hypothesis import HealthCheck, given, settings, strategies as st
+from hypothesis import HealthCheck, example, given, settings, strategies as st
 
 import oracle_py as O
 
@@ -57,6 +57,11 @@ def voxel_grid_numpy(pts, leaf):
     p = pts.astype(np.float32)
     inv = np.float32(1.0) / np.float32(leaf)
     mn, mx = p[:, :3].min(axis=0), p[:, :3].max(axis=0)
+    # PCL's int32 guard (voxel_grid.cpp applyFilter): when the cell count of
+    # the bounding box overflows int32 the filter warns and returns the input
+    cells = [int(np.float32((mx[a] - mn[a]) * inv)) + 1 for a in range(3)]
+    if cells[0] * cells[1] * cells[2] > 2**31 - 1:
+        return p.copy()
     minb = np.floor(mn * inv).astype(np.int64)
     maxb = np.floor(mx * inv).astype(np.int64)
     div = maxb - minb + 1
@@ -76,6 +81,8 @@ def voxel_grid_numpy(pts, leaf):
 @FAST
 @given(seed=st.integers(0, 2**31 - 1), n=st.integers(1, 400), leaf=st.sampled_from([0.2, 0.3, 0.4, 0.5]),
        spread=st.floats(0.5, 40.0))
+@example(seed=0, n=365, leaf=0.2, spread=40.0)   # 1368*1355*1165 cells > 2^31-1: the input comes back
+@example(seed=1, n=50, leaf=0.5, spread=1.0)     # far below the guard: a real filter
 def test_voxel_grid_matches_independent_restatement(seed, n, leaf, spread):
     rng = np.random.default_rng(seed)
     pts = np.zeros((n, 4), np.float32)
@@ -83,6 +90,8 @@ def test_voxel_grid_matches_independent_restatement(seed, n, leaf, spread):
     pts[:, 3] = rng.uniform(0, 64, size=n)
     got = O.voxel_grid(pts, leaf, stable=True)
     want = voxel_grid_numpy(pts, leaf)
+    if (seed, n, leaf, spread) == (0, 365, 0.2, 40.0):
+        assert want.tobytes() == pts.tobytes()   # the pinned example does take the overflow branch
     assert got.shape == want.shape and len(got) <= n
     assert got.view(np.uint32).tobytes() == want.view(np.uint32).tobytes()
 
