@@ -10,10 +10,16 @@ mapOptimization + SCManager, with the deterministic gating of SURVEY §8(d):
 mapping on every 4th scan, SC detect per saved keyframe).  Each rank owns
 --streams independent streams (weak scaling, slo_amd/dist.py); per step the
 ranks all-gather a 160-byte record per stream (poses + newest SC ring key)
-over RCCL.  Inputs are generated on the host and resident in HBM before
-timing.  Each stream's Scan Context history is seeded with --history earlier
-scans of its own trajectory so loop detection does its full K-NN + K
-candidate-distance work.
+over RCCL.
+
+Steady state: every stream first runs --preroll scans untimed (default 210:
+the local map holds its full 50 keyframes, MO:1127-1166, and Scan Context
+detect has >= 51 contexts, SCc:257), fed in chunks; then the --warmup and
+timed --steps scans are generated and resident in HBM before timing.  Inputs
+come from the device generator (csrc/slo_gendev.hip), bit-identical to the
+host generator the CPU baseline uses.  A one-stream leg (single_stream)
+reports the same pipeline for a single C3 stream: scans/s and per-scan
+latency.
 
 roofline: the dominant kernel (--roofline-kernel, mo_knn: the largest share of
 device time) timed with HIP events on its context's stream inside the timed
@@ -21,8 +27,12 @@ region; achieved = its algorithmic bytes per launch (DESIGN.md "Roofline",
 from the per-stream counts of a separate instrumented pass with the same
 launch mix) / that average launch time, against HBM peak.  `isolated` repeats
 it for the instrumented pass, where the contexts run one after the other.  cpu_baseline: the
-oracle (oracle/, C++ restatement of the reference path) on this host's cores,
-rank 0 at N = 1, a bounded sample of the same workload.
+oracle (oracle/, C++ restatement of the reference path), rank 0 at N = 1, on
+the same steady-state window: (B) one stream per host core available to the
+process (sched_getaffinity), --cpu-scans scans each after the pre-roll;
+(A) the reference's topology — one stream as a 3-stage pipeline
+(imageProjection | featureAssociation | mapOptimization, launch/run.launch) on
+3 cores — bounded by its slowest stage's per-scan time, measured.
 """
 import argparse
 import json
@@ -43,29 +53,36 @@ METRIC = "scans/sec end-to-end (proj+feat+LM+SC), 64-ring 1800-col, 1/2/4/8 GPU"
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--preroll", type=int, default=210,
+                    help="untimed scans per stream before the warmup (fills the 50-keyframe local map)")
+    ap.add_argument("--chunk", type=int, default=8, help="scans per device-generation chunk of the pre-roll")
     ap.add_argument("--streams", type=int, default=512, help="streams per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
-    ap.add_argument("--stagger", action="store_true",
-                    help="context g runs g scans ahead, so the streams of different contexts reach mapping on "
-                         "different steps (measured slower than the default lockstep phases: 39.1k vs 40.1k scans/s)")
     ap.add_argument("--preset", default="hdl64_1800")
     ap.add_argument("--keyframe-cap", type=int, default=32768,
                     help="slo_config.keyframe_cloud_cap: points per keyframe surf/outlier cloud (0 = worst case); "
                          "an overflow sets the stream's error bit, reported as stream_errors")
     ap.add_argument("--config-id", type=int, default=3)
-    ap.add_argument("--history", type=int, default=60, help="seeded Scan Context history per stream")
+    ap.add_argument("--history", type=int, default=0,
+                    help="extra Scan Context history per stream (scans before scan 0); the pre-roll builds the real one")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
     ap.add_argument("--roofline-kernel", default="mo_knn",
                     help="kernel timed with HIP events inside the timed region (the roofline's kernel)")
-    ap.add_argument("--cpu-scans", type=int, default=40, help="scans per CPU thread in the baseline (0 = skip)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cores available)")
+    ap.add_argument("--cpu-scans", type=int, default=6, help="timed scans per CPU stream in the baseline (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in sched_getaffinity")
+    ap.add_argument("--cpu-distinct", type=int, default=8,
+                    help="distinct CPU streams pre-rolled in parallel; the others continue from copies of them")
+    ap.add_argument("--single-steps", type=int, default=100, help="timed scans of the one-stream leg (0 = skip)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
     ap.add_argument("--icp-jobs", type=int, default=64,
                     help="loop-verification ICP alignments per batch in the separate ICP measurement (0 = skip)")
+    ap.add_argument("--roctx", action="store_true",
+                    help="bracket the timed steps with roctxProfilerResume/Pause, so `rocprofv3 --selected-regions` "
+                         "traces exactly the timed window (profiles/ README)")
     ap.add_argument("--traffic-from", default=None,
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
     return ap.parse_args()
@@ -193,6 +210,102 @@ def icp_bench(torch, slo_amd, pid, a, local, gthreads, reps=3):
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])}}
 
 
+def host_info():
+    """nproc, cores this process may run on, cgroup CPU quota, CPU model, glibc"""
+    import platform
+    info = {"nproc": os.cpu_count()}
+    try:
+        info["affinity_cores"] = len(os.sched_getaffinity(0))
+    except Exception:
+        info["affinity_cores"] = os.cpu_count()
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        info["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(per), 2)
+    except Exception:
+        info["cgroup_cpu_quota"] = None
+    try:
+        info["cpu_model"] = next(l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name"))
+    except Exception:
+        info["cpu_model"] = platform.processor() or None
+    try:
+        info["glibc"] = os.confstr("CS_GNU_LIBC_VERSION")
+    except Exception:
+        info["glibc"] = " ".join(platform.libc_ver())
+    return info
+
+
+def cpu_baseline(a, pid, ncpu):
+    """SURVEY §8(d) CPU baselines on the oracle (C++ restatement, g++ -O2), same window as the GPU"""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ctypes
+    import oracle_py as O
+    th = a.cpu_threads or ncpu
+    stage = (ctypes.c_double * 4)()
+    one = (ctypes.c_double * 4)()
+    t0 = time.time()
+    secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, a.preroll + a.warmup, a.history,
+                                min(a.cpu_distinct, th), stage, one)
+    wall = time.time() - t0
+    n = a.cpu_scans
+    # (A): one stream as the reference's 3 processes on 3 cores; the pipeline
+    # runs at the pace of its slowest stage (mapOptimization includes SC)
+    per = {"ip": one[0] / n, "fa": one[1] / n, "mo_sc": (one[2] + one[3]) / n}
+    a_val = 1.0 / max(per.values())
+    info = host_info()
+    return {"value": round(th * n / secs, 3), "unit": "scans/s", "cores": th, "kind": "port",
+            "sample": f"(B) {th} independent {a.preset} streams, one per core in sched_getaffinity, each timed over "
+                      f"scans {a.preroll + a.warmup}..{a.preroll + a.warmup + n - 1} after an untimed pre-roll "
+                      f"(the GPU's steady-state window); {min(a.cpu_distinct, th)} streams pre-rolled, the rest "
+                      f"continue from copies; oracle/ C++ restatement g++ -O2",
+            "seconds": round(secs, 2), "wall_seconds_incl_preroll": round(wall, 1),
+            "one_stream_scans_per_s": round(n / sum(one), 3),
+            "stage_seconds": {"ip": round(stage[0], 2), "fa": round(stage[1], 2), "mo": round(stage[2], 2),
+                              "sc": round(stage[3], 2)},
+            "A_reference_topology": {"value": round(a_val, 3), "unit": "scans/s", "cores": 3,
+                                     "stage_ms_per_scan": {k: round(v * 1e3, 3) for k, v in per.items()},
+                                     "note": "one stream, imageProjection | featureAssociation | mapOptimization "
+                                             "(launch/run.launch:14-17) on 3 cores: 1 / slowest stage's measured "
+                                             "per-scan time"},
+            "host": info}
+
+
+def single_stream(torch, slo_amd, a, cfg, pid, local):
+    """one C3 stream through the same pipeline: scans/s (async) and per-scan latency (synchronised)"""
+    P = cfg.max_points
+    ctx = slo_amd.Context(cfg, local, 1)
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
+    n = a.preroll + a.warmup + a.single_steps
+    try:
+        buf = torch.empty((n, 1, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+        gen.scans(0, n, buf.data_ptr())
+        cnt = torch.full((1,), P, dtype=torch.int32, device=f"cuda:{local}")
+        k0 = a.preroll + a.warmup
+        for k in range(k0):
+            ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        ctx.synchronize()
+        half = a.single_steps // 2
+        t0 = time.perf_counter()
+        for k in range(k0, k0 + half):    # back to back: launch overlap, the stream's throughput
+            ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        ctx.synchronize()
+        thr = half / (time.perf_counter() - t0)
+        lat = []
+        for k in range(k0 + half, k0 + a.single_steps):   # one at a time: the latency of a scan
+            t1 = time.perf_counter()
+            ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            ctx.synchronize()
+            lat.append(time.perf_counter() - t1)
+        lat = np.array(lat) * 1e3
+        kf = int(ctx.get(0, "n_keyframes")[0])
+        return {"value": round(thr, 2), "unit": "scans/s", "streams": 1, "scans_timed": half,
+                "latency_ms": {"mean": round(float(lat.mean()), 3), "p50": round(float(np.median(lat)), 3),
+                               "p99": round(float(np.percentile(lat, 99)), 3), "scans": len(lat)},
+                "keyframes_at_end": kf, "err": int(ctx.get(0, "err")[0])}
+    finally:
+        gen.close()
+        ctx.close()
+
+
 def main():
     a = parse()
     import torch
@@ -217,28 +330,24 @@ def main():
     pid = slo_amd.PRESETS[a.preset]
     P = cfg.max_points
     S = a.streams
-    lag = (lambda g: g) if a.stagger else (lambda g: 0)   # scans context g runs ahead
-    ntot = a.warmup + a.steps + a.profile_steps + (max(0, a.groups - 1) if a.stagger else 0)
     try:
         ncpu = len(os.sched_getaffinity(0))
     except Exception:
         ncpu = os.cpu_count() or 8
     gthreads = max(1, min(16, ncpu))
 
-    # ---- inputs (host generation, then resident in HBM)
+    # ---- contexts, then the resident window [preroll, preroll + warmup + steps + profile)
     t_gen = time.time()
     stream0, _ = sdist.stream_shard(rank, world, S)
-    dev = torch.empty((ntot, S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
-    for k0 in range(0, ntot, 4):
-        nk = min(4, ntot - k0)
-        dev[k0:k0 + nk].copy_(torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, k0, nk, P, gthreads)))
-    cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
-
     groups = sdist.group_slices(S, a.groups)
     free0 = torch.cuda.mem_get_info(local)[0]
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
     ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     n_ctx = len(ctxs)
+    nwin = a.warmup + a.steps + a.profile_steps
+    dev = torch.empty((max(nwin, a.chunk), S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+    cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
     rec_n = ctxs[0].L.slo_record_floats()
     rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
     gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
@@ -253,29 +362,36 @@ def main():
         for f in [pool.submit(fn, g, c, *groups[g]) for g, c in enumerate(ctxs)]:
             f.result()
 
-    # seed Scan Context history (makeAndSaveScancontextAndKeys) in chunks
-    for h0 in range(-a.history, 0, 4):
-        nh = min(4, -h0)
-        hist = torch.from_numpy(slo_amd.gen_batch(pid, a.config_id, stream0, S, h0, nh, P, gthreads)).cuda(local)
-        for h in range(nh):
-            each(lambda g, c, o, n: c.batch_sc_make(hist[h, o].data_ptr(), cnt[o].data_ptr()))
-        each(lambda g, c, o, n: c.synchronize())
-        del hist
-    t_gen = time.time() - t_gen
-
     def sync_all():
         each(lambda g, c, o, n: c.synchronize())
 
-    # staggered phases: context g first runs its first lag(g) scans alone; from
-    # then on every context advances one scan per step (scan k + lag(g))
-    for g, c in enumerate(ctxs):
-        o = groups[g][0]
-        for j in range(lag(g)):
-            c.batch_process(dev[j, o].data_ptr(), cnt[o].data_ptr(), 0.1 * j)
-    sync_all()
+    # optional extra Scan Context history (makeAndSaveScancontextAndKeys of scans before 0)
+    for h0 in range(-a.history, 0, a.chunk):
+        nh = min(a.chunk, -h0)
+        gen.scans(h0, nh, dev.data_ptr())
+        for h in range(nh):
+            each(lambda g, c, o, n: c.batch_sc_make(dev[h, o].data_ptr(), cnt[o].data_ptr()))
+        sync_all()
+    t_gen = time.time() - t_gen
 
-    def step(k):
-        each(lambda g, c, o, n: c.batch_process(dev[k + lag(g), o].data_ptr(), cnt[o].data_ptr(), 0.1 * (k + lag(g))))
+    # ---- pre-roll: scans [0, preroll), generated on the device a chunk at a time
+    t_pre = time.time()
+    for k0 in range(0, a.preroll, a.chunk):
+        nk = min(a.chunk, a.preroll - k0)
+        sync_all()
+        gen.scans(k0, nk, dev.data_ptr())
+        for j in range(nk):
+            each(lambda g, c, o, n: c.batch_process(dev[j, o].data_ptr(), cnt[o].data_ptr(), 0.1 * (k0 + j)))
+    sync_all()
+    t_pre = time.time() - t_pre
+    base = a.preroll
+    t1 = time.time()
+    gen.scans(base, nwin, dev.data_ptr())
+    gen.close()
+    t_gen += time.time() - t1
+
+    def step(k):   # k = index into the resident window; scan base + k
+        each(lambda g, c, o, n: c.batch_process(dev[k, o].data_ptr(), cnt[o].data_ptr(), 0.1 * (base + k)))
         if gather:   # records of every group, then one all-gather after all of them
             evs = []
             for g, c in enumerate(ctxs):
@@ -304,6 +420,11 @@ def main():
         c.timing(True)
         c.timing_filter(a.roofline_kernel)
         c.timing_reset()
+    roctx = None
+    if a.roctx:
+        import ctypes
+        roctx = ctypes.CDLL("librocprofiler-sdk-roctx.so")
+        roctx.roctxProfilerResume(ctypes.c_uint64(0))
     t0 = time.perf_counter()
     for k in range(a.warmup, a.warmup + a.steps):
         step(k)
@@ -312,6 +433,8 @@ def main():
     if world > 1:
         dist.barrier()
     el = sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
+    if roctx is not None:
+        roctx.roctxProfilerPause(ctypes.c_uint64(0))
     live_ms, live_n = 0.0, 0
     for c in ctxs:
         for kn, (kms, kcalls) in c.timing_read().items():
@@ -322,6 +445,7 @@ def main():
         c.timing_filter(None)
     value = S * a.steps * world / el
     errs = sum(int(c.get(s, "err")[0]) != 0 for c in ctxs for s in range(c.n_streams))
+    kfs = np.array([int(c.get(s, "n_keyframes")[0]) for c in ctxs for s in range(c.n_streams)])
 
     # ---- instrumented pass: per-kernel HIP-event times on each context's
     # stream, groups run one after the other so the events time each kernel alone
@@ -334,8 +458,7 @@ def main():
         map_steps = 0
         for k in range(k0, k0 + a.profile_steps):
             for g, c in enumerate(ctxs):
-                c.batch_process(dev[k + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
-                                0.1 * (k + lag(g)))
+                c.batch_process(dev[k, groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(), 0.1 * (base + k))
                 c.synchronize()
             map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
         for c in ctxs:
@@ -348,9 +471,6 @@ def main():
         workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1}
         total_ms = sum(v[0] for v in kt.values())
         name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
-        avg_s = ms / 1e3 / max(1, n)
-        b = algo_bytes(name, counts, cfg, S, a.profile_steps, map_steps)
-        ach = b / n / avg_s / 1e9 if b is not None else None
         for kn, (kms, kcalls) in kt.items():
             kb = algo_bytes(kn, counts, cfg, S, a.profile_steps, map_steps)
             if kb is not None and kms > 0:
@@ -382,6 +502,16 @@ def main():
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
                 "traffic": None, "kernel": a.roofline_kernel,
                 "avg_launch_us": round(live_ms / live_n * 1e3, 2), "launches_timed": live_n}
+    for c in ctxs:
+        c.close()
+    ctxs = []
+    del dev
+    torch.cuda.empty_cache()
+
+    # ---- one stream alone (C3 is defined on one KITTI replay)
+    one = None
+    if rank == 0 and a.single_steps > 0:
+        one = single_stream(torch, slo_amd, a, cfg, pid, local)
 
     # ---- loop verification (MO:964-1110), measured apart
     # from the headline (not part of the metric): a batch of --icp-jobs ICP
@@ -390,50 +520,42 @@ def main():
     # 4th point of the same scan (~29k points, a voxelised submap's density)
     icp = None
     if rank == 0 and a.icp_jobs > 0:
-        for c in ctxs:
-            c.close()
-        ctxs = []
         icp = icp_bench(torch, slo_amd, pid, a, local, gthreads)
 
     # ---- CPU baseline (oracle = C++ restatement of the reference), rank 0, N = 1
     cpu = None
     if rank == 0 and world == 1 and a.cpu_scans > 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import ctypes
-        import oracle_py as O
-        th = a.cpu_threads or max(1, min(16, ncpu))
-        stage = (ctypes.c_double * 4)()
-        secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, 4, a.history, stage)
-        per_stream = a.cpu_scans / (sum(stage) / th)
-        cpu = {"value": round(th * a.cpu_scans / secs, 3), "unit": "scans/s", "cores": th, "kind": "port",
-               "sample": f"{th} independent {a.preset} streams x {a.cpu_scans} scans (after 4 warm-up scans, "
-                         f"{a.history}-entry SC history), oracle/ C++ restatement g++ -O2, one stream per thread",
-               "seconds": round(secs, 2), "one_stream_scans_per_s": round(per_stream, 3),
-               "stage_seconds": {"ip": round(stage[0], 2), "fa": round(stage[1], 2), "mo": round(stage[2], 2),
-                                 "sc": round(stage[3], 2)}}
+        cpu = cpu_baseline(a, pid, ncpu)
 
     if rank == 0:
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10",
+            "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10, "
+                                   "steady state",
                        "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
-                       "scans_per_step": S * world,
-                       "sc_history_seed": a.history, "context_phase_lag": [lag(g) for g in range(n_ctx)],
+                       "scans_per_step": S * world, "preroll_scans": a.preroll,
+                       "timed_scans": [base + a.warmup, base + a.warmup + a.steps - 1],
+                       "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
+                       "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),
+                       "sc_history_seed": a.history,
                        "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
+            "speedup_vs_cpu_A": round(value / cpu["A_reference_topology"]["value"], 2) if cpu else None,
+            "single_stream": one,
+            "single_stream_speedup_vs_cpu_A": (round(one["value"] / cpu["A_reference_topology"]["value"], 2)
+                                               if (one and cpu) else None),
             "stream_errors": errs,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
             "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
-            "setup_seconds": round(t_gen, 1), "context_hbm_gb": round(ctx_bytes / 2**30, 2),
+            "setup_seconds": round(t_gen, 1), "preroll_seconds": round(t_pre, 1),
+            "context_hbm_gb": round(ctx_bytes / 2**30, 2),
             "loop_verify_icp": icp,
         }
         print(json.dumps(out), flush=True)
-    for c in ctxs:
-        c.close()
     if pool is not None:
         pool.shutdown()
     if gather:

@@ -261,6 +261,16 @@ int slo_gen_scan(int preset, int config_id, int stream_id, int scan_index, float
 int slo_gen_batch(int preset, int config_id, int stream0, int n_streams, int scan0, int n_scans, float* out,
                   int n_threads);
 
+/* The same generator on the device (csrc/slo_gendev.hip; benchmark inputs):
+ * scans of streams stream0 .. stream0+n_streams-1, bit-identical to
+ * slo_gen_batch.  slo_gen_device_scans writes [n_scans][n_streams][max_points][4]
+ * floats to device memory d_out on hip_stream (a hipStream_t, NULL = default)
+ * and returns when they are written; n_scans * n_streams <= 65535 per call. */
+typedef struct slo_gen_dev slo_gen_dev;
+int slo_gen_device_create(int preset, int config_id, int stream0, int n_streams, int hip_device, slo_gen_dev** out);
+int slo_gen_device_scans(slo_gen_dev* g, int scan0, int n_scans, void* d_out, void* hip_stream);
+void slo_gen_device_destroy(slo_gen_dev* g);
+
 /* Pose-graph back end (sc-lego-loam_amd/csrc/slo_pg.hip), host side.  Replaces
  * mapOptimization's GTSAM iSAM2 graph: prior + odometry between factors
  * (MO:365-368, 1541-1611), robust Cauchy loop factors (MO:985-997, 1038-1046,

@@ -331,31 +331,34 @@ int oracle_gen_scan(int preset, int config_id, int stream_id, int k, float* out)
     return slo_gen::stream_scan(s, k, out);
 }
 
-// ---- CPU baseline: n_threads independent streams, each processing n_scans
-// pre-generated scans (generation excluded from timing).  Returns wall
-// seconds of the processing; per-stage seconds summed over threads in stage_s[4]
-// (ip, fa, mo, sc).
-double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int warmup, int history, double* stage_s) {
+// ---- CPU baseline (bench.py cpu_baseline leg; SURVEY §8(d) "(B) all host
+// cores"): n_threads independent streams, one per thread, each timed over
+// scans [preroll, preroll + n_scans) after an untimed pre-roll of scans
+// [0, preroll) that fills its local map and Scan Context history (the same
+// window the GPU bench times).  The pre-roll runs on n_distinct streams in
+// parallel; thread t then continues from a copy of stream t % n_distinct
+// (the state a stream reaches is data, not timing), so a many-core host pays
+// the pre-roll once per distinct stream.  `history` seeds the SC history with
+// that many earlier scans (bench --history).  Returns the wall seconds of the
+// timed window; stage_s[4] = per-stage seconds summed over threads (ip, fa,
+// mo, sc); stage_one[4] = the same for thread 0 alone (the reference's
+// one-stream 3-process topology, SURVEY (A)).
+double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int preroll, int history, int n_distinct,
+                    double* stage_s, double* stage_one) {
     slo_config cfg;
-    if (slo_config_preset_impl(preset, &cfg)) return -1;
+    if (slo_config_preset_impl(preset, &cfg) || n_threads <= 0 || n_scans <= 0) return -1;
+    if (n_distinct <= 0 || n_distinct > n_threads) n_distinct = n_threads;
     const int P = cfg.n_scan * cfg.horizon_scan;
-    std::vector<std::vector<float>> scans((size_t)n_threads * (n_scans + warmup));
-    std::vector<OracleStream*> streams(n_threads, nullptr);
+    std::vector<OracleStream*> base(n_distinct, nullptr);
+    std::vector<std::vector<float>> scans((size_t)n_distinct * n_scans);
     {
         std::vector<std::thread> g;
-        for (int t = 0; t < n_threads; ++t)
+        for (int t = 0; t < n_distinct; ++t)
             g.emplace_back([&, t]() {
                 slo_gen::Stream s = slo_gen::make_stream(cfg, config_id, t);
-                for (int k = 0; k < n_scans + warmup; ++k) {
-                    auto& v = scans[(size_t)t * (n_scans + warmup) + k];
-                    v.resize((size_t)P * 4);
-                    slo_gen::stream_scan(s, k, v.data());
-                }
-                // Scan Context history of `history` earlier scans (same as
-                // slo_batch_sc_make in bench.py): VoxelGrid(0.5) + make&save
-                streams[t] = new OracleStream(cfg);
+                base[t] = new OracleStream(cfg);
                 std::vector<float> buf((size_t)P * 4);
-                for (int h = 0; h < history; ++h) {
+                for (int h = 0; h < history; ++h) {   // SC history seed: VoxelGrid(leaf_sc) + make&save
                     slo_gen::stream_scan(s, h - history, buf.data());
                     Cloud c, ds;
                     for (int i = 0; i < P; ++i) {
@@ -363,11 +366,22 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
                         if (std::isfinite(p[0]) && std::isfinite(p[1]) && std::isfinite(p[2])) c.push_back({p[0], p[1], p[2], p[3]});
                     }
                     voxel_grid(c, cfg.leaf_sc, ds, false);
-                    streams[t]->mo.sc.makeAndSaveScancontextAndKeys(ds);
+                    base[t]->mo.sc.makeAndSaveScancontextAndKeys(ds);
+                }
+                for (int k = 0; k < preroll; ++k) {
+                    slo_gen::stream_scan(s, k, buf.data());
+                    base[t]->step(buf.data(), P, 0.1 * k);
+                }
+                for (int k = 0; k < n_scans; ++k) {
+                    auto& v = scans[(size_t)t * n_scans + k];
+                    v.resize((size_t)P * 4);
+                    slo_gen::stream_scan(s, preroll + k, v.data());
                 }
             });
         for (auto& th : g) th.join();
     }
+    std::vector<OracleStream*> streams(n_threads, nullptr);
+    for (int t = 0; t < n_threads; ++t) streams[t] = t < n_distinct ? base[t] : new OracleStream(*base[t % n_distinct]);
     std::vector<double> st(4 * n_threads, 0.0);
     std::atomic<int> ready{0};
     std::atomic<bool> go{false};
@@ -376,13 +390,14 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
     for (int t = 0; t < n_threads; ++t)
         th.emplace_back([&, t]() {
             OracleStream& s = *streams[t];
-            for (int k = 0; k < warmup; ++k) s.step(scans[(size_t)t * (n_scans + warmup) + k].data(), P, 0.1 * k);
+            const int src = t % n_distinct;
             ready++;
             while (!go.load()) std::this_thread::yield();
             auto T0 = std::chrono::steady_clock::now();
             tstart[t] = std::chrono::duration<double>(T0.time_since_epoch()).count();
-            for (int k = warmup; k < n_scans + warmup; ++k) {
-                const float* p = scans[(size_t)t * (n_scans + warmup) + k].data();
+            for (int k = 0; k < n_scans; ++k) {
+                const float* p = scans[(size_t)src * n_scans + k].data();
+                const double tk = 0.1 * (preroll + k);
                 auto a = std::chrono::steady_clock::now();
                 s.det_valid = false;
                 s.ip.cloudHandler(p, P);
@@ -392,7 +407,7 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
                 bool kf = false;
                 if (s.fa.published_to_mapping) {
                     bool ran = s.mo.run(s.fa.laserCloudCornerLast, s.fa.laserCloudSurfLast, s.fa.outlierCloud,
-                                        s.fa.transformSum, p, P, 0.1 * k);
+                                        s.fa.transformSum, p, P, tk);
                     kf = ran && s.mo.saved_keyframe;
                 }
                 auto d = std::chrono::steady_clock::now();
@@ -412,12 +427,17 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int w
     for (auto* p : streams) delete p;
     double t0 = *std::min_element(tstart.begin(), tstart.end());
     double t1 = *std::max_element(tend.begin(), tend.end());
-    if (stage_s)
-        for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 4; ++k) {
+        if (stage_s) {
             stage_s[k] = 0;
             for (int t = 0; t < n_threads; ++t) stage_s[k] += st[4 * t + k];
         }
+        if (stage_one) stage_one[k] = st[k];
+    }
     return t1 - t0;
 }
+
+// keyframes held by a stream after `preroll` scans (what the bench's window sees)
+int oracle_stream_keyframes(void* h) { return (int)((OracleStream*)h)->mo.keyPoses.size(); }
 
 }  // extern "C"

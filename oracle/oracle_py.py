@@ -72,8 +72,7 @@ def lib():
         L.oracle_libm_selftest.restype = ctypes.c_long
         L.oracle_libm_selftest.argtypes = [ctypes.c_long, ctypes.c_ulong]
         L.oracle_bench.restype = ctypes.c_double
-        L.oracle_bench.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
-                                   ctypes.c_void_p]
+        L.oracle_bench.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_sc_distance.restype = ctypes.c_double
         L.oracle_sc_distance.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_int)]

@@ -15,7 +15,12 @@
 // removeNaNFromPointCloud (imageProjection.cpp:170) is exercised.
 //
 // Everything is integer hashing plus +,-,*,/,sqrt and slo_libm trig, so the
-// stream is bit-identical on every host.
+// stream is bit-identical on every host.  The per-ray work (ray_point) is
+// __host__ __device__: it uses only IEEE-exact operations (+ - * / sqrt
+// floor fabs, integer hashing) on values the host prepares once — ray
+// direction tables, the sensor pose with its yaw cos/sin, the objects near
+// the pose — so the device generator (slo_gendev.hip) emits the same bits
+// as the host loop below (tests/test_gpu_gen.py).
 #pragma once
 
 #include <stdint.h>
@@ -25,18 +30,25 @@
 #include "slo_config.h"
 #include "slo_libm.h"
 
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define SLO_GEN_HD __host__ __device__ inline
+#else
+#define SLO_GEN_HD inline
+#endif
+
 namespace slo_gen {
 
-inline uint64_t mix64(uint64_t x) {
+SLO_GEN_HD uint64_t mix64(uint64_t x) {
     x ^= x >> 30; x *= 0xbf58476d1ce4e5b9ULL;
     x ^= x >> 27; x *= 0x94d049bb133111ebULL;
     x ^= x >> 31;
     return x;
 }
 // uniform in [0,1)
-inline double u01(uint64_t h) { return (double)(mix64(h) >> 11) * (1.0 / 9007199254740992.0); }
+SLO_GEN_HD double u01(uint64_t h) { return (double)(mix64(h) >> 11) * (1.0 / 9007199254740992.0); }
 // approx N(0,1) by Irwin-Hall(4): pure arithmetic, platform independent
-inline double gauss(uint64_t h) {
+SLO_GEN_HD double gauss(uint64_t h) {
     double s = u01(h) + u01(h ^ 0x9e3779b97f4a7c15ULL) + u01(h ^ 0x3c6ef372fe94f82bULL) +
                u01(h ^ 0xdaa66d2c7ddf743fULL);
     return (s - 2.0) * 1.7320508075688772;  // var(sum)=1/3
@@ -139,19 +151,23 @@ inline Scene make_scene(uint64_t seed) {
     return sc;
 }
 
-inline float ground_height(const Scene& s, double x, double y) {
+// lattice value of ground_height (the signed products wrap, computed unsigned)
+SLO_GEN_HD double ground_lattice(uint64_t seed, int64_t a, int64_t b) {
+    return 0.02 * (2.0 * u01((seed * 1000003ULL + (uint64_t)a * 73856093ULL) ^ ((uint64_t)b * 19349663ULL)) - 1.0);
+}
+
+SLO_GEN_HD float ground_height_seed(uint64_t seed, double x, double y) {
     // smooth-ish roughness (+-2 cm) from a hashed 2 m lattice, bilinear
     double gx = x * 0.5, gy = y * 0.5;
     double fx = floor(gx), fy = floor(gy);
     int64_t ix = (int64_t)fx, iy = (int64_t)fy;
     double tx = gx - fx, ty = gy - fy;
-    auto hv = [&](int64_t a, int64_t b) {
-        return 0.02 * (2.0 * u01((s.seed * 1000003ULL + (uint64_t)(a * 73856093LL)) ^ (uint64_t)(b * 19349663LL)) - 1.0);
-    };
-    double v = (1 - tx) * (1 - ty) * hv(ix, iy) + tx * (1 - ty) * hv(ix + 1, iy) +
-               (1 - tx) * ty * hv(ix, iy + 1) + tx * ty * hv(ix + 1, iy + 1);
+    double v = (1 - tx) * (1 - ty) * ground_lattice(seed, ix, iy) + tx * (1 - ty) * ground_lattice(seed, ix + 1, iy) +
+               (1 - tx) * ty * ground_lattice(seed, ix, iy + 1) + tx * ty * ground_lattice(seed, ix + 1, iy + 1);
     return (float)v;
 }
+
+inline float ground_height(const Scene& s, double x, double y) { return ground_height_seed(s.seed, x, y); }
 
 struct SensorPose { double x, y, z, yaw; };
 
@@ -185,92 +201,110 @@ inline RayTables make_rays(const slo_config& cfg) {
     return t;
 }
 
+// One ray: firing column direction (ca, sa) in the sensor frame, ring
+// elevation (ce, se), the sensor pose (its yaw cos/sin precomputed), the
+// objects near the pose in scene order.  Writes x, y, z, intensity (NaN for
+// no return / drop-out).
+SLO_GEN_HD void ray_point(double ca, double sa, double ce, double se, double px, double py, double pz,
+                          double cyaw, double syaw, const Box* boxes, int nbox, const Pole* poles, int npole,
+                          uint64_t scene_seed, uint64_t scan_seed, uint64_t ray_index, float* o) {
+    const double maxr = 120.0;
+    // world-frame horizontal direction of this firing column
+    double dxh = ca * cyaw - sa * syaw;
+    double dyh = ca * syaw + sa * cyaw;
+    double dx = dxh * ce, dy = dyh * ce, dz = se;
+    double tbest = maxr;
+    int kind = 0;
+    if (dz < -1e-6) {
+        double t = (pz - 0.0) / (-dz);
+        if (t < tbest) {
+            double gx = px + dx * t, gy = py + dy * t;
+            double gz = ground_height_seed(scene_seed, gx, gy);
+            t = (pz - gz) / (-dz);
+            if (t < tbest) { tbest = t; kind = 1; }
+        }
+    }
+    for (int bi = 0; bi < nbox; ++bi) {
+        const Box& B = boxes[bi];
+        double t0 = 0.0, t1 = tbest;
+        const double org[3] = {px, py, pz};
+        const double d[3] = {dx, dy, dz};
+        const double lo[3] = {B.x0, B.y0, B.z0}, hi[3] = {B.x1, B.y1, B.z1};
+        bool hit = true;
+        for (int a = 0; a < 3 && hit; ++a) {
+            if (fabs(d[a]) < 1e-12) {
+                if (org[a] < lo[a] || org[a] > hi[a]) hit = false;
+            } else {
+                double inv = 1.0 / d[a];
+                double ta = (lo[a] - org[a]) * inv, tb = (hi[a] - org[a]) * inv;
+                if (ta > tb) { double tmp = ta; ta = tb; tb = tmp; }
+                if (ta > t0) t0 = ta;
+                if (tb < t1) t1 = tb;
+                if (t0 > t1) hit = false;
+            }
+        }
+        if (hit && t0 > 0.5 && t0 < tbest) { tbest = t0; kind = 2; }
+    }
+    for (int pi = 0; pi < npole; ++pi) {
+        const Pole& P = poles[pi];
+        double ox = px - P.cx, oy = py - P.cy;
+        double a = dx * dx + dy * dy, b = 2 * (ox * dx + oy * dy), c = ox * ox + oy * oy - (double)P.r * P.r;
+        double disc = b * b - 4 * a * c;
+        if (disc < 0 || a < 1e-12) continue;
+        double t = (-b - sqrt(disc)) / (2 * a);
+        if (t > 0.5 && t < tbest) {
+            double z = pz + dz * t;
+            if (z >= 0 && z <= P.h) { tbest = t; kind = 3; }
+        }
+    }
+    uint64_t h = mix64(scan_seed * 0x100000001b3ULL + ray_index);
+    if (kind == 0 || u01(h) < 0.03) {
+        const float qnan = __builtin_nanf("");
+        o[0] = o[1] = o[2] = qnan; o[3] = qnan;
+    } else {
+        double r = tbest + 0.02 * gauss(h + 17);
+        // sensor frame: x forward, y left, z up
+        double lx = ca * ce * r, ly = sa * ce * r, lz = se * r;
+        o[0] = (float)lx; o[1] = (float)ly; o[2] = (float)lz;
+        o[3] = (float)u01(h + 29);
+    }
+}
+
+// Objects within the sensor's range of `pose`, in scene order (ties in the
+// nearest-hit test go to the earlier object, so the order is part of the data)
+inline void cull(const Scene& sc, const SensorPose& pose, std::vector<Box>& boxes, std::vector<Pole>& poles) {
+    const double maxr = 120.0;
+    boxes.clear();
+    poles.clear();
+    for (int b = 0; b < (int)sc.boxes.size(); ++b) {
+        const Box& B = sc.boxes[b];
+        double dx = std::max({(double)B.x0 - pose.x, 0.0, pose.x - (double)B.x1});
+        double dy = std::max({(double)B.y0 - pose.y, 0.0, pose.y - (double)B.y1});
+        if (dx * dx + dy * dy < maxr * maxr) boxes.push_back(B);
+    }
+    for (int p = 0; p < (int)sc.poles.size(); ++p) {
+        double dx = sc.poles[p].cx - pose.x, dy = sc.poles[p].cy - pose.y;
+        if (dx * dx + dy * dy < maxr * maxr) poles.push_back(sc.poles[p]);
+    }
+}
+
 // Generate one scan into out (x,y,z,intensity) float4s, R*C points.
 // Returns the number of points written (= R*C; NaN for no return).
 inline int generate_scan(const slo_config& cfg, const Scene& sc, const RayTables& rt,
                          const SensorPose& pose, uint64_t scan_seed, float* out) {
     const int R = cfg.n_scan, C = cfg.horizon_scan;
-    const double maxr = 120.0;
     const double cyaw = cos(pose.yaw), syaw = sin(pose.yaw);
-    // cull objects to the neighbourhood
-    std::vector<int> boxes, poles;
-    for (int b = 0; b < (int)sc.boxes.size(); ++b) {
-        const Box& B = sc.boxes[b];
-        double dx = std::max({(double)B.x0 - pose.x, 0.0, pose.x - (double)B.x1});
-        double dy = std::max({(double)B.y0 - pose.y, 0.0, pose.y - (double)B.y1});
-        if (dx * dx + dy * dy < maxr * maxr) boxes.push_back(b);
-    }
-    for (int p = 0; p < (int)sc.poles.size(); ++p) {
-        double dx = sc.poles[p].cx - pose.x, dy = sc.poles[p].cy - pose.y;
-        if (dx * dx + dy * dy < maxr * maxr) poles.push_back(p);
-    }
-    const float qnan = __builtin_nanf("");
+    std::vector<Box> boxes;
+    std::vector<Pole> poles;
+    cull(sc, pose, boxes, poles);
     int n = 0;
-    for (int f = 0; f < C; ++f) {
-        // world-frame horizontal direction of this firing column
-        double dxh = rt.ca[f] * cyaw - rt.sa[f] * syaw;
-        double dyh = rt.ca[f] * syaw + rt.sa[f] * cyaw;
+    for (int f = 0; f < C; ++f)
         for (int i = 0; i < R; ++i) {
-            double ce = rt.ce[i], se = rt.se[i];
-            double dx = dxh * ce, dy = dyh * ce, dz = se;
-            double tbest = maxr;
-            int kind = 0;
-            if (dz < -1e-6) {
-                double t = (pose.z - 0.0) / (-dz);
-                if (t < tbest) {
-                    double gx = pose.x + dx * t, gy = pose.y + dy * t;
-                    double gz = ground_height(sc, gx, gy);
-                    t = (pose.z - gz) / (-dz);
-                    if (t < tbest) { tbest = t; kind = 1; }
-                }
-            }
-            for (int bi : boxes) {
-                const Box& B = sc.boxes[bi];
-                double t0 = 0.0, t1 = tbest;
-                const double o[3] = {pose.x, pose.y, pose.z};
-                const double d[3] = {dx, dy, dz};
-                const double lo[3] = {B.x0, B.y0, B.z0}, hi[3] = {B.x1, B.y1, B.z1};
-                bool hit = true;
-                for (int a = 0; a < 3 && hit; ++a) {
-                    if (fabs(d[a]) < 1e-12) {
-                        if (o[a] < lo[a] || o[a] > hi[a]) hit = false;
-                    } else {
-                        double inv = 1.0 / d[a];
-                        double ta = (lo[a] - o[a]) * inv, tb = (hi[a] - o[a]) * inv;
-                        if (ta > tb) std::swap(ta, tb);
-                        if (ta > t0) t0 = ta;
-                        if (tb < t1) t1 = tb;
-                        if (t0 > t1) hit = false;
-                    }
-                }
-                if (hit && t0 > 0.5 && t0 < tbest) { tbest = t0; kind = 2; }
-            }
-            for (int pi : poles) {
-                const Pole& P = sc.poles[pi];
-                double ox = pose.x - P.cx, oy = pose.y - P.cy;
-                double a = dx * dx + dy * dy, b = 2 * (ox * dx + oy * dy), c = ox * ox + oy * oy - (double)P.r * P.r;
-                double disc = b * b - 4 * a * c;
-                if (disc < 0 || a < 1e-12) continue;
-                double t = (-b - sqrt(disc)) / (2 * a);
-                if (t > 0.5 && t < tbest) {
-                    double z = pose.z + dz * t;
-                    if (z >= 0 && z <= P.h) { tbest = t; kind = 3; }
-                }
-            }
-            uint64_t h = mix64(scan_seed * 0x100000001b3ULL + (uint64_t)(f * R + i));
-            float* o = out + 4 * (size_t)n;
-            if (kind == 0 || u01(h) < 0.03) {
-                o[0] = o[1] = o[2] = qnan; o[3] = qnan;
-            } else {
-                double r = tbest + 0.02 * gauss(h + 17);
-                // sensor frame: x forward, y left, z up
-                double lx = rt.ca[f] * ce * r, ly = rt.sa[f] * ce * r, lz = se * r;
-                o[0] = (float)lx; o[1] = (float)ly; o[2] = (float)lz;
-                o[3] = (float)u01(h + 29);
-            }
+            ray_point(rt.ca[f], rt.sa[f], rt.ce[i], rt.se[i], pose.x, pose.y, pose.z, cyaw, syaw, boxes.data(),
+                      (int)boxes.size(), poles.data(), (int)poles.size(), sc.seed, scan_seed,
+                      (uint64_t)(f * R + i), out + 4 * (size_t)n);
             ++n;
         }
-    }
     return n;
 }
 

@@ -66,6 +66,45 @@ def gen_batch(preset_id, config_id, stream0, n_streams, scan0, n_scans, n_points
     return out
 
 
+class DeviceGenerator:
+    """slo_gen on the device (csrc/slo_gendev.hip): the scans gen_batch makes,
+    bit for bit, written straight into device memory."""
+
+    def __init__(self, preset_id, config_id, stream0, n_streams, device=0):
+        preset_id = PRESETS.get(preset_id, preset_id)
+        self.L = _abi.lib()
+        self.h = ctypes.c_void_p()
+        self.n_streams = n_streams
+        self.max_points = preset(preset_id).max_points
+        rc = self.L.slo_gen_device_create(int(preset_id), int(config_id), int(stream0), int(n_streams), int(device),
+                                          ctypes.byref(self.h))
+        if rc != 0:
+            raise SloError(f"slo_gen_device_create failed ({rc})")
+
+    def scans(self, scan0, n_scans, d_out, hip_stream=None):
+        """write scans scan0 .. scan0+n_scans-1 of every stream to the device
+        pointer d_out ([n_scans][n_streams][max_points][4] float32)"""
+        per_scan = self.n_streams * self.max_points * 16
+        step = max(1, 65535 // self.n_streams)
+        for k in range(0, n_scans, step):
+            nk = min(step, n_scans - k)
+            rc = self.L.slo_gen_device_scans(self.h, int(scan0 + k), int(nk), ctypes.c_void_p(int(d_out) + k * per_scan),
+                                             hip_stream)
+            if rc != 0:
+                raise SloError(f"slo_gen_device_scans failed ({rc})")
+
+    def close(self):
+        if self.h:
+            self.L.slo_gen_device_destroy(self.h)
+            self.h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def gen_scan(preset_id, config_id, stream_id, k, n_points):
     out = np.empty((n_points, 4), np.float32)
     n = _abi.lib().slo_gen_scan(int(preset_id), int(config_id), int(stream_id), int(k), out.ctypes.data)

@@ -97,6 +97,8 @@ EXPORTS = [
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
     "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
+    # synthetic stream generator on the device (csrc/slo_gendev.hip)
+    "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
     # pose-graph back end (csrc/slo_pg.hip, host side)
     "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform",
 ]
@@ -153,6 +155,9 @@ def lib():
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
+    L.slo_gen_device_create.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(P)]
+    L.slo_gen_device_scans.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
+    L.slo_gen_device_destroy.argtypes = [P]
     L.slo_batch_loop_closure.argtypes = [P]
     L.slo_loop_closure.argtypes = [P, P]
     L.slo_icp_align_batch.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_size_t, P, P]

@@ -47,3 +47,37 @@ def test_wide_streams_voxel_grid_matches_oracle():
             assert mismatch(got, want) == 0, s
     finally:
         ctx.close()
+
+
+def test_voxel_grid_int32_overflow_returns_the_input():
+    # PCL's guard: when the bounding box holds more than
+    # INT32_MAX cells the filter returns its input unchanged.  Streams whose
+    # clouds are stretched to ~40 km x 40 km x 1.5 km (> 2^31 cells at 0.5 m)
+    # sit between ordinary streams in one batched call.
+    import torch
+    assert torch.cuda.is_available(), "no HIP device"
+    pid, S = 0, 6
+    cfg = slo_amd.preset(pid)
+    P = cfg.max_points
+    clouds = []
+    for s in range(S):
+        p = O.gen_scan(pid, 1, s, 0).copy()
+        if s % 2 == 1:
+            p[:, :2] *= np.float32(400.0)
+            p[:, 2] *= np.float32(100.0)
+        clouds.append(p)
+    ctx = slo_amd.Context(cfg, 0, S)
+    try:
+        dev = torch.from_numpy(np.stack(clouds)).cuda()
+        cnt = torch.full((S,), P, dtype=torch.int32, device="cuda")
+        ctx.batch_sc_make(dev.data_ptr(), cnt.data_ptr())
+        ctx.synchronize()
+        for s in range(S):
+            fin = clouds[s][np.isfinite(clouds[s][:, :3]).all(1)]
+            want = O.voxel_grid(clouds[s], cfg.leaf_sc, stable=True)
+            if s % 2 == 1:
+                assert want.tobytes() == fin.tobytes()      # the oracle takes the overflow branch
+            got = ctx.get(s, "raw_ds")
+            assert mismatch(got, want) == 0, s
+    finally:
+        ctx.close()
