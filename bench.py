@@ -71,7 +71,7 @@ def parse():
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
     ap.add_argument("--roofline-kernel", default="mo_knn",
                     help="kernel timed with HIP events inside the timed region (the roofline's kernel)")
-    ap.add_argument("--cpu-scans", type=int, default=6, help="timed scans per CPU stream in the baseline (0 = skip)")
+    ap.add_argument("--cpu-scans", type=int, default=8, help="timed scans per CPU stream in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in sched_getaffinity")
     ap.add_argument("--cpu-distinct", type=int, default=8,
                     help="distinct CPU streams pre-rolled in parallel; the others continue from copies of them")

@@ -49,8 +49,9 @@ struct OracleStream {
         if (fa.published_to_mapping) {
             bool ran = mo.run(fa.laserCloudCornerLast, fa.laserCloudSurfLast, fa.outlierCloud, fa.transformSum, pts, n, t);
             if (ran) flags |= 2;
-            if (ran && mo.saved_keyframe) {
-                flags |= 4;
+            if (ran && mo.saved_keyframe) flags |= 4;
+            // loopClosureThread returns at once without loop closure (MO:831-832)
+            if (ran && mo.saved_keyframe && cfg.loop_closure_enable) {
                 det = mo.sc.detectLoopClosureID();
                 det_valid = true;
                 flags |= 8;
@@ -171,6 +172,10 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
         return cp(s->loop, 2, (int)sizeof(LoopResult));
     }
     if (name == "key_times") return cp(s->mo.keyTimes.data(), (int)s->mo.keyTimes.size(), 8);
+    if (name == "map_ids") {   // surroundingExistingKeyPosesID (loop closure disabled only)
+        if (s->cfg.loop_closure_enable) return -1;
+        return cp(s->mo.surroundingExistingKeyPosesID.data(), (int)s->mo.surroundingExistingKeyPosesID.size(), 4);
+    }
     if (name == "detect_f") {
         if (!s->det_valid) return 0;
         double v[2] = {(double)s->det.yaw, s->det.min_dist};
@@ -341,8 +346,9 @@ int oracle_gen_scan(int preset, int config_id, int stream_id, int k, float* out)
 // the pre-roll once per distinct stream.  `history` seeds the SC history with
 // that many earlier scans (bench --history).  Returns the wall seconds of the
 // timed window; stage_s[4] = per-stage seconds summed over threads (ip, fa,
-// mo, sc); stage_one[4] = the same for thread 0 alone (the reference's
-// one-stream 3-process topology, SURVEY (A)).
+// mo, sc); stage_one[4] = the same for a copy of stream 0 run over the same
+// scans alone, before the parallel run (the reference's one-stream
+// 3-process topology, SURVEY (A)).
 double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int preroll, int history, int n_distinct,
                     double* stage_s, double* stage_one) {
     slo_config cfg;
@@ -380,6 +386,37 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int p
             });
         for (auto& th : g) th.join();
     }
+    // one scan of stream s through the three nodes (+ SC detect), per-stage seconds added to acc[4]
+    auto run_scan = [&](OracleStream& s, const float* p, int k, double* acc) {
+        const double tk = 0.1 * (preroll + k);
+        auto a = std::chrono::steady_clock::now();
+        s.det_valid = false;
+        s.ip.cloudHandler(p, P);
+        auto b = std::chrono::steady_clock::now();
+        s.fa.run(s.ip.segmentedCloud, s.ip.segMsg, s.ip.outlierCloud);
+        auto c = std::chrono::steady_clock::now();
+        bool kf = false;
+        if (s.fa.published_to_mapping) {
+            bool ran = s.mo.run(s.fa.laserCloudCornerLast, s.fa.laserCloudSurfLast, s.fa.outlierCloud,
+                                s.fa.transformSum, p, P, tk);
+            kf = ran && s.mo.saved_keyframe;
+        }
+        auto d = std::chrono::steady_clock::now();
+        if (kf && cfg.loop_closure_enable) s.det = s.mo.sc.detectLoopClosureID();
+        auto e = std::chrono::steady_clock::now();
+        s.scan_index++;
+        acc[0] += std::chrono::duration<double>(b - a).count();
+        acc[1] += std::chrono::duration<double>(c - b).count();
+        acc[2] += std::chrono::duration<double>(d - c).count();
+        acc[3] += std::chrono::duration<double>(e - d).count();
+    };
+    // (A): stream 0 alone on an otherwise idle process, so its stage times are
+    // not diluted by the other streams' threads
+    if (stage_one) {
+        OracleStream solo(*base[0]);
+        for (int k = 0; k < 4; ++k) stage_one[k] = 0;
+        for (int k = 0; k < n_scans; ++k) run_scan(solo, scans[(size_t)k].data(), k, stage_one);
+    }
     std::vector<OracleStream*> streams(n_threads, nullptr);
     for (int t = 0; t < n_threads; ++t) streams[t] = t < n_distinct ? base[t] : new OracleStream(*base[t % n_distinct]);
     std::vector<double> st(4 * n_threads, 0.0);
@@ -395,30 +432,7 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int p
             while (!go.load()) std::this_thread::yield();
             auto T0 = std::chrono::steady_clock::now();
             tstart[t] = std::chrono::duration<double>(T0.time_since_epoch()).count();
-            for (int k = 0; k < n_scans; ++k) {
-                const float* p = scans[(size_t)src * n_scans + k].data();
-                const double tk = 0.1 * (preroll + k);
-                auto a = std::chrono::steady_clock::now();
-                s.det_valid = false;
-                s.ip.cloudHandler(p, P);
-                auto b = std::chrono::steady_clock::now();
-                s.fa.run(s.ip.segmentedCloud, s.ip.segMsg, s.ip.outlierCloud);
-                auto c = std::chrono::steady_clock::now();
-                bool kf = false;
-                if (s.fa.published_to_mapping) {
-                    bool ran = s.mo.run(s.fa.laserCloudCornerLast, s.fa.laserCloudSurfLast, s.fa.outlierCloud,
-                                        s.fa.transformSum, p, P, tk);
-                    kf = ran && s.mo.saved_keyframe;
-                }
-                auto d = std::chrono::steady_clock::now();
-                if (kf) s.det = s.mo.sc.detectLoopClosureID();
-                auto e = std::chrono::steady_clock::now();
-                s.scan_index++;
-                st[4 * t + 0] += std::chrono::duration<double>(b - a).count();
-                st[4 * t + 1] += std::chrono::duration<double>(c - b).count();
-                st[4 * t + 2] += std::chrono::duration<double>(d - c).count();
-                st[4 * t + 3] += std::chrono::duration<double>(e - d).count();
-            }
+            for (int k = 0; k < n_scans; ++k) run_scan(s, scans[(size_t)src * n_scans + k].data(), k, &st[4 * t]);
             tend[t] = std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
         });
     while (ready.load() < n_threads) std::this_thread::yield();
@@ -432,7 +446,6 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int p
             stage_s[k] = 0;
             for (int t = 0; t < n_threads; ++t) stage_s[k] += st[4 * t + k];
         }
-        if (stage_one) stage_one[k] = st[k];
     }
     return t1 - t0;
 }

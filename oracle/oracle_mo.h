@@ -33,6 +33,9 @@ struct MapOptimization {
     double timeLaserOdometry = 0;
     std::deque<Cloud> recentCorner, recentSurf, recentOutlier;
     int latestFrameID = 0;
+    // loopClosureEnableFlag == false: the keyframes of the local map, in order (MO:1181-1214)
+    std::vector<int> surroundingExistingKeyPosesID;
+    std::vector<Cloud> surroundingCorner, surroundingSurf, surroundingOutlier;
     Pt previousRobotPosPoint{0, 0, 0, 0}, currentRobotPosPoint{0, 0, 0, 0};
     double timeLastProcessing = -1;
     Cloud laserCloudRaw, laserCloudRawDS, laserCloudCornerLast, laserCloudSurfLast, laserCloudOutlierLast;
@@ -175,8 +178,61 @@ struct MapOptimization {
         return out;
     }
 
+    // loopClosureEnableFlag == false (MO:1167-1222): radius search of the key
+    // positions around currentRobotPosPoint (PCL KdTreeFLANN::radiusSearch:
+    // FLANN L2 of query - point, kept when < (float)(radius * radius)), the
+    // hits VoxelGrid'ed at leaf 1.0 with intensity = key index (so a voxel's
+    // id is (int) of the mean of its members' indices, MO:1176-1183), then
+    // the existing list updated in place: ids no longer present erased in
+    // order, new ids appended in voxel order, their clouds transformed
+    void extractSurroundingRadius() {
+        const float r2 = (float)((double)cfg.surrounding_keyframe_search_radius *
+                                 (double)cfg.surrounding_keyframe_search_radius);
+        Cloud near;
+        for (size_t i = 0; i < keyPoses.size(); ++i) {
+            const Pt p{keyPoses[i].x, keyPoses[i].y, keyPoses[i].z, (float)i};
+            if (sqdist(currentRobotPosPoint, p) < r2) near.push_back(p);
+        }
+        Cloud ds;
+        voxel_grid(near, cfg.leaf_surrounding_key_poses, ds, stable_voxel);
+        for (size_t i = 0; i < surroundingExistingKeyPosesID.size(); ++i) {
+            bool existing = false;
+            for (const Pt& q : ds)
+                if (surroundingExistingKeyPosesID[i] == (int)q.intensity) { existing = true; break; }
+            if (!existing) {
+                surroundingExistingKeyPosesID.erase(surroundingExistingKeyPosesID.begin() + i);
+                surroundingCorner.erase(surroundingCorner.begin() + i);
+                surroundingSurf.erase(surroundingSurf.begin() + i);
+                surroundingOutlier.erase(surroundingOutlier.begin() + i);
+                --i;
+            }
+        }
+        for (const Pt& q : ds) {
+            const int k = (int)q.intensity;
+            bool existing = false;
+            for (int id : surroundingExistingKeyPosesID)
+                if (id == k) { existing = true; break; }
+            if (existing) continue;
+            surroundingExistingKeyPosesID.push_back(k);
+            surroundingCorner.push_back(transformPointCloud(cornerCloudKeyFrames[k], keyPoses[k]));
+            surroundingSurf.push_back(transformPointCloud(surfCloudKeyFrames[k], keyPoses[k]));
+            surroundingOutlier.push_back(transformPointCloud(outlierCloudKeyFrames[k], keyPoses[k]));
+        }
+        for (size_t i = 0; i < surroundingExistingKeyPosesID.size(); ++i) {
+            laserCloudCornerFromMap.insert(laserCloudCornerFromMap.end(), surroundingCorner[i].begin(), surroundingCorner[i].end());
+            laserCloudSurfFromMap.insert(laserCloudSurfFromMap.end(), surroundingSurf[i].begin(), surroundingSurf[i].end());
+            laserCloudSurfFromMap.insert(laserCloudSurfFromMap.end(), surroundingOutlier[i].begin(), surroundingOutlier[i].end());
+        }
+    }
+
     void extractSurroundingKeyFrames() {
         if (keyPoses.empty()) return;
+        if (!cfg.loop_closure_enable) {
+            extractSurroundingRadius();
+            voxel_grid(laserCloudCornerFromMap, cfg.leaf_corner, laserCloudCornerFromMapDS, stable_voxel);
+            voxel_grid(laserCloudSurfFromMap, cfg.leaf_surf, laserCloudSurfFromMapDS, stable_voxel);
+            return;
+        }
         const int N = cfg.surrounding_keyframe_search_num;
         if ((int)recentCorner.size() < N) {
             recentCorner.clear(); recentSurf.clear(); recentOutlier.clear();

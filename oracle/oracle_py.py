@@ -47,6 +47,8 @@ class SloConfig(ctypes.Structure):
         ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
+        ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32),
     ]
 
 
@@ -116,6 +118,7 @@ def gen_scan(pid, config_id, stream_id, k):
 
 
 _DTYPES = {
+    "map_ids": np.int32,
     "range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8, "seg_col": np.uint32,
     "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32, "orient": np.float32,
     "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32, "smooth_ind": np.int32,

@@ -101,6 +101,21 @@ typedef struct slo_config {
        is its "ring" field instead of its elevation (IP:225-226); rings come
        from slo_batch_set_rings or the PointCloud2's uint16 "ring" field */
     int32_t use_cloud_ring;
+    /* loopClosureEnableFlag == false branch of extractSurroundingKeyFrames
+       (MO:1167-1222): key poses within surroundingKeyframeSearchRadius of
+       the robot (kd-tree radius search), VoxelGrid'ed at 1 m, form the local
+       map.  The reference then keeps every keyframe's clouds, so:
+         map_keyframes   keyframes the local map may hold (0 = default:
+                         surroundingKeyframeSearchNum with loop closure, 128
+                         without); more sets SLO_ERR_MAP_CAPACITY
+         keyframe_ring   keyframe cloud slots (0 = default:
+                         surroundingKeyframeSearchNum + 2 with loop closure,
+                         1024 without); a map that needs a keyframe whose
+                         slot was reused sets SLO_ERR_MAP_CAPACITY */
+    float surrounding_keyframe_search_radius;   /* 50.0 m (utility.h:133) */
+    float leaf_surrounding_key_poses;           /* 1.0 (downSizeFilterSurroundingKeyPoses, MO:269) */
+    int32_t map_keyframes;
+    int32_t keyframe_ring;
 } slo_config;
 
 /* preset ids */
@@ -144,7 +159,7 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
         case SLO_PRESET_OS64_1800:
             R = 64; C = 1800; rx = (float)(360.0 / (float)C); ry = (float)(33.2 / (float)(R - 1));
             bot = (float)(16.6 + 0.1); gsi = 15; break;
-        case SLO_PRESET_HDL64_1800:
+        case SLO_PRESET_HDL64_1800:   /* gsi 50: the LeGO-LOAM KITTI parameter set in common use */
             R = 64; C = 1800; rx = (float)(360.0 / (float)C); ry = (float)(26.9 / (float)(R - 1));
             bot = (float)(24.9 + 0.1); gsi = 50; break;
         case SLO_PRESET_DENSE128:
@@ -209,6 +224,10 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->icp_transformation_epsilon = 1e-6;
     c->icp_fitness_epsilon = 1e-6;
     c->use_cloud_ring = 0;
+    c->surrounding_keyframe_search_radius = (float)50.0;
+    c->leaf_surrounding_key_poses = (float)1.0;
+    c->map_keyframes = 0;
+    c->keyframe_ring = 0;
     return 0;
 }
 #endif

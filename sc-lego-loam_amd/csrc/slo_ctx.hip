@@ -85,6 +85,9 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         cfg->sc_num_sector < 1 || cfg->sc_num_sector > SLO_SC_MAX_SECTOR ||
         cfg->sc_num_ring * cfg->sc_num_sector > SLO_SC_MAX_CELLS || cfg->surrounding_keyframe_search_num < 1 ||
         cfg->surrounding_keyframe_search_num + 2 > 64 || cfg->sc_tree_making_period < 1 ||
+        cfg->map_keyframes < 0 || cfg->map_keyframes > SLO_MAPK_MAX || cfg->keyframe_ring < 0 ||
+        (cfg->loop_closure_enable && cfg->keyframe_ring && cfg->keyframe_ring < cfg->surrounding_keyframe_search_num + 2) ||
+        (!cfg->loop_closure_enable && !(cfg->leaf_surrounding_key_poses > 0)) ||
         !(cfg->nearest_feature_search_sq_dist >= 0.0f) ||
         std::ceil(std::sqrt(cfg->nearest_feature_search_sq_dist) / SLO_ODO_SURF_CELL) > SLO_ODO_SURF_R)
         return SLO_E_ARG;   // the odometry surf search box (SLO_ODO_SURF_R cells) must cover the gate
@@ -167,16 +170,20 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // a subset-DS of <= H points, the outlier cloud keeps every 5th column
     // (IP:341-345) of at most R rows.
     const int NKF = cfg->surrounding_keyframe_search_num;
-    v.KFR = NKF + 2;     // keyframe cloud slots: the recent-NKF deque + the one being added
+    const bool radius = !cfg->loop_closure_enable;   // MO:1167-1222 branch
+    // keyframe cloud slots: the recent-NKF deque + the one being added; the
+    // radius branch may bring back any keyframe (the reference keeps all)
+    v.KFR = cfg->keyframe_ring > 0 ? cfg->keyframe_ring : (radius ? 1024 : NKF + 2);
     v.KFMAX = SLO_KFMAX;
+    v.MAPK = cfg->map_keyframes > 0 ? cfg->map_keyframes : (radius ? 128 : NKF);
     v.cap_kc = v.cap_less_sharp;
     v.cap_ks = (int)H;
     v.cap_ko = R * ((C + 4) / 5);
-    v.cap_mc = NKF * v.cap_kc;
+    v.cap_mc = v.MAPK * v.cap_kc;
     const int kcap = cfg->keyframe_cloud_cap;
     v.cap_kfs = kcap > 0 ? std::min(v.cap_ks, kcap) : v.cap_ks;
     v.cap_kfo = kcap > 0 ? std::min(v.cap_ko, kcap) : v.cap_ko;
-    v.cap_ms = NKF * (v.cap_kfs + v.cap_kfo);
+    v.cap_ms = v.MAPK * (v.cap_kfs + v.cap_kfo);
     v.cap_st = (int)H + v.cap_ko;
     const size_t NRS = (size_t)cfg->sc_num_ring * cfg->sc_num_sector;
     c.add(&v.outl_cam, S * H);
@@ -185,6 +192,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.kf_outl, S * v.KFR * v.cap_kfo);
     c.add(&v.kf_n, S * v.KFR * 3);
     c.add(&v.kf_pose, S * v.KFMAX * 6);
+    c.add(&v.map_ids, S * v.MAPK);
     c.add(&v.map_c, S * v.cap_mc);
     c.add(&v.map_s, S * v.cap_ms);
     c.add(&v.map_c_ds, S * v.cap_mc);
@@ -348,6 +356,9 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     if (r) return r;
     r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
     if (r) return r;
+    // without loop closure the loop thread returns at once (MO:831-832): the
+    // keyframes still get descriptors (MO:1630), nothing queries them
+    if (!ctx->cfg.loop_closure_enable) return SLO_OK;
     r = slo_batch_sc_detect(ctx);
     if (r || !ctx->cfg.loop_verify) return r;
     return slo_batch_loop_closure(ctx);
@@ -444,6 +455,10 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
+    else if (name == "map_ids") {   // keyframes of the last local map, in concatenation order
+        if (v.cfg.loop_closure_enable) { tmp.resize(4 * st.recent_n); memcpy(tmp.data(), st.recent_ids, 4 * st.recent_n); count = st.recent_n; esz = 4; }
+        else dev(v.map_ids + s * v.MAPK, st.recent_n, 4);
+    }
     else if (name == "raw_ds") dev(v.cur_raw_ds + s * v.P, st.n_raw_ds, 16);
     else if (name == "corner_ds") dev(v.cur_c_ds + s * v.cap_less_sharp, st.n_corner_ds, 16);
     else if (name == "surf_total_ds") dev(v.cur_st_ds + s * v.cap_st, st.n_surf_total_ds, 16);

@@ -158,6 +158,8 @@ struct DevView {
     // ---- mapping (mapOptmization.cpp)
     int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
     int KFMAX;           // keyframe pose / Scan Context history capacity
+    int MAPK;            // keyframes the local map may hold (map_ids row length)
+    int32_t* map_ids;    // [S][MAPK] loopClosureEnableFlag == false: surroundingExistingKeyPosesID
     int cap_kc, cap_ks, cap_ko, cap_mc, cap_ms, cap_st;
     int cap_kfs, cap_kfo;  // keyframe surf / outlier cloud slots (cfg.keyframe_cloud_cap)
     float4* outl_cam;    // [S][H]          outlier cloud, camera frame (adjustOutlierCloud)
@@ -202,6 +204,7 @@ struct DevView {
 #define SLO_SC_MAX_SECTOR 64
 #define SLO_SC_MAX_CELLS 1200   // PC_NUM_RING * PC_NUM_SECTOR limit (20 x 60)
 // StreamState::err bits (sticky; read with slo_get(.., "err"))
+#define SLO_MAPK_MAX 1024       // map_keyframes bound (radius branch)
 #define SLO_ERR_KEYFRAMES 1     // keyframe pose history full: keyframe dropped
 #define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
 #define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud

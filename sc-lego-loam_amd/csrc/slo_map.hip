@@ -40,6 +40,137 @@ __device__ inline void mo_store_trig(StreamState& st) {
     o[6] = t[3]; o[7] = t[4]; o[8] = t[5];
 }
 
+__device__ inline unsigned int ford(float f) {
+    unsigned int u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ inline float unord(unsigned int u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
+}
+
+// the keyframe ids of stream s's local map, in concatenation order
+__device__ inline const int32_t* mo_map_ids(const DevView& v, int s, const StreamState& st) {
+    return v.cfg.loop_closure_enable ? st.recent_ids : v.map_ids + (size_t)s * v.MAPK;
+}
+
+// extractSurroundingKeyFrames, loopClosureEnableFlag == false (MO:1167-1222),
+// one workgroup per stream:
+//  1. radiusSearch(currentRobotPosPoint, surroundingKeyframeSearchRadius) over
+//     cloudKeyPoses3D: FLANN's L2 of (query - point), kept when < (float)r^2;
+//     currentRobotPosPoint is the last run's transformAftMapped position
+//     (MO:1527-1529; the keyframe round trip leaves translations unchanged);
+//  2. downSizeFilterSurroundingKeyPoses (VoxelGrid 1.0, intensity = key index):
+//     the hits sorted by (voxel index, key index) in LDS; a voxel's id is
+//     (int) of the float mean of its members' indices (an exact integer sum);
+//     voxels in index order;
+//  3. surroundingExistingKeyPosesID: ids no longer present erased in order,
+//     new ids appended in voxel order (MO:1181-1214).
+// A bounding box of more than INT32_MAX voxels (PCL returns its input then,
+// radius >> 1000 leaves) is not supported and flags SLO_ERR_MAP_CAPACITY.
+constexpr int kSurrMax = 4096;   // hits sorted in LDS (<= SLO_KFMAX)
+__device__ void mo_surrounding_radius(const DevView& v, int s, StreamState& st) {
+    __shared__ unsigned long long key[kSurrMax];
+    __shared__ int nsel, ds_n, bad;
+    __shared__ unsigned int bmin[3], bmax[3];
+    __shared__ int ds_id[kSurrMax];
+    const int nk = min(st.n_keyframes, v.KFMAX);
+    const float qx = st.transformAftMapped[3], qy = st.transformAftMapped[4], qz = st.transformAftMapped[5];
+    const float r2 = (float)((double)v.cfg.surrounding_keyframe_search_radius *
+                             (double)v.cfg.surrounding_keyframe_search_radius);
+    if (threadIdx.x == 0) {
+        nsel = 0; bad = 0;
+        for (int a = 0; a < 3; ++a) { bmin[a] = ford(FLT_MAX); bmax[a] = ford(-FLT_MAX); }
+    }
+    __syncthreads();
+    const float* kp = v.kf_pose + (size_t)s * v.KFMAX * 6;
+    for (int i = threadIdx.x; i < nk; i += blockDim.x) {
+        const float px = kp[6 * i], py = kp[6 * i + 1], pz = kp[6 * i + 2];
+        const float d0 = qx - px, d1 = qy - py, d2 = qz - pz;
+        float d = 0.0f;
+        d += d0 * d0;
+        d += d1 * d1;
+        d += d2 * d2;
+        if (d < r2) {
+            const int j = atomicAdd(&nsel, 1);
+            key[j] = (unsigned long long)i;   // index now, voxel index after the bounds
+            atomicMin(&bmin[0], ford(px)); atomicMin(&bmin[1], ford(py)); atomicMin(&bmin[2], ford(pz));
+            atomicMax(&bmax[0], ford(px)); atomicMax(&bmax[1], ford(py)); atomicMax(&bmax[2], ford(pz));
+        }
+    }
+    __syncthreads();
+    const int n = nsel;
+    const float inv = 1.0f / v.cfg.leaf_surrounding_key_poses;
+    const float mn[3] = {unord(bmin[0]), unord(bmin[1]), unord(bmin[2])};
+    const float mx[3] = {unord(bmax[0]), unord(bmax[1]), unord(bmax[2])};
+    const long long dx = (long long)((mx[0] - mn[0]) * inv) + 1, dy = (long long)((mx[1] - mn[1]) * inv) + 1,
+                    dz = (long long)((mx[2] - mn[2]) * inv) + 1;
+    const int minb0 = (int)floorf(mn[0] * inv), minb1 = (int)floorf(mn[1] * inv), minb2 = (int)floorf(mn[2] * inv);
+    const int divx = (int)floorf(mx[0] * inv) - minb0 + 1, divy = (int)floorf(mx[1] * inv) - minb1 + 1;
+    if (n > 0 && dx * dy * dz > 2147483647LL) {
+        if (threadIdx.x == 0) st.err |= SLO_ERR_MAP_CAPACITY;
+        bad = 1;
+    }
+    // (voxel index << 32 | key index), padded to a power of two with ~0
+    int n2 = 1;
+    while (n2 < n) n2 <<= 1;
+    for (int j = threadIdx.x; j < n2; j += blockDim.x) {
+        if (j < n) {
+            const int i = (int)key[j];
+            const float px = kp[6 * i], py = kp[6 * i + 1], pz = kp[6 * i + 2];
+            const int i0 = (int)(floorf(px * inv) - (float)minb0), i1 = (int)(floorf(py * inv) - (float)minb1),
+                      i2 = (int)(floorf(pz * inv) - (float)minb2);
+            const unsigned int idx = (unsigned int)(i0 + i1 * divx + i2 * divx * divy);
+            key[j] = ((unsigned long long)idx << 32) | (unsigned int)i;
+        } else {
+            key[j] = ~0ull;
+        }
+    }
+    __syncthreads();
+    for (int k = 2; k <= n2; k <<= 1)          // bitonic sort, ascending
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int t = threadIdx.x; t < n2; t += blockDim.x) {
+                const int u = t ^ j;
+                if (u > t) {
+                    const unsigned long long a = key[t], b = key[u];
+                    if (((t & k) == 0) == (a > b)) { key[t] = b; key[u] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    if (threadIdx.x == 0) {
+        // voxel centroids' intensity, voxels in index order
+        int m = 0;
+        for (int j = 0; j < n && !bad;) {
+            const unsigned int vox = (unsigned int)(key[j] >> 32);
+            float sum = 0.0f;
+            int c = 0;
+            while (j < n && (unsigned int)(key[j] >> 32) == vox) { sum += (float)(unsigned int)key[j]; ++c; ++j; }
+            ds_id[m++] = (int)(sum / (float)c);
+        }
+        ds_n = m;
+        // the existing list: erase what left the region, append what entered
+        int32_t* ex = v.map_ids + (size_t)s * v.MAPK;
+        int ne = st.recent_n, w = 0;
+        for (int i = 0; i < ne; ++i) {
+            bool keep = false;
+            for (int j = 0; j < m; ++j) if (ds_id[j] == ex[i]) { keep = true; break; }
+            if (keep) ex[w++] = ex[i];
+        }
+        ne = w;
+        for (int j = 0; j < m; ++j) {
+            bool have = false;
+            for (int i = 0; i < ne; ++i) if (ex[i] == ds_id[j]) { have = true; break; }
+            if (have) continue;
+            if (ne < v.MAPK) ex[ne++] = ds_id[j];
+            else st.err |= SLO_ERR_MAP_CAPACITY;
+        }
+        st.recent_n = ne;
+        // a keyframe whose cloud slot a newer keyframe reused
+        for (int i = 0; i < ne; ++i)
+            if (ex[i] < nk - v.KFR) st.err |= SLO_ERR_MAP_CAPACITY;
+    }
+}
+
 __global__ void k_mo_prepare(DevView v) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
@@ -48,6 +179,9 @@ __global__ void k_mo_prepare(DevView v) {
         float4 p = v.outlier[(size_t)s * v.H + i];
         v.outl_cam[(size_t)s * v.H + i] = make_float4(p.y, p.z, p.x, p.w);
     }
+    // extractSurroundingKeyFrames without loop closure: the radius branch
+    // reads the pose of the last run, before associate_to_map below
+    if (!v.cfg.loop_closure_enable && st.n_keyframes > 0) mo_surrounding_radius(v, s, st);
     if (threadIdx.x != 0) return;
     st.mo_ran = 1;
     st.kf_saved = 0;
@@ -60,7 +194,9 @@ __global__ void k_mo_prepare(DevView v) {
     // extractSurroundingKeyFrames: recent keyframe deque
     const int nk = st.n_keyframes;
     const int N = v.cfg.surrounding_keyframe_search_num;
-    if (nk > 0) {
+    if (!v.cfg.loop_closure_enable) {
+        // list built above
+    } else if (nk > 0) {
         if (st.recent_n < N) {
             int cnt = 0;
             int ids[64];
@@ -78,9 +214,10 @@ __global__ void k_mo_prepare(DevView v) {
     } else {
         st.recent_n = 0;
     }
+    const int32_t* ids = mo_map_ids(v, s, st);
     int nc = 0, ns = 0;
     for (int k = 0; k < st.recent_n; ++k) {
-        const int slot = st.recent_ids[k] % v.KFR;
+        const int slot = ids[k] % v.KFR;
         const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
         nc += kn[0];
         ns += kn[1] + kn[2];
@@ -95,14 +232,15 @@ __global__ void k_mo_prepare(DevView v) {
 __global__ void k_mo_assemble(DevView v) {
     const int s = blockIdx.y, e = blockIdx.x;
     const StreamState& st = v.st[s];
-    if (e >= st.recent_n) return;
+    if (!st.mo_ran || e >= st.recent_n) return;
+    const int32_t* ids = mo_map_ids(v, s, st);
     int oc = 0, os = 0;
     for (int k = 0; k < e; ++k) {
-        const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + st.recent_ids[k] % v.KFR) * 3;
+        const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + ids[k] % v.KFR) * 3;
         oc += kn[0];
         os += kn[1] + kn[2];
     }
-    const int slot = st.recent_ids[e] % v.KFR;
+    const int slot = ids[e] % v.KFR;
     const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
     const size_t ks = (size_t)s * v.KFR + slot;
     for (int i = threadIdx.x; i < kn[0]; i += blockDim.x)
@@ -443,13 +581,6 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
 // ---------------------------------------------------------------- keyframe + Scan Context make
 __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
 
-__device__ inline unsigned int ford(float f) {
-    unsigned int u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ inline float unord(unsigned int u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
 
 // Eigen 3.3 SSE2 packet-order sum (Appendix A Q12d), stride in elements
 __device__ inline double eigen_sum(const double* x, int n, int stride) {
@@ -618,7 +749,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     StreamState* st0 = v.st;
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
     SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.cfg.surrounding_keyframe_search_num, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
     // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263)
     int r;
     if ((r = vg_run(ctx, "map_corner", v.map_c, v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner,

@@ -46,6 +46,8 @@ class SloConfig(ctypes.Structure):
         ("icp_max_corr_dist", ctypes.c_double), ("icp_transformation_epsilon", ctypes.c_double),
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
+        ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32),
     ]
 
 

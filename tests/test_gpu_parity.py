@@ -62,6 +62,42 @@ def test_pipeline_bit_exact(preset, config, streams, scans):
     assert sum(1 for r in rep if r["flags_cpu"] & 2) >= 1        # mapping ran and was compared
 
 
+def test_c3_steady_state_parity():
+    """One C3 stream for 240 scans: the local map passes its 50-keyframe
+    deque (MO:1127-1166: rebuild while filling, then pop-oldest/push-newest),
+    and Scan Context detect runs in the pipeline with >= 51 contexts, a tree
+    snapshot (SCc:257-276) and K = 10 candidate distances.  Poses, keyframes,
+    map DS clouds, descriptors and detect records are compared at every
+    mapping step; the front end every 10th scan."""
+    _torch()
+    rep, worst, counts = _run(6, 3, 1, 240, every=10)
+    _assert_clean(rep, worst, counts)
+    kf = [r["n_kf"][1] for r in rep if "n_kf" in r]
+    assert kf[-1] >= 55                                           # deque full and rolling for >= 5 mapping steps
+    full = [r for r in rep if "detect_cpu" in r and len(r["detect_cpu"]) >= 3 and r["detect_cpu"][2] == 10]
+    assert len(full) >= 5                                         # detects that searched the tree snapshot
+
+
+def _sc_off(cfg):
+    cfg.loop_closure_enable = 0
+
+
+def test_c2_sc_off_parity():
+    """C2: os64_1800 (OS1-64 vertical geometry, 1800 columns), Scan Context
+    off (loopClosureEnableFlag = false, UT:108): the local map comes from the
+    radius-search branch of extractSurroundingKeyFrames (MO:1167-1222) —
+    key poses within 50 m, VoxelGrid'ed at 1 m, the existing-keyframe list
+    updated in place — and no loop detection runs (MO:831-832).  Keyframe
+    lists, maps, poses compared at every mapping step."""
+    _torch()
+    rep, worst, counts = _run(5, 2, 1, 160, every=10, cfg_edit=_sc_off)
+    _assert_clean(rep, worst, counts)
+    rows = [r for r in rep if "n_map_ids" in r]
+    assert rows and all(r["n_map_ids"][0] == r["n_map_ids"][1] for r in rows)
+    assert rows[-1]["n_map_ids"][0] < rows[-1]["n_kf"][1] - 5      # keyframes left the 50 m region
+    assert counts["detects"] == 0
+
+
 def test_ragged_empty_and_all_nan_scans():
     _torch()
     cfg = slo_amd.preset(0)

@@ -148,3 +148,29 @@ def test_atan2_bracket_contains_glibc_atan2f(tmp_path):
     bad, cases, worst = subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()
     assert int(cases) > 40_000_000 and int(bad) == 0
     assert float(worst) < 1e-6   # 2.5e-6 half-width: > 2x margin
+
+
+def test_radius_branch_keeps_the_keyframes_near_the_robot():
+    """loopClosureEnableFlag = false (MO:1167-1222): the local map's keyframes
+    are the key poses within 50 m of the last mapped position, downsampled at
+    1 m; the list is updated in place, so it holds no duplicates, and
+    keyframes that fell out of range leave it."""
+    cfg = O.preset(0)
+    cfg.loop_closure_enable = 0
+    o = O.OracleStream(cfg, stable_voxel=True)
+    last = None
+    dropped = False
+    for k in range(120):
+        fl = o.step(O.gen_scan(0, 1, 0, k), 0.1 * k)
+        if fl & 2:
+            ids = o.get("map_ids")
+            kp = o.get("keyposes").reshape(-1, 6)
+            assert len(set(ids.tolist())) == len(ids)
+            if last is not None and len(ids):
+                # every listed keyframe was within radius + a voxel diagonal of the robot
+                d = np.linalg.norm(kp[ids, :3] - last, axis=1)
+                assert (d < 50.0 + np.sqrt(3.0)).all()
+                dropped |= ids.min() > 0
+            last = o.get("mapped")[3:6].astype(np.float64)
+            assert not (fl & 8)                          # no loop detection without loop closure
+    assert dropped

@@ -50,6 +50,8 @@ COMMON = {
     "surf_threshold": f32(0.1),                      # UT:128
     "nearest_feature_search_sq_dist": f32(25),       # UT:129
     "surrounding_keyframe_search_num": 50,           # UT:134
+    "surrounding_keyframe_search_radius": f32(50.0), # UT:133
+    "leaf_surrounding_key_poses": f32(1.0),          # MO:269
     "history_keyframe_search_radius": f32(20.0),     # UT:137
     "history_keyframe_search_num": 25,               # UT:138
     "history_keyframe_fitness_score": f32(1.5),      # UT:139

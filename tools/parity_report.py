@@ -61,7 +61,7 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 S = len(ors[s].get("seg_pts"))
                 for name in ("curvature", "picked", "cloud_label"):
                     row[name] = mismatch(ctx.get(s, name)[:S], ors[s].get(name)[:S])
-                cfg_o = O.preset(preset_id)
+                cfg_o = ocfg
                 cv, sg = ors[s].get("curvature"), ors[s].get("seg_ground")
                 rso, reo = ors[s].get("ring_start"), ors[s].get("ring_end")
                 cs = [canon_smooth(x[:S], cv, sg, rso, reo, cfg_o.edge_threshold, cfg_o.surf_threshold)
@@ -80,6 +80,10 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                     row[name] = mismatch(g, o)
                     if row[name] < 0:
                         row[name + "_len"] = [len(g), len(o)]
+                if not cfg.loop_closure_enable:   # surroundingExistingKeyPosesID (MO:1181-1214)
+                    ig, io = ctx.get(s, "map_ids"), ors[s].get("map_ids")
+                    row["map_ids"] = mismatch(ig, io)
+                    row["n_map_ids"] = [len(ig), len(io)]
                 kg, ko = ctx.get(s, "keyposes"), ors[s].get("keyposes")
                 row["n_kf"] = [len(kg) // 6, len(ko) // 6]
                 if len(kg) == len(ko):
