@@ -111,7 +111,7 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
     srch = lambda it: (it + 4) // 5  # noqa: E731  search iterations actually run
     if name == "fa_search_surf":  # per search: queries + 3 indices, the target cloud once
         return steps * int((srch(c["fa_iters"][:, 0]) * (c["flat"] * 28 + c["surf_last"] * 16)).sum())
-    if name == "fa_search_corner":
+    if name == "fa_search_corner":  # per search: queries + 2 indices, the target cloud once
         return steps * int((srch(c["fa_iters"][:, 1]) * (c["sharp"] * 24 + c["corner_last"] * 16)).sum())
     if name == "fa_iter_surf":    # per iteration: query + 3 indices + 3 matched points
         return steps * int((c["fa_iters"][:, 0] * c["flat"] * (16 + 12 + 48)).sum())

@@ -150,7 +150,6 @@ struct DevView {
     // / surf_next sorted by x, w = the point's index in the cloud (int bits)
     float4* sx_surf_last;    // [S][cap_less_flat]
     float4* sx_surf_next;    // [S][cap_less_flat]
-    float4* sx_kd_corner;    // [S][cap_less_sharp] the corner "tree" cloud sorted by x (w = index)
     int32_t* sharp_perm;     // [S][cap_sharp] sharp points in x order (query grouping)
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2

@@ -29,15 +29,19 @@ def posediff(a, b):
 
 
 def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1, n_points=None,
-        scan_fn=None):
+        scan_fn=None, cfg_edit=None):
     """n_points(k, s) -> points of stream s's scan k handed over (ragged and
     empty scans; default: all); scan_fn(k, s) -> the scan itself (default: the
-    synthetic generator)."""
+    synthetic generator); cfg_edit(cfg) changes both configs (GPU and oracle)."""
     import torch
     cfg = slo_amd.preset(preset_id)
+    ocfg = O.preset(preset_id)
+    if cfg_edit:
+        cfg_edit(cfg)
+        cfg_edit(ocfg)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, n_streams)
-    ors = [O.OracleStream(O.preset(preset_id), stable_voxel=True) for _ in range(n_streams)]
+    ors = [O.OracleStream(ocfg, stable_voxel=True) for _ in range(n_streams)]
     report = []
     worst = {"odom": 0.0, "map": 0.0, "keypose": 0.0}
     counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0, "flag_mismatch": 0}
