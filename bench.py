@@ -80,9 +80,9 @@ def parse():
                     help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
     ap.add_argument("--icp-jobs", type=int, default=64,
                     help="loop-verification ICP alignments per batch in the separate ICP measurement (0 = skip)")
-    ap.add_argument("--roctx", action="store_true",
-                    help="bracket the timed steps with roctxProfilerResume/Pause, so `rocprofv3 --selected-regions` "
-                         "traces exactly the timed window (profiles/ README)")
+    ap.add_argument("--trace-marker", action="store_true",
+                    help="launch a torch spin kernel before and after the timed steps, so a rocprofv3 kernel trace of "
+                         "the run can be cut to exactly the timed window (tools/trace_window.py)")
     ap.add_argument("--traffic-from", default=None,
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
     return ap.parse_args()
@@ -420,11 +420,9 @@ def main():
         c.timing(True)
         c.timing_filter(a.roofline_kernel)
         c.timing_reset()
-    roctx = None
-    if a.roctx:
-        import ctypes
-        roctx = ctypes.CDLL("librocprofiler-sdk-roctx.so")
-        roctx.roctxProfilerResume(ctypes.c_uint64(0))
+    if a.trace_marker:   # a torch spin kernel on either side of the timed steps (tools/trace_window.py)
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(a.warmup, a.warmup + a.steps):
         step(k)
@@ -433,8 +431,9 @@ def main():
     if world > 1:
         dist.barrier()
     el = sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
-    if roctx is not None:
-        roctx.roctxProfilerPause(ctypes.c_uint64(0))
+    if a.trace_marker:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     live_ms, live_n = 0.0, 0
     for c in ctxs:
         for kn, (kms, kcalls) in c.timing_read().items():

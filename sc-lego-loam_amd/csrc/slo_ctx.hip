@@ -456,6 +456,9 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
+    else if (name == "map_raw_n") {   // laserCloudCornerFromMap / laserCloudSurfFromMap sizes before their VoxelGrids
+        int32_t a[2] = {st.n_corner_map, st.n_surf_map}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
+    }
     else if (name == "map_ids") {   // keyframes of the last local map, in concatenation order
         if (v.cfg.loop_closure_enable) { tmp.resize(4 * st.recent_n); memcpy(tmp.data(), st.recent_ids, 4 * st.recent_n); count = st.recent_n; esz = 4; }
         else dev(v.map_ids + s * v.MAPK, st.recent_n, 4);

@@ -262,6 +262,9 @@ __global__ void k_vg_count(const int* rank, const int32_t* off, int S, int32_t* 
 static int ensure_ws(slo_ctx* ctx, size_t items) {
     MapWs& w = ctx->mws;
     if (items <= w.items) return 0;
+    // grow geometrically: a local map creeping up by a few points per mapping
+    // step must not reallocate (a device-wide synchronisation) every time
+    items = std::max(items, w.items + w.items / 2);
     void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.starts, w.ends, w.longv, w.temp};
     for (void* p : old) if (p) hipFree(p);
     w.items = items;

@@ -27,7 +27,7 @@ PRESETS = {
 
 _CLOUD_OUT = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "less_sharp", "flat", "less_flat",
               "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"}
-_DT = {"map_ids": np.int32, "range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8,
+_DT = {"map_ids": np.int32, "map_raw_n": np.int32, "range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8,
        "seg_col": np.uint32, "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32,
        "orient": np.float32, "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32,
        "smooth_ind": np.int32, "transform_sum": np.float32, "transform_cur": np.float32, "integrated": np.float32,

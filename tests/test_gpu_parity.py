@@ -78,6 +78,29 @@ def test_c3_steady_state_parity():
     assert len(full) >= 5                                         # detects that searched the tree snapshot
 
 
+def _k50(cfg):
+    cfg.sc_num_candidates = 50
+
+
+def test_c5_dense_steady_state_k50():
+    """C5: 128 x 2048 (262 k points per scan) until the local map holds its 50
+    keyframes — a raw surf map of ~10^6 points before its VoxelGrid — with
+    Scan Context detect in the pipeline at K = 50 candidates (SCh:87 raised as
+    C5 asks).  Mapping results compared at every mapping step, front end every
+    25th scan."""
+    torch = _torch()
+    import parity_report
+    rep, worst, counts = parity_report.run(7, 5, 1, 212, verbose=False, every=25, cfg_edit=_k50)
+    _assert_clean(rep, worst, counts)
+    full = [r for r in rep if "detect_cpu" in r and len(r["detect_cpu"]) >= 3 and r["detect_cpu"][2] == 50]
+    assert len(full) >= 1
+    kf = [r["n_kf"][1] for r in rep if "n_kf" in r]
+    assert kf[-1] >= 52
+    raw = max(r["map_raw_n"][1] for r in rep if "map_raw_n" in r)
+    print(f"C5 raw surf map before VoxelGrid: {raw} points")
+    assert raw >= 500_000
+
+
 def _sc_off(cfg):
     cfg.loop_closure_enable = 0
 

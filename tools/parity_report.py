@@ -88,6 +88,7 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                     ig, io = ctx.get(s, "map_ids"), ors[s].get("map_ids")
                     row["map_ids"] = mismatch(ig, io)
                     row["n_map_ids"] = [len(ig), len(io)]
+                row["map_raw_n"] = ctx.get(s, "map_raw_n").tolist()
                 kg, ko = ctx.get(s, "keyposes"), ors[s].get("keyposes")
                 row["n_kf"] = [len(kg) // 6, len(ko) // 6]
                 if len(kg) == len(ko):
