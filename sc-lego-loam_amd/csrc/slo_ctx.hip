@@ -233,7 +233,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << 17, v.cap_ms, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL) ||
-        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 13, v.cap_less_sharp, SLO_ODO_SURF_CELL)) {
+        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 12, v.cap_less_sharp, SLO_ODO_SURF_CELL)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }

@@ -473,50 +473,69 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
     ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
 }
 
-// findCorrespondingCornerFeatures (FA:1044-1153), one thread per query (in x
-// order, sharp_perm, so a workgroup's queries walk neighbouring cells): exact
-// 1-NN in the corner tree cloud through its 1 m hash grid (nn1_grid: rings of
-// cells nearest first, stopped by the best distance so far, ties to the
-// lowest index — the reference's exact nearest neighbour), then the 2nd point
-// by the reference's walk over rings cscan-2 .. cscan+2 of corner_last (index
-// ranges cut at the ring boundaries, WalkBest's visiting-order tie rule).
-__global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
-    int s, chunk;
-    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
-    if (s >= v.S) return;
+// findCorrespondingCornerFeatures (FA:1044-1153): one workgroup per stream,
+// one thread per query.  The corner tree cloud is small (~2-3 k points at
+// C3), so its 1 m hash grid (built by grid_build_lds) is copied into LDS once
+// per workgroup and every query's exact 1-NN (nn1_grid: rings of cells
+// nearest first, stopped by the best distance so far, ties to the lowest
+// index — the reference's exact nearest neighbour) walks it there instead of
+// chaining dependent loads through L2; a cloud larger than the LDS copy walks
+// the grid in global memory.  Then the 2nd point by the reference's walk
+// over rings cscan-2 .. cscan+2 of corner_last (index ranges cut at the ring
+// boundaries, WalkBest's visiting-order tie rule).
+#define SLO_OC_T 4096        // corner grid buckets (grid_oc)
+#define SLO_OC_LDS 6144      // corner points the LDS copy holds
+__global__ void __launch_bounds__(1024) k_fa_search_corner(DevView v) {
+    const int s = blockIdx.x;
     const StreamState& st = v.st[s];
     if (st.odo_phase != 1) return;
     const int nq = st.n_sharp;
-    if (chunk * (int)blockDim.x >= nq) return;   // uniform
-    const int pos = chunk * blockDim.x + threadIdx.x;
-    if (pos >= nq) return;
-    const int i = v.sharp_perm[(size_t)s * v.cap_sharp + pos];
+    __shared__ int32_t s_off[SLO_OC_T + 1];
+    __shared__ float4 s_ent[SLO_OC_LDS];
+    const int n = st.kdCornerNum;
+    const bool in_lds = n <= SLO_OC_LDS && v.g_oc.T == SLO_OC_T;
+    GridView g = v.g_oc;
+    int gs = s;
+    if (in_lds) {
+        const int32_t* O = v.g_oc.off + (size_t)s * (SLO_OC_T + 1);
+        const float4* E = v.g_oc.ent + (size_t)s * v.g_oc.es;
+        for (int k = threadIdx.x; k <= SLO_OC_T; k += blockDim.x) s_off[k] = O[k];
+        for (int k = threadIdx.x; k < n; k += blockDim.x) s_ent[k] = E[k];
+        __syncthreads();
+        g.off = s_off;
+        g.ent = s_ent;
+        g.es = 0;
+        gs = 0;
+    }
     const float gate = v.cfg.nearest_feature_search_sq_dist;
     const int R = v.cfg.n_scan;
     float tc[6];
     for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-    const P4 sel = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
-    int bi = -1;
-    float bd = FLT_MAX;
-    nn1_grid(v.g_oc, s, gate, sel, bi, bd);
     const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
     const int32_t* rf = v.roff_last + ((size_t)s * 2 + 0) * (R + 1);
     auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
     const int cornerLastNum = st.cornerLastNum;
-    const bool found = bi >= 0 && bd < gate && bi < cornerLastNum;
-    WalkBest wb;
-    wb.init(gate);
-    if (found) {
-        const int cscan = (int)clast[bi].w;
-        const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
-        const int f0 = max(bi + 1, ring_first(cscan + 1)), f1 = min(ring_first(cscan + 3), lim);
-        const int b0 = ring_first(cscan - 2), b1 = min(ring_first(cscan), bi);
-        for (int r = cscan - 2; r <= cscan + 2; ++r)
-            if (r != cscan) ring_walk_linear(clast, rf, R, r, sel, f0, f1, b0, b1, wb);
-    }
     int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
-    indc[2 * i] = found ? bi : -1;
-    indc[2 * i + 1] = found ? wb.index() : -1;
+    for (int pos = threadIdx.x; pos < nq; pos += blockDim.x) {
+        const int i = v.sharp_perm[(size_t)s * v.cap_sharp + pos];
+        const P4 sel = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
+        int bi = -1;
+        float bd = FLT_MAX;
+        nn1_grid(g, gs, gate, sel, bi, bd);
+        const bool found = bi >= 0 && bd < gate && bi < cornerLastNum;
+        WalkBest wb;
+        wb.init(gate);
+        if (found) {
+            const int cscan = (int)clast[bi].w;
+            const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
+            const int f0 = max(bi + 1, ring_first(cscan + 1)), f1 = min(ring_first(cscan + 3), lim);
+            const int b0 = ring_first(cscan - 2), b1 = min(ring_first(cscan), bi);
+            for (int r = cscan - 2; r <= cscan + 2; ++r)
+                if (r != cscan) ring_walk_linear(clast, rf, R, r, sel, f0, f1, b0, b1, wb);
+        }
+        indc[2 * i] = found ? bi : -1;
+        indc[2 * i + 1] = found ? wb.index() : -1;
+    }
 }
 
 // iterations iter0 .. iter0+4 of calculateTransformationSurf (FA:1270-1377)
@@ -719,13 +738,13 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
     if (!first_scan) {
-        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 255) / 256;
+        const int nbs = (v.cap_flat + 255) / 256;
         for (int b = 0; b < 5; ++b) {
             SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
             SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
         }
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
+            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(S), dim3(1024), 0, v);
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
