@@ -9,8 +9,11 @@ A step = one scan of every stream on this rank through the whole pipeline
 mapOptimization + SCManager, with the deterministic gating of SURVEY §8(d):
 mapping on every 4th scan, SC detect per saved keyframe).  Each rank owns
 --streams independent streams (weak scaling, slo_amd/dist.py); per step the
-ranks all-gather a 160-byte record per stream (poses + newest SC ring key)
-over RCCL.
+ranks all-gather a 4960-byte record per stream (poses, ids, loop result and —
+when the stream saved a keyframe — its exact Scan Context descriptor) over
+RCCL, and every rank's cross-stream store (slo_amd.xsc) ingests the gathered
+table and runs the multi-session loop query for its own streams (SURVEY
+§8(e)).
 
 Steady state: every stream first runs --preroll scans untimed (default 210:
 the local map holds its full 50 keyframes, MO:1127-1166, and Scan Context
@@ -78,6 +81,8 @@ def parse():
     ap.add_argument("--single-steps", type=int, default=100, help="timed scans of the one-stream leg (0 = skip)")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
+    ap.add_argument("--xsc-cap", type=int, default=64,
+                    help="keyframes per stream in the cross-stream Scan Context store (gather mode)")
     ap.add_argument("--icp-jobs", type=int, default=64,
                     help="loop-verification ICP alignments per batch in the separate ICP measurement (0 = skip)")
     ap.add_argument("--trace-marker", action="store_true",
@@ -351,6 +356,11 @@ def main():
     rec_n = ctxs[0].L.slo_record_floats()
     rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
     gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
+    xsc, matches = None, None
+    if gather:   # cross-stream Scan Context store over every rank's streams
+        from slo_amd import xsc as X
+        xsc = X.CrossSession(cfg, world * S, a.xsc_cap, local)
+        matches = torch.zeros((S, X.MATCH_DTYPE.itemsize // 4), dtype=torch.int32, device=f"cuda:{local}")
     exts = [torch.cuda.ExternalStream(c.stream_handle) for c in ctxs]
     pool = ThreadPoolExecutor(max_workers=len(ctxs)) if len(ctxs) > 1 else None
 
@@ -403,6 +413,9 @@ def main():
                 exts[0].wait_event(ev)
             with torch.cuda.stream(exts[0]):
                 sdist.gather_records(rec, gathered)
+                h = exts[0].cuda_stream
+                xsc.ingest(gathered.data_ptr(), h)
+                xsc.query(gathered[stream0].data_ptr(), S, stream0, matches.data_ptr(), h)
                 done = torch.cuda.Event()
                 done.record(exts[0])
             for e in exts[1:]:
@@ -557,6 +570,8 @@ def main():
         print(json.dumps(out), flush=True)
     if pool is not None:
         pool.shutdown()
+    if xsc is not None:
+        xsc.close()
     if gather:
         dist.destroy_process_group()
 

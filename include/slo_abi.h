@@ -24,7 +24,7 @@
 
 #include <stddef.h>
 #include <stdint.h>
-#include "../sc-lego-loam_amd/csrc/slo_config.h"
+#include "slo_config.h"
 
 #ifdef __cplusplus
 extern "C" {
@@ -159,11 +159,52 @@ int slo_icp_align_batch(slo_ctx* ctx, const void* d_src, size_t src_stride, cons
                         size_t tgt_stride, const int32_t* d_ntgt, slo_loop_result* h_out);
 
 /* ---------------------------------------------------------------- multi-GPU records
- * Pack one fixed-size record per stream (odometry pose, mapped pose,
- * keyframe count, loop result, newest ring key) into device memory d_out
- * [n_streams][slo_record_floats()] for the RCCL all-gather. */
+ * Pack one fixed-size record per stream into device memory d_out
+ * [n_streams][SLO_RECORD_FLOATS] floats for the RCCL all-gather (SURVEY
+ * §8(e)): odometry pose (transformSum), mapped pose (transformAftMapped),
+ * keyframe count, keyframe-saved flag, this step's loop result, the newest
+ * ring key, and — when a keyframe was saved — its Scan Context descriptor
+ * (20 x 60 cell maxima: floats or 0, so the f32 copy is exact; the ring and
+ * sector keys are derived from it bit for bit, Scancontext.cpp:198-227). */
+#define SLO_RECORD_FLOATS 1240
+#define SLO_REC_POSE 0          /* [6] transformSum */
+#define SLO_REC_MAPPED 6        /* [6] transformAftMapped */
+#define SLO_REC_N_KEYFRAMES 12
+#define SLO_REC_KF_SAVED 13     /* 1 when this step saved a keyframe */
+#define SLO_REC_LOOP_ID 14      /* detect: loop id, -1 none, -2 no detect this step */
+#define SLO_REC_MIN_DIST 15
+#define SLO_REC_RING_KEY 16     /* [20] newest ring key (f32 tree row) */
+#define SLO_REC_SC_COUNT 36
+#define SLO_REC_ERR 37
+#define SLO_REC_KF_INDEX 38     /* keyframe index of the descriptor, -1 none */
+#define SLO_REC_YAW 39
+#define SLO_REC_DESC 40         /* [NR*NS <= 1200] descriptor, row-major (ring, sector) */
 int slo_pack_records(slo_ctx* ctx, void* d_out);
 int slo_record_floats(void);
+
+/* Cross-stream Scan Context store over the all-gathered records (multi-
+ * session loop candidates, csrc/slo_xsc.hip).  One store per rank holds the
+ * descriptor history of all n_streams global streams (a ring of `cap` per
+ * stream).  slo_xsc_ingest appends the descriptors of the records that saved
+ * a keyframe (d_records = the whole gathered table, n_records == n_streams);
+ * slo_xsc_query runs detectLoopClosureID (SCc:247-338) for each of n_query
+ * records (global stream ids global0 ..) against every OTHER stream's
+ * history: K nearest ring keys (exact f32 L2), distanceBtnScanContext, first
+ * minimum, loop when below sc_dist_thres.  Asynchronous on hip_stream. */
+typedef struct slo_xsc slo_xsc;
+typedef struct slo_xsc_match {
+    int32_t valid;          /* the record carried a new keyframe */
+    int32_t n_cand;         /* candidates compared (<= sc_num_candidates) */
+    int32_t nn_stream;      /* global stream of the best candidate, -1 none */
+    int32_t nn_keyframe;    /* its keyframe index */
+    int32_t loop;           /* min_dist < sc_dist_thres */
+    float yaw;              /* alignment shift in radians */
+    double min_dist;
+} slo_xsc_match;
+int slo_xsc_create(const slo_config* cfg, int hip_device, int n_streams, int cap, slo_xsc** out);
+void slo_xsc_destroy(slo_xsc* g);
+int slo_xsc_ingest(slo_xsc* g, const void* d_records, int n_records, void* hip_stream);
+int slo_xsc_query(slo_xsc* g, const void* d_records, int n_query, int global0, void* d_out, void* hip_stream);
 
 /* ---------------------------------------------------------------- readback
  * Copy a named per-stream result to host memory (synchronises).  Returns the

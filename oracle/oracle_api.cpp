@@ -16,6 +16,7 @@
 #include <atomic>
 #include <string>
 #include "../sc-lego-loam_amd/csrc/slo_gen.h"
+#include "../include/slo_abi.h"   // the record layout (SLO_REC_*) of the interface the oracle checks
 
 using namespace oracle;
 
@@ -172,6 +173,7 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
         return cp(s->loop, 2, (int)sizeof(LoopResult));
     }
     if (name == "key_times") return cp(s->mo.keyTimes.data(), (int)s->mo.keyTimes.size(), 8);
+    if (name == "sc_count") { int v = (int)s->mo.sc.polarcontexts_.size(); return cp(&v, 1, 4); }
     if (name == "map_ids") {   // surroundingExistingKeyPosesID (loop closure disabled only)
         if (s->cfg.loop_closure_enable) return -1;
         return cp(s->mo.surroundingExistingKeyPosesID.data(), (int)s->mo.surroundingExistingKeyPosesID.size(), 4);
@@ -278,6 +280,88 @@ void oracle_sc_knn(const slo_config* cfg, const float* data, int n, const float*
     std::vector<float> cd;
     m.knn_search(q, K, ci, cd);
     for (int c = 0; c < K; ++c) { idx[c] = ci[c]; dist[c] = cd[c]; }
+}
+
+// ---- cross-stream Scan Context store (slo_xsc.hip) restated: per-stream
+// rings of `cap` descriptors taken from the all-gathered records; a query runs
+// detectLoopClosureID's candidate search (SCc:247-338) against every other
+// stream's entries: K nearest ring keys by (nanoflann float L2, entry code =
+// stream * cap + slot), distanceBtnScanContext each, first minimum, loop when
+// below SC_DIST_THRES
+struct XscOracle {
+    slo_config cfg;
+    int N, cap, NR, NS;
+    SCManager m;
+    std::vector<std::vector<double>> desc, sect;
+    std::vector<std::vector<float>> ring;
+    std::vector<int> kfi, cnt;
+    XscOracle(const slo_config& c, int n, int k)
+        : cfg(c), N(n), cap(k), NR(c.sc_num_ring), NS(c.sc_num_sector), m(c), desc((size_t)n * k), sect((size_t)n * k),
+          ring((size_t)n * k), kfi((size_t)n * k, -1), cnt(n, 0) {}
+    std::vector<double> desc_of(const float* rec) const {
+        std::vector<double> d(NR * NS);
+        for (int i = 0; i < NR * NS; ++i) d[i] = (double)rec[SLO_REC_DESC + i];
+        return d;
+    }
+    std::vector<float> ring_of(const std::vector<double>& d) const {
+        auto rk = m.makeRingkey(d);
+        std::vector<float> f(NR);
+        for (int r = 0; r < NR; ++r) f[r] = (float)rk[r];
+        return f;
+    }
+};
+void* oracle_xsc_create(const slo_config* cfg, int n_streams, int cap) { return new XscOracle(*cfg, n_streams, cap); }
+void oracle_xsc_destroy(void* h) { delete (XscOracle*)h; }
+void oracle_xsc_ingest(void* h, const float* recs, int n) {
+    XscOracle& x = *(XscOracle*)h;
+    for (int r = 0; r < n && r < x.N; ++r) {
+        const float* rec = recs + (size_t)r * SLO_RECORD_FLOATS;
+        if (rec[SLO_REC_KF_SAVED] == 0.0f || rec[SLO_REC_KF_INDEX] < 0.0f) continue;
+        const size_t slot = (size_t)r * x.cap + x.cnt[r] % x.cap;
+        x.desc[slot] = x.desc_of(rec);
+        x.sect[slot] = x.m.makeSectorkey(x.desc[slot]);
+        x.ring[slot] = x.ring_of(x.desc[slot]);
+        x.kfi[slot] = (int)rec[SLO_REC_KF_INDEX];
+        x.cnt[r]++;
+    }
+}
+// out_i [nq][5] = valid, n_cand, nn_stream, nn_keyframe, loop; out_f [nq][2] = yaw, min_dist
+void oracle_xsc_query(void* h, const float* recs, int nq, int global0, int32_t* out_i, double* out_f) {
+    XscOracle& x = *(XscOracle*)h;
+    const int K = x.cfg.sc_num_candidates;
+    for (int q = 0; q < nq; ++q) {
+        const float* rec = recs + (size_t)q * SLO_RECORD_FLOATS;
+        int32_t* oi = out_i + 5 * q;
+        double* of = out_f + 2 * q;
+        oi[0] = 0; oi[1] = 0; oi[2] = -1; oi[3] = -1; oi[4] = 0; of[0] = 0; of[1] = 0;
+        if (rec[SLO_REC_KF_SAVED] == 0.0f || rec[SLO_REC_KF_INDEX] < 0.0f) continue;
+        const int self = global0 + q;
+        auto qd = x.desc_of(rec);
+        auto qr = x.ring_of(qd);
+        std::vector<std::pair<float, long long>> all;
+        for (int t = 0; t < x.N; ++t) {
+            if (t == self) continue;
+            for (int j = 0; j < std::min(x.cnt[t], x.cap); ++j) {
+                const long long e = (long long)t * x.cap + j;
+                all.push_back({SCManager::l2_nf(qr.data(), x.ring[e].data(), x.NR), e});
+            }
+        }
+        std::sort(all.begin(), all.end());
+        const int nc = std::min<int>(K, (int)all.size());
+        double md = 10000000;
+        int am = 0, bc = -1;
+        for (int c = 0; c < nc; ++c) {
+            auto r = x.m.distanceBtnScanContext(qd, x.desc[all[c].second]);
+            if (r.first < md) { md = r.first; am = r.second; bc = c; }
+        }
+        oi[0] = 1; oi[1] = nc;
+        of[1] = md;
+        if (bc >= 0) {
+            const long long e = all[bc].second;
+            oi[2] = (int)(e / x.cap); oi[3] = x.kfi[e]; oi[4] = md < x.cfg.sc_dist_thres ? 1 : 0;
+            of[0] = (float)((float)(am * (360.0 / (double)x.NS)) * M_PI / 180.0);
+        }
+    }
 }
 
 // ---- slo_ddsum.h under test: sum of the exact float products a[i]*b[i]

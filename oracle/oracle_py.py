@@ -96,6 +96,12 @@ def lib():
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
         L.oracle_set_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_xsc_create.restype = ctypes.c_void_p
+        L.oracle_xsc_create.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_int, ctypes.c_int]
+        L.oracle_xsc_destroy.argtypes = [ctypes.c_void_p]
+        L.oracle_xsc_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_xsc_query.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_void_p]
         L.oracle_ddsum.restype = ctypes.c_float
         L.oracle_ddsum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         L.oracle_libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
@@ -118,7 +124,7 @@ def gen_scan(pid, config_id, stream_id, k):
 
 
 _DTYPES = {
-    "map_ids": np.int32,
+    "map_ids": np.int32, "sc_count": np.int32,
     "range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8, "seg_col": np.uint32,
     "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32, "orient": np.float32,
     "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32, "smooth_ind": np.int32,
@@ -252,3 +258,60 @@ class OracleStream:
         if n:
             lib().oracle_get(self.h, name.encode(), out.ctypes.data, n)
         return out
+
+
+# ---- records (include/slo_abi.h SLO_REC_*) and the cross-stream store (slo_xsc)
+RECORD_FLOATS = 1240
+
+
+def record(o, kf_saved):
+    """The record slo_pack_records writes for an OracleStream after a step
+    (kf_saved: this step saved a keyframe; its descriptor travels as floats)."""
+    r = np.zeros(RECORD_FLOATS, np.float32)
+    r[0:6] = o.get("transform_sum")
+    r[6:12] = o.get("mapped")
+    nkf = int(o.get("n_keyframes")[0])
+    r[12] = nkf
+    det = o.get("detect")
+    detf = o.get("detect_f")
+    r[14] = det[0] if len(det) else -2
+    r[15] = np.float32(detf[1]) if len(detf) else 0
+    r[39] = np.float32(detf[0]) if len(detf) else 0
+    ring = o.get("ring_key")
+    if len(ring):
+        r[16:16 + len(ring)] = ring.astype(np.float32)
+    desc = o.get("sc_desc")
+    nsc = int(o.get("sc_count")[0])
+    r[36] = nsc
+    r[38] = -1
+    if kf_saved and len(desc):
+        r[13] = 1
+        r[38] = nsc - 1
+        r[40:40 + len(desc)] = desc.astype(np.float32)
+    return r
+
+
+class XscOracle:
+    """oracle_xsc_* (the cross-stream store restated)"""
+
+    def __init__(self, cfg, n_streams, cap=64):
+        self.h = lib().oracle_xsc_create(ctypes.byref(cfg), int(n_streams), int(cap))
+        self.n = n_streams
+
+    def ingest(self, recs):
+        recs = np.ascontiguousarray(recs, np.float32)
+        assert recs.shape == (self.n, RECORD_FLOATS)
+        lib().oracle_xsc_ingest(self.h, recs.ctypes.data, len(recs))
+
+    def query(self, recs, global0):
+        recs = np.ascontiguousarray(recs, np.float32).reshape(-1, RECORD_FLOATS)
+        oi = np.zeros((len(recs), 5), np.int32)
+        of = np.zeros((len(recs), 2), np.float64)
+        lib().oracle_xsc_query(self.h, recs.ctypes.data, len(recs), int(global0), oi.ctypes.data, of.ctypes.data)
+        return oi, of
+
+    def __del__(self):
+        try:
+            lib().oracle_xsc_destroy(self.h)
+        except Exception:
+            pass

@@ -159,6 +159,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.roff_last, S * 2 * (R + 1));
     c.add(&v.sx_surf_last, S * v.cap_less_flat);
     c.add(&v.sx_surf_next, S * v.cap_less_flat);
+    c.add(&v.sx_kd_corner, S * v.cap_less_sharp);
     c.add(&v.sharp_perm, S * v.cap_sharp);
     c.add(&v.ind_surf, S * v.cap_flat * 3);
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
@@ -232,8 +233,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // slo_vg.hip); the sparse corner cloud is searched by brute force.
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << 17, v.cap_ms, 0.5f) ||
-        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL) ||
-        slo::grid_alloc(ctx, ctx->grid_oc, 1 << 12, v.cap_less_sharp, SLO_ODO_SURF_CELL)) {
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
@@ -242,7 +242,6 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         return SLO_E_HIP;
     }
     v.g_os = slo::grid_view(ctx->grid_os);
-    v.g_oc = slo::grid_view(ctx->grid_oc);
     v.g_mc = slo::grid_view(ctx->grid_c);
     v.g_ms = slo::grid_view(ctx->grid_s);
     *out = ctx;

@@ -150,6 +150,7 @@ struct DevView {
     // / surf_next sorted by x, w = the point's index in the cloud (int bits)
     float4* sx_surf_last;    // [S][cap_less_flat]
     float4* sx_surf_next;    // [S][cap_less_flat]
+    float4* sx_kd_corner;    // [S][cap_less_sharp] the corner "tree" cloud sorted by x (w = index)
     int32_t* sharp_perm;     // [S][cap_sharp] sharp points in x order (query grouping)
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
@@ -194,7 +195,6 @@ struct DevView {
 #endif
 #define SLO_MO_BLOCKS 64
 #define SLO_MO_PART 55          // 27 double-double sums (21 AtA + 6 AtB) + correspondence count
-#define SLO_RECORD_FLOATS 40
 #define SLO_ODO_SURF_CELL 1.0f  // odometry surf grid cell (m, power of two)
 #define SLO_ODO_SURF_R 5        // its search box radius in cells: covers sqrt(nearest_feature_search_sq_dist)
 #define SLO_EX_CNT 16

@@ -22,6 +22,7 @@
 #include "slo_libm.h"
 #include "slo_pose.h"
 #include "slo_linalg.h"
+#include "slo_scdist.h"
 #include <float.h>
 
 namespace slo {
@@ -581,25 +582,6 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
 // ---------------------------------------------------------------- keyframe + Scan Context make
 __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
 
-
-// Eigen 3.3 SSE2 packet-order sum (Appendix A Q12d), stride in elements
-__device__ inline double eigen_sum(const double* x, int n, int stride) {
-    if (n < 2) return n ? x[0] : 0.0;
-    const int a2 = (n / 4) * 4, a1 = (n / 2) * 2;
-    double p0a = x[0], p0b = x[stride];
-    if (a1 > 2) {
-        double p1a = x[2 * stride], p1b = x[3 * stride];
-        for (int i = 4; i < a2; i += 4) {
-            p0a += x[i * stride]; p0b += x[(i + 1) * stride];
-            p1a += x[(i + 2) * stride]; p1b += x[(i + 3) * stride];
-        }
-        p0a += p1a; p0b += p1b;
-        if (a1 > a2) { p0a += x[a2 * stride]; p0b += x[(a2 + 1) * stride]; }
-    }
-    double r = p0a + p0b;
-    for (int i = a1; i < n; ++i) r += x[i * stride];
-    return r;
-}
 
 __device__ inline float sc_xy2theta(float x, float y, int atan_float) {
     auto at = [&](float t) -> double { return atan_float ? (double)slo_libm::atanf_(t) : atan((double)t); };

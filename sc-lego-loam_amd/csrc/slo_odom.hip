@@ -309,6 +309,49 @@ __global__ void __launch_bounds__(256) k_fa_sx_long(DevView v, int nb) {
     }
 }
 
+// one workgroup per stream: the corner "tree" cloud sorted by x, whenever the
+// tree is (re)built (checkSystemInitialization, or publishCloudsLast with
+// enough points, FA:1779-1786)
+template <int NP>
+__global__ void __launch_bounds__(1024) k_fa_sx_kd(DevView v) {
+    const int s = blockIdx.x;
+    const StreamState& st = v.st[s];
+    if (!(st.odo_phase == 3 || (st.n_less_sharp > 10 && st.n_less_flat > 100))) return;
+    const int n = st.kdCornerNum;
+    const float4* in = v.kd_corner + (size_t)s * v.cap_less_sharp;
+    float4* out = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
+    __shared__ uint64_t key[NP];
+    for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sx_key(in[i].x, i);
+    int np = 1;
+    while (np < n) np <<= 1;
+    lds_bitonic(key, n, np);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const int idx = (int)(uint32_t)key[i];
+        const float4 p = in[idx];
+        out[i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
+    }
+}
+
+// the same as sx_lower, by a whole wave (every lane gets the result): each
+// round loads 64 equally spaced x values and narrows [lo, hi) to one stride
+// by a ballot of the (monotone) "x < qx" predicate, so a cloud of <= 4096
+// points takes two dependent loads instead of a dozen
+__device__ inline int sx_lower_wave(const float4* a, int lo, int hi, float qx) {
+    const int lane = threadIdx.x & 63;
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) / 64;
+        const int idx = lo + lane * step;
+        const bool p = idx < hi && a[idx].x < qx;
+        const int c = __popcll(__ballot(p));
+        const int nlo = c == 0 ? lo : lo + (c - 1) * step + 1;
+        hi = min(hi, lo + c * step);
+        lo = nlo;
+    }
+    const int idx = lo + lane;
+    const bool p = idx < hi && a[idx].x < qx;
+    return lo + __popcll(__ballot(p));
+}
+
 // first position in a[lo, hi) whose x is >= qx
 __device__ inline int sx_lower(const float4* a, int lo, int hi, float qx) {
     while (lo < hi) {
@@ -473,69 +516,121 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
     ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
 }
 
-// findCorrespondingCornerFeatures (FA:1044-1153): one workgroup per stream,
-// one thread per query.  The corner tree cloud is small (~2-3 k points at
-// C3), so its 1 m hash grid (built by grid_build_lds) is copied into LDS once
-// per workgroup and every query's exact 1-NN (nn1_grid: rings of cells
-// nearest first, stopped by the best distance so far, ties to the lowest
-// index — the reference's exact nearest neighbour) walks it there instead of
-// chaining dependent loads through L2; a cloud larger than the LDS copy walks
-// the grid in global memory.  Then the 2nd point by the reference's walk
-// over rings cscan-2 .. cscan+2 of corner_last (index ranges cut at the ring
-// boundaries, WalkBest's visiting-order tie rule).
-#define SLO_OC_T 4096        // corner grid buckets (grid_oc)
-#define SLO_OC_LDS 6144      // corner points the LDS copy holds
-__global__ void __launch_bounds__(1024) k_fa_search_corner(DevView v) {
-    const int s = blockIdx.x;
+// findCorrespondingCornerFeatures (FA:1044-1153): one workgroup = 64 queries
+// (consecutive in x order, sharp_perm) x 4 waves.  1-NN by brute force over
+// the x-window of the x-sorted tree cloud that can hold a point within the
+// gate of any of the 64 queries (a wider margin than float rounding needs;
+// every point outside it is farther than the gate, where the reference
+// rejects the neighbour anyway), streamed through LDS: wave w takes a quarter
+// of each 256-point tile, every lane keeps four independent minimum chains,
+// and the 16 partial minima of a query merge by (distance, index) — the
+// result of the reference's exact nearest neighbour with ties to the lowest
+// index.  Then the 2nd point: wave w walks ring cscan + {-2, -1, +1, +2}[w]
+// and the four WalkBests merge in LDS.
+__global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
     const StreamState& st = v.st[s];
     if (st.odo_phase != 1) return;
     const int nq = st.n_sharp;
-    __shared__ int32_t s_off[SLO_OC_T + 1];
-    __shared__ float4 s_ent[SLO_OC_LDS];
-    const int n = st.kdCornerNum;
-    const bool in_lds = n <= SLO_OC_LDS && v.g_oc.T == SLO_OC_T;
-    GridView g = v.g_oc;
-    int gs = s;
-    if (in_lds) {
-        const int32_t* O = v.g_oc.off + (size_t)s * (SLO_OC_T + 1);
-        const float4* E = v.g_oc.ent + (size_t)s * v.g_oc.es;
-        for (int k = threadIdx.x; k <= SLO_OC_T; k += blockDim.x) s_off[k] = O[k];
-        for (int k = threadIdx.x; k < n; k += blockDim.x) s_ent[k] = E[k];
-        __syncthreads();
-        g.off = s_off;
-        g.ent = s_ent;
-        g.es = 0;
-        gs = 0;
-    }
+    if (chunk * 64 >= nq) return;   // uniform
+#if SLO_DIAG_ODO
+    unsigned long long t_d = clock64();
+#endif
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int pos = chunk * 64 + lane;
+    const bool active = pos < nq;
+    const int i = active ? v.sharp_perm[(size_t)s * v.cap_sharp + pos] : 0;
     const float gate = v.cfg.nearest_feature_search_sq_dist;
     const int R = v.cfg.n_scan;
-    float tc[6];
-    for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    // TransformToStart of the 64 queries once (wave 0), shared through LDS
+    __shared__ float4 s_sel[64];
+    if (w == 0) {
+        float tc[6];
+        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+        const P4 q = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
+        s_sel[lane] = make_float4(q.x, q.y, q.z, q.w);
+    }
+    __syncthreads();
+    const float4 sel4 = s_sel[lane];
+    const P4 sel{sel4.x, sel4.y, sel4.z, sel4.w};
+    const bool fin = active && isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z);
+    // the workgroup's x-window (every wave computes the same one)
+    float xmin = fin ? sel.x : FLT_MAX, xmax = fin ? sel.x : -FLT_MAX;
+    for (int o = 32; o > 0; o >>= 1) {
+        xmin = fminf(xmin, __shfl_xor(xmin, o, 64));
+        xmax = fmaxf(xmax, __shfl_xor(xmax, o, 64));
+    }
+    const float4* kx = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
+    const int n = st.kdCornerNum;
+    int lo = 0, hi = 0;
+    if (xmin <= xmax) {   // wave-uniform: xmin / xmax are wave reductions
+        const float rr = sqrtf(gate) * 1.001f + 1e-3f + 1e-5f * fmaxf(fabsf(xmin), fabsf(xmax));
+        lo = sx_lower_wave(kx, 0, n, xmin - rr);
+        hi = sx_lower_wave(kx, lo, n, xmax + rr);
+    }
+    __shared__ float4 tile[256];
+    __shared__ float s_d[4][64];
+    __shared__ int s_i[4][64], s_c[4][64];
+    float cd[4] = {FLT_MAX, FLT_MAX, FLT_MAX, FLT_MAX};
+    int ci[4] = {INT_MAX, INT_MAX, INT_MAX, INT_MAX};
+    auto take = [&](int c, const float4& p) {
+        const float d = sqdist_flann(sel, p);
+        const int idx = __float_as_int(p.w);
+        if (d < cd[c] || (d == cd[c] && idx < ci[c])) { cd[c] = d; ci[c] = idx; }
+    };
+    for (int t0 = lo; t0 < hi; t0 += 256) {
+        __syncthreads();
+        if (t0 + tid < hi) tile[tid] = kx[t0 + tid];
+        __syncthreads();
+        const int m = min(256, hi - t0) - w * 64;   // this wave's share of the tile: [w*64, w*64 + m)
+        if (fin && m > 0) {
+            if (m >= 64) {
+#pragma unroll 4
+                for (int j = 0; j < 64; j += 4)
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) take(c, tile[w * 64 + j + c]);
+            } else {
+                for (int j = 0; j < m; ++j) take(j & 3, tile[w * 64 + j]);
+            }
+        }
+    }
+    for (int c = 1; c < 4; ++c)
+        if (cd[c] < cd[0] || (cd[c] == cd[0] && ci[c] < ci[0])) { cd[0] = cd[c]; ci[0] = ci[c]; }
+    s_d[w][lane] = cd[0]; s_i[w][lane] = ci[0];
+    __syncthreads();
+    float bd = s_d[0][lane];
+    int bi = s_i[0][lane];
+    for (int k = 1; k < 4; ++k) {
+        const float d = s_d[k][lane];
+        const int x = s_i[k][lane];
+        if (d < bd || (d == bd && x < bi)) { bd = d; bi = x; }
+    }
+    ODO_STAMP(2);
     const float4* clast = v.corner_last + (size_t)s * v.cap_less_sharp;
     const int32_t* rf = v.roff_last + ((size_t)s * 2 + 0) * (R + 1);
     auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
     const int cornerLastNum = st.cornerLastNum;
-    int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
-    for (int pos = threadIdx.x; pos < nq; pos += blockDim.x) {
-        const int i = v.sharp_perm[(size_t)s * v.cap_sharp + pos];
-        const P4 sel = slo_pose::transform_to_start(ld4(v.sharp + (size_t)s * v.cap_sharp, i), tc);
-        int bi = -1;
-        float bd = FLT_MAX;
-        nn1_grid(g, gs, gate, sel, bi, bd);
-        const bool found = bi >= 0 && bd < gate && bi < cornerLastNum;
-        WalkBest wb;
-        wb.init(gate);
-        if (found) {
-            const int cscan = (int)clast[bi].w;
-            const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
-            const int f0 = max(bi + 1, ring_first(cscan + 1)), f1 = min(ring_first(cscan + 3), lim);
-            const int b0 = ring_first(cscan - 2), b1 = min(ring_first(cscan), bi);
-            for (int r = cscan - 2; r <= cscan + 2; ++r)
-                if (r != cscan) ring_walk_linear(clast, rf, R, r, sel, f0, f1, b0, b1, wb);
-        }
-        indc[2 * i] = found ? bi : -1;
-        indc[2 * i + 1] = found ? wb.index() : -1;
+    const bool found = fin && bi != INT_MAX && bd < gate && bi < cornerLastNum;
+    WalkBest wb;
+    wb.init(gate);
+    if (found) {
+        const int cscan = (int)clast[bi].w;
+        const int lim = min(nq, cornerLastNum);                      // Q7: bounded by the sharp count
+        const int f0 = max(bi + 1, ring_first(cscan + 1)), f1 = min(ring_first(cscan + 3), lim);
+        const int b0 = ring_first(cscan - 2), b1 = min(ring_first(cscan), bi);
+        const int r = cscan + (w < 2 ? w - 2 : w - 1);
+        ring_walk_linear(clast, rf, R, r, sel, f0, f1, b0, b1, wb);
     }
+    __syncthreads();   // s_d / s_i reads above are done
+    s_d[w][lane] = wb.d; s_c[w][lane] = wb.cls; s_i[w][lane] = wb.t;
+    __syncthreads();
+    ODO_STAMP(3);
+    if (w != 0 || !active) return;
+    for (int k = 1; k < 4; ++k) wb.offer(s_d[k][lane], s_c[k][lane], s_i[k][lane]);
+    int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
+    indc[2 * i] = found ? bi : -1; indc[2 * i + 1] = found ? wb.index() : -1;
 }
 
 // iterations iter0 .. iter0+4 of calculateTransformationSurf (FA:1270-1377)
@@ -738,13 +833,13 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
     if (!first_scan) {
-        const int nbs = (v.cap_flat + 255) / 256;
+        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 63) / 64;
         for (int b = 0; b < 5; ++b) {
             SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
             SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
         }
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(S), dim3(1024), 0, v);
+            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
@@ -757,16 +852,18 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
         if (v.cfg.horizon_scan > 512)
             SLO_LAUNCH(ctx, "fa_sx_long", k_fa_sx_long, dim3(xcd_grid(S, R)), dim3(256), 0, v, R);
     }
+    if (v.cap_less_sharp <= 4096) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<4096>, dim3(S), dim3(1024), 0, v);
+    else if (v.cap_less_sharp <= 8192) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<8192>, dim3(S), dim3(1024), 0, v);
+    else SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<16384>, dim3(S), dim3(1024), 0, v);
     SLO_CHECK(hipGetLastError());
     // the clouds just written become *Last for the next scan
     std::swap(ctx->v.corner_last, ctx->v.corner_next);
     std::swap(ctx->v.surf_last, ctx->v.surf_next);
     std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
-    // setInputCloud: hash grids over the (possibly unchanged) tree clouds
+    // setInputCloud: hash grid over the (possibly unchanged) surf tree cloud
+    // (the corner tree by a windowed brute force over its x-sorted copy, k_fa_sx_kd)
     const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
-    int r = grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
-    if (r) return r;
-    return grid_build(ctx, ctx->grid_oc, v.kd_corner, v.cap_less_sharp, &v.st->kdCornerNum, SS);
+    return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
 }
 
 }  // namespace slo

@@ -11,48 +11,10 @@
 // per-shift sums run in column order, so every f64 value is the reference's
 // (Eigen SSE2 reduction order, Q12d).
 #include "slo_internal.h"
+#include "slo_scdist.h"
 #include <float.h>
 
 namespace slo {
-
-struct Cand { float d; int i; };
-
-__device__ inline bool cand_less(const Cand& a, const Cand& b) { return a.d < b.d || (a.d == b.d && a.i < b.i); }
-
-__device__ inline float l2_nf(const float* a, const float* b, int n) {
-    float result = 0;
-    int d = 0;
-    for (; d + 3 < n; d += 4) {
-        const float d0 = a[d] - b[d], d1 = a[d + 1] - b[d + 1], d2 = a[d + 2] - b[d + 2], d3 = a[d + 3] - b[d + 3];
-        result += d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3;
-    }
-    for (; d < n; ++d) { const float d0 = a[d] - b[d]; result += d0 * d0; }
-    return result;
-}
-
-// streaming Eigen SSE2 sum: 4 lane accumulators, combined (0+2)+(1+3)
-struct ESum {
-    double a0, a1, a2, a3;
-    int n;
-    __device__ ESum() : a0(0), a1(0), a2(0), a3(0), n(0) {}
-    __device__ void add(double x) {
-        switch (n & 3) { case 0: a0 = n < 4 ? x : a0 + x; break; case 1: a1 = n < 4 ? x : a1 + x; break;
-                         case 2: a2 = n < 4 ? x : a2 + x; break; default: a3 = n < 4 ? x : a3 + x; }
-        ++n;
-    }
-    __device__ double get() const { return (a0 + a2) + (a1 + a3); }  // valid for n % 4 == 0, n >= 4
-};
-
-#define SC_K SLO_SC_MAX_K
-#define SC_NS SLO_SC_MAX_SECTOR
-
-__device__ inline unsigned long long wave_min_u64(unsigned long long x) {
-    for (int o = 32; o > 0; o >>= 1) {
-        const unsigned long long y = __shfl_xor(x, o, 64);
-        x = y < x ? y : x;
-    }
-    return x;
-}
 
 __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     const int s = blockIdx.x;
@@ -68,11 +30,7 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     __shared__ unsigned long long keys[SLO_KFMAX];   // (f32 L2 bits << 32 | index) of the snapshot
     __shared__ unsigned long long wmin[4];
     __shared__ int cands[SC_K];
-    __shared__ double sim[7 * SC_NS];
-    __shared__ int simok[7 * SC_NS];
-    __shared__ double dist7[7];
-    __shared__ double shnorm[SC_NS];
-    __shared__ int shifts[7];
+    __shared__ ScPairLds pl;
     __shared__ double cdist[SC_K];
     __shared__ int calign[SC_K];
     if (tid == 0) {
@@ -122,73 +80,8 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     const double* vk1 = v.sc_sect + (hb + N - 1) * NS;
     for (int c = 0; c < K; ++c) {
         const int ci = cands[c];
-        const double* sc2 = v.sc_desc + (hb + ci) * NR * NS;
-        const double* vk2 = v.sc_sect + (hb + ci) * NS;
-        // fastAlignUsingVkey: 60 shifts on 60 lanes
-        if (tid < NS) {
-            ESum e;
-            for (int j = 0; j < NS; ++j) {
-                double d = vk1[j] - vk2[((j - tid) % NS + NS) % NS];
-                e.add(d * d);
-            }
-            shnorm[tid] = sqrt(e.get());
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int argmin = 0;
-            double mn = 10000000;
-            for (int sh = 0; sh < NS; ++sh)
-                if (shnorm[sh] < mn) { argmin = sh; mn = shnorm[sh]; }
-            const int R = (int)round(0.5 * v.cfg.sc_search_ratio * NS);
-            int sp[7], n = 0;
-            sp[n++] = argmin;
-            for (int ii = 1; ii < R + 1 && n < 7; ii++) {
-                sp[n++] = (argmin + ii + NS) % NS;
-                sp[n++] = (argmin - ii + NS) % NS;
-            }
-            for (int a = 1; a < n; ++a) {  // ascending (std::sort on 7 ints)
-                int x = sp[a], b = a - 1;
-                while (b >= 0 && sp[b] > x) { sp[b + 1] = sp[b]; --b; }
-                sp[b + 1] = x;
-            }
-            for (int k = 0; k < 7; ++k) shifts[k] = k < n ? sp[k] : -1;
-        }
-        __syncthreads();
-        // column cosines for the 7 shifts
-        for (int t = tid; t < 7 * NS; t += blockDim.x) {
-            const int k = t / NS, j = t - k * NS;
-            const int sh = shifts[k];
-            simok[t] = 0;
-            if (sh < 0) continue;
-            const int j2 = ((j - sh) % NS + NS) % NS;
-            ESum n1, n2, dt;
-            for (int r = 0; r < NR; ++r) {
-                double a = sc1[r * NS + j], b = sc2[r * NS + j2];
-                n1.add(a * a); n2.add(b * b); dt.add(a * b);
-            }
-            double nn1 = sqrt(n1.get()), nn2 = sqrt(n2.get());
-            if ((nn1 == 0) | (nn2 == 0)) continue;
-            sim[t] = dt.get() / (nn1 * nn2);
-            simok[t] = 1;
-        }
-        __syncthreads();
-        if (tid < 7) {
-            double sum = 0;
-            int ne = 0;
-            for (int j = 0; j < NS; ++j)
-                if (simok[tid * NS + j]) { sum = sum + sim[tid * NS + j]; ne = ne + 1; }
-            dist7[tid] = shifts[tid] < 0 ? 10000000 : 1.0 - sum / ne;
-        }
-        __syncthreads();
-        if (tid == 0) {
-            int am = 0;
-            double md = 10000000;
-            for (int k = 0; k < 7; ++k)
-                if (shifts[k] >= 0 && dist7[k] < md) { am = shifts[k]; md = dist7[k]; }
-            cdist[c] = md;
-            calign[c] = am;
-        }
-        __syncthreads();
+        sc_pair_distance(sc1, vk1, v.sc_desc + (hb + ci) * NR * NS, v.sc_sect + (hb + ci) * NS, NR, NS,
+                         v.cfg.sc_search_ratio, pl, &cdist[c], &calign[c]);
     }
     if (tid == 0) {
         double min_dist = 10000000;
@@ -221,26 +114,35 @@ int sc_detect_run_one(slo_ctx* ctx) {
 }
 
 // Per-stream record shared across ranks by the RCCL all-gather (SURVEY §8(e)
-// mode M): odometry pose, mapped pose, keyframe count, loop result and the
-// newest ring key.  40 floats = 160 B per stream.
-__global__ void k_pack_records(DevView v, float* out) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= v.S) return;
+// mode M; layout SLO_REC_* in include/slo_abi.h): poses, ids, this step's
+// loop result, the newest ring key and, when a keyframe was saved, its
+// descriptor as exact floats.  One workgroup per stream.
+__global__ void __launch_bounds__(256) k_pack_records(DevView v, float* out) {
+    const int s = blockIdx.x;
     const StreamState& st = v.st[s];
     float* o = out + (size_t)s * SLO_RECORD_FLOATS;
-    for (int k = 0; k < 6; ++k) { o[k] = st.transformSum[k]; o[6 + k] = st.transformAftMapped[k]; }
-    o[12] = (float)st.n_keyframes;
-    o[13] = (float)st.kf_saved;
-    o[14] = st.det_valid ? (float)st.det_loop_id : -2.0f;
-    o[15] = st.det_valid ? (float)st.det_min_dist : 0.0f;
-    const int NR = v.cfg.sc_num_ring;
+    const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
+    const int kf = st.sc_count - 1;
+    const bool saved = st.kf_saved && kf >= 0;
+    const double* d = saved ? v.sc_desc + ((size_t)s * v.KFMAX + kf) * NR * NS : nullptr;
+    for (int i = threadIdx.x; i < SLO_SC_MAX_CELLS; i += blockDim.x)
+        o[SLO_REC_DESC + i] = (saved && i < NR * NS) ? (float)d[i] : 0.0f;
+    if (threadIdx.x != 0) return;
+    for (int k = 0; k < 6; ++k) { o[SLO_REC_POSE + k] = st.transformSum[k]; o[SLO_REC_MAPPED + k] = st.transformAftMapped[k]; }
+    o[SLO_REC_N_KEYFRAMES] = (float)st.n_keyframes;
+    o[SLO_REC_KF_SAVED] = saved ? 1.0f : 0.0f;
+    o[SLO_REC_LOOP_ID] = st.det_valid ? (float)st.det_loop_id : -2.0f;
+    o[SLO_REC_MIN_DIST] = st.det_valid ? (float)st.det_min_dist : 0.0f;
     const float* rk = st.sc_count > 0 ? v.sc_ring + ((size_t)s * v.KFMAX + st.sc_count - 1) * NR : nullptr;
-    for (int k = 0; k < 20; ++k) o[16 + k] = (rk && k < NR) ? rk[k] : 0.0f;
-    o[36] = (float)st.sc_count; o[37] = (float)st.err; o[38] = 0; o[39] = 0;
+    for (int k = 0; k < 20; ++k) o[SLO_REC_RING_KEY + k] = (rk && k < NR) ? rk[k] : 0.0f;
+    o[SLO_REC_SC_COUNT] = (float)st.sc_count;
+    o[SLO_REC_ERR] = (float)st.err;
+    o[SLO_REC_KF_INDEX] = saved ? (float)kf : -1.0f;
+    o[SLO_REC_YAW] = st.det_valid ? st.det_yaw : 0.0f;
 }
 
 int pack_records_run(slo_ctx* ctx, float* d_out) {
-    SLO_LAUNCH(ctx, "pack_records", k_pack_records, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v, d_out);
+    SLO_LAUNCH(ctx, "pack_records", k_pack_records, dim3(ctx->S), dim3(256), 0, ctx->v, d_out);
     SLO_CHECK(hipGetLastError());
     return 0;
 }

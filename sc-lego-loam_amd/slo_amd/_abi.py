@@ -90,6 +90,19 @@ class MapView(ctypes.Structure):
                 ("transform_aft_mapped", ctypes.c_float * 6)]
 
 
+class XscMatch(ctypes.Structure):
+    """slo_xsc_match (include/slo_abi.h)"""
+    _fields_ = [("valid", ctypes.c_int32), ("n_cand", ctypes.c_int32), ("nn_stream", ctypes.c_int32),
+                ("nn_keyframe", ctypes.c_int32), ("loop", ctypes.c_int32), ("yaw", ctypes.c_float),
+                ("min_dist", ctypes.c_double)]
+
+
+# record layout (include/slo_abi.h SLO_REC_*)
+RECORD_FLOATS = 1240
+REC = {"pose": 0, "mapped": 6, "n_keyframes": 12, "kf_saved": 13, "loop_id": 14, "min_dist": 15, "ring_key": 16,
+       "sc_count": 36, "err": 37, "kf_index": 38, "yaw": 39, "desc": 40}
+
+
 # symbols declared in include/slo_abi.h (tests check every one is exported)
 EXPORTS = [
     "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
@@ -99,6 +112,8 @@ EXPORTS = [
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
     "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
+    # cross-stream Scan Context store over the gathered records (csrc/slo_xsc.hip)
+    "slo_xsc_create", "slo_xsc_destroy", "slo_xsc_ingest", "slo_xsc_query",
     # synthetic stream generator on the device (csrc/slo_gendev.hip)
     "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
     # pose-graph back end (csrc/slo_pg.hip, host side)
@@ -157,6 +172,10 @@ def lib():
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
+    L.slo_xsc_create.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
+    L.slo_xsc_destroy.argtypes = [P]
+    L.slo_xsc_ingest.argtypes = [P, P, ctypes.c_int, P]
+    L.slo_xsc_query.argtypes = [P, P, ctypes.c_int, ctypes.c_int, P, P]
     L.slo_gen_device_create.argtypes = [ctypes.c_int] * 5 + [ctypes.POINTER(P)]
     L.slo_gen_device_scans.argtypes = [P, ctypes.c_int, ctypes.c_int, P, P]
     L.slo_gen_device_destroy.argtypes = [P]

@@ -4,11 +4,12 @@ One process per GPU.  Streams are independent (each owns its pose chain,
 local map and Scan Context history), so rank r owns the contiguous global
 stream ids [r*S, (r+1)*S) and the data path needs no collective: every rank
 advances its own S streams one scan per step (weak scaling).  The only
-exchange is one batched all-gather per step of a fixed 160-byte record per
+exchange is one batched all-gather per step of a fixed 4960-byte record per
 stream (odometry pose, mapped pose, keyframe count, loop result, newest ring
-key; slo_pack_records), so every rank sees every stream's state for
-cross-stream (multi-session) loop candidates.  Over RCCL that is
-world*S*160 B, latency-bound and far below xGMI bandwidth.
+key and, on a keyframe, the exact Scan Context descriptor; slo_pack_records),
+so every rank holds every stream's descriptor history for cross-stream
+(multi-session) loop candidates (slo_amd.xsc).  Over RCCL that is
+world*S*4960 B per step (20 MB at 8 x 512 streams), a few tens of us on xGMI.
 """
 import torch
 import torch.distributed as dist
