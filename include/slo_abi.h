@@ -336,6 +336,13 @@ int slo_pg_optimize(slo_pg* g, int max_iters, int* iters_out, double* cost_out);
 /* correctPoses: all key poses, 6 floats each; returns the count or a negative code */
 int slo_pg_get_key_poses(slo_pg* g, float* out6, int cap);
 int slo_pg_last_transform(slo_pg* g, float out[6]);
+/* correctPoses into a stream's device state (synchronises): key poses
+ * [0, n) (cloudKeyPoses6D order x y z roll pitch yaw); transform6 (may be
+ * NULL) becomes transformAftMapped, transformLast and transformTobeMapped
+ * (MO:1601-1611); the recent keyframe deque is cleared, so the next mapping
+ * step rebuilds its local map from the corrected poses (MO:1642-1664).
+ * cfg.pose_graph does this itself; a caller driving slo_pg by hand uses it. */
+int slo_set_key_poses(slo_ctx* ctx, int stream, const float* poses6, int n, const float* transform6);
 
 #ifdef __cplusplus
 }

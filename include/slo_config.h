@@ -113,6 +113,13 @@ typedef struct slo_config {
     float leaf_surrounding_key_poses;           /* 1.0 (downSizeFilterSurroundingKeyPoses, MO:269) */
     int32_t map_keyframes;
     int32_t keyframe_ring;
+    /* pose-graph back end in the batched pipeline (csrc/slo_pgwire.hip): the
+       key poses come from an SE(3) factor graph per stream (GTSAM iSAM2's
+       role, MO:1541-1611) that takes the loops loop_verify accepts, and a
+       closed loop rewrites every key pose (correctPoses, MO:1642-1664).
+       0 = off (the keyframe estimate is its initial value, as in the
+       reference while no loop is closed) */
+    int32_t pose_graph;
 } slo_config;
 
 /* preset ids */

@@ -34,6 +34,11 @@ struct OracleStream {
 
     // returns bit flags: 1 = FA odometry ran, 2 = mapping ran, 4 = keyframe, 8 = detect ran
     int step(const float* pts, int n, double t) {
+        const int f = step_map(pts, n, t);
+        return f | step_loop(f, t);
+    }
+    // the nodes up to mapOptimization::run (flags 1, 2, 4)
+    int step_map(const float* pts, int n, double t) {
         int flags = 0;
         det_valid = false;
         ip.cloudHandler(pts, n);
@@ -51,18 +56,23 @@ struct OracleStream {
             bool ran = mo.run(fa.laserCloudCornerLast, fa.laserCloudSurfLast, fa.outlierCloud, fa.transformSum, pts, n, t);
             if (ran) flags |= 2;
             if (ran && mo.saved_keyframe) flags |= 4;
-            // loopClosureThread returns at once without loop closure (MO:831-832)
-            if (ran && mo.saved_keyframe && cfg.loop_closure_enable) {
-                det = mo.sc.detectLoopClosureID();
-                det_valid = true;
-                flags |= 8;
-                if (cfg.loop_verify) {
-                    perform_loop_closure(cfg, mo, det.loop_id, t, loop, mo.stable_voxel);
-                    if (loop[1].ran) flags |= 16;
-                }
-            }
         }
         scan_index++;
+        return flags;
+    }
+    // the loop thread after a keyframe (flags 8, 16): detect + verification
+    int step_loop(int map_flags, double t) {
+        int flags = 0;
+        // loopClosureThread returns at once without loop closure (MO:831-832)
+        if ((map_flags & 4) && cfg.loop_closure_enable) {
+            det = mo.sc.detectLoopClosureID();
+            det_valid = true;
+            flags |= 8;
+            if (cfg.loop_verify) {
+                perform_loop_closure(cfg, mo, det.loop_id, t, loop, mo.stable_voxel);
+                if (loop[1].ran) flags |= 16;
+            }
+        }
         return flags;
     }
 };
@@ -80,6 +90,33 @@ void* oracle_create(const slo_config* cfg, int stable_voxel) {
 void oracle_destroy(void* h) { delete (OracleStream*)h; }
 
 int oracle_step(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step(pts, n, t); }
+int oracle_step_map(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step_map(pts, n, t); }
+int oracle_step_loop(void* h, int map_flags, double t) { return ((OracleStream*)h)->step_loop(map_flags, t); }
+void oracle_set_key_poses(void* h, const float* poses6, int n, const float* transform6) {
+    ((OracleStream*)h)->mo.set_key_poses(poses6, n, transform6);
+}
+// the RS loop factor's poseFrom (MO:1027-1037) as RzRyRx / Point3 arguments:
+// pcl::getTransformation of the lidar-axes correction times that of the
+// newest key pose, read back by pcl::getTranslationAndEulerAngles; float
+// products row by column left to right (Eigen's order unpinned)
+void oracle_rs_loop_from(const float* corr, const float* latest, float* out) {
+    auto gt = [](float x, float y, float z, float roll, float pitch, float yaw, float* T) {
+        const float A = cosf(yaw), B = sinf(yaw), C = cosf(pitch), D = sinf(pitch), E = cosf(roll), F = sinf(roll);
+        const float DE = D * E, DF = D * F;
+        const float m[16] = {A * C, A * DF - B * E, B * F + A * DE, x, B * C, A * E + B * DF, B * DE - A * F, y,
+                             -D,    C * F,          C * E,          z, 0,     0,              0,              1};
+        memcpy(T, m, sizeof m);
+    };
+    float L[16], W[16], M[16];
+    gt(corr[2], corr[0], corr[1], corr[5], corr[3], corr[4], L);         // correctionLidarFrame
+    gt(latest[2], latest[0], latest[1], latest[5], latest[3], latest[4], W);   // tWrong
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) M[4 * r + c] = (L[4 * r] * W[c] + L[4 * r + 1] * W[4 + c]) + L[4 * r + 2] * W[8 + c];
+        M[4 * r + 3] = ((L[4 * r] * W[3] + L[4 * r + 1] * W[7]) + L[4 * r + 2] * W[11]) + L[4 * r + 3];
+    }
+    out[0] = atan2f(M[9], M[10]); out[1] = asinf(-M[8]); out[2] = atan2f(M[4], M[0]);
+    out[3] = M[3]; out[4] = M[7]; out[5] = M[11];
+}
 
 // useCloudRing input for the next scans (the message's ring field, unfiltered order)
 void oracle_set_rings(void* h, const uint16_t* rings, int n) { ((OracleStream*)h)->ip.rings.assign(rings, rings + n); }
@@ -173,6 +210,7 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
         return cp(s->loop, 2, (int)sizeof(LoopResult));
     }
     if (name == "key_times") return cp(s->mo.keyTimes.data(), (int)s->mo.keyTimes.size(), 8);
+    if (name == "kf_pre") return cp(s->mo.kfPre, 6, 4);
     if (name == "sc_count") { int v = (int)s->mo.sc.polarcontexts_.size(); return cp(&v, 1, 4); }
     if (name == "map_ids") {   // surroundingExistingKeyPosesID (loop closure disabled only)
         if (s->cfg.loop_closure_enable) return -1;

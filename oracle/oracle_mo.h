@@ -54,6 +54,23 @@ struct MapOptimization {
     bool ran = false, saved_keyframe = false;
     // /aft_mapped_to_init as TransformFusion decodes it (publishTF MO:680-705 -> TF:222-241)
     float tfAft[6] = {0}, tfBef[6] = {0};
+    // the transform the last saved keyframe hands to the pose graph (MO:1541-1555)
+    float kfPre[6] = {0};
+
+    // correctPoses (MO:1642-1664) from a pose-graph estimate: key poses
+    // [0, n), the recent deques cleared; transform (may be null) becomes
+    // transformAftMapped / Last / TobeMapped (MO:1601-1611) and publishTF
+    // hands it on (MO:1701)
+    void set_key_poses(const float* poses6, int n, const float* transform) {
+        for (int i = 0; i < n && i < (int)keyPoses.size(); ++i)
+            keyPoses[i] = Pose6{poses6[6 * i], poses6[6 * i + 1], poses6[6 * i + 2], poses6[6 * i + 3],
+                                poses6[6 * i + 4], poses6[6 * i + 5]};
+        if (transform) {
+            for (int k = 0; k < 6; ++k) { transformAftMapped[k] = transform[k]; transformLast[k] = transform[k]; transformTobeMapped[k] = transform[k]; }
+            odom_handoff(transformAftMapped, tfAft);
+        }
+        recentCorner.clear(); recentSurf.clear(); recentOutlier.clear();
+    }
 
     explicit MapOptimization(const slo_config& c) : cfg(c), sc(c) {}
 
@@ -443,6 +460,7 @@ struct MapOptimization {
         // iSAM2 estimate of the new node == its initial value, read back
         // through Rot3::RzRyRx -> pitch()/yaw()/roll() (oracle_tf.h)
         float est[6];
+        for (int i = 0; i < 6; ++i) kfPre[i] = keyPoses.empty() ? transformTobeMapped[i] : transformAftMapped[i];
         if (keyPoses.empty()) {
             for (int i = 0; i < 6; ++i) transformLast[i] = transformTobeMapped[i];
             keyframe_estimate(transformTobeMapped, est);

@@ -150,3 +150,57 @@ class Graph:
 
     def key_poses(self):
         return np.array([to_key_pose6d(T) for T in self.est])
+
+
+class PipelineWithGraph:
+    """TEST INFRASTRUCTURE: the oracle pipeline (oracle_py.OracleStream) with
+    this numpy graph as its back end, driven in the order slo_pgwire.hip
+    follows (mapOptmization.cpp): after each mapping step the saved keyframe
+    adds its odometry factor and, once a loop is closed, the estimate is
+    written back (saveKeyFramesAndFactor MO:1541-1611 + correctPoses
+    MO:1642-1664); after SC detect + verification, accepted RS / SC
+    candidates add Cauchy loop factors and the graph is solved
+    (MO:1030-1046, 1078-1091)."""
+
+    def __init__(self, stream):
+        self.st, self.g, self.pending, self.snap = stream, Graph(), False, None
+        self.loops = 0
+
+    def step(self, pts, t):
+        import oracle_py as O
+        f = self.st.step_map(pts, t)
+        if f & 2:
+            if f & 4:
+                self.g.add_keyframe(self.st.get("kf_pre"))
+                if self.pending:
+                    tf = self.g.last if len(self.g.est) > 1 else None
+                    self.st.set_key_poses(self.g.key_poses().astype(np.float32),
+                                          None if tf is None else np.asarray(tf, np.float32))
+                    self.pending = False
+            elif self.pending:
+                self.st.set_key_poses(self.snap)
+                self.pending = False
+        f |= self.st.step_loop(f, t)
+        if (f & 8) and (f & 4):
+            lp = self.st.get("loop")
+            if len(lp) == 2:
+                rs, sc = lp[0], lp[1]
+                use_rs = rs["ran"] and rs["accepted"] and rs["id"] >= 0
+                use_sc = sc["ran"] and sc["accepted"] and sc["id"] >= 0
+                latest = len(self.g.est) - 1
+                if (use_rs or use_sc) and latest >= 0:
+                    self.snap = self.g.key_poses().astype(np.float32)
+                    kp = self.st.get("keyposes").reshape(-1, 6)
+                    if use_rs:
+                        frm = O.rs_loop_from(rs["xyzrpy"], kp[latest])
+                        p = kp[rs["id"]]
+                        to = np.array([p[5], p[3], p[4], p[2], p[0], p[1]], np.float32)
+                        self.g.add_loop(latest, int(rs["id"]), frm, to)
+                    if use_sc:
+                        x = np.asarray(sc["xyzrpy"], np.float32)
+                        self.g.add_loop(latest, int(sc["id"]), np.array([x[3], x[4], x[5], x[0], x[1], x[2]], np.float32),
+                                        np.zeros(6, np.float32))
+                    self.g.optimize()
+                    self.pending = True
+                    self.loops += 1
+        return f

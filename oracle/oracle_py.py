@@ -48,7 +48,7 @@ class SloConfig(ctypes.Structure):
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
         ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
-        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32),
     ]
 
 
@@ -96,6 +96,10 @@ def lib():
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
         L.oracle_set_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_step_map.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        L.oracle_step_loop.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        L.oracle_set_key_poses.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+        L.oracle_rs_loop_from.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_xsc_create.restype = ctypes.c_void_p
         L.oracle_xsc_create.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_int, ctypes.c_int]
         L.oracle_xsc_destroy.argtypes = [ctypes.c_void_p]
@@ -124,7 +128,7 @@ def gen_scan(pid, config_id, stream_id, k):
 
 
 _DTYPES = {
-    "map_ids": np.int32, "sc_count": np.int32,
+    "map_ids": np.int32, "sc_count": np.int32, "kf_pre": np.float32,
     "range": np.float32, "label": np.int32, "ground": np.int8, "seg_ground": np.uint8, "seg_col": np.uint32,
     "seg_range": np.float32, "ring_start": np.int32, "ring_end": np.int32, "orient": np.float32,
     "curvature": np.float32, "picked": np.int32, "cloud_label": np.int32, "smooth_ind": np.int32,
@@ -238,6 +242,21 @@ class OracleStream:
         pts = np.ascontiguousarray(pts, np.float32)
         return lib().oracle_step(self.h, pts.ctypes.data, len(pts), float(t))
 
+    def step_map(self, pts, t):
+        """the nodes up to mapOptimization::run: flags 1, 2, 4"""
+        pts = np.ascontiguousarray(pts, np.float32)
+        return lib().oracle_step_map(self.h, pts.ctypes.data, len(pts), float(t))
+
+    def step_loop(self, map_flags, t):
+        """SC detect + loop verification after a keyframe: flags 8, 16"""
+        return lib().oracle_step_loop(self.h, int(map_flags), float(t))
+
+    def set_key_poses(self, poses6, transform=None):
+        """correctPoses from a pose-graph estimate (MapOptimization::set_key_poses)"""
+        p = np.ascontiguousarray(poses6, np.float32).reshape(-1, 6)
+        t = None if transform is None else np.ascontiguousarray(transform, np.float32).reshape(6)
+        lib().oracle_set_key_poses(self.h, p.ctypes.data, len(p), None if t is None else t.ctypes.data)
+
     def set_rings(self, rings):
         """useCloudRing (cfg.use_cloud_ring): ring per input point, message order"""
         r = np.ascontiguousarray(rings, np.uint16)
@@ -315,3 +334,12 @@ class XscOracle:
             lib().oracle_xsc_destroy(self.h)
         except Exception:
             pass
+
+
+def rs_loop_from(corr_xyzrpy, latest_pose6):
+    """the RS loop factor's poseFrom arguments (oracle_rs_loop_from, MO:1027-1037)"""
+    c = np.ascontiguousarray(corr_xyzrpy, np.float32).reshape(6)
+    k = np.ascontiguousarray(latest_pose6, np.float32).reshape(6)
+    out = np.zeros(6, np.float32)
+    lib().oracle_rs_loop_from(c.ctypes.data, k.ctypes.data, out.ctypes.data)
+    return out

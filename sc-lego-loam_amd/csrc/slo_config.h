@@ -107,6 +107,7 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->leaf_surrounding_key_poses = (float)1.0;
     c->map_keyframes = 0;
     c->keyframe_ring = 0;
+    c->pose_graph = 0;
     return 0;
 }
 #endif

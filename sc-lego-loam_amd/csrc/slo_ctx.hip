@@ -237,6 +237,10 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
+    if (cfg->pose_graph && slo::pg_alloc(ctx)) {
+        slo_destroy(ctx);
+        return SLO_E_CAPACITY;
+    }
     if (cfg->loop_verify && slo::lc_alloc(ctx)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
@@ -259,6 +263,7 @@ void slo_destroy(slo_ctx* ctx) {
     slo::grid_free(ctx->grid_oc);
     slo::grid_free(ctx->grid_os);
     slo::lc_free(ctx);
+    slo::pg_free(ctx);
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->h_st) hipHostFree(ctx->h_st);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
@@ -335,11 +340,15 @@ int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t
     if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
     SLO_CHECK(hipSetDevice(ctx->dev));
     SLO_LAUNCH(ctx, "clear_flags", slo::k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
+    ctx->mapped_now = false;
     if (!ctx->fa_published) return SLO_OK;
     if (!(t_scan - ctx->t_last_processing >= ctx->cfg.mapping_process_interval)) return SLO_OK;
     ctx->t_last_processing = t_scan;
     int r = slo::map_run(ctx, (const float4*)d_points, d_counts);
     if (r) return r;
+    ctx->mapped_now = true;
+    // the graph half of saveKeyFramesAndFactor, then correctPoses (MO:1697-1699)
+    if (ctx->cfg.pose_graph && (r = slo::pg_after_mapping(ctx))) return r;
     return slo::lc_archive_run(ctx, t_scan);   // keyframe archive for loop verification (cfg.loop_verify)
 }
 
@@ -361,7 +370,9 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     if (!ctx->cfg.loop_closure_enable) return SLO_OK;
     r = slo_batch_sc_detect(ctx);
     if (r || !ctx->cfg.loop_verify) return r;
-    return slo_batch_loop_closure(ctx);
+    r = slo_batch_loop_closure(ctx);
+    if (r || !ctx->cfg.pose_graph || !ctx->mapped_now) return r;
+    return slo::pg_after_loops(ctx);   // the loop factors (MO:1038-1046, 1083-1091)
 }
 
 int slo_batch_loop_closure(slo_ctx* ctx) {

@@ -65,6 +65,10 @@ struct StreamState {
     // transformFusion (transformFusion.cpp): /aft_mapped_to_init as it
     // decodes it (publishTF, MO:680-705) and its /integrated_to_init
     float tf_aft[6], tf_bef[6], integrated[6];
+    // the transform a saved keyframe hands to the pose graph
+    // (transformTobeMapped for the first, else transformAftMapped before
+    // the estimate replaces it, MO:1541-1555)
+    float kf_pre[6];
     // scan context
     int32_t sc_count, sc_tree_n, sc_counter;
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];
@@ -456,6 +460,13 @@ struct slo_ctx {
     slo::LcView lc{};
     slo::HashGrid grid_lc;
     int32_t* h_lc_active = nullptr;     // pinned copy of lc.n_active
+    // pose-graph back end (cfg.pose_graph, slo_pgwire.hip)
+    std::vector<slo_pg*> pg;            // one graph per stream
+    std::vector<char> pg_pending;       // aLoopIsClosed
+    std::vector<std::vector<float>> pg_snap;   // key poses of the last save, for correctPoses without a new keyframe
+    float* d_pg_poses = nullptr;
+    size_t pg_cap = 0;
+    bool mapped_now = false;            // this batch step ran the mapping stage
 };
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -463,6 +474,11 @@ namespace slo {
 void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a);
 bool timing_on(const slo_ctx* ctx, const char* name);
 void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a);
+struct PgTf { float t[6]; };
+int pg_alloc(slo_ctx* ctx);
+void pg_free(slo_ctx* ctx);
+int pg_after_mapping(slo_ctx* ctx);
+int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
 int fa_odometry_run(slo_ctx* ctx, bool first_scan);

@@ -9,10 +9,12 @@
 // initial value) with the Scan Context descriptor build of the keyframe
 // (Scancontext.cpp:151-244).
 //
-// Layout: keyframe clouds are stored once, already in the map frame
-// (transformPointCloud with the keyframe pose, MO:566-596 — the pose never
-// changes on this path, so transforming at save time equals the reference's
-// transform at deque insertion).  Each LM iteration is two launches: every
+// Layout: keyframe clouds are stored once in their body frame and
+// transformed with the current key pose when the local map is assembled
+// (transformPointCloud, MO:566-596): between correctPoses the poses do not
+// change, so this equals the reference's transform at deque insertion, and a
+// correctPoses (slo_set_key_poses) takes effect at the next assembly, as the
+// reference's cleared-and-rebuilt deque does (MO:1642-1664).  Each LM iteration is two launches: every
 // workgroup of a stream takes a contiguous slice of its corner+surf queries,
 // does the exact 5-NN in the hash grid, the 3x3 Jacobi / 5x3 QR of the
 // reference and accumulates A^T A, A^T b in double-double (slo_ddsum.h); a
@@ -244,12 +246,29 @@ __global__ void k_mo_assemble(DevView v) {
     const int slot = ids[e] % v.KFR;
     const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
     const size_t ks = (size_t)s * v.KFR + slot;
+    // transformPointCloud with cloudKeyPoses6D[id] (MO:566-596): the ring
+    // keeps body-frame clouds, so a pose correctPoses rewrote is used as is
+    __shared__ float tr[9];
+    if (threadIdx.x == 0) {
+        const float* kp = v.kf_pose + ((size_t)s * v.KFMAX + ids[e]) * 6;
+        tr[0] = slo_libm::cosf_(kp[3]); tr[1] = slo_libm::sinf_(kp[3]);
+        tr[2] = slo_libm::cosf_(kp[4]); tr[3] = slo_libm::sinf_(kp[4]);
+        tr[4] = slo_libm::cosf_(kp[5]); tr[5] = slo_libm::sinf_(kp[5]);
+        tr[6] = kp[0]; tr[7] = kp[1]; tr[8] = kp[2];
+    }
+    __syncthreads();
+    const float ctRoll = tr[0], stRoll = tr[1], ctPitch = tr[2], stPitch = tr[3], ctYaw = tr[4], stYaw = tr[5];
+    auto xf = [&](const float4 p) {
+        const float x1 = ctYaw * p.x - stYaw * p.y, y1 = stYaw * p.x + ctYaw * p.y, z1 = p.z;
+        const float x2 = x1, y2 = ctRoll * y1 - stRoll * z1, z2 = stRoll * y1 + ctRoll * z1;
+        return make_float4(ctPitch * x2 + stPitch * z2 + tr[6], y2 + tr[7], -stPitch * x2 + ctPitch * z2 + tr[8], p.w);
+    };
     for (int i = threadIdx.x; i < kn[0]; i += blockDim.x)
-        if (oc + i < v.cap_mc) v.map_c[(size_t)s * v.cap_mc + oc + i] = v.kf_corner[ks * v.cap_kc + i];
+        if (oc + i < v.cap_mc) v.map_c[(size_t)s * v.cap_mc + oc + i] = xf(v.kf_corner[ks * v.cap_kc + i]);
     for (int i = threadIdx.x; i < kn[1]; i += blockDim.x)
-        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = v.kf_surf[ks * v.cap_kfs + i];
+        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = xf(v.kf_surf[ks * v.cap_kfs + i]);
     for (int i = threadIdx.x; i < kn[2]; i += blockDim.x)
-        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = v.kf_outl[ks * v.cap_kfo + i];
+        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = xf(v.kf_outl[ks * v.cap_kfo + i]);
 }
 
 __global__ void k_mo_concat(DevView v) {
@@ -611,6 +630,7 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
             if ((saveThis || st.n_keyframes == 0) && st.n_keyframes < v.KFMAX) {
                 st.prevPos[0] = cx; st.prevPos[1] = cy; st.prevPos[2] = cz;
                 float est[6];
+                for (int i = 0; i < 6; ++i) st.kf_pre[i] = st.n_keyframes == 0 ? st.transformTobeMapped[i] : st.transformAftMapped[i];
                 if (st.n_keyframes == 0) {   // iSAM2 estimate = initial value, through Rot3
                     for (int i = 0; i < 6; ++i) st.transformLast[i] = st.transformTobeMapped[i];
                     slo_pose::keyframe_estimate(st.transformTobeMapped, est);
@@ -637,11 +657,8 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
     }
     __syncthreads();
     if (!save) return;
-    // keyframe clouds in the map frame (transformPointCloud, MO:566-596)
-    using slo_libm::sinf_;
-    using slo_libm::cosf_;
-    const float ctRoll = cosf_(pose[3]), stRoll = sinf_(pose[3]), ctPitch = cosf_(pose[4]), stPitch = sinf_(pose[4]);
-    const float ctYaw = cosf_(pose[5]), stYaw = sinf_(pose[5]);
+    // the keyframe's DS clouds, body frame (cornerCloudKeyFrames & co,
+    // MO:1634-1636); k_mo_assemble transforms them with the key pose
     const int slot = kfid % v.KFR;
     const size_t ks = (size_t)s * v.KFR + slot;
     const int n3[3] = {min(st.n_corner_ds, v.cap_kc), min(st.n_surf_ds, v.cap_kfs), min(st.n_outl_ds, v.cap_kfo)};
@@ -649,12 +666,7 @@ __global__ void __launch_bounds__(256) k_mo_finish(DevView v) {
                             v.cur_o_ds + (size_t)s * v.cap_ko};
     float4* dst[3] = {v.kf_corner + ks * v.cap_kc, v.kf_surf + ks * v.cap_kfs, v.kf_outl + ks * v.cap_kfo};
     for (int c = 0; c < 3; ++c)
-        for (int i = threadIdx.x; i < n3[c]; i += blockDim.x) {
-            float4 p = src[c][i];
-            float x1 = ctYaw * p.x - stYaw * p.y, y1 = stYaw * p.x + ctYaw * p.y, z1 = p.z;
-            float x2 = x1, y2 = ctRoll * y1 - stRoll * z1, z2 = stRoll * y1 + ctRoll * z1;
-            dst[c][i] = make_float4(ctPitch * x2 + stPitch * z2 + pose[0], y2 + pose[1], -stPitch * x2 + ctPitch * z2 + pose[2], p.w);
-        }
+        for (int i = threadIdx.x; i < n3[c]; i += blockDim.x) dst[c][i] = src[c][i];
     if (threadIdx.x < 3) v.kf_n[ks * 3 + threadIdx.x] = n3[threadIdx.x];
     if (threadIdx.x == 0 && (n3[0] < st.n_corner_ds || n3[1] < st.n_surf_ds || n3[2] < st.n_outl_ds))
         st.err |= SLO_ERR_MAP_CAPACITY;

@@ -47,7 +47,7 @@ class SloConfig(ctypes.Structure):
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
         ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
-        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32),
     ]
 
 
@@ -117,7 +117,7 @@ EXPORTS = [
     # synthetic stream generator on the device (csrc/slo_gendev.hip)
     "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
     # pose-graph back end (csrc/slo_pg.hip, host side)
-    "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform",
+    "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform", "slo_set_key_poses",
 ]
 
 
@@ -172,6 +172,7 @@ def lib():
     L.slo_timing_read.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_int]
     L.slo_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, P]
     L.slo_gen_batch.argtypes = [ctypes.c_int] * 6 + [P, ctypes.c_int]
+    L.slo_set_key_poses.argtypes = [P, ctypes.c_int, P, ctypes.c_int, P]
     L.slo_xsc_create.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.POINTER(P)]
     L.slo_xsc_destroy.argtypes = [P]
     L.slo_xsc_ingest.argtypes = [P, P, ctypes.c_int, P]
