@@ -64,6 +64,8 @@ def parse():
     ap.add_argument("--streams", type=int, default=512, help="streams per GPU")
     ap.add_argument("--groups", type=int, default=3,
                     help="contexts per GPU, each on its own HIP stream and host thread (slo_amd.dist.group_slices)")
+    ap.add_argument("--stagger", action="store_true",
+                    help="context g runs g scans ahead (with 4 contexts each maps on its own step)")
     ap.add_argument("--preset", default="hdl64_1800")
     ap.add_argument("--keyframe-cap", type=int, default=32768,
                     help="slo_config.keyframe_cloud_cap: points per keyframe surf/outlier cloud (0 = worst case); "
@@ -349,7 +351,11 @@ def main():
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
     ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     n_ctx = len(ctxs)
-    nwin = a.warmup + a.steps + a.profile_steps
+    # --stagger: context g runs lag(g) = g scans ahead, so with as many
+    # contexts as the mapping period the contexts map on different steps
+    lag = (lambda g: g) if a.stagger else (lambda g: 0)
+    maxlag = max(lag(g) for g in range(len(groups)))
+    nwin = a.warmup + a.steps + a.profile_steps + maxlag
     dev = torch.empty((max(nwin, a.chunk), S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
     gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
@@ -386,12 +392,13 @@ def main():
 
     # ---- pre-roll: scans [0, preroll), generated on the device a chunk at a time
     t_pre = time.time()
-    for k0 in range(0, a.preroll, a.chunk):
-        nk = min(a.chunk, a.preroll - k0)
+    for k0 in range(0, a.preroll + maxlag, a.chunk):
+        nk = min(a.chunk, a.preroll + maxlag - k0)
         sync_all()
         gen.scans(k0, nk, dev.data_ptr())
         for j in range(nk):
-            each(lambda g, c, o, n: c.batch_process(dev[j, o].data_ptr(), cnt[o].data_ptr(), 0.1 * (k0 + j)))
+            each(lambda g, c, o, n: c.batch_process(dev[j, o].data_ptr(), cnt[o].data_ptr(), 0.1 * (k0 + j))
+                 if k0 + j < a.preroll + lag(g) else None)
     sync_all()
     t_pre = time.time() - t_pre
     base = a.preroll
@@ -400,8 +407,9 @@ def main():
     gen.close()
     t_gen += time.time() - t1
 
-    def step(k):   # k = index into the resident window; scan base + k
-        each(lambda g, c, o, n: c.batch_process(dev[k, o].data_ptr(), cnt[o].data_ptr(), 0.1 * (base + k)))
+    def step(k):   # k = index into the resident window; context g processes scan base + lag(g) + k
+        each(lambda g, c, o, n: c.batch_process(dev[k + lag(g), o].data_ptr(), cnt[o].data_ptr(),
+                                                0.1 * (base + lag(g) + k)))
         if gather:   # records of every group, then one all-gather after all of them
             evs = []
             for g, c in enumerate(ctxs):
@@ -470,7 +478,8 @@ def main():
         map_steps = 0
         for k in range(k0, k0 + a.profile_steps):
             for g, c in enumerate(ctxs):
-                c.batch_process(dev[k, groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(), 0.1 * (base + k))
+                c.batch_process(dev[k + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
+                                0.1 * (base + lag(g) + k))
                 c.synchronize()
             map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
         for c in ctxs:
@@ -548,6 +557,7 @@ def main():
                                    "steady state",
                        "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
                        "scans_per_step": S * world, "preroll_scans": a.preroll,
+                       "context_phase_lag": [lag(g) for g in range(n_ctx)],
                        "timed_scans": [base + a.warmup, base + a.warmup + a.steps - 1],
                        "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
                        "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),

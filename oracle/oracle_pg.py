@@ -162,8 +162,8 @@ class PipelineWithGraph:
     candidates add Cauchy loop factors and the graph is solved
     (MO:1030-1046, 1078-1091)."""
 
-    def __init__(self, stream):
-        self.st, self.g, self.pending, self.snap = stream, Graph(), False, None
+    def __init__(self, stream, graph=None):
+        self.st, self.g, self.pending, self.snap = stream, graph if graph is not None else Graph(), False, None
         self.loops = 0
 
     def step(self, pts, t):

@@ -104,9 +104,14 @@ Pose se3_exp(const double* d) {
 }
 
 void so3_log(const double* R, double* w) {
+    // theta = atan2(|axis sin|, cos): acos of (tr - 1) / 2 loses half the
+    // digits at the small angles the stiff odometry factors live at (an angle
+    // of 1e-7 rad would carry a 1 % error), which stalls the solve
     double tr = R[0] + R[4] + R[8];
-    double c = std::fmax(-1.0, std::fmin(1.0, 0.5 * (tr - 1)));
-    double th = std::acos(c);
+    double c = 0.5 * (tr - 1);
+    const double v[3] = {0.5 * (R[7] - R[5]), 0.5 * (R[2] - R[6]), 0.5 * (R[3] - R[1])};
+    const double sn = std::sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+    double th = std::atan2(sn, c);
     if (th > M_PI - 1e-4) {  // near pi: axis from the largest diagonal of (R + I)/2
         int k = (R[0] >= R[4] && R[0] >= R[8]) ? 0 : (R[4] >= R[8] ? 1 : 2);
         double a[3];
@@ -118,10 +123,10 @@ void so3_log(const double* R, double* w) {
         for (int i = 0; i < 3; ++i) w[i] = th * a[i] / n;
         return;
     }
-    double f = (th < 1e-5) ? 0.5 * (1 + th * th / 6) : th / (2 * std::sin(th));
-    w[0] = f * (R[7] - R[5]);
-    w[1] = f * (R[2] - R[6]);
-    w[2] = f * (R[3] - R[1]);
+    const double f = (sn < 1e-12) ? 1.0 + th * th / 6 : th / sn;   // theta / sin(theta)
+    w[0] = f * v[0];
+    w[1] = f * v[1];
+    w[2] = f * v[2];
 }
 
 void se3_log(const Pose& p, double* d) {

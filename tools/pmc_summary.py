@@ -41,19 +41,30 @@ def short(kname, names):
     return k
 
 
+def window(rows):
+    """rows between the last two bench.py --trace-marker spin kernels (by
+    Dispatch_Id), i.e. the timed steps; all rows when there are no markers"""
+    marks = sorted({int(r["Dispatch_Id"]) for r in rows if re.search(r"spin|sleep", r["Kernel_Name"], re.I)})
+    if len(marks) < 2:
+        return rows
+    lo, hi = marks[-2], marks[-1]
+    return [r for r in rows if lo < int(r["Dispatch_Id"]) < hi]
+
+
 def main(src, dst):
     names = launch_names()
     out = defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "fetch_kib": 0.0, "write_kib": 0.0,
                                "pmc_calls_fetch": 0, "pmc_calls_write": 0})
-    for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv"))):
+    kt = glob.glob(os.path.join(src, "kt", "**", "*kernel_trace.csv"), recursive=True)
+    for r in window(list(csv.DictReader(open(kt[0])))):
         n = short(r["Kernel_Name"], names)
         out[n]["calls"] += 1
         out[n]["total_ns"] += int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     for which, key in (("pmc_fetch", "fetch_kib"), ("pmc_write", "write_kib")):
-        p = os.path.join(src, which, "pmc_counter_collection.csv")
-        if not os.path.exists(p):
+        ps = glob.glob(os.path.join(src, which, "**", "*counter_collection.csv"), recursive=True)
+        if not ps:
             continue
-        for r in csv.DictReader(open(p)):
+        for r in window(list(csv.DictReader(open(ps[0])))):
             n = short(r["Kernel_Name"], names)
             out[n][key] += float(r["Counter_Value"])
             out[n]["pmc_calls_" + key.split("_")[0]] += 1
