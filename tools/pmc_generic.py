@@ -12,8 +12,11 @@ from collections import defaultdict
 def main(d, filt=""):
     acc = defaultdict(lambda: defaultdict(float))
     calls = defaultdict(lambda: defaultdict(int))
+    import os
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from pmc_summary import window   # the timed steps when bench.py ran with --trace-marker
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
-        for r in csv.DictReader(open(f)):
+        for r in window(list(csv.DictReader(open(f)))):
             k = re.sub(r"\(.*$", "", r["Kernel_Name"]).replace("void ", "").split("::")[-1][:40]
             if filt and filt not in k:
                 continue
