@@ -231,8 +231,8 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // the odometry surf grid answers 1-NN within 5 m (nearestFeatureSearchSqDist)
     // in 1 m cells (2^15 buckets: built in LDS by one workgroup per stream,
     // slo_vg.hip); the sparse corner cloud is searched by brute force.
-    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f, true) ||
-        slo::grid_alloc(ctx, ctx->grid_s, 1 << 17, v.cap_ms, 0.5f, true) ||
+    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
+        slo::grid_alloc(ctx, ctx->grid_s, 1 << 17, v.cap_ms, 0.5f) ||
         slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL)) {
         slo_destroy(ctx);
         return SLO_E_HIP;

@@ -91,7 +91,6 @@ struct GridView {
     size_t es;
     const int32_t *cnt, *off;
     const float4* ent;
-    const int32_t* eidx;   // keyed grids: entry -> point index (w holds the row key, grid_row_key)
 };
 
 // kernel-visible view of the context (passed by value)
@@ -223,13 +222,6 @@ __host__ __device__ inline unsigned int grid_hash(int x, int y, int z, int T) {
     return ((unsigned int)x + (unsigned int)y * 1031u + (unsigned int)z * 620531u) & (unsigned int)(T - 1);
 }
 __host__ __device__ inline int grid_cell(float x, float inv) { return (int)floorf(x * inv); }
-// keyed grids: an entry's w holds its (y, z) cell pair, 16 bits each; with
-// the x coefficient 1 of grid_hash, an entry of a row's bucket run whose key
-// matches lies in that row (a cell 2^16 cells away could share the key, but
-// it is far outside every search ball, so its distance rejects it)
-__host__ __device__ inline unsigned int grid_row_key(int cy, int cz) {
-    return ((unsigned int)cy & 0xffffu) | ((unsigned int)cz << 16);
-}
 
 // XCD-aware 1-D grids for (stream, chunk) work: blocks b and b + 8 share an
 // XCD (MI355X_MICROARCH.md "Workgroup dispatch"), so stream s goes to the XCD
@@ -367,58 +359,6 @@ __device__ inline void grid_ball(const GridView& g, int s, float qx, float qy, f
     grid_ball_rows<R, U>(g, s, qx, qy, qz, 0, GridRows<R>::N, 1, true, bound, f);
 }
 
-// grid_ball over a keyed grid: the row membership test is one integer compare
-// of the entry's key instead of three cell computations per point, and
-// f(p, e) gets the entry's position in the stream's entry run (the point
-// index is g.eidx[s * g.es + e], read only by a caller that keeps the point).  Same visiting order and early
-// stops as grid_ball_rows; the probed cell's own row skips the probed cell by
-// its x cell.
-template <int R, int U = GBALL_UNROLL, class B, class F>
-__device__ inline void grid_ball_keyed(const GridView& g, int s, float qx, float qy, float qz, B&& bound, F&& f) {
-    const float inv = g.inv, cell = g.cell, c2 = cell * cell;
-    const int cx = grid_cell(qx, inv), cy = grid_cell(qy, inv), cz = grid_cell(qz, inv);
-    const size_t gb = (size_t)s * (g.T + 1);
-    const int base = g.off[gb];
-    const float4* E = g.ent + (size_t)s * g.es;
-    auto run = [&](int e0, int e1, unsigned int key, bool skip_cx) {
-        for (int e = e0; e < e1; e += U) {
-            float4 p[U];
-#pragma unroll
-            for (int u = 0; u < U; ++u) p[u] = e + u < e1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-                if (e + u >= e1) break;
-                if (__float_as_uint(p[u].w) != key) continue;
-                if (skip_cx && grid_cell(p[u].x, inv) == cx) continue;
-                f(p[u], e + u);
-            }
-        }
-    };
-    {   // probe: the query's own cell
-        const int h0 = (int)grid_hash(cx, cy, cz, g.T);
-        run(g.off[gb + h0] - base, g.off[gb + h0 + 1] - base, grid_row_key(cy, cz), false);
-    }
-    for (int k = 0; k < GridRows<R>::N; ++k) {
-        const float b = bound();
-        if ((float)kGridRows<R>.gap[k] * c2 > b) break;
-        const int dy = kGridRows<R>.dy[k], dz = kGridRows<R>.dz[k];
-        const int yy = cy + dy, zz = cz + dz;
-        const float ey = dy > 0 ? (float)yy * cell - qy : (dy < 0 ? qy - (float)(yy + 1) * cell : 0.0f);
-        const float ez = dz > 0 ? (float)zz * cell - qz : (dz < 0 ? qz - (float)(zz + 1) * cell : 0.0f);
-        float lb = ey * ey;
-        lb += ez * ez;
-        if (lb > b) continue;
-        const float rx = sqrtf((b - lb) * 1.0001f + 1e-5f * b) + 1e-3f;
-        const int xa = max(cx - R, grid_cell(qx - rx, inv)), xb = min(cx + R, grid_cell(qx + rx, inv));
-        const int h = (int)grid_hash(xa, yy, zz, g.T), len = xb - xa + 1;
-        const int h2 = min(h + len, g.T);
-        const unsigned int key = grid_row_key(yy, zz);
-        run(g.off[gb + h] - base, g.off[gb + h2] - base, key, k == 0);
-        const int w1 = h + len - h2;   // buckets wrapped to the table start
-        if (w1 > 0) run(0, g.off[gb + w1] - base, key, k == 0);
-    }
-}
-
 // ---- loop-closure verification (slo_lc.hip; mapOptmization.cpp:841-1110)
 #define SLO_LC_MAX_N 64                      // historyKeyframeSearchNum limit
 #define SLO_LC_SEG (2 * SLO_LC_MAX_N + 1)    // submap keyframes id-N .. id+N
@@ -477,7 +417,6 @@ struct HashGrid {
     size_t ent_stride = 0;
     int32_t *cnt = nullptr, *cur = nullptr, *off = nullptr;
     float4* ent = nullptr;
-    int32_t* eidx = nullptr;   // keyed grid (grid_alloc keyed): point index per entry
     void* temp = nullptr;
     size_t temp_bytes = 0;
 };
@@ -547,7 +486,7 @@ int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);
-int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell, bool keyed = false);
+int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell);
 GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);

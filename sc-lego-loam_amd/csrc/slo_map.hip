@@ -318,10 +318,9 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
     if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return 0;
     auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
     int n = 0;
-    grid_ball_keyed<2, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p, int e) {
+    grid_ball<2, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
         const float d = sqd(q, p.x, p.y, p.z);
-        if (d > od[4]) return;
-        const int idx = g.eidx[(size_t)s * g.es + e];   // the index, only for a point that may enter
+        const int idx = __float_as_int(p.w);
         if (!less(d, idx, od[4], oi[4])) return;
         bool placed = false;
 #pragma unroll

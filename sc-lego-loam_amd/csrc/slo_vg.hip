@@ -367,21 +367,15 @@ __global__ void k_grid_count(const float4* pts, size_t stride, const int32_t* n,
 }
 
 __global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
-                               const int32_t* off, int32_t* cur, float4* ent, size_t ent_stride, int32_t* eidx) {
+                               const int32_t* off, int32_t* cur, float4* ent, size_t ent_stride) {
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
     const int base = off[(size_t)s * (T + 1)];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const float4 p = pts[(size_t)s * stride + i];
-        const int cy = grid_cell(p.y, inv), cz = grid_cell(p.z, inv);
-        const unsigned int b = grid_hash(grid_cell(p.x, inv), cy, cz, T);
+        const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
         const int pos = off[(size_t)s * (T + 1) + b] - base + atomicAdd(&cur[(size_t)s * (T + 1) + b], 1);
-        if (eidx) {   // keyed: w = the row key, the index beside
-            ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __uint_as_float(grid_row_key(cy, cz)));
-            eidx[(size_t)s * ent_stride + pos] = i;
-        } else {
-            ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
-        }
+        ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
     }
 }
 
@@ -463,7 +457,7 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
     size_t tb = g.temp_bytes;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)nb, ctx->stream));
     SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
-               g.off, g.cur, g.ent, g.ent_stride, g.eidx);
+               g.off, g.cur, g.ent, g.ent_stride);
     SLO_LAUNCH(ctx, "grid_clear", k_grid_clear, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt,
                g.cur);
     SLO_CHECK(hipGetLastError());
@@ -471,7 +465,7 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
 }
 
 // cell: power-of-two edge length in metres (exact floor(x / cell), GridView)
-int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell, bool keyed) {
+int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) {
     const int S = ctx->S;
     int e2;
     if (T <= 0 || (T & (T - 1)) || !(cell > 0) || frexpf(cell, &e2) != 0.5f) {
@@ -488,7 +482,6 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell, 
     SLO_CHECK(hipMemset(g.cnt, 0, sizeof(int32_t) * nb));   // kept zero between builds (k_grid_clear)
     SLO_CHECK(hipMemset(g.cur, 0, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.ent, sizeof(float4) * (size_t)S * ent_stride));
-    if (keyed) SLO_CHECK(hipMalloc(&g.eidx, sizeof(int32_t) * (size_t)S * ent_stride));
     size_t tb = 0;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g.cnt, g.off, (int)nb, ctx->stream));
     g.temp_bytes = tb;
@@ -505,7 +498,6 @@ GridView grid_view(const HashGrid& g) {
     v.cnt = g.cnt;
     v.off = g.off;
     v.ent = g.ent;
-    v.eidx = g.eidx;
     return v;
 }
 
@@ -514,7 +506,6 @@ void grid_free(HashGrid& g) {
     if (g.cur) hipFree(g.cur);
     if (g.off) hipFree(g.off);
     if (g.ent) hipFree(g.ent);
-    if (g.eidx) hipFree(g.eidx);
     if (g.temp) hipFree(g.temp);
     g = HashGrid();
 }
