@@ -93,3 +93,16 @@ def test_bad_arguments_are_rejected_without_a_device(lib):
     assert lib.slo_record_floats() == _abi.RECORD_FLOATS == 1240
     assert lib.slo_batch_process(None, None, None, 0.0) == -1
     assert lib.slo_get(None, 0, b"range", None, 0) == -1
+
+
+def test_c_caller_compiles_and_runs_against_the_public_header(lib, tmp_path):
+    """a C99 program that includes only include/slo_abi.h links against
+    libslo.so and runs the host-side entry points (no GPU needed)"""
+    exe = tmp_path / "abi_caller"
+    libdir = os.path.dirname(LIB)
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "tests", "cpp", "abi_caller.c"), "-o", str(exe), f"-L{libdir}", "-lslo",
+                    f"-Wl,-rpath,{libdir}", "-lm"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert "abi_caller ok" in r.stdout

@@ -6,7 +6,8 @@
 #      steps by tools/trace_window.py / tools/pmc_summary.py            -> gpurun_out/<tag>/kt/
 #   3. rocprofv3 --pmc FETCH_SIZE, then WRITE_SIZE (separate passes, no trace
 #      domains; MI355X_MICROARCH.md "rocprofv3 PMC slots"), same command  -> gpurun_out/<tag>/pmc_*/
-# then (here) python3 tools/pmc_summary.py gpurun_out/<tag> profiles/<tag>.
+# The summaries (tools/pmc_summary.py -> <tag>/summary/summary.json, tools/trace_window.py ->
+# <tag>/window.json) are made on the box; copy them to profiles/<tag>/.
 # Every GPU step has its own time limit and the chain stops at the first failure.
 set -euo pipefail
 TAG=${1:-r02}
@@ -24,4 +25,8 @@ echo "[profile] FETCH_SIZE" && timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE --ou
     -d "$OUT/pmc_fetch" -o pmc -- python3 bench.py $SHORT > "$OUT/pmc_fetch.log" 2>&1
 echo "[profile] WRITE_SIZE" && timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
     -d "$OUT/pmc_write" -o pmc -- python3 bench.py $SHORT > "$OUT/pmc_write.log" 2>&1
+# summaries on the box (the raw CSVs are too big to travel back), then drop the raw dirs
+python3 tools/pmc_summary.py "$OUT" "$OUT/summary" > "$OUT/summary.txt"
+find "$OUT/kt" -name "*kernel_stats.csv" -exec cp {} "$OUT/kt_kernel_stats_full_run.csv" \;
+rm -rf "$OUT/kt" "$OUT/pmc_fetch" "$OUT/pmc_write"
 echo "[profile] done"
