@@ -404,6 +404,7 @@ struct MapWs {  // VoxelGrid workspace
     int *starts = nullptr, *ends = nullptr, *longv = nullptr;   // per voxel; long-voxel list
     int32_t* meta = nullptr;     // [total, max cell count, long-voxel count]
     int32_t* h_meta = nullptr;   // pinned copy
+    int32_t* h_off = nullptr;    // pinned copy of off [S + 1] (sort group ranges)
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int32_t* off = nullptr;

@@ -19,6 +19,11 @@
 #include <hipcub/hipcub.hpp>
 #include <float.h>
 
+// a filter whose voxel indices need more than this many bits sorts 64-bit
+// keys in one sort; up to it, groups of 2^(32 - vbits) >= 8 streams sort
+// 32-bit keys (vg_sorted)
+#define SLO_VG_GROUP_MAX_VBITS 29
+
 namespace slo {
 
 __device__ inline unsigned int f2ord(float f) {
@@ -127,11 +132,11 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
 // index, which sorts after every voxel of the stream and is never a voxel
 template <class K>
 __global__ void k_vg_keys(const float4* in, size_t in_stride, const int32_t* off, const VgParams* prm, int vbits,
-                          K* keys, unsigned int* vals) {
+                          int G, K* keys, unsigned int* vals) {
     const int s = blockIdx.y;
     const int base = off[s], n = off[s + 1] - base;
     const VgParams p = prm[s];
-    const K hi = (K)s << vbits, none = ((K)1 << vbits) - 1;
+    const K hi = (K)(s % G) << vbits, none = ((K)1 << vbits) - 1;   // stream bits local to its sort group
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         float4 q = in[(size_t)s * in_stride + i];
         K k;
@@ -150,26 +155,43 @@ __global__ void k_vg_keys(const float4* in, size_t in_stride, const int32_t* off
     }
 }
 
+// item j starts a sort group (G < S: the keys of two groups are not comparable)
+__device__ inline bool vg_group_start(const int32_t* off, int S, int G, int j) {
+    for (int g = G; g < S; g += G)
+        if (off[g] == j) return true;
+    return false;
+}
+
 template <class K>
-__global__ void k_vg_heads(const K* keys, int total, int vbits, int* flags) {
+__global__ void k_vg_heads(const K* keys, int total, int vbits, const int32_t* off, int S, int G, int* flags) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j > total) return;
     if (j == total) { flags[j] = 0; return; }
     const K k = keys[j], none = ((K)1 << vbits) - 1;
-    flags[j] = (k & none) != none && (j == 0 || k != keys[j - 1]);
+    flags[j] = (k & none) != none && (j == 0 || k != keys[j - 1] || vg_group_start(off, S, G, j));
 }
 
 // voxel r = rank of its first item: its item range [starts[r], ends[r])
 template <class K>
-__global__ void k_vg_runs(const K* keys, const int* rank, int total, int vbits, int* starts, int* ends) {
+__global__ void k_vg_runs(const K* keys, const int* rank, int total, int vbits, const int32_t* off, int S, int G,
+                          int* starts, int* ends) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= total) return;
     const K k = keys[j], none = ((K)1 << vbits) - 1;
     if ((k & none) == none) return;
-    const bool head = j == 0 || keys[j - 1] != k;
+    const bool head = j == 0 || keys[j - 1] != k || vg_group_start(off, S, G, j);
     const int r = head ? rank[j] : rank[j] - 1;   // rank = heads strictly before j
     if (head) starts[r] = j;
-    if (j + 1 == total || keys[j + 1] != k) ends[r] = j + 1;
+    if (j + 1 == total || keys[j + 1] != k || vg_group_start(off, S, G, j + 1)) ends[r] = j + 1;
+}
+
+// the stream of sorted item a whose key carries the group-local stream l:
+// sort group g holds the items of streams [g*G, (g+1)*G), i.e. positions
+// [off[g*G], off[(g+1)*G])
+__device__ inline int vg_stream(const int32_t* off, int S, int G, int l, int a) {
+    int g = 0;
+    while ((g + 1) * G < S && off[(g + 1) * G] <= a) ++g;
+    return g * G + l;
 }
 
 // Centroid of one voxel: the points are summed in input order (the sort is
@@ -188,8 +210,8 @@ __device__ inline void vg_store(const VgOut& o, const int* rank, const int32_t* 
 
 template <class K>
 __global__ void k_vg_centroid(const float4* in, size_t in_stride, const K* keys, const unsigned int* vals,
-                              const int* rank, const int32_t* off, int total, int vbits, const int* starts,
-                              const int* ends, int32_t* meta, int* longv, VgOut o) {
+                              const int* rank, const int32_t* off, int total, int vbits, int S, int G,
+                              const int* starts, const int* ends, int32_t* meta, int* longv, VgOut o) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= rank[total]) return;
     const int a = starts[r], e = ends[r];
@@ -197,7 +219,7 @@ __global__ void k_vg_centroid(const float4* in, size_t in_stride, const K* keys,
         longv[atomicAdd(&meta[2], 1)] = r;
         return;
     }
-    const int s = (int)(keys[a] >> vbits);
+    const int s = vg_stream(off, S, G, (int)(keys[a] >> vbits), a);
     const float4* src = in + (size_t)s * in_stride;
     float sx = 0, sy = 0, sz = 0, si = 0;
     for (int j = a; j < e; j += 4) {
@@ -217,15 +239,15 @@ __global__ void k_vg_centroid(const float4* in, size_t in_stride, const K* keys,
 template <class K>
 __global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_stride, const K* keys,
                                                  const unsigned int* vals, const int* rank, const int32_t* off,
-                                                 int vbits, const int* starts, const int* ends, const int32_t* meta,
-                                                 const int* longv, VgOut o) {
+                                                 int vbits, int S, int G, const int* starts, const int* ends,
+                                                 const int32_t* meta, const int* longv, VgOut o) {
     __shared__ float4 buf[4][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nlong = meta[2];
     float4* b = buf[w];
     for (int t = blockIdx.x * 4 + w; t < nlong; t += gridDim.x * 4) {
         const int r = longv[t], a = starts[r], e = ends[r];
-        const int s = (int)(keys[a] >> vbits);
+        const int s = vg_stream(off, S, G, (int)(keys[a] >> vbits), a);
         const float4* src = in + (size_t)s * in_stride;
         float acc = 0.0f;
         for (int c0 = a; c0 < e; c0 += 256) {
@@ -289,34 +311,45 @@ static int ensure_ws(slo_ctx* ctx, size_t items) {
     return 0;
 }
 
+// G streams per sort group: the (group-local stream, voxel) keys of group g
+// occupy the item range [off[g*G], off[(g+1)*G]), sorted on their own, so a
+// filter whose voxel index and stream count need more than 32 bits together
+// still sorts 32-bit keys (a third less traffic per pass than 64-bit keys,
+// and one pass fewer)
 template <class K>
 static int vg_sorted(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, int total, int vbits, int sbits,
-                     const VgOut& o) {
+                     int G, const VgOut& o) {
     MapWs& w = ctx->mws;
     const int S = ctx->S, T = 256;
     const int bx = std::max(1, std::min(64, (int)((in_stride + T - 1) / T)));
     K* keys = (K*)w.keys;
     K* keys2 = (K*)w.keys2;
-    SLO_LAUNCH(ctx, "vg_keys", k_vg_keys<K>, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.prm, vbits, keys,
+    SLO_LAUNCH(ctx, "vg_keys", k_vg_keys<K>, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.prm, vbits, G, keys,
                w.vals);
     size_t tb = w.temp_bytes;
     hipEvent_t ev = nullptr;
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
     const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
-    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys, keys2, w.vals, w.vals2, total, 0, vbits + sbits,
-                                                 ctx->stream));
+    for (int g0 = 0; g0 < S; g0 += G) {   // one sort per group (G = S: one sort)
+        const int a = G >= S ? 0 : w.h_off[g0], e = G >= S ? total : w.h_off[std::min(S, g0 + G)];
+        if (e <= a) continue;
+        tb = w.temp_bytes;
+        SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys + a, keys2 + a, w.vals + a, w.vals2 + a, e - a, 0,
+                                                     vbits + sbits, ctx->stream));
+    }
     if (tm) timing_end(ctx, sort_name.c_str(), ev);
     const int gi = (total + T - 1) / T;
-    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits,
-               w.flags);
+    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits, w.off,
+               S, G, w.flags);
     tb = w.temp_bytes;
     SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.flags, w.rank, total + 1, ctx->stream));
-    SLO_LAUNCH(ctx, "vg_runs", k_vg_runs<K>, dim3(gi), dim3(T), 0, keys2, w.rank, total, vbits, w.starts, w.ends);
+    SLO_LAUNCH(ctx, "vg_runs", k_vg_runs<K>, dim3(gi), dim3(T), 0, keys2, w.rank, total, vbits, w.off, S, G, w.starts,
+               w.ends);
     SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid<K>, dim3(gi), dim3(T), 0, in, in_stride, keys2, w.vals2, w.rank,
-               w.off, total, vbits, w.starts, w.ends, w.meta, w.longv, o);
+               w.off, total, vbits, S, G, w.starts, w.ends, w.meta, w.longv, o);
     SLO_LAUNCH(ctx, "vg_long", k_vg_long<K>, dim3(std::min(1024, gi)), dim3(T), 0, in, in_stride, keys2, w.vals2,
-               w.rank, w.off, vbits, w.starts, w.ends, w.meta, w.longv, o);
+               w.rank, w.off, vbits, S, G, w.starts, w.ends, w.meta, w.longv, o);
     return 0;
 }
 
@@ -330,8 +363,10 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.bounds);
     SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm,
                w.meta);
-    // one host round trip per filter: the item count and the key width
+    // one host round trip per filter: the item count, the key width and the
+    // stream offsets (the sort groups' item ranges)
     SLO_CHECK(hipMemcpyAsync(w.h_meta, w.meta, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
+    SLO_CHECK(hipMemcpyAsync(w.h_off, w.off, (S + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
     SLO_CHECK(hipStreamSynchronize(ctx->stream));
     const int total = w.h_meta[0];
     int vbits = 1;   // every index < 2^vbits - 1 (the all-ones index marks non-finite points)
@@ -342,8 +377,15 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     if (int r = ensure_ws(ctx, (size_t)total + 1)) return r;
     if (total > 0) {
         const VgOut o{out, out_stride, out_cap};
-        const int r = vbits + sbits <= 32 && vbits < 32 ? vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, sbits, o)
-                                          : vg_sorted<unsigned long long>(ctx, tag, in, in_stride, total, vbits, sbits, o);
+        int r;
+        if (vbits + sbits <= 32 && vbits < 32) {
+            r = vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, sbits, S, o);
+        } else if (vbits <= SLO_VG_GROUP_MAX_VBITS) {   // groups of G streams on 32-bit keys
+            const int gbits = 32 - vbits;
+            r = vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, gbits, 1 << gbits, o);
+        } else {
+            r = vg_sorted<unsigned long long>(ctx, tag, in, in_stride, total, vbits, sbits, S, o);
+        }
         if (r) return r;
     } else {
         SLO_CHECK(hipMemsetAsync(w.rank, 0, sizeof(int), ctx->stream));
@@ -520,6 +562,7 @@ int vg_alloc(slo_ctx* ctx) {
     SLO_CHECK(hipMemset(w.errflag, 0, sizeof(int32_t)));
     SLO_CHECK(hipMalloc(&w.meta, 4 * sizeof(int32_t)));
     SLO_CHECK(hipHostMalloc((void**)&w.h_meta, 4 * sizeof(int32_t)));
+    SLO_CHECK(hipHostMalloc((void**)&w.h_off, (S + 1) * sizeof(int32_t)));
     return 0;
 }
 
@@ -529,6 +572,7 @@ void vg_free(slo_ctx* ctx) {
                   w.temp, w.off, w.bounds, w.prm, w.errflag, w.meta};
     for (void* p : ps) if (p) hipFree(p);
     if (w.h_meta) hipHostFree(w.h_meta);
+    if (w.h_off) hipHostFree(w.h_off);
     w = MapWs();
 }
 
