@@ -9,7 +9,10 @@ stream (odometry pose, mapped pose, keyframe count, loop result, newest ring
 key and, on a keyframe, the exact Scan Context descriptor; slo_pack_records),
 so every rank holds every stream's descriptor history for cross-stream
 (multi-session) loop candidates (slo_amd.xsc).  Over RCCL that is
-world*S*4960 B per step (20 MB at 8 x 512 streams), a few tens of us on xGMI.
+world*S*4960 B per step: each rank contributes 2.5 MB at S = 512 and receives
+the other ranks' (17.8 MB at 8 ranks), on the order of 0.1 ms of ring time on
+xGMI against a ~21 ms step; measured at world size 1 (pack + gather + store
+ingest + query) the exchange costs 0.73 ms per step, mostly the query.
 """
 import torch
 import torch.distributed as dist
