@@ -396,17 +396,17 @@ struct LcView {
 };
 
 struct VgParams;
-struct MapWs {  // VoxelGrid workspace
-    size_t items = 0;
-    void *keys = nullptr, *keys2 = nullptr;   // 32- or 64-bit sort keys (8 B per item allocated)
+struct MapWs {  // VoxelGrid workspace (slo_vg.hip), sized on the host from the input strides only
+    size_t items = 0;             // S * largest input stride so far
+    size_t tiles = 0;             // S * largest tile count per stream so far
+    unsigned int *keys = nullptr, *keys2 = nullptr;   // radix-pass ping-pong
     unsigned int *vals = nullptr, *vals2 = nullptr;
-    int *flags = nullptr, *rank = nullptr;
-    int *starts = nullptr, *ends = nullptr, *longv = nullptr;   // per voxel; long-voxel list
-    int32_t* meta = nullptr;     // [total, max cell count, long-voxel count]
-    int32_t* h_meta = nullptr;   // pinned copy
-    int32_t* h_off = nullptr;    // pinned copy of off [S + 1] (sort group ranges)
-    void* temp = nullptr;
-    size_t temp_bytes = 0;
+    int* cnt = nullptr;           // [S][256][maxT] digit counts -> scatter bases
+    int* hcnt = nullptr;          // [S][maxT] voxel heads per tile -> ranks
+    int4* longv = nullptr;        // long voxels (stream, first item, rank)
+    size_t nlong_cap = 0;
+    int32_t* meta = nullptr;      // [total, -, long-voxel count]
+    int32_t* nvox = nullptr;      // [S] voxels per stream (before the output clip)
     int32_t* off = nullptr;
     unsigned int* bounds = nullptr;
     VgParams* prm = nullptr;
@@ -417,9 +417,8 @@ struct HashGrid {
     float cell = 1.0f;
     size_t ent_stride = 0;
     int32_t *cnt = nullptr, *cur = nullptr, *off = nullptr;
+    int32_t* bsum = nullptr;   // per-stream block sums of the offset scan
     float4* ent = nullptr;
-    void* temp = nullptr;
-    size_t temp_bytes = 0;
 };
 
 }  // namespace slo

@@ -4,25 +4,22 @@
 // VoxelGrid (PCL 1.8 VoxelGrid<PointXYZI>::applyFilter + CentroidPoint, the
 // filter the reference calls at featureAssociation.cpp:779 and
 // mapOptmization.cpp:1224-1262): per stream the bounds give min_b and the
-// x-fastest linear voxel index; all streams' (stream<<32 | idx, point) pairs
-// are radix sorted together (stable, so the points of a voxel stay in input
-// order), every voxel's centroid is summed in that order by one thread and
-// written at its rank -> output sorted by voxel index exactly like PCL.
-// Non-finite points are skipped (the raw cloud is not dense, MO:1236); the
-// int32 overflow guard returns the input unchanged, as PCL does.
+// x-fastest linear voxel index; each stream's (idx, point) pairs are sorted
+// by a hand-written segmented LSD radix sort (four passes of <= 8 bits,
+// stable, so the points of a voxel stay in input order; no stream bits in
+// the key), every voxel's centroid is summed in that order and written at
+// its rank -> output sorted by voxel index exactly like PCL.  Non-finite
+// points are skipped (the raw cloud is not dense, MO:1236); the int32
+// overflow guard returns the input unchanged, as PCL does.  All sizes come
+// from the input strides and device-side counts: no host round trip.
 //
 // Hash grid: power-of-two cells, counting sort of the points into hashed
 // buckets [S][T + 1] (the last bucket of each stream stays empty, so a run of
 // consecutive buckets ends at off[h + 1]); queried by grid_ball
 // (slo_internal.h).
 #include "slo_internal.h"
-#include <hipcub/hipcub.hpp>
 #include <float.h>
-
-// a filter whose voxel indices need more than this many bits sorts 64-bit
-// keys in one sort; up to it, groups of 2^(32 - vbits) >= 8 streams sort
-// 32-bit keys (vg_sorted)
-#define SLO_VG_GROUP_MAX_VBITS 29
+#include <string>
 
 namespace slo {
 
@@ -95,20 +92,28 @@ __global__ void __launch_bounds__(256) k_vg_bounds(const float4* in, size_t in_s
     }
 }
 
-// voxel-index parameters (PCL applyFilter) and the largest cell count over
-// the streams (meta[1]), which sizes the sort keys
-struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; };
+// voxel-index parameters (PCL applyFilter) per stream, and the stream's key
+// width: vbits (every voxel index < 2^vbits - 1, the all-ones key marks a
+// non-finite point), split into VG_PASSES digits of dbits each
+struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, ntiles; };
 
-__global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm,
-                            int32_t* meta) {
+#define VG_T 256                      // threads per tile workgroup
+#define VG_IPT 16                     // items per thread
+#define VG_TILE (VG_T * VG_IPT)       // items per tile
+#define VG_PASSES 4                   // LSD radix passes of <= 8 bits over 32-bit keys
+#define VG_PAD(j) ((j) + ((j) >> 4))  // LDS index padded against 16-way bank conflicts (blocked reads)
+
+__global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     VgParams p;
     p.inv = 1.0f / leaf;
     p.overflow = 0;
     const int n = off[s + 1] - off[s];
-    if (n == 0 || bounds[6 * s] == 0xffffffffu) {
+    p.ntiles = (n + VG_TILE - 1) / VG_TILE;
+    if (n == 0 || bounds[6 * s] == 0xffffffffu) {   // empty, or no finite point: every key is "none"
         p.minb[0] = p.minb[1] = p.minb[2] = 0; p.mul1 = p.mul2 = 0;
+        p.vbits = 1; p.dbits = 1;
         prm[s] = p;
         return;
     }
@@ -122,76 +127,304 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
     int divx = maxbx - p.minb[0] + 1, divy = maxby - p.minb[1] + 1, divz = maxbz - p.minb[2] + 1;
     p.mul1 = divx;
     p.mul2 = divx * divy;
-    prm[s] = p;
     // indices are < divx*divy*divz (or < n: the overflow keys are positions)
     const long long cells = p.overflow ? (long long)n : (long long)divx * divy * divz;
-    atomicMax(&meta[1], (int)min(cells, 2147483647LL));
+    int vb = 1;
+    while (vb < 32 && (1LL << vb) <= cells) ++vb;
+    if (cells >= (1LL << 30)) vb = 32;   // int index arithmetic may wrap, as in PCL
+    p.vbits = vb;
+    p.dbits = (vb + VG_PASSES - 1) / VG_PASSES;
+    prm[s] = p;
 }
 
-// keys: (stream << vbits) | voxel index; non-finite points get the all-ones
-// index, which sorts after every voxel of the stream and is never a voxel
-template <class K>
-__global__ void k_vg_keys(const float4* in, size_t in_stride, const int32_t* off, const VgParams* prm, int vbits,
-                          int G, K* keys, unsigned int* vals) {
-    const int s = blockIdx.y;
-    const int base = off[s], n = off[s + 1] - base;
-    const VgParams p = prm[s];
-    const K hi = (K)(s % G) << vbits, none = ((K)1 << vbits) - 1;   // stream bits local to its sort group
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        float4 q = in[(size_t)s * in_stride + i];
-        K k;
-        if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) {
-            k = hi | none;
-        } else if (p.overflow) {
-            k = hi | (K)(unsigned int)i;
-        } else {
-            int ijk0 = (int)(floorf(q.x * p.inv) - (float)p.minb[0]);
-            int ijk1 = (int)(floorf(q.y * p.inv) - (float)p.minb[1]);
-            int ijk2 = (int)(floorf(q.z * p.inv) - (float)p.minb[2]);
-            k = hi | (K)(unsigned int)(ijk0 + ijk1 * p.mul1 + ijk2 * p.mul2);
-        }
-        keys[base + i] = k;
-        vals[base + i] = (unsigned int)i;
+__device__ inline unsigned int vg_none(const VgParams& p) { return p.vbits >= 32 ? 0xffffffffu : (1u << p.vbits) - 1u; }
+
+// the PCL voxel index of point i of a stream (positions on overflow)
+__device__ inline unsigned int vg_key(const float4& q, const VgParams& p, int i) {
+    if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return vg_none(p);
+    if (p.overflow) return (unsigned int)i;
+    const int ijk0 = (int)(floorf(q.x * p.inv) - (float)p.minb[0]);
+    const int ijk1 = (int)(floorf(q.y * p.inv) - (float)p.minb[1]);
+    const int ijk2 = (int)(floorf(q.z * p.inv) - (float)p.minb[2]);
+    return (unsigned int)(ijk0 + ijk1 * p.mul1 + ijk2 * p.mul2);
+}
+
+// exclusive scan over the workgroup (NW waves of 64); *total = the sum
+template <int NW, class T>
+__device__ inline T vg_block_scan(T x, T* wsum, T* total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    T incl = x;
+    for (int o = 1; o < 64; o <<= 1) {
+        const T y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    T before = 0, all = 0;
+    for (int k = 0; k < NW; ++k) {
+        if (k < w) before += wsum[k];
+        all += wsum[k];
+    }
+    __syncthreads();   // wsum reusable
+    *total = all;
+    return before + incl - x;
+}
+
+// ---- LSD radix passes.  The items of stream s occupy [off[s], off[s+1]) of
+// the workspace; tile t of the stream is items [t*VG_TILE, (t+1)*VG_TILE),
+// read as 4 wave slices of 1024 (item j = w*1024 + k*64 + lane).  Per pass:
+// k_vg_hist counts each tile's digits, k_vg_scan turns the counts of a
+// stream into global scatter bases (digit-major, tile-minor: the positions a
+// stable sort gives), k_vg_scatter ranks each tile's items by digit (wave
+// ballots: the lanes holding the same digit, then per-wave running counts in
+// LDS; stable), reorders the tile through LDS and writes each digit's run at
+// its base.  Pass 0 computes the keys from the points (vals = the point's
+// index in its stream).
+
+// lanes of this wave whose digit equals mine (among `act` lanes), dbits <= 8
+__device__ inline unsigned long long vg_peers(unsigned int d, int dbits, unsigned long long act) {
+    unsigned long long pe = act;
+    for (int b = 0; b < dbits; ++b) {
+        const bool x = (d >> b) & 1u;
+        const unsigned long long bb = __ballot(x);
+        pe &= x ? bb : ~bb;
+    }
+    return pe;
+}
+
+template <bool FIRST>
+__device__ inline void vg_load(const float4* in, size_t in_stride, const VgParams& p, int s, int base, int i,
+                               const unsigned int* kin, const unsigned int* vin, unsigned int& key, unsigned int& val) {
+    if (FIRST) {
+        key = vg_key(in[(size_t)s * in_stride + i], p, i);
+        val = (unsigned int)i;
+    } else {
+        key = kin[base + i];
+        val = vin ? vin[base + i] : 0u;
     }
 }
 
-// item j starts a sort group (G < S: the keys of two groups are not comparable)
-__device__ inline bool vg_group_start(const int32_t* off, int S, int G, int j) {
-    for (int g = G; g < S; g += G)
-        if (off[g] == j) return true;
-    return false;
+template <bool FIRST>
+__global__ void __launch_bounds__(VG_T) k_vg_hist(const float4* in, size_t in_stride, const int32_t* off,
+                                                  const VgParams* prm, int pass, const unsigned int* kin, int* cnt,
+                                                  int maxT) {
+    __shared__ int h[256];
+    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
+    const unsigned int mask = (unsigned int)nb - 1u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        if (tid < nb) h[tid] = 0;
+        __syncthreads();
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const bool ok = j < m;
+            unsigned int key = 0, val;
+            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, nullptr, key, val);
+            const unsigned int d = (key >> shift) & mask;
+            const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
+            if (ok && (pe & lt) == 0) atomicAdd(&h[d], __popcll(pe));   // one add per digit per wave slice
+        }
+        __syncthreads();
+        if (tid < nb) cnt[((size_t)s * 256 + tid) * maxT + t] = h[tid];
+        __syncthreads();
+    }
 }
 
-template <class K>
-__global__ void k_vg_heads(const K* keys, int total, int vbits, const int32_t* off, int S, int G, int* flags) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j > total) return;
-    if (j == total) { flags[j] = 0; return; }
-    const K k = keys[j], none = ((K)1 << vbits) - 1;
-    flags[j] = (k & none) != none && (j == 0 || k != keys[j - 1] || vg_group_start(off, S, G, j));
+__global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgParams* prm, int* cnt, int maxT) {
+    __shared__ int wsum[16];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const VgParams p = prm[s];
+    const int nt = p.ntiles, F = (1 << p.dbits) * nt;
+    if (F == 0) return;
+    const int L = (F + 1023) / 1024, f0 = min(F, tid * L), f1 = min(F, f0 + L);
+    int* c = cnt + (size_t)s * 256 * maxT;
+    int sum = 0;
+    for (int f = f0; f < f1; ++f) sum += c[(size_t)(f / nt) * maxT + f % nt];
+    int total;
+    int run = off[s] + vg_block_scan<16>(sum, wsum, &total);
+    for (int f = f0; f < f1; ++f) {
+        const size_t i = (size_t)(f / nt) * maxT + f % nt;
+        const int x = c[i];
+        c[i] = run;
+        run += x;
+    }
 }
 
-// voxel r = rank of its first item: its item range [starts[r], ends[r])
-template <class K>
-__global__ void k_vg_runs(const K* keys, const int* rank, int total, int vbits, const int32_t* off, int S, int G,
-                          int* starts, int* ends) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= total) return;
-    const K k = keys[j], none = ((K)1 << vbits) - 1;
-    if ((k & none) == none) return;
-    const bool head = j == 0 || keys[j - 1] != k || vg_group_start(off, S, G, j);
-    const int r = head ? rank[j] : rank[j] - 1;   // rank = heads strictly before j
-    if (head) starts[r] = j;
-    if (j + 1 == total || keys[j + 1] != k || vg_group_start(off, S, G, j + 1)) ends[r] = j + 1;
+template <bool FIRST>
+__global__ void __launch_bounds__(VG_T) k_vg_scatter(const float4* in, size_t in_stride, const int32_t* off,
+                                                     const VgParams* prm, int pass, const unsigned int* kin,
+                                                     const unsigned int* vin, unsigned int* kout, unsigned int* vout,
+                                                     const int* cnt, int maxT) {
+    __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
+    __shared__ int wc[4][256];   // per wave slice: running digit counts, then the slice's digit offsets
+    __shared__ int lb[256];      // global base of each digit minus its first position in the tile
+    __shared__ int wsum[4];
+    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
+    const unsigned int mask = (unsigned int)nb - 1u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        for (int d = tid; d < 4 * 256; d += VG_T) (&wc[0][0])[d] = 0;
+        __syncthreads();
+        unsigned int key[VG_IPT], val[VG_IPT];
+        int rk[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const bool ok = j < m;
+            key[k] = 0;
+            val[k] = 0;
+            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, vin, key[k], val[k]);
+            const unsigned int d = (key[k] >> shift) & mask;
+            const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
+            int before = 0;
+            if (ok) before = wc[w][d];   // all lanes read before the leader writes (in-order LDS of one wave)
+            rk[k] = before + __popcll(pe & lt);
+            if (ok && (pe & lt) == 0) wc[w][d] = before + __popcll(pe);
+        }
+        __syncthreads();
+        // digit-major, slice-minor exclusive scan of the counts: the tile-local
+        // position of each (digit, slice) run
+        {
+            const int d = tid;
+            int c[4], tot = 0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) { c[q] = d < nb ? wc[q][d] : 0; tot += c[q]; }
+            int total;
+            const int start = vg_block_scan<4>(tot, wsum, &total);
+            if (d < nb) {
+                int run = start;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { wc[q][d] = run; run += c[q]; }
+                if (tot) lb[d] = cnt[((size_t)s * 256 + d) * maxT + t] - start;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            if (j < m) {
+                const int pos = wc[w][(key[k] >> shift) & mask] + rk[k];
+                lk[pos] = key[k];
+                lv[pos] = val[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int k = 0; k < VG_IPT; ++k) {   // each digit's run is contiguous: coalesced writes
+            const int j = k * VG_T + tid;
+            if (j < m) {
+                const unsigned int key2 = lk[j];
+                const int o = lb[(key2 >> shift) & mask] + j;
+                kout[o] = key2;
+                vout[o] = lv[j];
+            }
+        }
+        __syncthreads();   // LDS reused by the next tile
+    }
 }
 
-// the stream of sorted item a whose key carries the group-local stream l:
-// sort group g holds the items of streams [g*G, (g+1)*G), i.e. positions
-// [off[g*G], off[(g+1)*G])
-__device__ inline int vg_stream(const int32_t* off, int S, int G, int l, int a) {
-    int g = 0;
-    while ((g + 1) * G < S && off[(g + 1) * G] <= a) ++g;
-    return g * G + l;
+// ---- voxels of the sorted items: a voxel starts at each key change (the
+// "none" key of non-finite points is no voxel).  k_vg_heads counts the starts
+// per tile, k_vg_hscan ranks the tiles (and sets the output counts),
+// k_vg_bounds2 writes each voxel's item range [starts[r], ends[r]) at its
+// rank (= its output position: the voxels are in index order), and
+// k_vg_centroid sums each voxel's points.
+__device__ inline bool vg_head(const unsigned int* k, int j, unsigned int none) {
+    const unsigned int x = k[j];
+    return x != none && (j == 0 || k[j - 1] != x);
+}
+
+__global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, const int32_t* off, const VgParams* prm,
+                                                   int* hcnt, int maxT) {
+    __shared__ int wsum[4];
+    const int s = blockIdx.y, tid = threadIdx.x;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base;
+    const unsigned int none = vg_none(p);
+    const unsigned int* k = keys + base;
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        int c = 0;
+#pragma unroll 4
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = q * VG_T + tid;
+            if (j < m) c += vg_head(k, a + j, none);
+        }
+        int total;
+        vg_block_scan<4>(c, wsum, &total);
+        if (tid == 0) hcnt[(size_t)s * maxT + t] = total;
+    }
+}
+
+__global__ void __launch_bounds__(1024) k_vg_hscan(const VgParams* prm, int* hcnt, int maxT, int32_t* nvox,
+                                                   int32_t* nout, int nout_stride, int out_cap, int32_t* errflag) {
+    __shared__ int wsum[16];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const int nt = prm[s].ntiles;
+    int* h = hcnt + (size_t)s * maxT;
+    const int L = (nt + 1023) / 1024, t0 = min(nt, tid * L), t1 = min(nt, t0 + L);
+    int sum = 0;
+    for (int t = t0; t < t1; ++t) sum += h[t];
+    int total;
+    int run = vg_block_scan<16>(sum, wsum, &total);
+    for (int t = t0; t < t1; ++t) {
+        const int x = h[t];
+        h[t] = run;
+        run += x;
+    }
+    if (tid == 0) {
+        nvox[s] = total;
+        int c = total;
+        if (c > out_cap) { c = out_cap; atomicOr(errflag, 1); }
+        nout[(size_t)s * nout_stride] = c;
+    }
+}
+
+// the item range of every voxel, at the voxel's rank (items in wave slices,
+// as the scatter reads them; ranks by ballot prefix counts)
+__global__ void __launch_bounds__(VG_T) k_vg_ranges(const unsigned int* keys, const int32_t* off, const VgParams* prm,
+                                                    const int* hcnt, int maxT, int* starts, int* ends) {
+    __shared__ int wsum[4];
+    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base;
+    const unsigned int none = vg_none(p);
+    const unsigned int* k = keys + base;
+    const unsigned long long le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        unsigned long long hm[VG_IPT];
+        int wrun = 0;
+#pragma unroll
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = w * (VG_TILE / 4) + q * 64 + lane;
+            hm[q] = __ballot(j < m && vg_head(k, a + j, none));
+            wrun += __popcll(hm[q]);
+        }
+        if (lane == 0) wsum[w] = wrun;
+        __syncthreads();
+        int r = hcnt[(size_t)s * maxT + t];
+        for (int q = 0; q < w; ++q) r += wsum[q];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = w * (VG_TILE / 4) + q * 64 + lane, i = a + j;
+            const int incl = r + __popcll(hm[q] & le);   // voxels started at or before item i
+            r += __popcll(hm[q]);
+            if (j < m) {
+                const unsigned int x = k[i];
+                if (x == none) continue;
+                if ((hm[q] >> lane) & 1ull) starts[base + incl - 1] = i;
+                if (i + 1 == n || k[i + 1] != x) ends[base + incl - 1] = i + 1;
+            }
+        }
+    }
 }
 
 // Centroid of one voxel: the points are summed in input order (the sort is
@@ -201,197 +434,160 @@ __device__ inline int vg_stream(const int32_t* off, int S, int G, int l, int a) 
 #define VG_SHORT 32
 struct VgOut { float4* out; size_t stride; int cap; };
 
-__device__ inline void vg_store(const VgOut& o, const int* rank, const int32_t* off, int s, int r, float sx, float sy,
-                                float sz, float si, int cnt) {
-    const int pos = r - rank[off[s]];
+__device__ inline void vg_store(const VgOut& o, int s, int r, float sx, float sy, float sz, float si, int cnt) {
     const float c = (float)cnt;
-    if (pos < o.cap) o.out[(size_t)s * o.stride + pos] = make_float4(sx / c, sy / c, sz / c, si / c);
+    if (r < o.cap) o.out[(size_t)s * o.stride + r] = make_float4(sx / c, sy / c, sz / c, si / c);
 }
 
-template <class K>
-__global__ void k_vg_centroid(const float4* in, size_t in_stride, const K* keys, const unsigned int* vals,
-                              const int* rank, const int32_t* off, int total, int vbits, int S, int G,
-                              const int* starts, const int* ends, int32_t* meta, int* longv, VgOut o) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= rank[total]) return;
-    const int a = starts[r], e = ends[r];
-    if (e - a > VG_SHORT) {
-        longv[atomicAdd(&meta[2], 1)] = r;
-        return;
-    }
-    const int s = vg_stream(off, S, G, (int)(keys[a] >> vbits), a);
+__global__ void __launch_bounds__(VG_T) k_vg_centroid(const float4* in, size_t in_stride, const unsigned int* vals,
+                                                      const int32_t* off, const int32_t* nvox, const int* starts,
+                                                      const int* ends, int32_t* meta, int4* longv, int nlong_cap,
+                                                      VgOut o) {
+    const int s = blockIdx.y;
+    const int base = off[s], nv = min(nvox[s], o.cap);
+    const unsigned int* v = vals + base;
     const float4* src = in + (size_t)s * in_stride;
-    float sx = 0, sy = 0, sz = 0, si = 0;
-    for (int j = a; j < e; j += 4) {
-        float4 p[4];
+    for (int r = blockIdx.x * VG_T + threadIdx.x; r < nv; r += gridDim.x * VG_T) {
+        const int j = starts[base + r], e = ends[base + r];
+        if (e - j > VG_SHORT) {
+            const int li = atomicAdd(&meta[2], 1);
+            if (li < nlong_cap) longv[li] = make_int4(s, j, r, e);
+            continue;
+        }
+        float sx = 0, sy = 0, sz = 0, si = 0;
+        for (int i = j; i < e; i += 4) {
+            float4 q4[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) p[u] = j + u < e ? src[vals[j + u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < 4; ++u) q4[u] = i + u < e ? src[v[i + u]] : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (j + u < e) { sx += p[u].x; sy += p[u].y; sz += p[u].z; si += p[u].w; }
+            for (int u = 0; u < 4; ++u)
+                if (i + u < e) { sx += q4[u].x; sy += q4[u].y; sz += q4[u].z; si += q4[u].w; }
+        }
+        vg_store(o, s, r, sx, sy, sz, si, e - j);
     }
-    vg_store(o, rank, off, s, r, sx, sy, sz, si, e - a);
 }
 
 // Long voxels, one wave each (persistent grid over the list): the wave
 // stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
 // intensity chains over them in order.
-template <class K>
-__global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_stride, const K* keys,
-                                                 const unsigned int* vals, const int* rank, const int32_t* off,
-                                                 int vbits, int S, int G, const int* starts, const int* ends,
-                                                 const int32_t* meta, const int* longv, VgOut o) {
+__global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_stride, const unsigned int* vals,
+                                                 const int32_t* off, const int32_t* meta, const int4* longv,
+                                                 int nlong_cap, VgOut o) {
     __shared__ float4 buf[4][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int nlong = meta[2];
+    const int nlong = min(meta[2], nlong_cap);
     float4* b = buf[w];
     for (int t = blockIdx.x * 4 + w; t < nlong; t += gridDim.x * 4) {
-        const int r = longv[t], a = starts[r], e = ends[r];
-        const int s = vg_stream(off, S, G, (int)(keys[a] >> vbits), a);
+        const int4 L = longv[t];
+        const int s = L.x, a = L.y, r = L.z, e = L.w;
+        const unsigned int* v = vals + off[s];
         const float4* src = in + (size_t)s * in_stride;
         float acc = 0.0f;
         for (int c0 = a; c0 < e; c0 += 256) {
             const int m = min(256, e - c0);
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int k = u * 64 + lane;
-                if (k < m) b[k] = src[vals[c0 + k]];
+                const int q = u * 64 + lane;
+                if (q < m) b[q] = src[v[c0 + q]];
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
             __builtin_amdgcn_wave_barrier();
             if (lane < 4) {
                 const float* f = reinterpret_cast<const float*>(b) + lane;
-                for (int k = 0; k < m; ++k) acc += f[4 * k];
+                for (int q = 0; q < m; ++q) acc += f[4 * q];
             }
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
             __builtin_amdgcn_wave_barrier();
         }
         const float sx = __shfl(acc, 0, 64), sy = __shfl(acc, 1, 64), sz = __shfl(acc, 2, 64),
                     si = __shfl(acc, 3, 64);
-        if (lane == 0) vg_store(o, rank, off, s, r, sx, sy, sz, si, e - a);
+        if (lane == 0) vg_store(o, s, r, sx, sy, sz, si, e - a);
     }
 }
 
-__global__ void k_vg_count(const int* rank, const int32_t* off, int S, int32_t* nout, int nout_stride, int out_cap,
-                           int32_t* errflag) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= S) return;
-    int c = rank[off[s + 1]] - rank[off[s]];
-    if (c > out_cap) { c = out_cap; atomicOr(errflag, 1); }
-    nout[(size_t)s * nout_stride] = c;
-}
-
-static int ensure_ws(slo_ctx* ctx, size_t items) {
+// workspace for S streams of up to `stride` items: allocated on the host from
+// the strides alone (never from a device count), grown geometrically
+static int ensure_ws(slo_ctx* ctx, size_t stride) {
     MapWs& w = ctx->mws;
-    if (items <= w.items) return 0;
-    // grow geometrically: a local map creeping up by a few points per mapping
-    // step must not reallocate (a device-wide synchronisation) every time
-    items = std::max(items, w.items + w.items / 2);
-    void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.starts, w.ends, w.longv, w.temp};
-    for (void* p : old) if (p) hipFree(p);
-    w.items = items;
-    SLO_CHECK(hipMalloc(&w.keys, 8 * items));
-    SLO_CHECK(hipMalloc(&w.keys2, 8 * items));
-    SLO_CHECK(hipMalloc(&w.vals, 4 * items));
-    SLO_CHECK(hipMalloc(&w.vals2, 4 * items));
-    SLO_CHECK(hipMalloc(&w.flags, 4 * (items + 1)));
-    SLO_CHECK(hipMalloc(&w.rank, 4 * (items + 1)));
-    SLO_CHECK(hipMalloc(&w.starts, 4 * items));
-    SLO_CHECK(hipMalloc(&w.ends, 4 * items));
-    SLO_CHECK(hipMalloc(&w.longv, 4 * items));
-    size_t t1 = 0, t2 = 0, t3 = 0;
-    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, (unsigned long long*)w.keys,
-                                                 (unsigned long long*)w.keys2, w.vals, w.vals2, (int)items, 0, 64,
-                                                 ctx->stream));
-    SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, t3, (unsigned int*)w.keys, (unsigned int*)w.keys2, w.vals,
-                                                 w.vals2, (int)items, 0, 32, ctx->stream));
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, t2, w.flags, w.rank, (int)items + 1, ctx->stream));
-    w.temp_bytes = std::max(std::max(t1, t2), t3);
-    SLO_CHECK(hipMalloc(&w.temp, w.temp_bytes));
-    return 0;
-}
-
-// G streams per sort group: the (group-local stream, voxel) keys of group g
-// occupy the item range [off[g*G], off[(g+1)*G]), sorted on their own, so a
-// filter whose voxel index and stream count need more than 32 bits together
-// still sorts 32-bit keys (a third less traffic per pass than 64-bit keys,
-// and one pass fewer)
-template <class K>
-static int vg_sorted(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, int total, int vbits, int sbits,
-                     int G, const VgOut& o) {
-    MapWs& w = ctx->mws;
-    const int S = ctx->S, T = 256;
-    const int bx = std::max(1, std::min(64, (int)((in_stride + T - 1) / T)));
-    K* keys = (K*)w.keys;
-    K* keys2 = (K*)w.keys2;
-    SLO_LAUNCH(ctx, "vg_keys", k_vg_keys<K>, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.prm, vbits, G, keys,
-               w.vals);
-    size_t tb = w.temp_bytes;
-    hipEvent_t ev = nullptr;
-    const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
-    const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
-    if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
-    for (int g0 = 0; g0 < S; g0 += G) {   // one sort per group (G = S: one sort)
-        const int a = G >= S ? 0 : w.h_off[g0], e = G >= S ? total : w.h_off[std::min(S, g0 + G)];
-        if (e <= a) continue;
-        tb = w.temp_bytes;
-        SLO_CHECK(hipcub::DeviceRadixSort::SortPairs(w.temp, tb, keys + a, keys2 + a, w.vals + a, w.vals2 + a, e - a, 0,
-                                                     vbits + sbits, ctx->stream));
+    const size_t S = (size_t)ctx->S;
+    const size_t items = S * stride, maxT = (stride + VG_TILE - 1) / VG_TILE, tiles = S * std::max<size_t>(1, maxT);
+    if (items > w.items) {
+        const size_t it = std::max(items, w.items + w.items / 2);
+        void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.longv};
+        for (void* q : old) if (q) hipFree(q);
+        w.items = it;
+        w.nlong_cap = it / VG_SHORT + 1;
+        SLO_CHECK(hipMalloc(&w.keys, 4 * it));
+        SLO_CHECK(hipMalloc(&w.keys2, 4 * it));
+        SLO_CHECK(hipMalloc(&w.vals, 4 * it));
+        SLO_CHECK(hipMalloc(&w.vals2, 4 * it));
+        SLO_CHECK(hipMalloc(&w.longv, sizeof(int4) * w.nlong_cap));
     }
-    if (tm) timing_end(ctx, sort_name.c_str(), ev);
-    const int gi = (total + T - 1) / T;
-    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads<K>, dim3((total + 1 + T - 1) / T), dim3(T), 0, keys2, total, vbits, w.off,
-               S, G, w.flags);
-    tb = w.temp_bytes;
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(w.temp, tb, w.flags, w.rank, total + 1, ctx->stream));
-    SLO_LAUNCH(ctx, "vg_runs", k_vg_runs<K>, dim3(gi), dim3(T), 0, keys2, w.rank, total, vbits, w.off, S, G, w.starts,
-               w.ends);
-    SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid<K>, dim3(gi), dim3(T), 0, in, in_stride, keys2, w.vals2, w.rank,
-               w.off, total, vbits, S, G, w.starts, w.ends, w.meta, w.longv, o);
-    SLO_LAUNCH(ctx, "vg_long", k_vg_long<K>, dim3(std::min(1024, gi)), dim3(T), 0, in, in_stride, keys2, w.vals2,
-               w.rank, w.off, vbits, S, G, w.starts, w.ends, w.meta, w.longv, o);
+    if (tiles > w.tiles) {
+        const size_t tt = std::max(tiles, w.tiles + w.tiles / 2);
+        if (w.cnt) hipFree(w.cnt);
+        if (w.hcnt) hipFree(w.hcnt);
+        w.tiles = tt;
+        SLO_CHECK(hipMalloc(&w.cnt, sizeof(int) * 256 * tt));
+        SLO_CHECK(hipMalloc(&w.hcnt, sizeof(int) * tt));
+    }
     return 0;
 }
 
+// One batched VoxelGrid over S streams: stream s's n = d_n[s * n_stride]
+// points at in + s * in_stride; its centroids go to out + s * out_stride (at
+// most out_cap; more sets errflag and is clipped) and their count to
+// d_nout[s * nout_stride].  Everything is sized from the strides, so the host
+// only issues launches (no round trip).
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
     MapWs& w = ctx->mws;
     const int S = ctx->S;
-    const int T = 256;
-    const int bx = std::max(1, std::min(64, (int)((in_stride + T - 1) / T)));
+    if (int r = ensure_ws(ctx, in_stride)) return r;
+    const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
+    const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
+    const int bx = std::max(1, std::min(64, (int)((in_stride + VG_T - 1) / VG_T)));
+    const dim3 grid(GX, S);
     SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, d_n, n_stride, S, w.off, w.bounds, w.meta);
-    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(T), 0, in, in_stride, w.off, w.bounds);
-    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm,
-               w.meta);
-    // one host round trip per filter: the item count, the key width and the
-    // stream offsets (the sort groups' item ranges)
-    SLO_CHECK(hipMemcpyAsync(w.h_meta, w.meta, 2 * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SLO_CHECK(hipMemcpyAsync(w.h_off, w.off, (S + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, ctx->stream));
-    SLO_CHECK(hipStreamSynchronize(ctx->stream));
-    const int total = w.h_meta[0];
-    int vbits = 1;   // every index < 2^vbits - 1 (the all-ones index marks non-finite points)
-    while (vbits < 32 && (1LL << vbits) <= (long long)w.h_meta[1]) ++vbits;
-    if (w.h_meta[1] >= (1 << 30)) vbits = 32;   // int index arithmetic may wrap, as in PCL
-    int sbits = 0;
-    while ((1 << sbits) < S) ++sbits;
-    if (int r = ensure_ws(ctx, (size_t)total + 1)) return r;
-    if (total > 0) {
-        const VgOut o{out, out_stride, out_cap};
-        int r;
-        if (vbits + sbits <= 32 && vbits < 32) {
-            r = vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, sbits, S, o);
-        } else if (vbits <= SLO_VG_GROUP_MAX_VBITS) {   // groups of G streams on 32-bit keys
-            const int gbits = 32 - vbits;
-            r = vg_sorted<unsigned int>(ctx, tag, in, in_stride, total, vbits, gbits, 1 << gbits, o);
+    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(VG_T), 0, in, in_stride, w.off, w.bounds);
+    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
+    hipEvent_t ev = nullptr;
+    const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
+    const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
+    if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
+    unsigned int *k0 = w.keys, *v0 = w.vals, *k1 = w.keys2, *v1 = w.vals2;
+    for (int pass = 0; pass < VG_PASSES; ++pass) {
+        if (pass == 0) {
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass, k0,
+                       w.cnt, maxT);
         } else {
-            r = vg_sorted<unsigned long long>(ctx, tag, in, in_stride, total, vbits, sbits, S, o);
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass, k0,
+                       w.cnt, maxT);
         }
-        if (r) return r;
-    } else {
-        SLO_CHECK(hipMemsetAsync(w.rank, 0, sizeof(int), ctx->stream));
+        SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, w.cnt, maxT);
+        if (pass == 0) {
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass,
+                       k0, v0, k1, v1, w.cnt, maxT);
+        } else {
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass,
+                       k0, v0, k1, v1, w.cnt, maxT);
+        }
+        std::swap(k0, k1);
+        std::swap(v0, v1);
     }
-    SLO_LAUNCH(ctx, "vg_count", k_vg_count, dim3((S + 63) / 64), dim3(64), 0, w.rank, w.off, S, d_nout, nout_stride,
+    if (tm) timing_end(ctx, sort_name.c_str(), ev);
+    const VgOut o{out, out_stride, out_cap};
+    // the ping-pong buffers the sort is done with hold the voxel ranges
+    int* starts = (int*)k1;
+    int* ends = (int*)v1;
+    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT);
+    SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, w.prm, w.hcnt, maxT, w.nvox, d_nout, nout_stride,
                out_cap, w.errflag);
+    SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
+    SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid, dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S),
+               dim3(VG_T), 0, in, in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, in, in_stride, v0, w.off, w.meta, w.longv,
+               (int)w.nlong_cap, o);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
@@ -484,10 +680,80 @@ __global__ void __launch_bounds__(1024) k_grid_build_lds(const float4* pts, size
     }
 }
 
+// Per-stream exclusive scan of the bucket counts [S][N = T + 1] (offsets
+// relative to the stream's first entry), reduce-then-scan over blocks of
+// VG_TILE counts: block sums, a scan of each stream's block sums, then each
+// block rescanned from its base (coalesced loads / stores through LDS).
+__global__ void __launch_bounds__(VG_T) k_seg_reduce(const int32_t* in, int N, int nblk, int32_t* bsum) {
+    __shared__ int wsum[4];
+    const int s = blockIdx.y, tid = threadIdx.x;
+    const int32_t* c = in + (size_t)s * N;
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const int a = b * VG_TILE, m = min(VG_TILE, N - a);
+        int sum = 0;
+#pragma unroll 4
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = q * VG_T + tid;
+            if (j < m) sum += c[a + j];
+        }
+        int total;
+        vg_block_scan<4>(sum, wsum, &total);
+        if (tid == 0) bsum[(size_t)s * nblk + b] = total;
+    }
+}
+
+__global__ void k_seg_top(int nblk, int32_t* bsum) {   // one wave per stream
+    const int s = blockIdx.x, lane = threadIdx.x;
+    int32_t* bs = bsum + (size_t)s * nblk;
+    int run = 0;
+    for (int b0 = 0; b0 < nblk; b0 += 64) {
+        const int b = b0 + lane;
+        const int x = b < nblk ? bs[b] : 0;
+        int incl = x;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        if (b < nblk) bs[b] = run + incl - x;
+        run += __shfl(incl, 63, 64);
+    }
+}
+
+__global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int nblk, const int32_t* bsum,
+                                                   int32_t* out) {
+    __shared__ int l[VG_TILE + VG_TILE / 16];
+    __shared__ int wsum[4];
+    const int s = blockIdx.y, tid = threadIdx.x;
+    const int32_t* c = in + (size_t)s * N;
+    int32_t* o = out + (size_t)s * N;
+    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const int a = b * VG_TILE, m = min(VG_TILE, N - a);
+#pragma unroll 4
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = q * VG_T + tid;
+            l[VG_PAD(j)] = j < m ? c[a + j] : 0;
+        }
+        __syncthreads();
+        int x[VG_IPT], sum = 0;
+#pragma unroll
+        for (int q = 0; q < VG_IPT; ++q) { x[q] = l[VG_PAD(tid * VG_IPT + q)]; sum += x[q]; }
+        int total;
+        int run = bsum[(size_t)s * nblk + b] + vg_block_scan<4>(sum, wsum, &total);
+#pragma unroll
+        for (int q = 0; q < VG_IPT; ++q) { l[VG_PAD(tid * VG_IPT + q)] = run; run += x[q]; }
+        __syncthreads();
+#pragma unroll 4
+        for (int q = 0; q < VG_IPT; ++q) {
+            const int j = q * VG_T + tid;
+            if (j < m) o[a + j] = l[VG_PAD(j)];
+        }
+        __syncthreads();
+    }
+}
+
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride) {
     const int S = ctx->S;
-    const float inv = 1.0f / g.cell;
-    const size_t nb = (size_t)S * (g.T + 1);   // [S][T + 1]: a zero bucket ends each stream
+    const float inv = 1.0f / g.cell;   // buckets [S][T + 1]: a zero bucket ends each stream
     if (g.T <= SLO_GRID_LDS_T) {
         SLO_LAUNCH(ctx, "grid_build_lds", k_grid_build_lds, dim3(S), dim3(1024), 0, pts, stride, n, n_stride, g.T, inv,
                    g.off, g.ent, g.ent_stride);
@@ -496,8 +762,11 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
     }
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
     SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
-    size_t tb = g.temp_bytes;
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(g.temp, tb, g.cnt, g.off, (int)nb, ctx->stream));
+    const int N = g.T + 1, nblk = (N + VG_TILE - 1) / VG_TILE;
+    const dim3 sg(std::min(nblk, std::max(4, 2048 / S)), S);
+    SLO_LAUNCH(ctx, "grid_scan", k_seg_reduce, sg, dim3(VG_T), 0, g.cnt, N, nblk, g.bsum);
+    SLO_LAUNCH(ctx, "grid_scan", k_seg_top, dim3(S), dim3(64), 0, nblk, g.bsum);
+    SLO_LAUNCH(ctx, "grid_scan", k_seg_down, sg, dim3(VG_T), 0, g.cnt, N, nblk, g.bsum, g.off);
     SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
                g.off, g.cur, g.ent, g.ent_stride);
     SLO_LAUNCH(ctx, "grid_clear", k_grid_clear, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt,
@@ -524,10 +793,7 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) 
     SLO_CHECK(hipMemset(g.cnt, 0, sizeof(int32_t) * nb));   // kept zero between builds (k_grid_clear)
     SLO_CHECK(hipMemset(g.cur, 0, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.ent, sizeof(float4) * (size_t)S * ent_stride));
-    size_t tb = 0;
-    SLO_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, g.cnt, g.off, (int)nb, ctx->stream));
-    g.temp_bytes = tb;
-    SLO_CHECK(hipMalloc(&g.temp, tb));
+    SLO_CHECK(hipMalloc(&g.bsum, sizeof(int32_t) * (size_t)S * ((T + 1 + VG_TILE - 1) / VG_TILE)));
     return 0;
 }
 
@@ -548,7 +814,7 @@ void grid_free(HashGrid& g) {
     if (g.cur) hipFree(g.cur);
     if (g.off) hipFree(g.off);
     if (g.ent) hipFree(g.ent);
-    if (g.temp) hipFree(g.temp);
+    if (g.bsum) hipFree(g.bsum);
     g = HashGrid();
 }
 
@@ -561,18 +827,14 @@ int vg_alloc(slo_ctx* ctx) {
     SLO_CHECK(hipMalloc(&w.errflag, sizeof(int32_t)));
     SLO_CHECK(hipMemset(w.errflag, 0, sizeof(int32_t)));
     SLO_CHECK(hipMalloc(&w.meta, 4 * sizeof(int32_t)));
-    SLO_CHECK(hipHostMalloc((void**)&w.h_meta, 4 * sizeof(int32_t)));
-    SLO_CHECK(hipHostMalloc((void**)&w.h_off, (S + 1) * sizeof(int32_t)));
+    SLO_CHECK(hipMalloc(&w.nvox, sizeof(int32_t) * S));
     return 0;
 }
 
 void vg_free(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
-    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.flags, w.rank, w.starts, w.ends, w.longv,
-                  w.temp, w.off, w.bounds, w.prm, w.errflag, w.meta};
+    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta, w.nvox};
     for (void* p : ps) if (p) hipFree(p);
-    if (w.h_meta) hipHostFree(w.h_meta);
-    if (w.h_off) hipHostFree(w.h_off);
     w = MapWs();
 }
 
