@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--cpu-distinct", type=int, default=8,
                     help="distinct CPU streams pre-rolled in parallel; the others continue from copies of them")
     ap.add_argument("--single-steps", type=int, default=100, help="timed scans of the one-stream leg (0 = skip)")
+    ap.add_argument("--no-graphs", action="store_true",
+                    help="launch every kernel eagerly instead of replaying the captured per-step HIP graphs")
     ap.add_argument("--force-gather", action="store_true",
                     help="run the per-step record all-gather even at world size 1 (exercises the N>1 path)")
     ap.add_argument("--xsc-cap", type=int, default=64,
@@ -280,6 +282,7 @@ def single_stream(torch, slo_amd, a, cfg, pid, local):
     """one C3 stream through the same pipeline: scans/s (async) and per-scan latency (synchronised)"""
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, local, 1)
+    ctx.graph_mode(not a.no_graphs)
     gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
     n = a.preroll + a.warmup + a.single_steps
     try:
@@ -349,6 +352,8 @@ def main():
     groups = sdist.group_slices(S, a.groups)
     free0 = torch.cuda.mem_get_info(local)[0]
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
+    for c in ctxs:
+        c.graph_mode(not a.no_graphs)
     ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     n_ctx = len(ctxs)
     # --stagger: context g runs lag(g) = g scans ahead, so with as many
@@ -562,6 +567,7 @@ def main():
                        "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
                        "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),
                        "sc_history_seed": a.history,
+                       "launch": "eager" if a.no_graphs else "one HIP graph per context and step",
                        "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,
             "cpu_baseline": cpu,

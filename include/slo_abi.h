@@ -71,8 +71,14 @@ int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t
 /* SC loop detection for every stream that saved a keyframe this scan */
 int slo_batch_sc_detect(slo_ctx* ctx);
 /* whole pipeline for one scan per stream with the deterministic gating of
- * IP -> FA -> [mapping + SC make] -> [SC detect] */
+ * IP -> FA -> [mapping + SC make] -> [SC detect].  After the
+ * first scan each step is one HIP graph launch (captured per step kind, with
+ * and without the mapping stage) unless graphs are off, timing is on, or
+ * cfg.loop_verify / cfg.pose_graph need host round trips. */
 int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan);
+/* on != 0 (the default): slo_batch_process replays captured graphs; 0:
+ * every launch issued eagerly (the captured graphs are released) */
+int slo_graph_mode(slo_ctx* ctx, int on);
 
 /* ---------------------------------------------------------------- single scan (stream 0, host memory) */
 typedef struct slo_seg_view {

@@ -16,18 +16,47 @@ namespace slo {
 bool timing_on(const slo_ctx* ctx, const char* name) {
     return ctx->timing_only.empty() || ctx->timing_only == name;
 }
+__global__ void k_stamp(unsigned long long* st) {
+    const unsigned int i = atomicAdd((unsigned int*)(st + SLO_STAMP_CAP), 1u);
+    st[i % SLO_STAMP_CAP] = wall_clock64();
+}
+static bool stamping(const slo_ctx* ctx) { return !ctx->timing_only.empty() && ctx->d_stamp; }
 void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a) {
     (void)name;
+    if (stamping(ctx)) {
+        *a = nullptr;
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp);
+        return;
+    }
     hipEventCreate(a);
     hipEventRecord(*a, ctx->stream);
 }
 void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a) {
+    if (stamping(ctx)) {
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp);
+        return;
+    }
     hipEvent_t b;
     hipEventCreate(&b);
     hipEventRecord(b, ctx->stream);
     ctx->pending.push_back({name, {a, b}});
 }
 static void timing_flush(slo_ctx* ctx) {
+    if (stamping(ctx)) {   // consecutive (begin, end) stamps of the filtered kernel
+        std::vector<unsigned long long> h(SLO_STAMP_CAP + 1);
+        hipStreamSynchronize(ctx->stream);
+        hipMemcpy(h.data(), ctx->d_stamp, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1), hipMemcpyDeviceToHost);
+        const unsigned int n = (unsigned int)h[SLO_STAMP_CAP];
+        if (n >= 2) {
+            auto& k = ctx->ktimes[ctx->timing_only];
+            for (unsigned int i = 0; i + 1 < n && i + 1 < SLO_STAMP_CAP; i += 2) {
+                k.total_ms += (double)(h[i + 1] - h[i]) / ctx->stamp_khz;
+                k.n += 1;
+            }
+        }
+        hipMemsetAsync(ctx->d_stamp + SLO_STAMP_CAP, 0, sizeof(unsigned long long), ctx->stream);
+        hipStreamSynchronize(ctx->stream);
+    }
     if (ctx->pending.empty()) return;
     hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) {
@@ -40,6 +69,25 @@ static void timing_flush(slo_ctx* ctx) {
         hipEventDestroy(p.second.second);
     }
     ctx->pending.clear();
+}
+
+__global__ void k_set_io(SloIo* io, const float4* pts, const int32_t* npts) {
+    io->pts = pts;
+    io->npts = npts;
+}
+
+// the scan the following launches read (DevView::io), in stream order
+static int set_io(slo_ctx* ctx, const void* pts, const int32_t* npts) {
+    hipLaunchKernelGGL(k_set_io, dim3(1), dim3(1), 0, ctx->stream, ctx->d_io, (const float4*)pts, npts);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+void graphs_drop(slo_ctx* ctx) {
+    for (int k = 0; k < 4; ++k) {
+        if (ctx->graph_exec[k]) hipGraphExecDestroy(ctx->graph_exec[k]);
+        ctx->graph_exec[k] = nullptr;
+    }
 }
 
 }  // namespace slo
@@ -164,6 +212,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.ind_surf, S * v.cap_flat * 3);
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
+    c.add(&ctx->d_io, 1);
     // ---- mapping + Scan Context history
     // Capacities are worst-case bounds, so no cloud is ever clipped: a
     // VoxelGrid output is no larger than its input, the surf DS of a scan is
@@ -206,6 +255,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.mo_part, S * SLO_MO_BLOCKS * SLO_MO_PART);
     v.cap_q = v.cap_less_sharp + v.cap_st;
     c.add(&v.mo_nn, S * (size_t)v.cap_q * 5);
+    c.add(&v.mo_perm, S * (size_t)v.cap_q);
     c.add(&v.sc_desc, S * v.KFMAX * NRS);
     c.add(&v.sc_ring, S * v.KFMAX * cfg->sc_num_ring);
     c.add(&v.sc_ringd, S * v.KFMAX * cfg->sc_num_ring);
@@ -218,6 +268,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         return SLO_E_HIP;
     }
     c.assign((char*)ctx->arena);
+    v.io = ctx->d_io;
     // zero everything: persistent FA arrays start as the zero pages new[] gives
     if (hipMemsetAsync(ctx->arena, 0, ctx->arena_bytes, ctx->stream) != hipSuccess ||
         hipHostMalloc((void**)&ctx->h_st, sizeof(StreamState) * S) != hipSuccess ||
@@ -245,6 +296,15 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, hip_device) != hipSuccess || khz <= 0 ||
+        hipMalloc(&ctx->d_stamp, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1)) != hipSuccess ||
+        hipMemset(ctx->d_stamp, 0, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1)) != hipSuccess) {
+        slo_destroy(ctx);
+        return SLO_E_HIP;
+    }
+    ctx->stamp_khz = khz;
+    ctx->pp_corner0 = v.corner_last;
     v.g_os = slo::grid_view(ctx->grid_os);
     v.g_mc = slo::grid_view(ctx->grid_c);
     v.g_ms = slo::grid_view(ctx->grid_s);
@@ -257,6 +317,7 @@ void slo_destroy(slo_ctx* ctx) {
     hipSetDevice(ctx->dev);
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
+    slo::graphs_drop(ctx);
     slo::vg_free(ctx);
     slo::grid_free(ctx->grid_c);
     slo::grid_free(ctx->grid_s);
@@ -267,6 +328,7 @@ void slo_destroy(slo_ctx* ctx) {
     if (ctx->arena) hipFree(ctx->arena);
     if (ctx->h_st) hipHostFree(ctx->h_st);
     if (ctx->h_stage) hipHostFree(ctx->h_stage);
+    if (ctx->d_stamp) hipFree(ctx->d_stamp);
     if (ctx->stream) hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -280,7 +342,15 @@ int slo_synchronize(slo_ctx* ctx) {
 
 int slo_batch_set_rings(slo_ctx* ctx, const uint16_t* d_rings) {
     if (!ctx) return SLO_E_ARG;
+    if (ctx->v.rings != d_rings) slo::graphs_drop(ctx);   // the captured launches carry the old pointer
     ctx->v.rings = d_rings;
+    return SLO_OK;
+}
+
+int slo_graph_mode(slo_ctx* ctx, int on) {
+    if (!ctx) return SLO_E_ARG;
+    if (!on) slo::graphs_drop(ctx);
+    ctx->graphs = on != 0;
     return SLO_OK;
 }
 
@@ -291,20 +361,15 @@ int slo_batch_image_projection(slo_ctx* ctx, const void* d_points, const int32_t
         return SLO_E_STATE;
     }
     SLO_CHECK(hipSetDevice(ctx->dev));
-    ctx->v.pts = (const float4*)d_points;
-    ctx->v.npts = d_counts;
+    if (int r = slo::set_io(ctx, d_points, d_counts)) return r;
     return slo::ip_run(ctx);
 }
 
-int slo_batch_feature_association(slo_ctx* ctx) {
-    if (!ctx) return SLO_E_ARG;
-    SLO_CHECK(hipSetDevice(ctx->dev));
-    int r = slo::fa_features_run(ctx);
-    if (r) return r;
-    const bool first = !ctx->fa_inited;
-    r = slo::fa_odometry_run(ctx, first);
-    if (r) return r;
-    // FA frameCount / publish gate (FA:1790-1792); the init scan never publishes
+}  // extern "C"
+
+namespace slo {
+// FA frameCount / publish gate (FA:1790-1792); the init scan never publishes
+static void fa_advance(slo_ctx* ctx, bool first) {
     ctx->fa_published = false;
     if (first) {
         ctx->fa_inited = true;
@@ -317,6 +382,30 @@ int slo_batch_feature_association(slo_ctx* ctx) {
         }
     }
     ctx->scan_index++;
+}
+
+// MO's gate (MO:1685): this scan reached mapping (FA published it) and the
+// mapping interval has elapsed
+static bool map_gate(slo_ctx* ctx, double t_scan) {
+    ctx->mapped_now = false;
+    if (!ctx->fa_published) return false;
+    if (!(t_scan - ctx->t_last_processing >= ctx->cfg.mapping_process_interval)) return false;
+    ctx->t_last_processing = t_scan;
+    return true;
+}
+}  // namespace slo
+
+extern "C" {
+
+int slo_batch_feature_association(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    int r = slo::fa_features_run(ctx);
+    if (r) return r;
+    const bool first = !ctx->fa_inited;
+    r = slo::fa_odometry_run(ctx, first);
+    if (r) return r;
+    slo::fa_advance(ctx, first);
     return SLO_OK;
 }
 
@@ -339,12 +428,10 @@ extern "C" {
 int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
     if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
     SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::set_io(ctx, d_points, d_counts)) return r;
     SLO_LAUNCH(ctx, "clear_flags", slo::k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
-    ctx->mapped_now = false;
-    if (!ctx->fa_published) return SLO_OK;
-    if (!(t_scan - ctx->t_last_processing >= ctx->cfg.mapping_process_interval)) return SLO_OK;
-    ctx->t_last_processing = t_scan;
-    int r = slo::map_run(ctx, (const float4*)d_points, d_counts);
+    if (!slo::map_gate(ctx, t_scan)) return SLO_OK;
+    int r = slo::map_run(ctx);
     if (r) return r;
     ctx->mapped_now = true;
     // the graph half of saveKeyFramesAndFactor, then correctPoses (MO:1697-1699)
@@ -358,8 +445,99 @@ int slo_batch_sc_detect(slo_ctx* ctx) {
     return slo::sc_detect_run(ctx);
 }
 
+}  // extern "C"
+
+namespace slo {
+// One step of the batched pipeline after the first scan, without the host
+// round trips of loop verification and the pose graph: projection,
+// features, odometry, the mapping step when `map`, Scan Context detect.
+// Launches only (the host state is advanced by the caller), so the same
+// calls can be captured into a graph.
+static int step_launches(slo_ctx* ctx, bool map) {
+    int r = ip_run(ctx);
+    if (!r) r = fa_features_run(ctx);
+    if (!r) r = fa_odometry_run(ctx, false);
+    if (r) return r;
+    SLO_LAUNCH(ctx, "clear_flags", k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
+    if (map && (r = map_run(ctx))) return r;
+    if (ctx->cfg.loop_closure_enable) r = sc_detect_run(ctx);
+    return r;
+}
+
+// slo_batch_process as one HIP graph launch per scan.  A step's launch
+// sequence depends only on host state (FA's publish counter, the mapping
+// interval) and the kernels' arguments only on which half of the odometry
+// ping-pong buffers is current (fa_swap_last), so a step is one of four
+// graphs: with or without the mapping stage, times the two layouts.  Each
+// is captured once — after the step kind has run eagerly, so every workspace
+// has been sized — and then replayed.  The scan itself is read through the io
+// slot set before each launch.  Returns 1 when the step is not eligible
+// (eager path).
+static int step_graph(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
+    if (!ctx->graphs || (ctx->timing && ctx->timing_only.empty()) || !ctx->fa_inited || ctx->cfg.loop_verify ||
+        ctx->cfg.pose_graph)
+        return 1;   // per-kernel event timing and the host round trips need the eager path
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    fa_advance(ctx, false);
+    const bool map = map_gate(ctx, t_scan);
+    const int kind = map ? 1 : 0, key = 2 * kind + (ctx->v.corner_last == ctx->pp_corner0 ? 0 : 1);
+    if (int r = set_io(ctx, d_points, d_counts)) return r;
+    if (ctx->graph_exec[key] && (ctx->graph_ws[key] != ctx->ws_gen ||
+                                 memcmp(&ctx->graph_v[key], &ctx->v, sizeof(DevView)) != 0)) {
+        hipGraphExecDestroy(ctx->graph_exec[key]);   // its arguments are stale: capture again
+        ctx->graph_exec[key] = nullptr;
+    }
+    if (!ctx->graph_exec[key]) {
+        if (!ctx->graph_seen[kind]) {   // first occurrence of the kind: eager
+            ctx->graph_seen[kind] = 1;
+            int r = step_launches(ctx, map);
+            if (!r && map) ctx->mapped_now = true;
+            return r;
+        }
+        memcpy(&ctx->graph_v[key], &ctx->v, sizeof(DevView));
+        const unsigned int ws0 = ctx->ws_gen;
+        SLO_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
+        const int r = step_launches(ctx, map);   // swaps the ping-pong halves, as a replay does below
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
+        if (r || e != hipSuccess) {
+            if (g) hipGraphDestroy(g);
+            if (!r) ctx->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
+            return r ? r : SLO_E_HIP;
+        }
+        if (ctx->ws_gen != ws0) {   // a workspace moved while capturing (not expected): no graph
+            hipGraphDestroy(g);
+            ctx->err = "a workspace was reallocated during graph capture";
+            return SLO_E_STATE;
+        }
+        ctx->graph_ws[key] = ws0;
+        const hipError_t ei = hipGraphInstantiate(&ctx->graph_exec[key], g, nullptr, nullptr, 0);
+        hipGraphDestroy(g);
+        if (ei != hipSuccess) {
+            ctx->graph_exec[key] = nullptr;
+            ctx->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(ei);
+            return SLO_E_HIP;
+        }
+    } else {
+        fa_swap_last(ctx);   // what the captured fa_odometry_run did on the host
+    }
+    SLO_CHECK(hipGraphLaunch(ctx->graph_exec[key], ctx->stream));
+    if (map) ctx->mapped_now = true;
+    return 0;
+}
+}  // namespace slo
+
+extern "C" {
+
 int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
-    int r = slo_batch_image_projection(ctx, d_points, d_counts);
+    if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    if (ctx->cfg.use_cloud_ring && !ctx->v.rings) {
+        ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings";
+        return SLO_E_STATE;
+    }
+    int r = slo::step_graph(ctx, d_points, d_counts, t_scan);
+    if (r <= 0) return r;
+    r = slo_batch_image_projection(ctx, d_points, d_counts);
     if (r) return r;
     r = slo_batch_feature_association(ctx);
     if (r) return r;
@@ -514,11 +692,14 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
 
 int slo_timing_enable(slo_ctx* ctx, int enable) {
     if (!ctx) return SLO_E_ARG;
+    if (ctx->timing != (enable != 0)) slo::graphs_drop(ctx);   // captured graphs carry the timing launches
     ctx->timing = enable != 0;
     return SLO_OK;
 }
 int slo_timing_filter(slo_ctx* ctx, const char* name) {
     if (!ctx) return SLO_E_ARG;
+    slo::timing_flush(ctx);   // stamps of the previous filter
+    slo::graphs_drop(ctx);
     ctx->timing_only = name ? name : "";
     return SLO_OK;
 }
@@ -607,8 +788,7 @@ int slo_image_projection_ring(slo_ctx* ctx, const void* pts, size_t n, size_t st
         if (n) SLO_CHECK(hipMemcpyAsync(ctx->d_ring_in, rings, 2 * n, hipMemcpyHostToDevice, ctx->stream));
         ctx->v.rings = ctx->d_ring_in;
     }
-    ctx->v.pts = ctx->d_in;
-    ctx->v.npts = ctx->d_cnt;
+    if ((r = slo::set_io(ctx, ctx->d_in, ctx->d_cnt))) return r;
     r = slo::ip_run(ctx);
     if (r) return r;
     memset(out, 0, sizeof(*out));

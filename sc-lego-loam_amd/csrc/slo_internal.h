@@ -31,6 +31,12 @@ namespace slo {
 
 struct alignas(8) Smooth { float value; int32_t ind; };
 
+// The scan a batched call works on (device pointers [S][P] points, [S]
+// counts), kept in device memory and set by k_set_io at the start of each
+// call: kernels read it there, so a captured HIP graph replays on whatever
+// buffers the next call names.
+struct SloIo { const float4* pts; const int32_t* npts; };
+
 // Per-stream scalar state of the FA / MO nodes (one record per stream).
 struct StreamState {
     float transformCur[6];
@@ -101,8 +107,7 @@ struct DevView {
     int H;        // R*C
     int cap_sharp, cap_less_sharp, cap_flat, cap_less_flat;
     // inputs
-    const float4* pts;   // [S][P]
-    const int32_t* npts; // [S]
+    const SloIo* io;     // the input scan: io->pts [S][P], io->npts [S]
     const uint16_t* rings; // [S][P] ring per input point (cfg.use_cloud_ring), else unused
     // image projection
     int32_t* owner;      // [S][H]
@@ -185,6 +190,8 @@ struct DevView {
     double* mo_part;     // [S][MO_BLOCKS][SLO_MO_PART] partial A^T A / A^T b (double-double) + count
     int cap_q;           // mapping queries per stream: cap_less_sharp + cap_st
     int32_t* mo_nn;      // [S][cap_q][5] 5-NN map indices of each query (-1: rejected)
+    int32_t* mo_perm;    // [S][cap_q] the queries grouped by their body-frame 2 m cell (k_mo_perm): the order
+                         // k_mo_knn takes them in (any order gives the same result)
     // hash grids: odometry "kd-tree" clouds (corner / surf) and the DS maps
     GridView g_oc, g_os, g_mc, g_ms;
     // ---- Scan Context history (Scancontext.h:99-106)
@@ -444,6 +451,11 @@ struct slo_ctx {
     struct KT { std::vector<hipEvent_t> ev; double total_ms = 0; int64_t n = 0; };
     std::map<std::string, KT> ktimes;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
+    // with a filter (timing_only), the named kernel is timed by device
+    // timestamps written in-stream around each launch (k_stamp: the device's
+    // constant-rate wall clock), so the timing survives graph capture
+    unsigned long long* d_stamp = nullptr;   // [SLO_STAMP_CAP] timestamps + [1] counter
+    double stamp_khz = 0;
     // host staging for single-scan API
     void* h_stage = nullptr;
     size_t h_stage_bytes = 0;
@@ -467,6 +479,17 @@ struct slo_ctx {
     float* d_pg_poses = nullptr;
     size_t pg_cap = 0;
     bool mapped_now = false;            // this batch step ran the mapping stage
+    // the input slot (DevView::io) and the captured steps of slo_batch_process
+    // (slo_ctx.hip): step kind (0: no mapping, 1: mapping) x the layout of
+    // the odometry ping-pong halves (fa_swap_last)
+    slo::SloIo* d_io = nullptr;
+    bool graphs = true;                 // slo_graph_mode
+    int graph_seen[2] = {0, 0};         // the step kind has run once (its workspaces are sized)
+    hipGraphExec_t graph_exec[4] = {nullptr, nullptr, nullptr, nullptr};
+    slo::DevView graph_v[4];            // the kernel-argument view each graph was captured with
+    unsigned int graph_ws[4] = {0, 0, 0, 0};
+    unsigned int ws_gen = 0;            // bumped whenever a workspace behind a captured pointer moves
+    const float4* pp_corner0 = nullptr; // corner_last of layout 0
 };
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -482,6 +505,7 @@ int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
 int fa_odometry_run(slo_ctx* ctx, bool first_scan);
+void fa_swap_last(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
@@ -490,7 +514,8 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell);
 GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
-int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts);
+int map_run(slo_ctx* ctx);
+void graphs_drop(slo_ctx* ctx);
 int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams);
 int sc_detect_run(slo_ctx* ctx);
 int sc_detect_run_one(slo_ctx* ctx);
@@ -502,6 +527,8 @@ int lc_run(slo_ctx* ctx);
 int lc_icp_run(slo_ctx* ctx, const float4* src, size_t src_stride, const int32_t* nsrc, const float4* tgt,
                size_t tgt_stride, const int32_t* ntgt);
 }  // namespace slo
+
+#define SLO_STAMP_CAP 65536
 
 #define SLO_LAUNCH(ctx, name, kernel, grid, block, shmem, ...)                        \
     do {                                                                              \

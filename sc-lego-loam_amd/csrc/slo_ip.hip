@@ -74,11 +74,18 @@ __device__ inline bool project_point(const slo_config& c, float4 p, int ring, in
     return true;
 }
 
-__global__ void k_ip_init(DevView v) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= v.S) return;
-    v.fl[2 * s] = INT_MAX;
-    v.fl[2 * s + 1] = -1;
+// the owner image back to -1 (no point) and the first/last finite indices
+// reset; a kernel rather than a memset, so a captured step graph holds
+// plain kernel nodes only
+__global__ void __launch_bounds__(256) k_ip_init(DevView v) {
+    const size_t n4 = (size_t)v.S * v.H / 4, i0 = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int4* o = reinterpret_cast<int4*>(v.owner);
+    for (size_t i = i0; i < n4; i += (size_t)gridDim.x * blockDim.x) o[i] = make_int4(-1, -1, -1, -1);
+    for (size_t i = 4 * n4 + i0; i < (size_t)v.S * v.H; i += (size_t)gridDim.x * blockDim.x) v.owner[i] = -1;
+    if (i0 < (size_t)v.S) {
+        v.fl[2 * i0] = INT_MAX;
+        v.fl[2 * i0 + 1] = -1;
+    }
 }
 
 // A workgroup takes IP_PTS_PER_WG consecutive points (thread t: points t,
@@ -90,13 +97,13 @@ __global__ void k_ip_init(DevView v) {
 #define IP_PTS_PER_WG 2048
 __global__ void k_ip_project(DevView v) {
     const int s = blockIdx.y;
-    const int n = v.npts[s];
+    const int n = v.io->npts[s];
     const int R = v.cfg.n_scan;
     int fmin = INT_MAX, fmax = -1;
     for (int k = 0; k < IP_PTS_PER_WG / 256; ++k) {
         const int i = blockIdx.x * IP_PTS_PER_WG + k * 256 + threadIdx.x;
         if (i >= n) break;
-        float4 p = v.pts[(size_t)s * v.P + i];
+        float4 p = v.io->pts[(size_t)s * v.P + i];
         if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
             fmin = min(fmin, i); fmax = max(fmax, i);
             int row, col; float rg;
@@ -184,7 +191,7 @@ __global__ void __launch_bounds__(256) k_ip_tile(DevView v) {
     const int s = blockIdx.y, R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const int TC = ip_tile_cols(R), c0 = blockIdx.x * TC, nc = min(TC, C - c0), npx = R * TC;
     const size_t base = (size_t)s * v.H;
-    const float4* pts = v.pts + (size_t)s * v.P;
+    const float4* pts = v.io->pts + (size_t)s * v.P;
     const int gsi = v.cfg.ground_scan_ind, tid = threadIdx.x;
     __shared__ int l_a[IP_TILE_PX];   // owner, then the union-find parents
     __shared__ float l_rg[IP_TILE_PX];
@@ -508,7 +515,8 @@ __global__ void __launch_bounds__(256) k_ip_compact(DevView v) {
             int f0 = v.fl[2 * s], f1 = v.fl[2 * s + 1];
             float* orr = v.orient + 3 * s;
             if (f1 >= 0) {
-                float4 a = v.pts[(size_t)s * v.P + f0], b = v.pts[(size_t)s * v.P + f1];
+                const float4* ip = v.io->pts + (size_t)s * v.P;
+                float4 a = ip[f0], b = ip[f1];
                 float so = -slo_libm::atan2f_(a.y, a.x);
                 float eo = (float)(-slo_libm::atan2f_(b.y, b.x) + 2 * M_PI);
                 if (eo - so > 3 * M_PI) eo = (float)(eo - 2 * M_PI);
@@ -522,8 +530,8 @@ __global__ void __launch_bounds__(256) k_ip_compact(DevView v) {
 int ip_run(slo_ctx* ctx) {
     DevView& v = ctx->v;
     const int S = ctx->S;
-    SLO_CHECK(hipMemsetAsync(v.owner, 0xff, sizeof(int32_t) * (size_t)S * v.H, ctx->stream));
-    SLO_LAUNCH(ctx, "ip_init", k_ip_init, dim3((S + 63) / 64), dim3(64), 0, v);
+    const int gi = (int)std::max<size_t>((S + 255) / 256, std::min<size_t>(4096, ((size_t)S * v.H / 4 + 255) / 256));
+    SLO_LAUNCH(ctx, "ip_init", k_ip_init, dim3(gi), dim3(256), 0, v);
     const int T = 256;
     dim3 gp((v.P + IP_PTS_PER_WG - 1) / IP_PTS_PER_WG, S), gr(v.cfg.n_scan, S);
     SLO_LAUNCH(ctx, "ip_project", k_ip_project, gp, dim3(T), 0, v);

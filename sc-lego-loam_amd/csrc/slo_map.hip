@@ -376,6 +376,68 @@ __device__ inline P4 mo_query(const DevView& v, int s, const StreamState& st, in
     return P4{cPitch * x2 + sPitch * z2 + g.tX, y2 + g.tY, -sPitch * x2 + cPitch * z2 + g.tZ, po.w};
 }
 
+// k_mo_knn's query order: a counting sort of the queries by the Morton code
+// of their body-frame 4 m cell (corner queries first), in LDS, one workgroup
+// per stream — so the lanes of a wave walk neighbouring rows of the map grid.
+// Only the work order changes: mo_nn is indexed by query.
+#define MO_PERM_B 16384  // buckets per query kind (14-bit Morton codes)
+#ifndef MO_PERM_INV
+#define MO_PERM_INV 0.25f   // 1 / cell edge (4 m)
+#endif
+#ifndef SLO_MO_PERM
+#define SLO_MO_PERM 1
+#endif
+__global__ void __launch_bounds__(1024) k_mo_perm(DevView v) {
+    __shared__ int cnt[2 * MO_PERM_B];
+    __shared__ int wsum[16];
+    const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const StreamState& st = v.st[s];
+    if (!st.mo_ran) return;
+    const int nc = st.n_corner_ds, nq = nc + st.n_surf_total_ds;
+    const float4* qc = v.cur_c_ds + (size_t)s * v.cap_less_sharp;
+    const float4* qs = v.cur_st_ds + (size_t)s * v.cap_st;
+    // Morton code of the body-frame cell: x, z 5 bits, y 4 bits (clamped
+    // around the sensor), interleaved x z y from the top -> 14 bits
+    auto bucket = [&](int q) {
+        const float4 p = q < nc ? qc[q] : qs[q - nc];
+        unsigned int h = 0;
+        if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
+            const unsigned int a = (unsigned int)min(max(grid_cell(p.x, MO_PERM_INV) + 16, 0), 31);
+            const unsigned int b = (unsigned int)min(max(grid_cell(p.y, MO_PERM_INV) + 8, 0), 15);
+            const unsigned int c = (unsigned int)min(max(grid_cell(p.z, MO_PERM_INV) + 16, 0), 31);
+#pragma unroll
+            for (int k = 4; k >= 0; --k) {
+                h = (h << 1) | ((a >> k) & 1u);
+                h = (h << 1) | ((c >> k) & 1u);
+                if (k < 4) h = (h << 1) | ((b >> k) & 1u);
+            }
+        }
+        return (q < nc ? 0 : MO_PERM_B) + (int)h;
+    };
+    for (int b = tid; b < 2 * MO_PERM_B; b += 1024) cnt[b] = 0;
+    __syncthreads();
+    for (int q = tid; q < nq; q += 1024) atomicAdd(&cnt[bucket(q)], 1);
+    __syncthreads();
+    constexpr int PER = 2 * MO_PERM_B / 1024;
+    int c[PER], sum = 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) { c[k] = cnt[tid * PER + k]; sum += c[k]; }
+    int incl = sum;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    int run = incl - sum;
+    for (int k = 0; k < w; ++k) run += wsum[k];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) { cnt[tid * PER + k] = run; run += c[k]; }
+    __syncthreads();
+    int32_t* perm = v.mo_perm + (size_t)s * v.cap_q;
+    for (int q = tid; q < nq; q += 1024) perm[atomicAdd(&cnt[bucket(q)], 1)] = q;
+}
+
 // The 5-NN of every query, one thread per query, into mo_nn (index -1 in the
 // first slot = rejected: fewer than 5 within 1 m).  A kernel of its own so its
 // few registers give full occupancy to the latency-bound grid walk.
@@ -389,7 +451,13 @@ __global__ void __launch_bounds__(256) k_mo_knn(DevView v) {
     const int nc = st.n_corner_ds, nq = nc + st.n_surf_total_ds, per = (nq + SLO_MO_BLOCKS - 1) / SLO_MO_BLOCKS;
     const int q0 = chunk * per, q1 = min(nq, q0 + per);
     int32_t* nn = v.mo_nn + (size_t)s * v.cap_q * 5;
-    for (int q = q0 + (int)threadIdx.x; q < q1; q += blockDim.x) {
+    const int32_t* perm = v.mo_perm + (size_t)s * v.cap_q;
+    for (int qi = q0 + (int)threadIdx.x; qi < q1; qi += blockDim.x) {
+#if SLO_MO_PERM
+        const int q = perm[qi];   // grouped by 2 m cell: a wave's queries are neighbours
+#else
+        const int q = qi;
+#endif
         P4 po;
         const P4 sel = mo_query(v, s, st, q, g, po);
         int ind[5];
@@ -736,7 +804,7 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
     if (threadIdx.x == 0) st.sc_count = kfid + 1;
 }
 
-int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
+int map_run(slo_ctx* ctx) {
     DevView& v = ctx->v;
     const int S = ctx->S;
     const int SS = ST_STRIDE;
@@ -750,7 +818,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
                     v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc))) return r;
     if ((r = vg_run(ctx, "map_surf", v.map_s, v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf,
                     v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms))) return r;
-    if ((r = vg_run(ctx, "raw", d_points, v.P, d_counts, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
+    if ((r = vg_run(ctx, "raw", nullptr, v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
                     fld(&StreamState::n_raw_ds), SS, v.P))) return r;
     if ((r = vg_run(ctx, "corner", v.corner_last, v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS,
                     v.cfg.leaf_corner, v.cur_c_ds, v.cap_less_sharp, fld(&StreamState::n_corner_ds), SS,
@@ -762,6 +830,7 @@ int map_run(slo_ctx* ctx, const float4* d_points, const int32_t* d_counts) {
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
     if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
                     v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;
+    if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(1024), 0, v);
     // hash grids over the DS maps
     if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
     if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;

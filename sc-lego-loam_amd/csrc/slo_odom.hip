@@ -828,6 +828,15 @@ __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
     }
 }
 
+// the clouds just written become *Last for the next scan (a host-side swap
+// of the ping-pong halves: DevView alternates between two layouts, and a
+// captured step graph is kept per layout, slo_ctx.hip)
+void fa_swap_last(slo_ctx* ctx) {
+    std::swap(ctx->v.corner_last, ctx->v.corner_next);
+    std::swap(ctx->v.surf_last, ctx->v.surf_next);
+    std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
+}
+
 int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     DevView& v = ctx->v;
     const int S = ctx->S;
@@ -856,10 +865,7 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     else if (v.cap_less_sharp <= 8192) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<8192>, dim3(S), dim3(1024), 0, v);
     else SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<16384>, dim3(S), dim3(1024), 0, v);
     SLO_CHECK(hipGetLastError());
-    // the clouds just written become *Last for the next scan
-    std::swap(ctx->v.corner_last, ctx->v.corner_next);
-    std::swap(ctx->v.surf_last, ctx->v.surf_next);
-    std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
+    fa_swap_last(ctx);
     // setInputCloud: hash grid over the (possibly unchanged) surf tree cloud
     // (the corner tree by a windowed brute force over its x-sorted copy, k_fa_sx_kd)
     const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));

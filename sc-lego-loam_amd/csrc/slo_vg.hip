@@ -23,6 +23,16 @@
 
 namespace slo {
 
+// a VoxelGrid input: a cloud [S][stride] with counts n[s * n_stride], or
+// (in == nullptr) the context's input scan through its io slot
+struct VgSrc {
+    const float4* in;
+    const int32_t* n;
+    const SloIo* io;
+    __device__ const float4* pts() const { return in ? in : io->pts; }
+    __device__ const int32_t* cnt() const { return in ? n : io->npts; }
+};
+
 __device__ inline unsigned int f2ord(float f) {
     unsigned int u = __float_as_uint(f);
     return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
@@ -33,8 +43,9 @@ __device__ inline float ord2f(unsigned int u) {
 
 // stream offsets of the concatenated input (block scan), bounds init, and the
 // meta words [total, max cell count, long-voxel count]
-__global__ void __launch_bounds__(1024) k_vg_prefix(const int32_t* n, int n_stride, int S, int32_t* off,
+__global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int S, int32_t* off,
                                                     unsigned int* bounds, int32_t* meta) {
+    const int32_t* n = src.cnt();
     __shared__ int wsum[16];
     __shared__ int carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -62,8 +73,9 @@ __global__ void __launch_bounds__(1024) k_vg_prefix(const int32_t* n, int n_stri
         for (int k = 0; k < 3; ++k) { bounds[6 * s + k] = 0xffffffffu; bounds[6 * s + 3 + k] = 0u; }
 }
 
-__global__ void __launch_bounds__(256) k_vg_bounds(const float4* in, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, const int32_t* off,
                                                    unsigned int* bounds) {
+    const float4* in = src.pts();
     const int s = blockIdx.y;
     const int n = off[s + 1] - off[s];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
@@ -205,9 +217,10 @@ __device__ inline void vg_load(const float4* in, size_t in_stride, const VgParam
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) k_vg_hist(const float4* in, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, const int32_t* off,
                                                   const VgParams* prm, int pass, const unsigned int* kin, int* cnt,
                                                   int maxT) {
+    const float4* in = FIRST ? src.pts() : nullptr;
     __shared__ int h[256];
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
@@ -254,7 +267,7 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) k_vg_scatter(const float4* in, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
                                                      const VgParams* prm, int pass, const unsigned int* kin,
                                                      const unsigned int* vin, unsigned int* kout, unsigned int* vout,
                                                      const int* cnt, int maxT) {
@@ -262,6 +275,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_scatter(const float4* in, size_t in
     __shared__ int wc[4][256];   // per wave slice: running digit counts, then the slice's digit offsets
     __shared__ int lb[256];      // global base of each digit minus its first position in the tile
     __shared__ int wsum[4];
+    const float4* in = FIRST ? src.pts() : nullptr;
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
@@ -439,14 +453,14 @@ __device__ inline void vg_store(const VgOut& o, int s, int r, float sx, float sy
     if (r < o.cap) o.out[(size_t)s * o.stride + r] = make_float4(sx / c, sy / c, sz / c, si / c);
 }
 
-__global__ void __launch_bounds__(VG_T) k_vg_centroid(const float4* in, size_t in_stride, const unsigned int* vals,
+__global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, size_t in_stride, const unsigned int* vals,
                                                       const int32_t* off, const int32_t* nvox, const int* starts,
                                                       const int* ends, int32_t* meta, int4* longv, int nlong_cap,
                                                       VgOut o) {
     const int s = blockIdx.y;
     const int base = off[s], nv = min(nvox[s], o.cap);
     const unsigned int* v = vals + base;
-    const float4* src = in + (size_t)s * in_stride;
+    const float4* src = srcv.pts() + (size_t)s * in_stride;
     for (int r = blockIdx.x * VG_T + threadIdx.x; r < nv; r += gridDim.x * VG_T) {
         const int j = starts[base + r], e = ends[base + r];
         if (e - j > VG_SHORT) {
@@ -470,7 +484,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_centroid(const float4* in, size_t i
 // Long voxels, one wave each (persistent grid over the list): the wave
 // stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
 // intensity chains over them in order.
-__global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_stride, const unsigned int* vals,
+__global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, const unsigned int* vals,
                                                  const int32_t* off, const int32_t* meta, const int4* longv,
                                                  int nlong_cap, VgOut o) {
     __shared__ float4 buf[4][256];
@@ -481,7 +495,7 @@ __global__ void __launch_bounds__(256) k_vg_long(const float4* in, size_t in_str
         const int4 L = longv[t];
         const int s = L.x, a = L.y, r = L.z, e = L.w;
         const unsigned int* v = vals + off[s];
-        const float4* src = in + (size_t)s * in_stride;
+        const float4* src = srcv.pts() + (size_t)s * in_stride;
         float acc = 0.0f;
         for (int c0 = a; c0 < e; c0 += 256) {
             const int m = min(256, e - c0);
@@ -517,6 +531,7 @@ static int ensure_ws(slo_ctx* ctx, size_t stride) {
         for (void* q : old) if (q) hipFree(q);
         w.items = it;
         w.nlong_cap = it / VG_SHORT + 1;
+        ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.keys, 4 * it));
         SLO_CHECK(hipMalloc(&w.keys2, 4 * it));
         SLO_CHECK(hipMalloc(&w.vals, 4 * it));
@@ -528,19 +543,21 @@ static int ensure_ws(slo_ctx* ctx, size_t stride) {
         if (w.cnt) hipFree(w.cnt);
         if (w.hcnt) hipFree(w.hcnt);
         w.tiles = tt;
+        ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.cnt, sizeof(int) * 256 * tt));
         SLO_CHECK(hipMalloc(&w.hcnt, sizeof(int) * tt));
     }
     return 0;
 }
 
-// One batched VoxelGrid over S streams: stream s's n = d_n[s * n_stride]
-// points at in + s * in_stride; its centroids go to out + s * out_stride (at
-// most out_cap; more sets errflag and is clipped) and their count to
-// d_nout[s * nout_stride].  Everything is sized from the strides, so the host
-// only issues launches (no round trip).
-int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
-           float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
+// The segmented sort of S streams' (key, point index) items: stream s's n =
+// d_n[s * n_stride] points at in + s * in_stride, keyed by their PCL voxel
+// index at `leaf`.
+// On return *keys / *vals hold the sorted items of stream s at [off[s],
+// off[s + 1]) of the workspace, *spare_k / *spare_v the free ping-pong halves.
+static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
+                   float leaf, unsigned int** keys, unsigned int** vals, unsigned int** spare_k,
+                   unsigned int** spare_v) {
     MapWs& w = ctx->mws;
     const int S = ctx->S;
     if (int r = ensure_ws(ctx, in_stride)) return r;
@@ -548,8 +565,9 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     const int bx = std::max(1, std::min(64, (int)((in_stride + VG_T - 1) / VG_T)));
     const dim3 grid(GX, S);
-    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, d_n, n_stride, S, w.off, w.bounds, w.meta);
-    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(VG_T), 0, in, in_stride, w.off, w.bounds);
+    const VgSrc src{in, d_n, ctx->v.io};
+    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta);
+    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(VG_T), 0, src, in_stride, w.off, w.bounds);
     SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
     hipEvent_t ev = nullptr;
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
@@ -558,25 +576,45 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     unsigned int *k0 = w.keys, *v0 = w.vals, *k1 = w.keys2, *v1 = w.vals2;
     for (int pass = 0; pass < VG_PASSES; ++pass) {
         if (pass == 0) {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass, k0,
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, k0,
                        w.cnt, maxT);
         } else {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass, k0,
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, k0,
                        w.cnt, maxT);
         }
         SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, w.cnt, maxT);
         if (pass == 0) {
-            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass,
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
                        k0, v0, k1, v1, w.cnt, maxT);
         } else {
-            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, in, in_stride, w.off, w.prm, pass,
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
                        k0, v0, k1, v1, w.cnt, maxT);
         }
         std::swap(k0, k1);
         std::swap(v0, v1);
     }
     if (tm) timing_end(ctx, sort_name.c_str(), ev);
+    *keys = k0; *vals = v0; *spare_k = k1; *spare_v = v1;
+    return 0;
+}
+
+// One batched VoxelGrid over S streams: stream s's n = d_n[s * n_stride]
+// points at in + s * in_stride (in == nullptr: the context's input scan,
+// DevView::io); its centroids go to out + s * out_stride (at
+// most out_cap; more sets errflag and is clipped) and their count to
+// d_nout[s * nout_stride].  Everything is sized from the strides, so the host
+// only issues launches (no round trip).
+int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
+           float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
+    MapWs& w = ctx->mws;
+    const int S = ctx->S;
+    unsigned int *k0, *v0, *k1, *v1;
+    if (int r = vg_sort(ctx, tag, in, in_stride, d_n, n_stride, leaf, &k0, &v0, &k1, &v1)) return r;
+    const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
+    const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
+    const dim3 grid(GX, S);
     const VgOut o{out, out_stride, out_cap};
+    const VgSrc src{in, d_n, ctx->v.io};
     // the ping-pong buffers the sort is done with hold the voxel ranges
     int* starts = (int*)k1;
     int* ends = (int*)v1;
@@ -585,8 +623,8 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
                out_cap, w.errflag);
     SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
     SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid, dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S),
-               dim3(VG_T), 0, in, in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
-    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, in, in_stride, v0, w.off, w.meta, w.longv,
+               dim3(VG_T), 0, src, in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, in_stride, v0, w.off, w.meta, w.longv,
                (int)w.nlong_cap, o);
     SLO_CHECK(hipGetLastError());
     return 0;

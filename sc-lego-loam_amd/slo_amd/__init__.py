@@ -166,6 +166,10 @@ class Context:
     def batch_process(self, d_pts, d_cnt, t_scan):
         self._ok(self.L.slo_batch_process(self.h, d_pts, d_cnt, float(t_scan)), "slo_batch_process")
 
+    def graph_mode(self, on=True):
+        """slo_graph_mode: replay captured HIP graphs in batch_process (default) or launch eagerly"""
+        self._ok(self.L.slo_graph_mode(self.h, 1 if on else 0), "slo_graph_mode")
+
     def batch_sc_make(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_sc_make(self.h, d_pts, d_cnt), "slo_batch_sc_make")
 

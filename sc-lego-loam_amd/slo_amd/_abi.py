@@ -107,7 +107,7 @@ REC = {"pose": 0, "mapped": 6, "n_keyframes": 12, "kf_saved": 13, "loop_id": 14,
 EXPORTS = [
     "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
-    "slo_batch_sc_detect", "slo_batch_process", "slo_image_projection", "slo_feature_association",
+    "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_image_projection", "slo_feature_association",
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
@@ -155,6 +155,7 @@ def lib():
     L.slo_batch_map_optimization.argtypes = [P, P, P, ctypes.c_double]
     L.slo_batch_sc_detect.argtypes = [P]
     L.slo_batch_process.argtypes = [P, P, P, ctypes.c_double]
+    L.slo_graph_mode.argtypes = [P, ctypes.c_int]
     L.slo_image_projection.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                        ctypes.POINTER(SegView)]
     L.slo_feature_association.argtypes = [P, ctypes.c_double, ctypes.POINTER(FaView)]

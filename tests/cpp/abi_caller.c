@@ -21,6 +21,7 @@ int main(void) {
     slo_ctx* ctx = NULL;
     CHECK(slo_create(NULL, 0, 1, &ctx) == SLO_E_ARG);
     CHECK(slo_batch_process(NULL, NULL, NULL, 0.0) == SLO_E_ARG);
+    CHECK(slo_graph_mode(NULL, 1) == SLO_E_ARG);
     CHECK(slo_record_floats() == SLO_RECORD_FLOATS);
     CHECK(SLO_REC_DESC + 20 * 60 <= SLO_RECORD_FLOATS);
 
