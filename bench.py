@@ -144,10 +144,11 @@ def pmc_traffic(path, kernel):
     (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, MI355X_MICROARCH.md), or None."""
     import glob
     import json
-    if path is None:   # the latest round's profile: profiles/rNN/
+    if path is None:   # the latest round's profile: profiles/rNN[a-z]/
         import re
-        cands = [(int(m.group(1)), p) for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json"))
-                 for m in [re.search(r"profiles/r(\d+)/summary\.json$", p)] if m]
+        cands = [((int(m.group(1)), m.group(2)), p)
+                 for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json"))
+                 for m in [re.search(r"profiles/r(\d+)([a-z]?)/summary\.json$", p)] if m]
         path = max(cands)[1] if cands else None
     if path is None or not os.path.exists(path):
         return None, None
