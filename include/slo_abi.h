@@ -80,6 +80,31 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
  * every launch issued eagerly (the captured graphs are released) */
 int slo_graph_mode(slo_ctx* ctx, int on);
 
+/* ---------------------------------------------------------------- IMU (FeatureAssociation::imuHandler)
+ * sensor_msgs/Imu as imuHandler reads it (featureAssociation.cpp:459-486):
+ * header stamp, orientation quaternion, linear acceleration, angular
+ * velocity, all float64.  Each message is pushed on the stream's 200-entry
+ * IMU ring (imuQueLength) and integrated (AccumulateIMUShiftAndRotation,
+ * FA:417-457); the next scans deskew against the ring (adjustDistortion,
+ * FA:525-616), seed the odometry (updateInitialGuess, FA:1639-1664) and
+ * plug the IMU rotation into the integration (FA:1697-1725).  Without any
+ * message every IMU term is the reference's zero. */
+typedef struct slo_imu_msg {
+    double stamp;
+    double qx, qy, qz, qw;
+    double ax, ay, az;
+    double wx, wy, wz;
+} slo_imu_msg;
+/* d_msgs: device [n_streams][msgs_per_stream]; d_counts: device int32
+ * [n_streams]: the messages each stream's imuHandler receives, in order,
+ * before its next scan (async on slo_stream()) */
+int slo_batch_imu(slo_ctx* ctx, const slo_imu_msg* d_msgs, int msgs_per_stream, const int32_t* d_counts);
+/* the stamp of the scan the next feature step deskews (cloudHeader.stamp,
+ * FA:488-491; slo_batch_process and slo_feature_association set it) */
+int slo_batch_scan_time(slo_ctx* ctx, double t_scan);
+/* imuHandler of a one-stream context on a host message */
+int slo_imu_handler(slo_ctx* ctx, const slo_imu_msg* msg);
+
 /* ---------------------------------------------------------------- single scan (stream 0, host memory) */
 typedef struct slo_seg_view {
     int32_t n_segmented;           /* |segmentedCloud| */

@@ -42,7 +42,7 @@ struct OracleStream {
         int flags = 0;
         det_valid = false;
         ip.cloudHandler(pts, n);
-        fa.run(ip.segmentedCloud, ip.segMsg, ip.outlierCloud);
+        fa.run(ip.segmentedCloud, ip.segMsg, ip.outlierCloud, t);
         if (fa.systemInitedLM && scan_index > 0) flags |= 1;
         if (flags & 1) {
             // TransformFusion::laserOdometryHandler (TF:186-219) on this scan's
@@ -119,6 +119,13 @@ void oracle_rs_loop_from(const float* corr, const float* latest, float* out) {
 }
 
 // useCloudRing input for the next scans (the message's ring field, unfiltered order)
+// imuHandler on n messages (slo_imu_msg layout), in order
+void oracle_imu(void* h, const double* msgs, int n) {
+    for (int k = 0; k < n; ++k) {
+        const double* m = msgs + 11 * k;
+        ((OracleStream*)h)->fa.imuHandler(ImuMsg{m[0], m[1], m[2], m[3], m[4], m[5], m[6], m[7], m[8], m[9], m[10]});
+    }
+}
 void oracle_set_rings(void* h, const uint16_t* rings, int n) { ((OracleStream*)h)->ip.rings.assign(rings, rings + n); }
 
 // image projection only (for front-end parity of a single scan)
@@ -171,6 +178,16 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
     if (name == "corner_last") return copy_cloud(s->fa.laserCloudCornerLast, (float*)out, cap);
     if (name == "surf_last") return copy_cloud(s->fa.laserCloudSurfLast, (float*)out, cap);
     if (name == "transform_sum") return cp(s->fa.transformSum, 6, 4);
+    if (name == "imu") {   // the IMU scalars in slo_get("imu")'s order
+        const FeatureAssociation& f = s->fa;
+        const double a[23] = {(double)f.imuPointerLast, (double)f.imuPointerLastIteration, f.imuRollStart,
+                              f.imuPitchStart, f.imuYawStart, f.imuVeloXStart, f.imuVeloYStart, f.imuVeloZStart,
+                              f.imuRollCur, f.imuPitchCur, f.imuYawCur, f.imuVeloFromStartXCur, f.imuVeloFromStartYCur,
+                              f.imuVeloFromStartZCur, f.imuAngularRotationXLast, f.imuAngularRotationYLast,
+                              f.imuAngularRotationZLast, f.imuAngularFromStartX, f.imuAngularFromStartY,
+                              f.imuAngularFromStartZ, f.imuRollLast, f.imuPitchLast, f.imuYawLast};
+        return cp(a, 23, 8);
+    }
     if (name == "integrated") return cp(s->integrated, 6, 4);
     if (name == "transform_cur") return cp(s->fa.transformCur, 6, 4);
     if (name == "fa_iters") { int v[2] = {s->fa.iters_surf, s->fa.iters_corner}; return cp(v, 2, 4); }
@@ -515,7 +532,7 @@ double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int p
         s.det_valid = false;
         s.ip.cloudHandler(p, P);
         auto b = std::chrono::steady_clock::now();
-        s.fa.run(s.ip.segmentedCloud, s.ip.segMsg, s.ip.outlierCloud);
+        s.fa.run(s.ip.segmentedCloud, s.ip.segMsg, s.ip.outlierCloud, tk);
         auto c = std::chrono::steady_clock::now();
         bool kf = false;
         if (s.fa.published_to_mapping) {

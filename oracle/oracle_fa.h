@@ -1,22 +1,29 @@
 // oracle_fa.h — TEST INFRASTRUCTURE ONLY: CPU restatement of
-// featureAssociation.cpp (non-IMU path): adjustDistortion 491-619,
+// featureAssociation.cpp: adjustDistortion 491-619 with its IMU branch,
 // calculateSmoothness 621-641, markOccludedPoints 643-678, extractFeatures
 // 680-784, TransformToStart/End 860-953, PluginIMURotation 955-1013,
 // AccumulateRotation 1015-1032, correspondence search 1044-1268, the two
 // 3-DOF solvers 1270-1478, checkSystemInitialization 1605-1637,
 // updateTransformation 1666-1695, integrateTransformation 1697-1725,
-// adjustOutlierCloud 1746-1757, publishCloudsLast 1759-1815.
-// The IMU queue is never filled (no IMU topic), so every imu* quantity stays
-// at its initial value exactly as in the reference (imuPointerLast = -1).
+// adjustOutlierCloud 1746-1757, publishCloudsLast 1759-1815, and the IMU
+// path: imuHandler 459-486, AccumulateIMUShiftAndRotation 417-457,
+// VeloToStartIMU 349-365, TransformToStartIMU 367-392, updateInitialGuess
+// 1639-1664.  Without IMU messages (imuPointerLast = -1) every imu* quantity
+// stays at its initial value exactly as in the reference.
 // Persistent per-scan arrays (cloudCurvature, cloudNeighborPicked, cloudLabel,
 // cloudSmoothness) keep their stale contents across scans (Appendix A Q5).
 #pragma once
 
 #include "oracle_ip.h"
+#include "oracle_tf.h"
 
 namespace oracle {
 
 struct Smooth { float value; size_t ind; };
+
+// sensor_msgs/Imu as imuHandler reads it (the layout of slo_imu_msg)
+struct ImuMsg { double stamp, qx, qy, qz, qw, ax, ay, az, wx, wy, wz; };
+constexpr int imuQueLength = 200;   // utility.h:113
 
 struct FeatureAssociation {
     slo_config cfg;
@@ -41,13 +48,33 @@ struct FeatureAssociation {
     std::vector<float> pointSearchSurfInd1, pointSearchSurfInd2, pointSearchSurfInd3;
     bool isDegenerate = false;
     float matP[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};
-    // imu quantities (all remain 0: imuPointerLast == -1)
+    // imu quantities (initializationValue, FA:249-295)
+    double timeScanCur = 0;
+    int imuPointerFront = 0, imuPointerLast = -1, imuPointerLastIteration = 0;
     float imuRollStart = 0, imuPitchStart = 0, imuYawStart = 0;
     float cosImuRollStart = 0, cosImuPitchStart = 0, cosImuYawStart = 0;
     float sinImuRollStart = 0, sinImuPitchStart = 0, sinImuYawStart = 0;
     float imuRollCur = 0, imuPitchCur = 0, imuYawCur = 0;
+    float imuVeloXStart = 0, imuVeloYStart = 0, imuVeloZStart = 0;
+    float imuShiftXStart = 0, imuShiftYStart = 0, imuShiftZStart = 0;
+    float imuVeloXCur = 0, imuVeloYCur = 0, imuVeloZCur = 0;
+    float imuShiftXCur = 0, imuShiftYCur = 0, imuShiftZCur = 0;
+    float imuShiftFromStartXCur = 0, imuShiftFromStartYCur = 0, imuShiftFromStartZCur = 0;
+    float imuVeloFromStartXCur = 0, imuVeloFromStartYCur = 0, imuVeloFromStartZCur = 0;
+    float imuAngularRotationXCur = 0, imuAngularRotationYCur = 0, imuAngularRotationZCur = 0;
+    float imuAngularRotationXLast = 0, imuAngularRotationYLast = 0, imuAngularRotationZLast = 0;
+    float imuAngularFromStartX = 0, imuAngularFromStartY = 0, imuAngularFromStartZ = 0;
+    double imuTime[imuQueLength] = {};
+    float imuRoll[imuQueLength] = {}, imuPitch[imuQueLength] = {}, imuYaw[imuQueLength] = {};
+    float imuAccX[imuQueLength] = {}, imuAccY[imuQueLength] = {}, imuAccZ[imuQueLength] = {};
+    float imuVeloX[imuQueLength] = {}, imuVeloY[imuQueLength] = {}, imuVeloZ[imuQueLength] = {};
+    float imuShiftX[imuQueLength] = {}, imuShiftY[imuQueLength] = {}, imuShiftZ[imuQueLength] = {};
+    float imuAngularVeloX[imuQueLength] = {}, imuAngularVeloY[imuQueLength] = {}, imuAngularVeloZ[imuQueLength] = {};
+    float imuAngularRotationX[imuQueLength] = {}, imuAngularRotationY[imuQueLength] = {},
+          imuAngularRotationZ[imuQueLength] = {};
     float imuRollLast = 0, imuPitchLast = 0, imuYawLast = 0;
     float imuShiftFromStartX = 0, imuShiftFromStartY = 0, imuShiftFromStartZ = 0;
+    float imuVeloFromStartX = 0, imuVeloFromStartY = 0, imuVeloFromStartZ = 0;
     // outputs of the last scan
     bool published_to_mapping = false;
     int iters_surf = 0, iters_corner = 0;
@@ -61,6 +88,103 @@ struct FeatureAssociation {
         pointSearchCornerInd1.assign(H, 0); pointSearchCornerInd2.assign(H, 0);
         pointSearchSurfInd1.assign(H, 0); pointSearchSurfInd2.assign(H, 0); pointSearchSurfInd3.assign(H, 0);
         frameCount = cfg.skip_frame_num;
+    }
+
+    // ------------------------------------------------------------ IMU
+    void updateImuRollPitchYawStartSinCos() {
+        using namespace slo_libm;
+        cosImuRollStart = cosf_(imuRollStart); cosImuPitchStart = cosf_(imuPitchStart); cosImuYawStart = cosf_(imuYawStart);
+        sinImuRollStart = sinf_(imuRollStart); sinImuPitchStart = sinf_(imuPitchStart); sinImuYawStart = sinf_(imuYawStart);
+    }
+
+    void VeloToStartIMU() {
+        imuVeloFromStartXCur = imuVeloXCur - imuVeloXStart;
+        imuVeloFromStartYCur = imuVeloYCur - imuVeloYStart;
+        imuVeloFromStartZCur = imuVeloZCur - imuVeloZStart;
+        float x1 = cosImuYawStart * imuVeloFromStartXCur - sinImuYawStart * imuVeloFromStartZCur;
+        float y1 = imuVeloFromStartYCur;
+        float z1 = sinImuYawStart * imuVeloFromStartXCur + cosImuYawStart * imuVeloFromStartZCur;
+        float x2 = x1;
+        float y2 = cosImuPitchStart * y1 + sinImuPitchStart * z1;
+        float z2 = -sinImuPitchStart * y1 + cosImuPitchStart * z1;
+        imuVeloFromStartXCur = cosImuRollStart * x2 + sinImuRollStart * y2;
+        imuVeloFromStartYCur = -sinImuRollStart * x2 + cosImuRollStart * y2;
+        imuVeloFromStartZCur = z2;
+    }
+
+    void TransformToStartIMU(Pt* p) {
+        using namespace slo_libm;
+        float x1 = cosf_(imuRollCur) * p->x - sinf_(imuRollCur) * p->y;
+        float y1 = sinf_(imuRollCur) * p->x + cosf_(imuRollCur) * p->y;
+        float z1 = p->z;
+        float x2 = x1;
+        float y2 = cosf_(imuPitchCur) * y1 - sinf_(imuPitchCur) * z1;
+        float z2 = sinf_(imuPitchCur) * y1 + cosf_(imuPitchCur) * z1;
+        float x3 = cosf_(imuYawCur) * x2 + sinf_(imuYawCur) * z2;
+        float y3 = y2;
+        float z3 = -sinf_(imuYawCur) * x2 + cosf_(imuYawCur) * z2;
+        float x4 = cosImuYawStart * x3 - sinImuYawStart * z3;
+        float y4 = y3;
+        float z4 = sinImuYawStart * x3 + cosImuYawStart * z3;
+        float x5 = x4;
+        float y5 = cosImuPitchStart * y4 + sinImuPitchStart * z4;
+        float z5 = -sinImuPitchStart * y4 + cosImuPitchStart * z4;
+        p->x = cosImuRollStart * x5 + sinImuRollStart * y5 + imuShiftFromStartXCur;
+        p->y = -sinImuRollStart * x5 + cosImuRollStart * y5 + imuShiftFromStartYCur;
+        p->z = z5 + imuShiftFromStartZCur;
+    }
+
+    void AccumulateIMUShiftAndRotation() {
+        using namespace slo_libm;
+        float roll = imuRoll[imuPointerLast];
+        float pitch = imuPitch[imuPointerLast];
+        float yaw = imuYaw[imuPointerLast];
+        float accX = imuAccX[imuPointerLast];
+        float accY = imuAccY[imuPointerLast];
+        float accZ = imuAccZ[imuPointerLast];
+        float x1 = cosf_(roll) * accX - sinf_(roll) * accY;
+        float y1 = sinf_(roll) * accX + cosf_(roll) * accY;
+        float z1 = accZ;
+        float x2 = x1;
+        float y2 = cosf_(pitch) * y1 - sinf_(pitch) * z1;
+        float z2 = sinf_(pitch) * y1 + cosf_(pitch) * z1;
+        accX = cosf_(yaw) * x2 + sinf_(yaw) * z2;
+        accY = y2;
+        accZ = -sinf_(yaw) * x2 + cosf_(yaw) * z2;
+        int imuPointerBack = (imuPointerLast + imuQueLength - 1) % imuQueLength;
+        double timeDiff = imuTime[imuPointerLast] - imuTime[imuPointerBack];
+        if (timeDiff < cfg.scan_period) {
+            imuShiftX[imuPointerLast] = imuShiftX[imuPointerBack] + imuVeloX[imuPointerBack] * timeDiff + accX * timeDiff * timeDiff / 2;
+            imuShiftY[imuPointerLast] = imuShiftY[imuPointerBack] + imuVeloY[imuPointerBack] * timeDiff + accY * timeDiff * timeDiff / 2;
+            imuShiftZ[imuPointerLast] = imuShiftZ[imuPointerBack] + imuVeloZ[imuPointerBack] * timeDiff + accZ * timeDiff * timeDiff / 2;
+            imuVeloX[imuPointerLast] = imuVeloX[imuPointerBack] + accX * timeDiff;
+            imuVeloY[imuPointerLast] = imuVeloY[imuPointerBack] + accY * timeDiff;
+            imuVeloZ[imuPointerLast] = imuVeloZ[imuPointerBack] + accZ * timeDiff;
+            imuAngularRotationX[imuPointerLast] = imuAngularRotationX[imuPointerBack] + imuAngularVeloX[imuPointerBack] * timeDiff;
+            imuAngularRotationY[imuPointerLast] = imuAngularRotationY[imuPointerBack] + imuAngularVeloY[imuPointerBack] * timeDiff;
+            imuAngularRotationZ[imuPointerLast] = imuAngularRotationZ[imuPointerBack] + imuAngularVeloZ[imuPointerBack] * timeDiff;
+        }
+    }
+
+    void imuHandler(const ImuMsg& imuIn) {
+        using namespace slo_libm;
+        double roll, pitch, yaw;
+        tf_get_rpy(TfQuat{imuIn.qx, imuIn.qy, imuIn.qz, imuIn.qw}, roll, pitch, yaw);
+        float accX = imuIn.ay - sin_d(roll) * cos_d(pitch) * 9.81;
+        float accY = imuIn.az - cos_d(roll) * cos_d(pitch) * 9.81;
+        float accZ = imuIn.ax + sin_d(pitch) * 9.81;
+        imuPointerLast = (imuPointerLast + 1) % imuQueLength;
+        imuTime[imuPointerLast] = imuIn.stamp;
+        imuRoll[imuPointerLast] = roll;
+        imuPitch[imuPointerLast] = pitch;
+        imuYaw[imuPointerLast] = yaw;
+        imuAccX[imuPointerLast] = accX;
+        imuAccY[imuPointerLast] = accY;
+        imuAccZ[imuPointerLast] = accZ;
+        imuAngularVeloX[imuPointerLast] = imuIn.wx;
+        imuAngularVeloY[imuPointerLast] = imuIn.wy;
+        imuAngularVeloZ[imuPointerLast] = imuIn.wz;
+        AccumulateIMUShiftAndRotation();
     }
 
     // ------------------------------------------------------------ features
@@ -84,8 +208,84 @@ struct FeatureAssociation {
             }
             float relTime = (ori - segInfo.startOrientation) / segInfo.orientationDiff;
             point.intensity = (float)(int)segmentedCloud[i].intensity + cfg.scan_period * relTime;
+            if (imuPointerLast >= 0) {
+                float pointTime = relTime * cfg.scan_period;
+                imuPointerFront = imuPointerLastIteration;
+                while (imuPointerFront != imuPointerLast) {
+                    if (timeScanCur + pointTime < imuTime[imuPointerFront]) break;
+                    imuPointerFront = (imuPointerFront + 1) % imuQueLength;
+                }
+                if (timeScanCur + pointTime > imuTime[imuPointerFront]) {
+                    imuRollCur = imuRoll[imuPointerFront];
+                    imuPitchCur = imuPitch[imuPointerFront];
+                    imuYawCur = imuYaw[imuPointerFront];
+                    imuVeloXCur = imuVeloX[imuPointerFront];
+                    imuVeloYCur = imuVeloY[imuPointerFront];
+                    imuVeloZCur = imuVeloZ[imuPointerFront];
+                    imuShiftXCur = imuShiftX[imuPointerFront];
+                    imuShiftYCur = imuShiftY[imuPointerFront];
+                    imuShiftZCur = imuShiftZ[imuPointerFront];
+                } else {
+                    int imuPointerBack = (imuPointerFront + imuQueLength - 1) % imuQueLength;
+                    float ratioFront = (timeScanCur + pointTime - imuTime[imuPointerBack]) /
+                                       (imuTime[imuPointerFront] - imuTime[imuPointerBack]);
+                    float ratioBack = (imuTime[imuPointerFront] - timeScanCur - pointTime) /
+                                      (imuTime[imuPointerFront] - imuTime[imuPointerBack]);
+                    imuRollCur = imuRoll[imuPointerFront] * ratioFront + imuRoll[imuPointerBack] * ratioBack;
+                    imuPitchCur = imuPitch[imuPointerFront] * ratioFront + imuPitch[imuPointerBack] * ratioBack;
+                    if (imuYaw[imuPointerFront] - imuYaw[imuPointerBack] > M_PI) {
+                        imuYawCur = imuYaw[imuPointerFront] * ratioFront + (imuYaw[imuPointerBack] + 2 * M_PI) * ratioBack;
+                    } else if (imuYaw[imuPointerFront] - imuYaw[imuPointerBack] < -M_PI) {
+                        imuYawCur = imuYaw[imuPointerFront] * ratioFront + (imuYaw[imuPointerBack] - 2 * M_PI) * ratioBack;
+                    } else {
+                        imuYawCur = imuYaw[imuPointerFront] * ratioFront + imuYaw[imuPointerBack] * ratioBack;
+                    }
+                    imuVeloXCur = imuVeloX[imuPointerFront] * ratioFront + imuVeloX[imuPointerBack] * ratioBack;
+                    imuVeloYCur = imuVeloY[imuPointerFront] * ratioFront + imuVeloY[imuPointerBack] * ratioBack;
+                    imuVeloZCur = imuVeloZ[imuPointerFront] * ratioFront + imuVeloZ[imuPointerBack] * ratioBack;
+                    imuShiftXCur = imuShiftX[imuPointerFront] * ratioFront + imuShiftX[imuPointerBack] * ratioBack;
+                    imuShiftYCur = imuShiftY[imuPointerFront] * ratioFront + imuShiftY[imuPointerBack] * ratioBack;
+                    imuShiftZCur = imuShiftZ[imuPointerFront] * ratioFront + imuShiftZ[imuPointerBack] * ratioBack;
+                }
+                if (i == 0) {
+                    imuRollStart = imuRollCur;
+                    imuPitchStart = imuPitchCur;
+                    imuYawStart = imuYawCur;
+                    imuVeloXStart = imuVeloXCur;
+                    imuVeloYStart = imuVeloYCur;
+                    imuVeloZStart = imuVeloZCur;
+                    imuShiftXStart = imuShiftXCur;
+                    imuShiftYStart = imuShiftYCur;
+                    imuShiftZStart = imuShiftZCur;
+                    if (timeScanCur + pointTime > imuTime[imuPointerFront]) {
+                        imuAngularRotationXCur = imuAngularRotationX[imuPointerFront];
+                        imuAngularRotationYCur = imuAngularRotationY[imuPointerFront];
+                        imuAngularRotationZCur = imuAngularRotationZ[imuPointerFront];
+                    } else {
+                        int imuPointerBack = (imuPointerFront + imuQueLength - 1) % imuQueLength;
+                        float ratioFront = (timeScanCur + pointTime - imuTime[imuPointerBack]) /
+                                           (imuTime[imuPointerFront] - imuTime[imuPointerBack]);
+                        float ratioBack = (imuTime[imuPointerFront] - timeScanCur - pointTime) /
+                                          (imuTime[imuPointerFront] - imuTime[imuPointerBack]);
+                        imuAngularRotationXCur = imuAngularRotationX[imuPointerFront] * ratioFront + imuAngularRotationX[imuPointerBack] * ratioBack;
+                        imuAngularRotationYCur = imuAngularRotationY[imuPointerFront] * ratioFront + imuAngularRotationY[imuPointerBack] * ratioBack;
+                        imuAngularRotationZCur = imuAngularRotationZ[imuPointerFront] * ratioFront + imuAngularRotationZ[imuPointerBack] * ratioBack;
+                    }
+                    imuAngularFromStartX = imuAngularRotationXCur - imuAngularRotationXLast;
+                    imuAngularFromStartY = imuAngularRotationYCur - imuAngularRotationYLast;
+                    imuAngularFromStartZ = imuAngularRotationZCur - imuAngularRotationZLast;
+                    imuAngularRotationXLast = imuAngularRotationXCur;
+                    imuAngularRotationYLast = imuAngularRotationYCur;
+                    imuAngularRotationZLast = imuAngularRotationZCur;
+                    updateImuRollPitchYawStartSinCos();
+                } else {
+                    VeloToStartIMU();
+                    TransformToStartIMU(&point);
+                }
+            }
             segmentedCloud[i] = point;
         }
+        imuPointerLastIteration = imuPointerLast;
     }
 
     void calculateSmoothness() {
@@ -596,12 +796,6 @@ struct FeatureAssociation {
         transformSum[3] = tx; transformSum[4] = ty; transformSum[5] = tz;
     }
 
-    void updateImuRollPitchYawStartSinCos() {
-        using namespace slo_libm;
-        cosImuRollStart = cosf_(imuRollStart); cosImuPitchStart = cosf_(imuPitchStart); cosImuYawStart = cosf_(imuYawStart);
-        sinImuRollStart = sinf_(imuRollStart); sinImuPitchStart = sinf_(imuPitchStart); sinImuYawStart = sinf_(imuYawStart);
-    }
-
     void publishCloudsLast() {
         updateImuRollPitchYawStartSinCos();
         for (auto& p : cornerPointsLessSharp) TransformToEnd(p, p);
@@ -635,8 +829,32 @@ struct FeatureAssociation {
         systemInitedLM = true;
     }
 
-    // runFeatureAssociation (FA:1817-1860) on one segmented scan.
-    void run(const Cloud& seg, const SegInfo& info, const Cloud& outlier) {
+    void updateInitialGuess() {
+        imuPitchLast = imuPitchCur;
+        imuYawLast = imuYawCur;
+        imuRollLast = imuRollCur;
+        imuShiftFromStartX = imuShiftFromStartXCur;
+        imuShiftFromStartY = imuShiftFromStartYCur;
+        imuShiftFromStartZ = imuShiftFromStartZCur;
+        imuVeloFromStartX = imuVeloFromStartXCur;
+        imuVeloFromStartY = imuVeloFromStartYCur;
+        imuVeloFromStartZ = imuVeloFromStartZCur;
+        if (imuAngularFromStartX != 0 || imuAngularFromStartY != 0 || imuAngularFromStartZ != 0) {
+            transformCur[0] = -imuAngularFromStartY;
+            transformCur[1] = -imuAngularFromStartZ;
+            transformCur[2] = -imuAngularFromStartX;
+        }
+        if (imuVeloFromStartX != 0 || imuVeloFromStartY != 0 || imuVeloFromStartZ != 0) {
+            transformCur[3] -= imuVeloFromStartX * cfg.scan_period;
+            transformCur[4] -= imuVeloFromStartY * cfg.scan_period;
+            transformCur[5] -= imuVeloFromStartZ * cfg.scan_period;
+        }
+    }
+
+    // runFeatureAssociation (FA:1817-1860) on one segmented scan stamped t
+    // (cloudHeader.stamp: read only by the IMU path)
+    void run(const Cloud& seg, const SegInfo& info, const Cloud& outlier, double t) {
+        timeScanCur = t;
         segmentedCloud = seg;
         segInfo = info;
         outlierCloud = outlier;
@@ -649,7 +867,7 @@ struct FeatureAssociation {
             checkSystemInitialization();
             return;
         }
-        // updateInitialGuess (FA:1639-1664): every imu term is 0 -> no change
+        updateInitialGuess();
         updateTransformation();
         integrateTransformation();
         publishCloudsLast();

@@ -95,6 +95,7 @@ def lib():
         L.oracle_umeyama.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
         L.oracle_svd3.argtypes = [ctypes.c_void_p] * 4
         L.oracle_set_rings.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+        L.oracle_imu.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_pose_roundtrip.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_step_map.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         L.oracle_step_loop.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
@@ -144,6 +145,7 @@ LOOP_DTYPE = np.dtype([("id", "<i4"), ("ran", "<i4"), ("converged", "<i4"), ("ac
                        ("T", "<f4", (16,)), ("xyzrpy", "<f4", (6,))])
 assert LOOP_DTYPE.itemsize == 128
 _DTYPES["loop"] = LOOP_DTYPE
+_DTYPES["imu"] = np.float64
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
            "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"}
 
@@ -241,6 +243,12 @@ class OracleStream:
     def step(self, pts, t):
         pts = np.ascontiguousarray(pts, np.float32)
         return lib().oracle_step(self.h, pts.ctypes.data, len(pts), float(t))
+
+    def imu(self, msgs):
+        """FeatureAssociation::imuHandler on each message, in order: msgs = (n, 11) float64
+        (stamp, qx, qy, qz, qw, ax, ay, az, wx, wy, wz)"""
+        m = np.ascontiguousarray(msgs, np.float64).reshape(-1, 11)
+        lib().oracle_imu(self.h, m.ctypes.data, len(m))
 
     def step_map(self, pts, t):
         """the nodes up to mapOptimization::run: flags 1, 2, 4"""

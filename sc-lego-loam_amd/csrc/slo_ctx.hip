@@ -71,14 +71,24 @@ static void timing_flush(slo_ctx* ctx) {
     ctx->pending.clear();
 }
 
-__global__ void k_set_io(SloIo* io, const float4* pts, const int32_t* npts) {
-    io->pts = pts;
-    io->npts = npts;
+// what = 1: the scan's points, 2: its stamp, 3: both
+__global__ void k_set_io(SloIo* io, const float4* pts, const int32_t* npts, double t_scan, int what) {
+    if (what & 1) {
+        io->pts = pts;
+        io->npts = npts;
+    }
+    if (what & 2) io->t_scan = t_scan;
 }
 
 // the scan the following launches read (DevView::io), in stream order
 static int set_io(slo_ctx* ctx, const void* pts, const int32_t* npts) {
-    hipLaunchKernelGGL(k_set_io, dim3(1), dim3(1), 0, ctx->stream, ctx->d_io, (const float4*)pts, npts);
+    hipLaunchKernelGGL(k_set_io, dim3(1), dim3(1), 0, ctx->stream, ctx->d_io, (const float4*)pts, npts, 0.0, 1);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+static int set_io_time(slo_ctx* ctx, const void* pts, const int32_t* npts, double t_scan, int what) {
+    hipLaunchKernelGGL(k_set_io, dim3(1), dim3(1), 0, ctx->stream, ctx->d_io, (const float4*)pts, npts, t_scan,
+                       what);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
@@ -213,6 +223,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.ind_corner, S * v.cap_sharp * 2);
     c.add(&v.st, S);
     c.add(&ctx->d_io, 1);
+    c.add(&v.imu, S);
     // ---- mapping + Scan Context history
     // Capacities are worst-case bounds, so no cloud is ever clipped: a
     // VoxelGrid output is no larger than its input, the surf DS of a scan is
@@ -305,6 +316,10 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     }
     ctx->stamp_khz = khz;
     ctx->pp_corner0 = v.corner_last;
+    if (slo::imu_init(ctx) || hipStreamSynchronize(ctx->stream) != hipSuccess) {
+        slo_destroy(ctx);
+        return SLO_E_HIP;
+    }
     v.g_os = slo::grid_view(ctx->grid_os);
     v.g_mc = slo::grid_view(ctx->grid_c);
     v.g_ms = slo::grid_view(ctx->grid_s);
@@ -345,6 +360,12 @@ int slo_batch_set_rings(slo_ctx* ctx, const uint16_t* d_rings) {
     if (ctx->v.rings != d_rings) slo::graphs_drop(ctx);   // the captured launches carry the old pointer
     ctx->v.rings = d_rings;
     return SLO_OK;
+}
+
+int slo_batch_scan_time(slo_ctx* ctx, double t_scan) {
+    if (!ctx) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::set_io_time(ctx, nullptr, nullptr, t_scan, 2);
 }
 
 int slo_graph_mode(slo_ctx* ctx, int on) {
@@ -481,7 +502,7 @@ static int step_graph(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     fa_advance(ctx, false);
     const bool map = map_gate(ctx, t_scan);
     const int kind = map ? 1 : 0, key = 2 * kind + (ctx->v.corner_last == ctx->pp_corner0 ? 0 : 1);
-    if (int r = set_io(ctx, d_points, d_counts)) return r;
+    if (int r = set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     if (ctx->graph_exec[key] && (ctx->graph_ws[key] != ctx->ws_gen ||
                                  memcmp(&ctx->graph_v[key], &ctx->v, sizeof(DevView)) != 0)) {
         hipGraphExecDestroy(ctx->graph_exec[key]);   // its arguments are stale: capture again
@@ -537,6 +558,7 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     }
     int r = slo::step_graph(ctx, d_points, d_counts, t_scan);
     if (r <= 0) return r;
+    if ((r = slo_batch_scan_time(ctx, t_scan))) return r;
     r = slo_batch_image_projection(ctx, d_points, d_counts);
     if (r) return r;
     r = slo_batch_feature_association(ctx);
@@ -643,6 +665,16 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
+    else if (name == "imu") {   // FA's IMU scalars (slo::ImuState), as float64
+        slo::ImuState m;
+        SLO_CHECK(hipMemcpy(&m, v.imu + stream, sizeof(m), hipMemcpyDeviceToHost));
+        const double a[23] = {(double)m.last, (double)m.last_iter, m.rollStart, m.pitchStart, m.yawStart,
+                              m.veloStart[0], m.veloStart[1], m.veloStart[2], m.rollCur, m.pitchCur, m.yawCur,
+                              m.veloFromStartCur[0], m.veloFromStartCur[1], m.veloFromStartCur[2], m.angLast[0],
+                              m.angLast[1], m.angLast[2], m.angFromStart[0], m.angFromStart[1], m.angFromStart[2],
+                              m.rollLast, m.pitchLast, m.yawLast};
+        tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 23; esz = 8;
+    }
     else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
     else if (name == "map_raw_n") {   // laserCloudCornerFromMap / laserCloudSurfFromMap sizes before their VoxelGrids
         int32_t a[2] = {st.n_corner_map, st.n_surf_map}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
@@ -824,10 +856,10 @@ int slo_image_projection(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
 // (start of sweep); less_sharp/less_flat are laserCloudCornerLast /
 // laserCloudSurfLast after TransformToEnd (what FA publishes, FA:1790-1814).
 int slo_feature_association(slo_ctx* ctx, double t_scan, slo_fa_view* out) {
-    (void)t_scan;  // the non-IMU path never reads the stamp (Q13)
     if (!ctx || !out) return SLO_E_ARG;
     int r = single_stream(ctx);
     if (r) return r;
+    if ((r = slo_batch_scan_time(ctx, t_scan))) return r;   // cloudHeader.stamp: read by the IMU path only (Q13)
     r = slo_batch_feature_association(ctx);
     if (r) return r;
     memset(out, 0, sizeof(*out));

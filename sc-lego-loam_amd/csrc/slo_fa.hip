@@ -22,6 +22,7 @@
 #include "slo_internal.h"
 #include "slo_libm.h"
 #include "slo_introsort.h"
+#include "slo_imu.h"
 #include <float.h>
 
 namespace slo {
@@ -53,6 +54,35 @@ __global__ void k_fa_halfpass(DevView v) {
     if ((threadIdx.x & 63) == 0 && hit != INT_MAX) atomicMin(&v.st[s].first_half, hit);
 }
 
+// adjustDistortion's IMU state for the scan (FA:525-616), one lane per
+// stream: the first point's IMU values become the scan's start (rpy,
+// velocity; the angular rotation since the last scan), and the ring position
+// the deskew starts from is latched before imuPointerLastIteration moves on
+// (FA:616).  The other points are deskewed in k_fa_points.
+__global__ void k_fa_imu_start(DevView v) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    ImuState& m = v.imu[s];
+    m.iter_scan = m.last_iter;
+    if (m.last >= 0 && v.st[s].seg_count > 0) {
+        const float4 q = v.seg[(size_t)s * v.H];
+        const float start = v.orient[3 * s], diff = v.orient[3 * s + 2];
+        const float ori = ori_first_half(-slo_libm::atan2f_(q.y, q.x), start);   // point 0: first half
+        const float relTime = (ori - start) / diff;
+        const float pointTime = relTime * v.cfg.scan_period;
+        const slo_imu::ImuAt c = slo_imu::imu_at(m, m.iter_scan, v.io->t_scan, pointTime);
+        m.rollStart = m.rollCur = c.roll;
+        m.pitchStart = m.pitchCur = c.pitch;
+        m.yawStart = m.yawCur = c.yaw;
+        for (int k = 0; k < 3; ++k) {
+            m.veloStart[k] = c.velo[k];
+            m.angFromStart[k] = c.ang[k] - m.angLast[k];
+            m.angLast[k] = c.ang[k];
+        }
+    }
+    m.last_iter = m.last;
+}
+
 // deskew + curvature + occlusion marks, one thread per position
 __global__ void k_fa_points(DevView v) {
     const int s = blockIdx.y;
@@ -74,7 +104,21 @@ __global__ void k_fa_points(DevView v) {
             else if (ori > end + M_PI / 2) ori = (float)(ori - 2 * M_PI);
         }
         float relTime = (ori - start) / diff;
-        v.fpts[base + p] = make_float4(px, py, pz, (float)(int)q.w + v.cfg.scan_period * relTime);
+        const float intensity = (float)(int)q.w + v.cfg.scan_period * relTime;
+        ImuState& m = v.imu[s];
+        if (m.last >= 0 && p > 0) {   // VeloToStartIMU + TransformToStartIMU (FA:609-612)
+            const float pointTime = relTime * v.cfg.scan_period;
+            const slo_imu::ImuAt c = slo_imu::imu_at(m, m.iter_scan, v.io->t_scan, pointTime);
+            const slo_imu::ImuStartTrig t = slo_imu::start_trig(m.rollStart, m.pitchStart, m.yawStart);
+            if (p == S - 1) {   // the imu*Cur the scan leaves behind (updateInitialGuess reads them)
+                slo_imu::imu_velo_to_start(c.velo, m.veloStart, t, m.veloFromStartCur);
+                m.rollCur = c.roll;
+                m.pitchCur = c.pitch;
+                m.yawCur = c.yaw;
+            }
+            slo_imu::imu_to_start(px, py, pz, c, t);
+        }
+        v.fpts[base + p] = make_float4(px, py, pz, intensity);
     }
     const float* r = v.seg_range + base;
     const uint32_t* col = v.seg_col + base;
@@ -804,6 +848,7 @@ int fa_features_run(slo_ctx* ctx) {
     const int T = 256;
     dim3 gh((v.H + T - 1) / T, S);
     SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
+    SLO_LAUNCH(ctx, "fa_imu_start", k_fa_imu_start, dim3((S + 63) / 64), dim3(64), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);

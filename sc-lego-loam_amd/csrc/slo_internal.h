@@ -35,7 +35,33 @@ struct alignas(8) Smooth { float value; int32_t ind; };
 // counts), kept in device memory and set by k_set_io at the start of each
 // call: kernels read it there, so a captured HIP graph replays on whatever
 // buffers the next call names.
-struct SloIo { const float4* pts; const int32_t* npts; };
+struct SloIo { const float4* pts; const int32_t* npts; double t_scan; };
+
+// FeatureAssociation's IMU state of one stream (featureAssociation.cpp:85-158,
+// imuQueLength = 200, utility.h:113): the ring of imuHandler messages with the
+// shift / velocity / rotation AccumulateIMUShiftAndRotation integrates, and
+// the per-scan quantities adjustDistortion, updateInitialGuess,
+// TransformToEnd and integrateTransformation exchange.  imuShiftFromStart*Cur
+// stays 0: LeGO-LOAM never calls ShiftToStartIMU, so the shift terms are the
+// zero the constructor sets (kept literally).
+#define SLO_IMU_QUE 200
+struct ImuState {
+    int32_t last;                       // imuPointerLast (-1: no message yet)
+    int32_t last_iter;                  // imuPointerLastIteration
+    int32_t iter_scan;                  // the value this scan's deskew starts from
+    int32_t pad;
+    float rollStart, pitchStart, yawStart;
+    float veloStart[3];
+    float rollCur, pitchCur, yawCur;    // the last deskewed point's (imu*Cur after adjustDistortion)
+    float veloFromStartCur[3];
+    float angLast[3], angFromStart[3];  // imuAngularRotation*Last, imuAngularFromStart*
+    float rollLast, pitchLast, yawLast; // updateInitialGuess
+    float shiftFromStart[3], veloFromStart[3];
+    double time[SLO_IMU_QUE];
+    float roll[SLO_IMU_QUE], pitch[SLO_IMU_QUE], yaw[SLO_IMU_QUE];
+    float acc[3][SLO_IMU_QUE], velo[3][SLO_IMU_QUE], shift[3][SLO_IMU_QUE];
+    float angVelo[3][SLO_IMU_QUE], angRot[3][SLO_IMU_QUE];
+};
 
 // Per-stream scalar state of the FA / MO nodes (one record per stream).
 struct StreamState {
@@ -164,6 +190,7 @@ struct DevView {
     int32_t* ind_surf;   // [S][cap_flat][3]   pointSearchSurfInd1..3 (Q9: exact ints)
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
     StreamState* st;     // [S]
+    ImuState* imu;       // [S] (slo_batch_imu / slo_imu_handler)
     // ---- mapping (mapOptmization.cpp)
     int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
     int KFMAX;           // keyframe pose / Scan Context history capacity
@@ -516,6 +543,7 @@ void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx);
 void graphs_drop(slo_ctx* ctx);
+int imu_init(slo_ctx* ctx);
 int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams);
 int sc_detect_run(slo_ctx* ctx);
 int sc_detect_run_one(slo_ctx* ctx);

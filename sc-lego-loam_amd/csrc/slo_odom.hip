@@ -187,10 +187,33 @@ __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan)
             st.kdCornerNum = nLS; st.kdSurfNum = nLF;
             st.iters_surf = st.iters_corner = 0;
             st.odo_phase = 3;
+            st.transformSum[0] += v.imu[s].pitchStart;   // FA:1633-1634
+            st.transformSum[2] += v.imu[s].rollStart;
         }
         return;
     }
-    if (tid == 0) {  // updateTransformation (FA:1666-1672)
+    if (tid == 0) {
+        // updateInitialGuess (FA:1639-1664)
+        ImuState& m = v.imu[s];
+        m.pitchLast = m.pitchCur;
+        m.yawLast = m.yawCur;
+        m.rollLast = m.rollCur;
+        for (int k = 0; k < 3; ++k) {
+            m.shiftFromStart[k] = 0.0f;   // imuShiftFromStart*Cur: never set (no ShiftToStartIMU call)
+            m.veloFromStart[k] = m.veloFromStartCur[k];
+        }
+        float* tcur = st.transformCur;
+        if (m.angFromStart[0] != 0 || m.angFromStart[1] != 0 || m.angFromStart[2] != 0) {
+            tcur[0] = -m.angFromStart[1];
+            tcur[1] = -m.angFromStart[2];
+            tcur[2] = -m.angFromStart[0];
+        }
+        if (m.veloFromStart[0] != 0 || m.veloFromStart[1] != 0 || m.veloFromStart[2] != 0) {
+            tcur[3] -= m.veloFromStart[0] * v.cfg.scan_period;
+            tcur[4] -= m.veloFromStart[1] * v.cfg.scan_period;
+            tcur[5] -= m.veloFromStart[2] * v.cfg.scan_period;
+        }
+        // updateTransformation (FA:1666-1672)
         st.iters_surf = st.iters_corner = 0;
         st.odo_phase = (st.cornerLastNum < 10 || st.surfLastNum < 100) ? 2 : 0;
     }
@@ -783,9 +806,16 @@ __global__ void __launch_bounds__(256) k_fa_to_end(DevView v) {
     const StreamState& st = v.st[s];
     if (st.odo_phase == 3) return;
     __shared__ float tc[6], tct[6];
+    __shared__ slo_pose::ImuEnd im;
     if (threadIdx.x < 6) tc[threadIdx.x] = st.transformCur[threadIdx.x];
     __syncthreads();
-    if (threadIdx.x == 0) slo_pose::tc_trig(tc, tct);
+    if (threadIdx.x == 0) {
+        slo_pose::tc_trig(tc, tct);
+        // publishCloudsLast: updateImuRollPitchYawStartSinCos, then TransformToEnd (FA:1759-1771)
+        const ImuState& m = v.imu[s];
+        im = slo_pose::imu_end(m.rollStart, m.pitchStart, m.yawStart, m.shiftFromStart, m.yawLast, m.pitchLast,
+                               m.rollLast);
+    }
     __syncthreads();
     const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
     const bool rebuild = nLS > 10 && nLF > 100;
@@ -798,7 +828,7 @@ __global__ void __launch_bounds__(256) k_fa_to_end(DevView v) {
     for (int i = chunk * blockDim.x + threadIdx.x; i < nLS + nLF; i += SLO_TOEND_BLOCKS * blockDim.x) {
         const bool corner = i < nLS;
         const int k = corner ? i : i - nLS;
-        const P4 q = slo_pose::transform_to_end(ld4(corner ? lsharp : lflat, k), tc, tct);
+        const P4 q = slo_pose::transform_to_end(ld4(corner ? lsharp : lflat, k), tc, tct, im);
         const float4 o = make_float4(q.x, q.y, q.z, q.w);
         (corner ? cnext : snext)[k] = o;
         if (rebuild) (corner ? kdc : kds)[k] = o;
@@ -814,7 +844,10 @@ __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
     if (threadIdx.x == 0) {
         float tc[6];
         for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-        slo_pose::integrate(st.transformSum, tc);
+        const ImuState& m = v.imu[s];
+        const float imu[9] = {m.shiftFromStart[0], m.shiftFromStart[1], m.shiftFromStart[2], m.pitchStart, m.yawStart,
+                              m.rollStart, m.pitchLast, m.yawLast, m.rollLast};
+        slo_pose::integrate(st.transformSum, tc, imu);
         // TransformFusion::laserOdometryHandler (TF:186-219): this scan's
         // odometry through the tf round trip, associated to the map with the
         // last published mapping result (this scan's mapping comes after)

@@ -2,8 +2,9 @@
 // All trig through slo_libm (glibc float bits); float evaluation order as
 // in the reference expressions.
 //   transform_to_start  featureAssociation.cpp:860-883
-//   transform_to_end    featureAssociation.cpp:885-953 (IMU terms are the
-//                       reference's zero-IMU constants, kept literally: Q17)
+//   transform_to_end    featureAssociation.cpp:885-953 (the IMU terms from
+//                       ImuEnd; without an IMU they are the reference's
+//                       zero-IMU values, cos 1 / sin 0: Q17)
 //   plugin_imu_rotation featureAssociation.cpp:955-1013
 //   accumulate_rotation featureAssociation.cpp:1015-1032
 //   integrate           featureAssociation.cpp:1697-1725
@@ -52,14 +53,33 @@ SLO_P_HD P4 transform_to_start(P4 pi, const float* tc) {
     return o;
 }
 
-// imu quantities are the reference's values without an IMU: start angles 0
-// (so cos=1, sin=0 after updateImuRollPitchYawStartSinCos), shifts 0, last 0
+// The IMU terms of TransformToEnd as publishCloudsLast sees them:
+// cos/sin of the scan's start angles (updateImuRollPitchYawStartSinCos),
+// imuShiftFromStart*, and cos/sin of imu{Yaw,Pitch,Roll}Last (the reference
+// evaluates these per point; one evaluation gives the same bits).  Without an
+// IMU every angle and shift is 0.
+struct ImuEnd {
+    float cRS, cPS, cYS, sRS, sPS, sYS;   // start
+    float shx, shy, shz;                  // imuShiftFromStart
+    float cYL, sYL, cPL, sPL, cRL, sRL;   // last
+};
+SLO_P_HD ImuEnd imu_end(float rollStart, float pitchStart, float yawStart, const float* shift, float yawLast,
+                        float pitchLast, float rollLast) {
+    ImuEnd e;
+    e.cRS = cosf_(rollStart); e.cPS = cosf_(pitchStart); e.cYS = cosf_(yawStart);
+    e.sRS = sinf_(rollStart); e.sPS = sinf_(pitchStart); e.sYS = sinf_(yawStart);
+    e.shx = shift[0]; e.shy = shift[1]; e.shz = shift[2];
+    e.cYL = cosf_(yawLast); e.sYL = sinf_(yawLast);
+    e.cPL = cosf_(pitchLast); e.sPL = sinf_(pitchLast);
+    e.cRL = cosf_(rollLast); e.sRL = sinf_(rollLast);
+    return e;
+}
+
 // tct = sin/cos of tc[0..2]: {srx, crx, sry, cry, srz, crz} (sincosf_)
-SLO_P_HD P4 transform_to_end(P4 pi, const float* tc, const float* tct) {
-    const float cosImuRollStart = cosf_(0.0f), cosImuPitchStart = cosf_(0.0f), cosImuYawStart = cosf_(0.0f);
-    const float sinImuRollStart = sinf_(0.0f), sinImuPitchStart = sinf_(0.0f), sinImuYawStart = sinf_(0.0f);
-    const float imuShiftFromStartX = 0, imuShiftFromStartY = 0, imuShiftFromStartZ = 0;
-    const float imuYawLast = 0, imuPitchLast = 0, imuRollLast = 0;
+SLO_P_HD P4 transform_to_end(P4 pi, const float* tc, const float* tct, const ImuEnd& im) {
+    const float cosImuRollStart = im.cRS, cosImuPitchStart = im.cPS, cosImuYawStart = im.cYS;
+    const float sinImuRollStart = im.sRS, sinImuPitchStart = im.sPS, sinImuYawStart = im.sYS;
+    const float imuShiftFromStartX = im.shx, imuShiftFromStartY = im.shy, imuShiftFromStartZ = im.shz;
     float s = 10 * (pi.w - (float)(int)pi.w);
     float rx = s * tc[0], ry = s * tc[1], rz = s * tc[2];
     float tx = s * tc[3], ty = s * tc[4], tz = s * tc[5];
@@ -96,15 +116,15 @@ SLO_P_HD P4 transform_to_end(P4 pi, const float* tc, const float* tct) {
     float x9 = cosImuYawStart * x8 + sinImuYawStart * z8;
     float y9 = y8;
     float z9 = -sinImuYawStart * x8 + cosImuYawStart * z8;
-    float x10 = cosf_(imuYawLast) * x9 - sinf_(imuYawLast) * z9;
+    float x10 = im.cYL * x9 - im.sYL * z9;
     float y10 = y9;
-    float z10 = sinf_(imuYawLast) * x9 + cosf_(imuYawLast) * z9;
+    float z10 = im.sYL * x9 + im.cYL * z9;
     float x11 = x10;
-    float y11 = cosf_(imuPitchLast) * y10 + sinf_(imuPitchLast) * z10;
-    float z11 = -sinf_(imuPitchLast) * y10 + cosf_(imuPitchLast) * z10;
+    float y11 = im.cPL * y10 + im.sPL * z10;
+    float z11 = -im.sPL * y10 + im.cPL * z10;
     P4 o;
-    o.x = cosf_(imuRollLast) * x11 + sinf_(imuRollLast) * y11;
-    o.y = -sinf_(imuRollLast) * x11 + cosf_(imuRollLast) * y11;
+    o.x = im.cRL * x11 + im.sRL * y11;
+    o.y = -im.sRL * x11 + im.cRL * y11;
     o.z = z11;
     o.w = (float)(int)pi.w;
     return o;
@@ -116,10 +136,10 @@ SLO_P_HD void tc_trig(const float* tc, float* tct) {
     slo_libm::sincosf_(tc[2], &tct[4], &tct[5]);
 }
 
-SLO_P_HD P4 transform_to_end(P4 pi, const float* tc) {
+SLO_P_HD P4 transform_to_end(P4 pi, const float* tc, const ImuEnd& im) {
     float tct[6];
     tc_trig(tc, tct);
-    return transform_to_end(pi, tc, tct);
+    return transform_to_end(pi, tc, tct, im);
 }
 
 SLO_P_HD void plugin_imu_rotation(float bcx, float bcy, float bcz, float blx, float bly, float blz, float alx,
@@ -162,11 +182,13 @@ SLO_P_HD void accumulate_rotation(float cx, float cy, float cz, float lx, float 
     oz = atan2f_(srzcrx / cosf_(ox), crzcrx / cosf_(ox));
 }
 
-// integrateTransformation: sum <- sum (+) cur, zero IMU
-SLO_P_HD void integrate(float* sum, const float* cur) {
+// integrateTransformation: sum <- sum (+) cur; imu = {imuShiftFromStart x, y,
+// z, imuPitchStart, imuYawStart, imuRollStart, imuPitchLast, imuYawLast,
+// imuRollLast} (all 0 without an IMU)
+SLO_P_HD void integrate(float* sum, const float* cur, const float* imu) {
     float rx, ry, rz, tx, ty, tz;
     accumulate_rotation(sum[0], sum[1], sum[2], -cur[0], -cur[1], -cur[2], rx, ry, rz);
-    const float sx = 0, sy = 0, sz = 0;  // imuShiftFromStart*
+    const float sx = imu[0], sy = imu[1], sz = imu[2];  // imuShiftFromStart*
     float x1 = cosf_(rz) * (cur[3] - sx) - sinf_(rz) * (cur[4] - sy);
     float y1 = sinf_(rz) * (cur[3] - sx) + cosf_(rz) * (cur[4] - sy);
     float z1 = cur[5] - sz;
@@ -176,7 +198,7 @@ SLO_P_HD void integrate(float* sum, const float* cur) {
     tx = sum[3] - (cosf_(ry) * x2 + sinf_(ry) * z2);
     ty = sum[4] - y2;
     tz = sum[5] - (-sinf_(ry) * x2 + cosf_(ry) * z2);
-    plugin_imu_rotation(rx, ry, rz, 0, 0, 0, 0, 0, 0, rx, ry, rz);
+    plugin_imu_rotation(rx, ry, rz, imu[3], imu[4], imu[5], imu[6], imu[7], imu[8], rx, ry, rz);
     sum[0] = rx; sum[1] = ry; sum[2] = rz;
     sum[3] = tx; sum[4] = ty; sum[5] = tz;
 }

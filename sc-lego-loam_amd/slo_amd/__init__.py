@@ -17,7 +17,7 @@ import ctypes
 import numpy as np
 
 from . import _abi
-from ._abi import SloConfig, SegView, FaView, MapView
+from ._abi import SloConfig, SegView, FaView, MapView, IMU_DTYPE
 from . import wire
 
 PRESETS = {
@@ -41,6 +41,7 @@ LOOP_DTYPE = np.dtype([("id", "<i4"), ("ran", "<i4"), ("converged", "<i4"), ("ac
                        ("T", "<f4", (16,)), ("xyzrpy", "<f4", (6,))])
 assert LOOP_DTYPE.itemsize == 128
 _DT["loop"] = LOOP_DTYPE
+_DT["imu"] = np.float64
 
 
 class SloError(RuntimeError):
@@ -165,6 +166,19 @@ class Context:
 
     def batch_process(self, d_pts, d_cnt, t_scan):
         self._ok(self.L.slo_batch_process(self.h, d_pts, d_cnt, float(t_scan)), "slo_batch_process")
+
+    def batch_imu(self, d_msgs, msgs_per_stream, d_counts):
+        """slo_batch_imu: device IMU_DTYPE [S][msgs_per_stream], device int32 counts [S] -> each stream's imuHandler"""
+        self._ok(self.L.slo_batch_imu(self.h, d_msgs, int(msgs_per_stream), d_counts), "slo_batch_imu")
+
+    def scan_time(self, t_scan):
+        """slo_batch_scan_time: the stamp the next feature step deskews against the IMU ring"""
+        self._ok(self.L.slo_batch_scan_time(self.h, float(t_scan)), "slo_batch_scan_time")
+
+    def imu_handler(self, msg):
+        """slo_imu_handler (one-stream context): msg = one IMU_DTYPE record"""
+        m = np.ascontiguousarray(np.asarray(msg, _abi.IMU_DTYPE).reshape(1))
+        self._ok(self.L.slo_imu_handler(self.h, m.ctypes.data), "slo_imu_handler")
 
     def graph_mode(self, on=True):
         """slo_graph_mode: replay captured HIP graphs in batch_process (default) or launch eagerly"""
@@ -291,7 +305,16 @@ class ImageProjection(_Node):
 
 
 class FeatureAssociation(_Node):
-    """Mirror of FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1817-1859)."""
+    """Mirror of FeatureAssociation::runFeatureAssociation (featureAssociation.cpp:1817-1859)
+    and its imuHandler (FA:459-486)."""
+
+    def imuHandler(self, msg):
+        """one sensor_msgs/Imu as a slo_amd.IMU_DTYPE record or an 11-sequence
+        (stamp, qx, qy, qz, qw, ax, ay, az, wx, wy, wz)"""
+        m = np.asarray(msg)
+        if m.dtype != _abi.IMU_DTYPE:
+            m = np.ascontiguousarray(m, np.float64).reshape(-1, 11)[0].view(_abi.IMU_DTYPE)
+        self.ctx.imu_handler(m)
 
     def runFeatureAssociation(self, t_scan=0.0):
         v = FaView()

@@ -5,6 +5,8 @@ host language.  There is no CPU fallback: if libslo.so is
 missing or no HIP device is present the calls raise.
 """
 import ctypes
+
+import numpy as np
 import os
 import subprocess
 
@@ -97,6 +99,10 @@ class XscMatch(ctypes.Structure):
                 ("min_dist", ctypes.c_double)]
 
 
+# slo_imu_msg (include/slo_abi.h): sensor_msgs/Imu as imuHandler reads it
+IMU_DTYPE = np.dtype([("stamp", "<f8"), ("qx", "<f8"), ("qy", "<f8"), ("qz", "<f8"), ("qw", "<f8"),
+                      ("ax", "<f8"), ("ay", "<f8"), ("az", "<f8"), ("wx", "<f8"), ("wy", "<f8"), ("wz", "<f8")])
+
 # record layout (include/slo_abi.h SLO_REC_*)
 RECORD_FLOATS = 1240
 REC = {"pose": 0, "mapped": 6, "n_keyframes": 12, "kf_saved": 13, "loop_id": 14, "min_dist": 15, "ring_key": 16,
@@ -107,7 +113,8 @@ REC = {"pose": 0, "mapped": 6, "n_keyframes": 12, "kf_saved": 13, "loop_id": 14,
 EXPORTS = [
     "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
-    "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_image_projection", "slo_feature_association",
+    "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_batch_imu", "slo_batch_scan_time",
+    "slo_imu_handler", "slo_image_projection", "slo_feature_association",
     "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
@@ -156,6 +163,9 @@ def lib():
     L.slo_batch_sc_detect.argtypes = [P]
     L.slo_batch_process.argtypes = [P, P, P, ctypes.c_double]
     L.slo_graph_mode.argtypes = [P, ctypes.c_int]
+    L.slo_batch_imu.argtypes = [P, P, ctypes.c_int, P]
+    L.slo_batch_scan_time.argtypes = [P, ctypes.c_double]
+    L.slo_imu_handler.argtypes = [P, P]
     L.slo_image_projection.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                        ctypes.POINTER(SegView)]
     L.slo_feature_association.argtypes = [P, ctypes.c_double, ctypes.POINTER(FaView)]

@@ -29,10 +29,12 @@ def posediff(a, b):
 
 
 def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1, n_points=None,
-        scan_fn=None, cfg_edit=None):
+        scan_fn=None, cfg_edit=None, imu_fn=None):
     """n_points(k, s) -> points of stream s's scan k handed over (ragged and
     empty scans; default: all); scan_fn(k, s) -> the scan itself (default: the
-    synthetic generator); cfg_edit(cfg) changes both configs (GPU and oracle)."""
+    synthetic generator); cfg_edit(cfg) changes both configs (GPU and oracle);
+    imu_fn(k, s) -> (n, 11) float64 IMU messages (slo_imu_msg) stream s's
+    imuHandler receives before scan k (both sides)."""
     import torch
     cfg = slo_amd.preset(preset_id)
     ocfg = O.preset(preset_id)
@@ -50,6 +52,16 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
         ns = [min(P, n_points(k, s)) if n_points else P for s in range(n_streams)]
         pts = torch.from_numpy(np.stack(scans)).cuda()
         cnt = torch.tensor(ns, dtype=torch.int32, device="cuda")
+        if imu_fn:
+            msgs = [np.asarray(imu_fn(k, s), np.float64).reshape(-1, 11) for s in range(n_streams)]
+            per = max(1, max(len(m) for m in msgs))
+            buf = np.zeros((n_streams, per, 11), np.float64)
+            for s, m in enumerate(msgs):
+                buf[s, :len(m)] = m
+                ors[s].imu(m)
+            d_imu = torch.from_numpy(buf).cuda()
+            d_n = torch.tensor([len(m) for m in msgs], dtype=torch.int32, device="cuda")
+            ctx.batch_imu(d_imu.data_ptr(), per, d_n.data_ptr())
         ctx.batch_process(pts.data_ptr(), cnt.data_ptr(), 0.1 * k)
         ctx.synchronize()
         for s in range(n_streams):
@@ -73,6 +85,8 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 row["smooth_ind"] = mismatch(cs[0], cs[1])
             if fl_o & 1:   # transformFusion's /integrated_to_init for this scan
                 row["integrated"] = mismatch(ctx.get(s, "integrated"), ors[s].get("integrated"))
+            if imu_fn:   # FA's IMU scalars (ring pointers, start / current / last angles, velocities)
+                row["imu"] = mismatch(ctx.get(s, "imu"), ors[s].get("imu"))
             row["odom"] = posediff(ctx.get(s, "transform_sum"), ors[s].get("transform_sum"))
             worst["odom"] = max(worst["odom"], row["odom"])
             if fl_o & 2:
