@@ -806,40 +806,46 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     if (threadIdx.x == T - 1) v.ring_cnt[rr * 4 + 3] = scan[T - 1];
 }
 
-// concatenate per-ring outputs in ring order (one block per stream)
-__global__ void k_fa_gather(DevView v) {
-    const int s = blockIdx.x;
+// concatenate per-ring outputs in ring order: one block per (ring, stream),
+// each summing the counts of the rings before its own
+__global__ void __launch_bounds__(256) k_fa_gather(DevView v) {
+    const int r = blockIdx.x, s = blockIdx.y;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
-    __shared__ int off[4][129];
+    __shared__ int off[4], tot[4];
     const int* rc = v.ring_cnt + (size_t)s * R * 4;
     if (threadIdx.x < 4) {
-        int a = 0;
-        for (int r = 0; r < R; ++r) { off[threadIdx.x][r] = a; a += rc[4 * r + threadIdx.x]; }
-        off[threadIdx.x][R] = a;
+        const int c = threadIdx.x;
+        int a = 0, b = 0;
+        for (int q = 0; q < R; ++q) {
+            const int x = rc[4 * q + c];
+            if (q < r) a += x;
+            b += x;
+        }
+        off[c] = a;
+        tot[c] = b;
     }
     __syncthreads();
     // ring boundaries of less_sharp / less_flat (the odometry's ring windows)
-    for (int r = threadIdx.x; r <= R; r += blockDim.x) {
-        v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + r] = off[1][r];
-        v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + r] = min(off[3][r], v.cap_less_flat);
-    }
-    StreamState& st = v.st[s];
     if (threadIdx.x == 0) {
-        st.n_sharp = off[0][R]; st.n_less_sharp = off[1][R]; st.n_flat = off[2][R];
-        st.n_less_flat = min(off[3][R], v.cap_less_flat);
+        v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + r] = off[1];
+        v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + r] = min(off[3], v.cap_less_flat);
+        if (r == R - 1) {
+            v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + R] = tot[1];
+            v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + R] = min(tot[3], v.cap_less_flat);
+            StreamState& st = v.st[s];
+            st.n_sharp = tot[0]; st.n_less_sharp = tot[1]; st.n_flat = tot[2];
+            st.n_less_flat = min(tot[3], v.cap_less_flat);
+        }
     }
-    for (int r = 0; r < R; ++r) {
-        const size_t rr = (size_t)s * R + r;
-        for (int i = threadIdx.x; i < rc[4 * r + 0]; i += blockDim.x)
-            v.sharp[(size_t)s * v.cap_sharp + off[0][r] + i] = v.r_sharp[rr * 12 + i];
-        for (int i = threadIdx.x; i < rc[4 * r + 1]; i += blockDim.x)
-            v.less_sharp[(size_t)s * v.cap_less_sharp + off[1][r] + i] = v.r_less_sharp[rr * 120 + i];
-        for (int i = threadIdx.x; i < rc[4 * r + 2]; i += blockDim.x)
-            v.flat[(size_t)s * v.cap_flat + off[2][r] + i] = v.r_flat[rr * 24 + i];
-        for (int i = threadIdx.x; i < rc[4 * r + 3]; i += blockDim.x)
-            if (off[3][r] + i < v.cap_less_flat)
-                v.less_flat[(size_t)s * v.cap_less_flat + off[3][r] + i] = v.r_lf_ds[rr * C + i];
-    }
+    const size_t rr = (size_t)s * R + r;
+    for (int i = threadIdx.x; i < rc[4 * r + 0]; i += blockDim.x)
+        v.sharp[(size_t)s * v.cap_sharp + off[0] + i] = v.r_sharp[rr * 12 + i];
+    for (int i = threadIdx.x; i < rc[4 * r + 1]; i += blockDim.x)
+        v.less_sharp[(size_t)s * v.cap_less_sharp + off[1] + i] = v.r_less_sharp[rr * 120 + i];
+    for (int i = threadIdx.x; i < rc[4 * r + 2]; i += blockDim.x)
+        v.flat[(size_t)s * v.cap_flat + off[2] + i] = v.r_flat[rr * 24 + i];
+    for (int i = threadIdx.x; i < rc[4 * r + 3]; i += blockDim.x)
+        if (off[3] + i < v.cap_less_flat) v.less_flat[(size_t)s * v.cap_less_flat + off[3] + i] = v.r_lf_ds[rr * C + i];
 }
 
 int fa_features_run(slo_ctx* ctx) {
@@ -856,7 +862,7 @@ int fa_features_run(slo_ctx* ctx) {
     int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
     while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
     SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
-    SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
