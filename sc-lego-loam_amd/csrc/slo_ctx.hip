@@ -289,12 +289,14 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     }
     memset(ctx->h_st, 0, sizeof(StreamState) * S);
     // Grid cells (powers of two, GridView): the map grids answer 5-NN within
-    // 1 m (MO:1281/1364) in 0.5 m cells (rings <= 2, usually done after 1);
+    // 1 m (MO:1281/1364) in 0.5 m cells (rings <= 2, usually done after 1)
+    // hashed into 2^19 buckets per stream (2^17 measured 1.3x slower in
+    // mo_knn: a row's bucket run then holds other cells' points);
     // the odometry surf grid answers 1-NN within 5 m (nearestFeatureSearchSqDist)
     // in 1 m cells (2^15 buckets: built in LDS by one workgroup per stream,
     // slo_vg.hip); the sparse corner cloud is searched by brute force.
-    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << 17, v.cap_mc, 0.5f) ||
-        slo::grid_alloc(ctx, ctx->grid_s, 1 << 17, v.cap_ms, 0.5f) ||
+    if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << SLO_MAP_TLOG2, v.cap_mc, SLO_MAP_CELL) ||
+        slo::grid_alloc(ctx, ctx->grid_s, 1 << SLO_MAP_TLOG2, v.cap_ms, SLO_MAP_CELL) ||
         slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL)) {
         slo_destroy(ctx);
         return SLO_E_HIP;

@@ -232,6 +232,15 @@ struct DevView {
 #define SLO_DIAG 0              // 1: kernels add phase cycle counts to StreamState::dbg
 #endif
 #define SLO_MO_BLOCKS 64
+#ifndef SLO_MAP_CELL
+#define SLO_MAP_CELL 0.5f       // map grid cell (m, power of two): the 5-NN ball of 1 m spans SLO_MAP_R cells
+#endif
+#ifndef SLO_MAP_R
+#define SLO_MAP_R 2
+#endif
+#ifndef SLO_MAP_TLOG2
+#define SLO_MAP_TLOG2 19        // map grid buckets per stream (log2): ~0.2 occupied cells per bucket at
+#endif                          // C3's ~145 k-point surf maps, so few hash collisions share a row's run
 #define SLO_MO_PART 55          // 27 double-double sums (21 AtA + 6 AtB) + correspondence count
 #define SLO_ODO_SURF_CELL 1.0f  // odometry surf grid cell (m, power of two)
 #define SLO_ODO_SURF_R 5        // its search box radius in cells: covers sqrt(nearest_feature_search_sq_dist)

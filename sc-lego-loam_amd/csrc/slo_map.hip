@@ -318,7 +318,7 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
     if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return 0;
     auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
     int n = 0;
-    grid_ball<2, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
+    grid_ball<SLO_MAP_R, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
         const float d = sqd(q, p.x, p.y, p.z);
         const int idx = __float_as_int(p.w);
         if (!less(d, idx, od[4], oi[4])) return;
