@@ -24,10 +24,12 @@ host generator the CPU baseline uses.  A one-stream leg (single_stream)
 reports the same pipeline for a single C3 stream: scans/s and per-scan
 latency.
 
-roofline: the dominant kernel (--roofline-kernel, mo_knn: the largest share of
-device time) timed with HIP events on its context's stream inside the timed
-region; achieved = its algorithmic bytes per launch (DESIGN.md "Roofline",
-from the per-stream counts of a separate instrumented pass with the same
+roofline: the dominant kernel (--roofline-kernel, vg_scatter: the largest
+single kernel by device time, the VoxelGrid radix scatter) timed by in-stream
+device timestamps on its context's stream inside the timed region (the same
+for --roofline-also, mo_knn, reported under roofline_also); achieved = its
+algorithmic bytes per launch (DESIGN.md "Roofline", from the per-stream counts
+of a separate instrumented pass with the same
 launch mix) / that average launch time, against HBM peak.  `isolated` repeats
 it for the instrumented pass, where the contexts run one after the other.  cpu_baseline: the
 oracle (oracle/, C++ restatement of the reference path), rank 0 at N = 1, on
@@ -74,7 +76,9 @@ def parse():
     ap.add_argument("--history", type=int, default=0,
                     help="extra Scan Context history per stream (scans before scan 0); the pre-roll builds the real one")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-kernel", default="mo_knn",
+    ap.add_argument("--roofline-also", default="mo_knn",
+                    help="further kernels timed live the same way, reported under roofline_also (comma list)")
+    ap.add_argument("--roofline-kernel", default="vg_scatter",
                     help="kernel timed with HIP events inside the timed region (the roofline's kernel)")
     ap.add_argument("--cpu-scans", type=int, default=8, help="timed scans per CPU stream in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in sched_getaffinity")
@@ -104,6 +108,7 @@ def stream_counts(ctx, S):
              "map_corner_ds", "map_surf_ds"]
     c = {n: np.array([ctx.get(s, n).shape[0] for s in range(S)], np.int64) for n in names}
     c["fa_iters"] = np.array([ctx.get(s, "fa_iters") for s in range(S)], np.int64)
+    c["vg_in"] = np.array([ctx.get(s, "vg_in") for s in range(S)], np.int64)   # [S][7] VoxelGrid items
     c["mo_iters"] = np.array([int(ctx.get(s, "mo_iters")[0]) for s in range(S)], np.int64)
     return c
 
@@ -132,6 +137,11 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
     if name == "mo_knn":          # per iteration: query + 5 neighbour indices out, the map clouds once
         per = (c["corner_ds"] + c["surf_total_ds"]) * (16 + 20) + (c["map_corner_ds"] + c["map_surf_ds"]) * 16
         return map_steps * int((c["mo_iters"] * per).sum())
+    if name == "vg_scatter":      # the mapping step's 7 VoxelGrid sorts, 4 radix passes each: pass 0 reads the
+        # point (16 B) and writes (key, index) 8 B, passes 1-3 read and write 8 B
+        return map_steps * int(c["vg_in"].sum()) * (16 + 8 + 3 * 16)
+    if name == "vg_hist":         # pass 0 reads the point, passes 1-3 the 4 B key
+        return map_steps * int(c["vg_in"].sum()) * (16 + 3 * 4)
     if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
         return steps * int(c["seg_pts"].sum()) * (8 + 8 + 4 + 1 + 2)
     if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
@@ -441,11 +451,13 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    # the roofline kernel alone is timed inside the timed region: two HIP
-    # events per launch on its context's stream, nothing else
+    # the roofline kernels alone are timed inside the timed region: two
+    # in-stream device timestamps per launch on its context's stream (captured
+    # into the step graphs), nothing else
+    rks = [a.roofline_kernel] + [k for k in a.roofline_also.split(",") if k and k != a.roofline_kernel]
     for c in ctxs:
         c.timing(True)
-        c.timing_filter(a.roofline_kernel)
+        c.timing_filter(",".join(rks))
         c.timing_reset()
     if a.trace_marker:   # a torch spin kernel on either side of the timed steps (tools/trace_window.py)
         torch.cuda._sleep(1000)
@@ -461,21 +473,22 @@ def main():
     if a.trace_marker:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
-    live_ms, live_n = 0.0, 0
+    live = {k: [0.0, 0] for k in rks}
     for c in ctxs:
         for kn, (kms, kcalls) in c.timing_read().items():
-            if kn == a.roofline_kernel:
-                live_ms += kms
-                live_n += kcalls
+            if kn in live:
+                live[kn][0] += kms
+                live[kn][1] += kcalls
         c.timing(False)
         c.timing_filter(None)
+    live_ms, live_n = live[a.roofline_kernel]
     value = S * a.steps * world / el
     errs = sum(int(c.get(s, "err")[0]) != 0 for c in ctxs for s in range(c.n_streams))
     kfs = np.array([int(c.get(s, "n_keyframes")[0]) for c in ctxs for s in range(c.n_streams)])
 
     # ---- instrumented pass: per-kernel HIP-event times on each context's
     # stream, groups run one after the other so the events time each kernel alone
-    roof, kt, workload, gbs = None, {}, None, {}
+    roof, roof_also, kt, workload, gbs = None, None, {}, None, {}
     if a.profile_steps > 0:
         for c in ctxs:
             c.timing(True)
@@ -496,7 +509,7 @@ def main():
         parts = [stream_counts(c, c.n_streams) for c in ctxs]
         counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1}
-        total_ms = sum(v[0] for v in kt.values())
+        total_ms = sum(v[0] for kn, v in kt.items() if not kn.startswith("vg_sort:"))   # groups double count
         name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
         for kn, (kms, kcalls) in kt.items():
             kb = algo_bytes(kn, counts, cfg, S, a.profile_steps, map_steps)
@@ -505,25 +518,31 @@ def main():
         # achieved = algorithmic bytes per launch (instrumented pass, same
         # launch mix) / the average launch time inside the timed region,
         # where the contexts' kernels share the device
-        rk = a.roofline_kernel
-        rms, rn = kt.get(rk, (0.0, 0))
-        rb = algo_bytes(rk, counts, cfg, S, a.profile_steps, map_steps)
-        bpl = rb / rn if (rb is not None and rn) else None
-        live_s = live_ms / 1e3 / live_n if live_n else None
-        live = bpl / live_s / 1e9 if (bpl is not None and live_s) else None
-        iso = bpl / (rms / 1e3 / rn) / 1e9 if (bpl is not None and rms > 0) else None
-        traffic, tsrc = pmc_traffic(a.traffic_from, rk)
-        roof = {"bound": "hbm", "achieved": round(live, 2) if live is not None else None, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(live / HBM_PEAK_GBS, 5) if live is not None else None,
-                "traffic": traffic, "traffic_source": tsrc, "kernel": rk,
-                "avg_launch_us": round(live_s * 1e6, 2) if live_s else None, "launches_timed": live_n,
-                "bytes_per_launch": int(bpl) if bpl is not None else None,
-                "isolated": {"achieved": round(iso, 2) if iso is not None else None,
-                             "frac": round(iso / HBM_PEAK_GBS, 5) if iso is not None else None,
-                             "avg_launch_us": round(rms / rn * 1e3, 2) if rn else None,
-                             "note": "instrumented steps, contexts one after the other"},
-                "share_of_device_time": round(rms / total_ms, 4) if total_ms else None,
-                "largest_kernel": name}
+        def roof_of(rk):
+            rms, rn = kt.get(rk, (0.0, 0))
+            rb = algo_bytes(rk, counts, cfg, S, a.profile_steps, map_steps)
+            bpl = rb / rn if (rb is not None and rn) else None
+            lms, ln = live.get(rk, (0.0, 0))
+            live_s = lms / 1e3 / ln if ln else None
+            ach = bpl / live_s / 1e9 if (bpl is not None and live_s) else None
+            iso = bpl / (rms / 1e3 / rn) / 1e9 if (bpl is not None and rms > 0) else None
+            traffic, tsrc = pmc_traffic(a.traffic_from, rk)
+            return {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
+                    "traffic": traffic, "traffic_source": tsrc, "kernel": rk,
+                    "avg_launch_us": round(live_s * 1e6, 2) if live_s else None, "launches_timed": ln,
+                    "bytes_per_launch": int(bpl) if bpl is not None else None,
+                    "isolated": {"achieved": round(iso, 2) if iso is not None else None,
+                                 "frac": round(iso / HBM_PEAK_GBS, 5) if iso is not None else None,
+                                 "avg_launch_us": round(rms / rn * 1e3, 2) if rn else None,
+                                 "note": "instrumented steps, contexts one after the other"},
+                    "share_of_device_time": round(rms / total_ms, 4) if total_ms else None}
+
+        # the largest single kernel (vg_sort:<filter> entries time groups of launches)
+        name = max(((kn, v) for kn, v in kt.items() if not kn.startswith("vg_sort:")), key=lambda kv: kv[1][0])[0]
+        roof = roof_of(a.roofline_kernel)
+        roof["largest_kernel"] = name
+        roof_also = {rk: roof_of(rk) for rk in rks[1:]}
 
     elif live_n:   # no instrumented pass: the live launch time alone (no byte counts)
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
@@ -571,6 +590,7 @@ def main():
                        "launch": "eager" if a.no_graphs else "one HIP graph per context and step",
                        "parallelism": f"streams sharded over {world} GPU(s)"},
             "roofline": roof,
+            "roofline_also": roof_also,
             "cpu_baseline": cpu,
             "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
             "speedup_vs_cpu_A": round(value / cpu["A_reference_topology"]["value"], 2) if cpu else None,

@@ -257,8 +257,11 @@ int slo_timing_enable(slo_ctx* ctx, int enable);
  * launch counts; returns number of kernels */
 int slo_timing_read(slo_ctx* ctx, char* names_buf, size_t buf_bytes, double* total_ms, int64_t* launches, int cap);
 int slo_timing_reset(slo_ctx* ctx);
-/* time only the launches named `name` (NULL or "" = all); the bench times
- * its dominant kernel this way inside the timed region */
+/* time only the launches named `name` — one name or a comma-separated list
+ * (NULL or "" = all, by HIP events, eager launches).  With a filter the
+ * launches are timed by in-stream device timestamps (the constant-rate wall
+ * clock) that are captured into the step graphs, so the bench times its
+ * roofline kernels this way inside the timed region */
 int slo_timing_filter(slo_ctx* ctx, const char* name);
 
 /* ---------------------------------------------------------------- wire format

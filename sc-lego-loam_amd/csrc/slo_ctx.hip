@@ -13,19 +13,26 @@ using slo::StreamState;
 
 namespace slo {
 
-bool timing_on(const slo_ctx* ctx, const char* name) {
-    return ctx->timing_only.empty() || ctx->timing_only == name;
+// the filter's names (slo_timing_filter: one name or a comma-separated list)
+static int stamp_id(const slo_ctx* ctx, const char* name) {
+    for (size_t k = 0; k < ctx->stamp_names.size(); ++k)
+        if (ctx->stamp_names[k] == name) return (int)k;
+    return -1;
 }
-__global__ void k_stamp(unsigned long long* st) {
-    const unsigned int i = atomicAdd((unsigned int*)(st + SLO_STAMP_CAP), 1u);
-    st[i % SLO_STAMP_CAP] = wall_clock64();
+bool timing_on(const slo_ctx* ctx, const char* name) {
+    return ctx->timing_only.empty() || stamp_id(ctx, name) >= 0;
+}
+// one timestamp of the device's constant-rate clock and the name it belongs to
+__global__ void k_stamp(unsigned long long* st, int id) {
+    const unsigned int i = atomicAdd((unsigned int*)(st + 2 * SLO_STAMP_CAP), 1u) % SLO_STAMP_CAP;
+    st[2 * i] = wall_clock64();
+    st[2 * i + 1] = (unsigned long long)id;
 }
 static bool stamping(const slo_ctx* ctx) { return !ctx->timing_only.empty() && ctx->d_stamp; }
 void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a) {
-    (void)name;
     if (stamping(ctx)) {
         *a = nullptr;
-        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp);
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp, stamp_id(ctx, name));
         return;
     }
     hipEventCreate(a);
@@ -33,7 +40,7 @@ void timing_begin(slo_ctx* ctx, const char* name, hipEvent_t* a) {
 }
 void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a) {
     if (stamping(ctx)) {
-        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp);
+        hipLaunchKernelGGL(k_stamp, dim3(1), dim3(1), 0, ctx->stream, ctx->d_stamp, stamp_id(ctx, name));
         return;
     }
     hipEvent_t b;
@@ -42,19 +49,19 @@ void timing_end(slo_ctx* ctx, const char* name, hipEvent_t a) {
     ctx->pending.push_back({name, {a, b}});
 }
 static void timing_flush(slo_ctx* ctx) {
-    if (stamping(ctx)) {   // consecutive (begin, end) stamps of the filtered kernel
-        std::vector<unsigned long long> h(SLO_STAMP_CAP + 1);
+    if (stamping(ctx)) {   // consecutive (begin, end) stamps of each filtered launch, in stream order
+        std::vector<unsigned long long> h(2 * SLO_STAMP_CAP + 1);
         hipStreamSynchronize(ctx->stream);
-        hipMemcpy(h.data(), ctx->d_stamp, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1), hipMemcpyDeviceToHost);
-        const unsigned int n = (unsigned int)h[SLO_STAMP_CAP];
-        if (n >= 2) {
-            auto& k = ctx->ktimes[ctx->timing_only];
-            for (unsigned int i = 0; i + 1 < n && i + 1 < SLO_STAMP_CAP; i += 2) {
-                k.total_ms += (double)(h[i + 1] - h[i]) / ctx->stamp_khz;
-                k.n += 1;
-            }
+        hipMemcpy(h.data(), ctx->d_stamp, sizeof(unsigned long long) * (2 * SLO_STAMP_CAP + 1), hipMemcpyDeviceToHost);
+        const unsigned int n = std::min((unsigned int)h[2 * SLO_STAMP_CAP], (unsigned int)SLO_STAMP_CAP);
+        for (unsigned int i = 0; i + 1 < n; i += 2) {
+            const int id = (int)h[2 * i + 1];
+            if (id < 0 || id >= (int)ctx->stamp_names.size() || (int)h[2 * i + 3] != id) continue;
+            auto& k = ctx->ktimes[ctx->stamp_names[id]];
+            k.total_ms += (double)(h[2 * i + 2] - h[2 * i]) / ctx->stamp_khz;
+            k.n += 1;
         }
-        hipMemsetAsync(ctx->d_stamp + SLO_STAMP_CAP, 0, sizeof(unsigned long long), ctx->stream);
+        hipMemsetAsync(ctx->d_stamp + 2 * SLO_STAMP_CAP, 0, sizeof(unsigned long long), ctx->stream);
         hipStreamSynchronize(ctx->stream);
     }
     if (ctx->pending.empty()) return;
@@ -311,8 +318,8 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     }
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, hip_device) != hipSuccess || khz <= 0 ||
-        hipMalloc(&ctx->d_stamp, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1)) != hipSuccess ||
-        hipMemset(ctx->d_stamp, 0, sizeof(unsigned long long) * (SLO_STAMP_CAP + 1)) != hipSuccess) {
+        hipMalloc(&ctx->d_stamp, sizeof(unsigned long long) * (2 * SLO_STAMP_CAP + 1)) != hipSuccess ||
+        hipMemset(ctx->d_stamp, 0, sizeof(unsigned long long) * (2 * SLO_STAMP_CAP + 1)) != hipSuccess) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
@@ -678,6 +685,15 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 23; esz = 8;
     }
     else if (name == "keyposes") dev(v.kf_pose + s * v.KFMAX * 6, (size_t)st.n_keyframes * 6, 4);
+    else if (name == "vg_in") {   // the items of the last mapping step's seven batched VoxelGrids (map_run order)
+        slo::SloIo io;
+        SLO_CHECK(hipMemcpy(&io, ctx->d_io, sizeof(io), hipMemcpyDeviceToHost));
+        int32_t raw = 0;
+        if (io.npts) SLO_CHECK(hipMemcpy(&raw, io.npts + stream, 4, hipMemcpyDeviceToHost));
+        const int32_t a[7] = {st.n_corner_map, st.n_surf_map, raw, st.cornerLastNum, st.surfLastNum,
+                              st.outlier_count, st.n_st};
+        tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 7; esz = 4;
+    }
     else if (name == "map_raw_n") {   // laserCloudCornerFromMap / laserCloudSurfFromMap sizes before their VoxelGrids
         int32_t a[2] = {st.n_corner_map, st.n_surf_map}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
     }
@@ -735,6 +751,13 @@ int slo_timing_filter(slo_ctx* ctx, const char* name) {
     slo::timing_flush(ctx);   // stamps of the previous filter
     slo::graphs_drop(ctx);
     ctx->timing_only = name ? name : "";
+    ctx->stamp_names.clear();
+    for (size_t a = 0; a < ctx->timing_only.size();) {
+        size_t b = ctx->timing_only.find(',', a);
+        if (b == std::string::npos) b = ctx->timing_only.size();
+        if (b > a) ctx->stamp_names.push_back(ctx->timing_only.substr(a, b - a));
+        a = b + 1;
+    }
     return SLO_OK;
 }
 int slo_timing_reset(slo_ctx* ctx) {

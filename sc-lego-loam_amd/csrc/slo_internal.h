@@ -483,14 +483,15 @@ struct slo_ctx {
     bool fa_published = false;
     // timing
     bool timing = false;
-    std::string timing_only;            // non-empty: time only launches of this name (slo_timing_filter)
+    std::string timing_only;            // non-empty: time only launches of these names (slo_timing_filter)
+    std::vector<std::string> stamp_names;   // timing_only split at commas
     struct KT { std::vector<hipEvent_t> ev; double total_ms = 0; int64_t n = 0; };
     std::map<std::string, KT> ktimes;
     std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> pending;
     // with a filter (timing_only), the named kernel is timed by device
     // timestamps written in-stream around each launch (k_stamp: the device's
     // constant-rate wall clock), so the timing survives graph capture
-    unsigned long long* d_stamp = nullptr;   // [SLO_STAMP_CAP] timestamps + [1] counter
+    unsigned long long* d_stamp = nullptr;   // [SLO_STAMP_CAP] (timestamp, name id) + [1] counter
     double stamp_khz = 0;
     // host staging for single-scan API
     void* h_stage = nullptr;

@@ -42,6 +42,7 @@ LOOP_DTYPE = np.dtype([("id", "<i4"), ("ran", "<i4"), ("converged", "<i4"), ("ac
 assert LOOP_DTYPE.itemsize == 128
 _DT["loop"] = LOOP_DTYPE
 _DT["imu"] = np.float64
+_DT["vg_in"] = np.int32
 
 
 class SloError(RuntimeError):
