@@ -459,7 +459,7 @@ struct HashGrid {
     int T = 0;
     float cell = 1.0f;
     size_t ent_stride = 0;
-    int32_t *cnt = nullptr, *cur = nullptr, *off = nullptr;
+    int32_t *cnt = nullptr, *off = nullptr;
     int32_t* bsum = nullptr;   // per-stream block sums of the offset scan
     float4* ent = nullptr;
 };

@@ -631,42 +631,45 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
 }
 
 // ---------------------------------------------------------------- spatial hash grid
-__global__ void k_grid_count(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
-                             int32_t* cnt) {
+// Global hash-grid build (T > SLO_GRID_LDS_T buckets), three passes over the
+// points and one over the buckets: k_grid_count (bucket counts by device-scope
+// atomics; each workgroup also sums its points per block of VG_TILE buckets
+// in LDS and adds those block sums once), k_seg_top + k_seg_down (the
+// per-stream exclusive scan of the counts from the block sums; down clears
+// each block sum for the next build), k_grid_scatter (each point's slot by an
+// atomic decrement of its bucket count, which so returns to zero for the next
+// build — no clearing pass).  Entries inside a bucket are unordered; every
+// reader is order-independent.
+#define GRID_MAX_BLK 1024   // block sums per stream held in LDS: T + 1 <= 1024 * VG_TILE
+__global__ void __launch_bounds__(256) k_grid_count(const float4* pts, size_t stride, const int32_t* n, int n_stride,
+                                                    int T, float inv, int32_t* cnt, int nblk, int32_t* bsum) {
+    __shared__ int bl[GRID_MAX_BLK];
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x) bl[k] = 0;
+    __syncthreads();
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const float4 p = pts[(size_t)s * stride + i];
         const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
         atomicAdd(&cnt[(size_t)s * (T + 1) + b], 1);
+        atomicAdd(&bl[b / VG_TILE], 1);
     }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nblk; k += blockDim.x)
+        if (bl[k]) atomicAdd(&bsum[(size_t)s * nblk + k], bl[k]);
 }
 
 __global__ void k_grid_scatter(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
-                               const int32_t* off, int32_t* cur, float4* ent, size_t ent_stride) {
+                               const int32_t* off, int32_t* cnt, float4* ent, size_t ent_stride) {
     const int s = blockIdx.y;
     const int m = n[(size_t)s * n_stride];
     const int base = off[(size_t)s * (T + 1)];
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
         const float4 p = pts[(size_t)s * stride + i];
         const unsigned int b = grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
-        const int pos = off[(size_t)s * (T + 1) + b] - base + atomicAdd(&cur[(size_t)s * (T + 1) + b], 1);
+        const size_t sb = (size_t)s * (T + 1) + b;
+        const int pos = off[sb] - base + atomicSub(&cnt[sb], 1) - 1;
         ent[(size_t)s * ent_stride + pos] = make_float4(p.x, p.y, p.z, __int_as_float(i));
-    }
-}
-
-// cnt / cur back to zero for the next build: only the buckets the points hit
-// are non-zero, so clearing those replaces two memsets of the whole [S][T + 1]
-// arrays (grid_alloc zeroes them once)
-__global__ void k_grid_clear(const float4* pts, size_t stride, const int32_t* n, int n_stride, int T, float inv,
-                             int32_t* cnt, int32_t* cur) {
-    const int s = blockIdx.y;
-    const int m = n[(size_t)s * n_stride];
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
-        const float4 p = pts[(size_t)s * stride + i];
-        const size_t b = (size_t)s * (T + 1) + grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
-        cnt[b] = 0;
-        cur[b] = 0;
     }
 }
 
@@ -722,24 +725,6 @@ __global__ void __launch_bounds__(1024) k_grid_build_lds(const float4* pts, size
 // relative to the stream's first entry), reduce-then-scan over blocks of
 // VG_TILE counts: block sums, a scan of each stream's block sums, then each
 // block rescanned from its base (coalesced loads / stores through LDS).
-__global__ void __launch_bounds__(VG_T) k_seg_reduce(const int32_t* in, int N, int nblk, int32_t* bsum) {
-    __shared__ int wsum[4];
-    const int s = blockIdx.y, tid = threadIdx.x;
-    const int32_t* c = in + (size_t)s * N;
-    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-        const int a = b * VG_TILE, m = min(VG_TILE, N - a);
-        int sum = 0;
-#pragma unroll 4
-        for (int q = 0; q < VG_IPT; ++q) {
-            const int j = q * VG_T + tid;
-            if (j < m) sum += c[a + j];
-        }
-        int total;
-        vg_block_scan<4>(sum, wsum, &total);
-        if (tid == 0) bsum[(size_t)s * nblk + b] = total;
-    }
-}
-
 __global__ void k_seg_top(int nblk, int32_t* bsum) {   // one wave per stream
     const int s = blockIdx.x, lane = threadIdx.x;
     int32_t* bs = bsum + (size_t)s * nblk;
@@ -757,7 +742,7 @@ __global__ void k_seg_top(int nblk, int32_t* bsum) {   // one wave per stream
     }
 }
 
-__global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int nblk, const int32_t* bsum,
+__global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int nblk, int32_t* bsum,
                                                    int32_t* out) {
     __shared__ int l[VG_TILE + VG_TILE / 16];
     __shared__ int wsum[4];
@@ -776,7 +761,8 @@ __global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int
 #pragma unroll
         for (int q = 0; q < VG_IPT; ++q) { x[q] = l[VG_PAD(tid * VG_IPT + q)]; sum += x[q]; }
         int total;
-        int run = bsum[(size_t)s * nblk + b] + vg_block_scan<4>(sum, wsum, &total);
+        const int top = bsum[(size_t)s * nblk + b];
+        int run = top + vg_block_scan<4>(sum, wsum, &total);
 #pragma unroll
         for (int q = 0; q < VG_IPT; ++q) { l[VG_PAD(tid * VG_IPT + q)] = run; run += x[q]; }
         __syncthreads();
@@ -786,6 +772,7 @@ __global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int
             if (j < m) o[a + j] = l[VG_PAD(j)];
         }
         __syncthreads();
+        if (tid == 0) bsum[(size_t)s * nblk + b] = 0;   // read by this block only (after the barrier): next build
     }
 }
 
@@ -799,16 +786,14 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
         return 0;
     }
     const int bx = std::max(1, std::min(128, (int)((stride + 255) / 256)));
-    SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt);
     const int N = g.T + 1, nblk = (N + VG_TILE - 1) / VG_TILE;
+    SLO_LAUNCH(ctx, "grid_count", k_grid_count, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt,
+               nblk, g.bsum);
     const dim3 sg(std::min(nblk, std::max(4, 2048 / S)), S);
-    SLO_LAUNCH(ctx, "grid_scan", k_seg_reduce, sg, dim3(VG_T), 0, g.cnt, N, nblk, g.bsum);
     SLO_LAUNCH(ctx, "grid_scan", k_seg_top, dim3(S), dim3(64), 0, nblk, g.bsum);
     SLO_LAUNCH(ctx, "grid_scan", k_seg_down, sg, dim3(VG_T), 0, g.cnt, N, nblk, g.bsum, g.off);
     SLO_LAUNCH(ctx, "grid_scatter", k_grid_scatter, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv,
-               g.off, g.cur, g.ent, g.ent_stride);
-    SLO_LAUNCH(ctx, "grid_clear", k_grid_clear, dim3(bx, S), dim3(256), 0, pts, stride, n, n_stride, g.T, inv, g.cnt,
-               g.cur);
+               g.off, g.cnt, g.ent, g.ent_stride);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
@@ -825,13 +810,17 @@ int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell) 
     g.cell = cell;
     g.ent_stride = ent_stride;
     const size_t nb = (size_t)S * (T + 1);
+    const size_t nblk = (T + 1 + VG_TILE - 1) / VG_TILE;
+    if (nblk > GRID_MAX_BLK) {
+        ctx->err = "grid_alloc: too many buckets";
+        return SLO_E_ARG;
+    }
     SLO_CHECK(hipMalloc(&g.cnt, sizeof(int32_t) * nb));
-    SLO_CHECK(hipMalloc(&g.cur, sizeof(int32_t) * nb));
     SLO_CHECK(hipMalloc(&g.off, sizeof(int32_t) * nb));
-    SLO_CHECK(hipMemset(g.cnt, 0, sizeof(int32_t) * nb));   // kept zero between builds (k_grid_clear)
-    SLO_CHECK(hipMemset(g.cur, 0, sizeof(int32_t) * nb));
+    SLO_CHECK(hipMemset(g.cnt, 0, sizeof(int32_t) * nb));   // back to zero after each build (k_grid_scatter)
     SLO_CHECK(hipMalloc(&g.ent, sizeof(float4) * (size_t)S * ent_stride));
-    SLO_CHECK(hipMalloc(&g.bsum, sizeof(int32_t) * (size_t)S * ((T + 1 + VG_TILE - 1) / VG_TILE)));
+    SLO_CHECK(hipMalloc(&g.bsum, sizeof(int32_t) * (size_t)S * nblk));
+    SLO_CHECK(hipMemset(g.bsum, 0, sizeof(int32_t) * (size_t)S * nblk));   // cleared by k_seg_down
     return 0;
 }
 
@@ -849,7 +838,6 @@ GridView grid_view(const HashGrid& g) {
 
 void grid_free(HashGrid& g) {
     if (g.cnt) hipFree(g.cnt);
-    if (g.cur) hipFree(g.cur);
     if (g.off) hipFree(g.off);
     if (g.ent) hipFree(g.ent);
     if (g.bsum) hipFree(g.bsum);
