@@ -5,10 +5,10 @@
 // filter the reference calls at featureAssociation.cpp:779 and
 // mapOptmization.cpp:1224-1262): per stream the bounds give min_b and the
 // x-fastest linear voxel index; each stream's (idx, point) pairs are sorted
-// by a hand-written segmented LSD radix sort (four passes of <= 8 bits,
-// stable, so the points of a voxel stay in input order; no stream bits in
-// the key), every voxel's centroid is summed in that order and written at
-// its rank -> output sorted by voxel index exactly like PCL.  Non-finite
+// by a hand-written segmented LSD radix sort (as many passes of <= VG_DMAX
+// bits as the stream's key width needs, at most four; stable, so the points
+// of a voxel stay in input order; no stream bits in the key), every voxel's
+// centroid is summed in that order and written at its rank -> output sorted by voxel index exactly like PCL.  Non-finite
 // points are skipped (the raw cloud is not dense, MO:1236); the int32
 // overflow guard returns the input unchanged, as PCL does.  All sizes come
 // from the input strides and device-side counts: no host round trip.
@@ -106,13 +106,18 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
 
 // voxel-index parameters (PCL applyFilter) per stream, and the stream's key
 // width: vbits (every voxel index < 2^vbits - 1, the all-ones key marks a
-// non-finite point), split into VG_PASSES digits of dbits each
-struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, ntiles; };
+// non-finite point), split into npass digits of dbits <= VG_DMAX each
+struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, npass, ntiles; };
 
 #define VG_T 256                      // threads per tile workgroup
 #define VG_IPT 16                     // items per thread
 #define VG_TILE (VG_T * VG_IPT)       // items per tile
-#define VG_PASSES 4                   // LSD radix passes of <= 8 bits over 32-bit keys
+#define VG_PASSES 4                   // LSD radix passes launched (a stream runs npass <= VG_PASSES of them)
+#ifndef VG_DMAX
+#define VG_DMAX 8                     // digit bits per pass at most; VG_PASSES * VG_DMAX >= 32
+#endif
+#define VG_NB (1 << VG_DMAX)          // digit bins
+static_assert(VG_PASSES * VG_DMAX >= 32 && VG_NB % VG_T == 0, "VoxelGrid digit layout");
 #define VG_PAD(j) ((j) + ((j) >> 4))  // LDS index padded against 16-way bank conflicts (blocked reads)
 
 __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
@@ -125,7 +130,7 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
     p.ntiles = (n + VG_TILE - 1) / VG_TILE;
     if (n == 0 || bounds[6 * s] == 0xffffffffu) {   // empty, or no finite point: every key is "none"
         p.minb[0] = p.minb[1] = p.minb[2] = 0; p.mul1 = p.mul2 = 0;
-        p.vbits = 1; p.dbits = 1;
+        p.vbits = 1; p.dbits = 1; p.npass = 1;
         prm[s] = p;
         return;
     }
@@ -145,7 +150,8 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
     while (vb < 32 && (1LL << vb) <= cells) ++vb;
     if (cells >= (1LL << 30)) vb = 32;   // int index arithmetic may wrap, as in PCL
     p.vbits = vb;
-    p.dbits = (vb + VG_PASSES - 1) / VG_PASSES;
+    p.npass = (vb + VG_DMAX - 1) / VG_DMAX;
+    p.dbits = (vb + p.npass - 1) / p.npass;
     prm[s] = p;
 }
 
@@ -191,9 +197,14 @@ __device__ inline T vg_block_scan(T x, T* wsum, T* total) {
 // ballots: the lanes holding the same digit, then per-wave running counts in
 // LDS; stable), reorders the tile through LDS and writes each digit's run at
 // its base.  Pass 0 computes the keys from the points (vals = the point's
-// index in its stream).
+// index in its stream).  A stream runs npass passes and skips the rest; its
+// passes alternate between the buffer pairs A and B so that the last one
+// always writes B (vg_out_b).
 
-// lanes of this wave whose digit equals mine (among `act` lanes), dbits <= 8
+// the pair pass `pass` of a stream writes: the last pass writes B
+__device__ inline bool vg_out_b(const VgParams& p, int pass) { return ((p.npass - 1 - pass) & 1) == 0; }
+
+// lanes of this wave whose digit equals mine (among `act` lanes), dbits <= VG_DMAX
 __device__ inline unsigned long long vg_peers(unsigned int d, int dbits, unsigned long long act) {
     unsigned long long pe = act;
     for (int b = 0; b < dbits; ++b) {
@@ -218,42 +229,53 @@ __device__ inline void vg_load(const float4* in, size_t in_stride, const VgParam
 
 template <bool FIRST>
 __global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, const int32_t* off,
-                                                  const VgParams* prm, int pass, const unsigned int* kin, int* cnt,
-                                                  int maxT) {
+                                                  const VgParams* prm, int pass, const unsigned int* ka,
+                                                  const unsigned int* kb, int* cnt, int maxT) {
     const float4* in = FIRST ? src.pts() : nullptr;
-    __shared__ int h[256];
+    __shared__ int h[VG_NB];
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
+    if (pass >= p.npass) return;
+    const unsigned int* kin = vg_out_b(p, pass - 1) ? kb : ka;
     const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
     const unsigned int mask = (unsigned int)nb - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
-        if (tid < nb) h[tid] = 0;
+        for (int d = tid; d < nb; d += VG_T) h[d] = 0;
         __syncthreads();
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        unsigned int key[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {   // all of the tile's loads in flight before the first use
+            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            unsigned int val;
+            key[k] = 0;
+            if (j < m) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, nullptr, key[k], val);
+        }
+#pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / 4) + k * 64 + lane;
             const bool ok = j < m;
-            unsigned int key = 0, val;
-            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, nullptr, key, val);
-            const unsigned int d = (key >> shift) & mask;
+            const unsigned int d = (key[k] >> shift) & mask;
             const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
             if (ok && (pe & lt) == 0) atomicAdd(&h[d], __popcll(pe));   // one add per digit per wave slice
         }
         __syncthreads();
-        if (tid < nb) cnt[((size_t)s * 256 + tid) * maxT + t] = h[tid];
+        for (int d = tid; d < nb; d += VG_T) cnt[((size_t)s * VG_NB + d) * maxT + t] = h[d];
         __syncthreads();
     }
 }
 
-__global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgParams* prm, int* cnt, int maxT) {
+__global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgParams* prm, int pass, int* cnt,
+                                                   int maxT) {
     __shared__ int wsum[16];
     const int s = blockIdx.x, tid = threadIdx.x;
     const VgParams p = prm[s];
+    if (pass >= p.npass) return;
     const int nt = p.ntiles, F = (1 << p.dbits) * nt;
     if (F == 0) return;
     const int L = (F + 1023) / 1024, f0 = min(F, tid * L), f1 = min(F, f0 + L);
-    int* c = cnt + (size_t)s * 256 * maxT;
+    int* c = cnt + (size_t)s * VG_NB * maxT;
     int sum = 0;
     for (int f = f0; f < f1; ++f) sum += c[(size_t)(f / nt) * maxT + f % nt];
     int total;
@@ -268,22 +290,28 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
 
 template <bool FIRST>
 __global__ void __launch_bounds__(VG_T) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
-                                                     const VgParams* prm, int pass, const unsigned int* kin,
-                                                     const unsigned int* vin, unsigned int* kout, unsigned int* vout,
+                                                     const VgParams* prm, int pass, unsigned int* ka,
+                                                     unsigned int* va, unsigned int* kb, unsigned int* vb,
                                                      const int* cnt, int maxT) {
     __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
-    __shared__ int wc[4][256];   // per wave slice: running digit counts, then the slice's digit offsets
-    __shared__ int lb[256];      // global base of each digit minus its first position in the tile
+    __shared__ int wc[4][VG_NB];   // per wave slice: running digit counts, then the slice's digit offsets
+    __shared__ int lb[VG_NB];      // global base of each digit minus its first position in the tile
     __shared__ int wsum[4];
     const float4* in = FIRST ? src.pts() : nullptr;
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
+    if (pass >= p.npass) return;
+    const bool ob = vg_out_b(p, pass);
+    const unsigned int* kin = ob ? ka : kb;
+    const unsigned int* vin = ob ? va : vb;
+    unsigned int* kout = ob ? kb : ka;
+    unsigned int* vout = ob ? vb : va;
     const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
     const unsigned int mask = (unsigned int)nb - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
-        for (int d = tid; d < 4 * 256; d += VG_T) (&wc[0][0])[d] = 0;
+        for (int d = tid; d < 4 * VG_NB; d += VG_T) (&wc[0][0])[d] = 0;
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
@@ -305,17 +333,24 @@ __global__ void __launch_bounds__(VG_T) k_vg_scatter(VgSrc src, size_t in_stride
         // digit-major, slice-minor exclusive scan of the counts: the tile-local
         // position of each (digit, slice) run
         {
-            const int d = tid;
-            int c[4], tot = 0;
+            constexpr int DPT = VG_NB / VG_T;   // consecutive digits per thread
+            const int d0 = tid * DPT;
+            int c[DPT][4], tot = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q) { c[q] = d < nb ? wc[q][d] : 0; tot += c[q]; }
+            for (int e = 0; e < DPT; ++e)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) { c[e][q] = d0 + e < nb ? wc[q][d0 + e] : 0; tot += c[e][q]; }
             int total;
-            const int start = vg_block_scan<4>(tot, wsum, &total);
-            if (d < nb) {
-                int run = start;
+            int run = vg_block_scan<4>(tot, wsum, &total);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { wc[q][d] = run; run += c[q]; }
-                if (tot) lb[d] = cnt[((size_t)s * 256 + d) * maxT + t] - start;
+            for (int e = 0; e < DPT; ++e) {
+                const int d = d0 + e;
+                if (d < nb) {
+                    const int start = run;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) { wc[q][d] = run; run += c[e][q]; }
+                    if (run != start) lb[d] = cnt[((size_t)s * VG_NB + d) * maxT + t] - start;
+                }
             }
         }
         __syncthreads();
@@ -544,7 +579,7 @@ static int ensure_ws(slo_ctx* ctx, size_t stride) {
         if (w.hcnt) hipFree(w.hcnt);
         w.tiles = tt;
         ++ctx->ws_gen;
-        SLO_CHECK(hipMalloc(&w.cnt, sizeof(int) * 256 * tt));
+        SLO_CHECK(hipMalloc(&w.cnt, sizeof(int) * VG_NB * tt));
         SLO_CHECK(hipMalloc(&w.hcnt, sizeof(int) * tt));
     }
     return 0;
@@ -573,28 +608,27 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
     const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
-    unsigned int *k0 = w.keys, *v0 = w.vals, *k1 = w.keys2, *v1 = w.vals2;
+    // pair A = keys2/vals2, pair B = keys/vals (every stream's last pass writes B)
+    unsigned int *ka = w.keys2, *va = w.vals2, *kb = w.keys, *vb = w.vals;
     for (int pass = 0; pass < VG_PASSES; ++pass) {
         if (pass == 0) {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, k0,
-                       w.cnt, maxT);
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
+                       kb, w.cnt, maxT);
         } else {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, k0,
-                       w.cnt, maxT);
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
+                       kb, w.cnt, maxT);
         }
-        SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, w.cnt, maxT);
+        SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, pass, w.cnt, maxT);
         if (pass == 0) {
             SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       k0, v0, k1, v1, w.cnt, maxT);
+                       ka, va, kb, vb, w.cnt, maxT);
         } else {
             SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       k0, v0, k1, v1, w.cnt, maxT);
+                       ka, va, kb, vb, w.cnt, maxT);
         }
-        std::swap(k0, k1);
-        std::swap(v0, v1);
     }
     if (tm) timing_end(ctx, sort_name.c_str(), ev);
-    *keys = k0; *vals = v0; *spare_k = k1; *spare_v = v1;
+    *keys = kb; *vals = vb; *spare_k = ka; *spare_v = va;
     return 0;
 }
 
