@@ -110,7 +110,9 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
 struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, npass, ntiles; };
 
 #define VG_T 256                      // threads per tile workgroup
+#ifndef VG_IPT
 #define VG_IPT 16                     // items per thread
+#endif
 #define VG_TILE (VG_T * VG_IPT)       // items per tile
 #define VG_PASSES 4                   // LSD radix passes launched (a stream runs npass <= VG_PASSES of them)
 #ifndef VG_DMAX
@@ -289,7 +291,7 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T, 4) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
                                                      const VgParams* prm, int pass, unsigned int* ka,
                                                      unsigned int* va, unsigned int* kb, unsigned int* vb,
                                                      const int* cnt, int maxT) {
