@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
             mn[k] = min(mn[k], (unsigned int)__shfl_xor((int)mn[k], o, 64));
             mx[k] = max(mx[k], (unsigned int)__shfl_xor((int)mx[k], o, 64));
         }
-    __shared__ unsigned int red[4][6];
+    __shared__ unsigned int red[16][6];   // up to 16 waves
     const int w = threadIdx.x >> 6;
     if ((threadIdx.x & 63) == 0)
         for (int k = 0; k < 3; ++k) { red[w][k] = mn[k]; red[w][3 + k] = mx[k]; }
@@ -109,7 +109,13 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
 // non-finite point), split into npass digits of dbits <= VG_DMAX each
 struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, npass, ntiles; };
 
+#ifndef VG_T
 #define VG_T 256                      // threads per tile workgroup
+#endif
+#define VG_W (VG_T / 64)              // waves per tile workgroup (each owns a slice of the tile)
+#ifndef VG_SCATTER_OCC
+#define VG_SCATTER_OCC (VG_W == 4 ? 4 : 6)   // vg_scatter waves per SIMD the register budget keeps
+#endif
 #ifndef VG_IPT
 #define VG_IPT 16                     // items per thread
 #endif
@@ -119,7 +125,7 @@ struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbit
 #define VG_DMAX 8                     // digit bits per pass at most; VG_PASSES * VG_DMAX >= 32
 #endif
 #define VG_NB (1 << VG_DMAX)          // digit bins
-static_assert(VG_PASSES * VG_DMAX >= 32 && VG_NB % VG_T == 0, "VoxelGrid digit layout");
+static_assert(VG_PASSES * VG_DMAX >= 32 && (VG_NB % VG_T == 0 || VG_T % VG_NB == 0), "VoxelGrid digit layout");
 #define VG_PAD(j) ((j) + ((j) >> 4))  // LDS index padded against 16-way bank conflicts (blocked reads)
 
 __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
@@ -249,14 +255,14 @@ __global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, c
         unsigned int key[VG_IPT];
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {   // all of the tile's loads in flight before the first use
-            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             unsigned int val;
             key[k] = 0;
             if (j < m) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, nullptr, key[k], val);
         }
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
-            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             const bool ok = j < m;
             const unsigned int d = (key[k] >> shift) & mask;
             const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
@@ -291,14 +297,14 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T, 4) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
                                                      const VgParams* prm, int pass, unsigned int* ka,
                                                      unsigned int* va, unsigned int* kb, unsigned int* vb,
                                                      const int* cnt, int maxT) {
     __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
-    __shared__ int wc[4][VG_NB];   // per wave slice: running digit counts, then the slice's digit offsets
-    __shared__ int lb[VG_NB];      // global base of each digit minus its first position in the tile
-    __shared__ int wsum[4];
+    __shared__ int wc[VG_W][VG_NB];   // per wave slice: running digit counts, then the slice's digit offsets
+    __shared__ int lb[VG_NB];         // global base of each digit minus its first position in the tile
+    __shared__ int wsum[VG_W];
     const float4* in = FIRST ? src.pts() : nullptr;
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
@@ -313,13 +319,13 @@ __global__ void __launch_bounds__(VG_T, 4) k_vg_scatter(VgSrc src, size_t in_str
     const unsigned long long lt = (1ull << lane) - 1ull;
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
-        for (int d = tid; d < 4 * VG_NB; d += VG_T) (&wc[0][0])[d] = 0;
+        for (int d = tid; d < VG_W * VG_NB; d += VG_T) (&wc[0][0])[d] = 0;
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
-            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             const bool ok = j < m;
             key[k] = 0;
             val[k] = 0;
@@ -335,22 +341,22 @@ __global__ void __launch_bounds__(VG_T, 4) k_vg_scatter(VgSrc src, size_t in_str
         // digit-major, slice-minor exclusive scan of the counts: the tile-local
         // position of each (digit, slice) run
         {
-            constexpr int DPT = VG_NB / VG_T;   // consecutive digits per thread
+            constexpr int DPT = VG_NB >= VG_T ? VG_NB / VG_T : 1;   // consecutive digits per thread
             const int d0 = tid * DPT;
-            int c[DPT][4], tot = 0;
+            int c[DPT][VG_W], tot = 0;
 #pragma unroll
             for (int e = 0; e < DPT; ++e)
 #pragma unroll
-                for (int q = 0; q < 4; ++q) { c[e][q] = d0 + e < nb ? wc[q][d0 + e] : 0; tot += c[e][q]; }
+                for (int q = 0; q < VG_W; ++q) { c[e][q] = d0 + e < nb ? wc[q][d0 + e] : 0; tot += c[e][q]; }
             int total;
-            int run = vg_block_scan<4>(tot, wsum, &total);
+            int run = vg_block_scan<VG_W>(tot, wsum, &total);
 #pragma unroll
             for (int e = 0; e < DPT; ++e) {
                 const int d = d0 + e;
                 if (d < nb) {
                     const int start = run;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) { wc[q][d] = run; run += c[e][q]; }
+                    for (int q = 0; q < VG_W; ++q) { wc[q][d] = run; run += c[e][q]; }
                     if (run != start) lb[d] = cnt[((size_t)s * VG_NB + d) * maxT + t] - start;
                 }
             }
@@ -358,7 +364,7 @@ __global__ void __launch_bounds__(VG_T, 4) k_vg_scatter(VgSrc src, size_t in_str
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
-            const int j = w * (VG_TILE / 4) + k * 64 + lane;
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             if (j < m) {
                 const int pos = wc[w][(key[k] >> shift) & mask] + rk[k];
                 lk[pos] = key[k];
@@ -393,7 +399,7 @@ __device__ inline bool vg_head(const unsigned int* k, int j, unsigned int none) 
 
 __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, const int32_t* off, const VgParams* prm,
                                                    int* hcnt, int maxT) {
-    __shared__ int wsum[4];
+    __shared__ int wsum[VG_W];
     const int s = blockIdx.y, tid = threadIdx.x;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base;
@@ -408,7 +414,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, con
             if (j < m) c += vg_head(k, a + j, none);
         }
         int total;
-        vg_block_scan<4>(c, wsum, &total);
+        vg_block_scan<VG_W>(c, wsum, &total);
         if (tid == 0) hcnt[(size_t)s * maxT + t] = total;
     }
 }
@@ -441,7 +447,7 @@ __global__ void __launch_bounds__(1024) k_vg_hscan(const VgParams* prm, int* hcn
 // as the scatter reads them; ranks by ballot prefix counts)
 __global__ void __launch_bounds__(VG_T) k_vg_ranges(const unsigned int* keys, const int32_t* off, const VgParams* prm,
                                                     const int* hcnt, int maxT, int* starts, int* ends) {
-    __shared__ int wsum[4];
+    __shared__ int wsum[VG_W];
     const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base;
@@ -454,7 +460,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_ranges(const unsigned int* keys, co
         int wrun = 0;
 #pragma unroll
         for (int q = 0; q < VG_IPT; ++q) {
-            const int j = w * (VG_TILE / 4) + q * 64 + lane;
+            const int j = w * (VG_TILE / VG_W) + q * 64 + lane;
             hm[q] = __ballot(j < m && vg_head(k, a + j, none));
             wrun += __popcll(hm[q]);
         }
@@ -465,7 +471,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_ranges(const unsigned int* keys, co
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < VG_IPT; ++q) {
-            const int j = w * (VG_TILE / 4) + q * 64 + lane, i = a + j;
+            const int j = w * (VG_TILE / VG_W) + q * 64 + lane, i = a + j;
             const int incl = r + __popcll(hm[q] & le);   // voxels started at or before item i
             r += __popcll(hm[q]);
             if (j < m) {
@@ -600,11 +606,11 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     if (int r = ensure_ws(ctx, in_stride)) return r;
     const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
-    const int bx = std::max(1, std::min(64, (int)((in_stride + VG_T - 1) / VG_T)));
+    const int bx = std::max(1, std::min(64, (int)((in_stride + 255) / 256)));
     const dim3 grid(GX, S);
     const VgSrc src{in, d_n, ctx->v.io};
     SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta);
-    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(VG_T), 0, src, in_stride, w.off, w.bounds);
+    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, in_stride, w.off, w.bounds);
     SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
     hipEvent_t ev = nullptr;
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
@@ -781,7 +787,7 @@ __global__ void k_seg_top(int nblk, int32_t* bsum) {   // one wave per stream
 __global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int nblk, int32_t* bsum,
                                                    int32_t* out) {
     __shared__ int l[VG_TILE + VG_TILE / 16];
-    __shared__ int wsum[4];
+    __shared__ int wsum[VG_W];
     const int s = blockIdx.y, tid = threadIdx.x;
     const int32_t* c = in + (size_t)s * N;
     int32_t* o = out + (size_t)s * N;
@@ -798,7 +804,7 @@ __global__ void __launch_bounds__(VG_T) k_seg_down(const int32_t* in, int N, int
         for (int q = 0; q < VG_IPT; ++q) { x[q] = l[VG_PAD(tid * VG_IPT + q)]; sum += x[q]; }
         int total;
         const int top = bsum[(size_t)s * nblk + b];
-        int run = top + vg_block_scan<4>(sum, wsum, &total);
+        int run = top + vg_block_scan<VG_W>(sum, wsum, &total);
 #pragma unroll
         for (int q = 0; q < VG_IPT; ++q) { l[VG_PAD(tid * VG_IPT + q)] = run; run += x[q]; }
         __syncthreads();
