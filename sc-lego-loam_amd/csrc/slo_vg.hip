@@ -388,10 +388,11 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
 
 // ---- voxels of the sorted items: a voxel starts at each key change (the
 // "none" key of non-finite points is no voxel).  k_vg_heads counts the starts
-// per tile, k_vg_hscan ranks the tiles (and sets the output counts),
-// k_vg_bounds2 writes each voxel's item range [starts[r], ends[r]) at its
-// rank (= its output position: the voxels are in index order), and
-// k_vg_centroid sums each voxel's points.
+// per tile, k_vg_hscan ranks the tiles (and sets the output counts), then
+// k_vg_reduce (default) sums each voxel's points at its rank (= its output
+// position: the voxels are in index order).  SLO_VG_FUSED=0 builds the
+// two-kernel form instead: k_vg_ranges writes each voxel's item range
+// [starts[r], ends[r]) at its rank and k_vg_centroid sums it.
 __device__ inline bool vg_head(const unsigned int* k, int j, unsigned int none) {
     const unsigned int x = k[j];
     return x != none && (j == 0 || k[j - 1] != x);
@@ -562,6 +563,93 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
     }
 }
 
+// The ranges and the centroids in one pass (SLO_VG_FUSED): each wave takes its
+// slice of a tile (1024 consecutive sorted items at VG_T = 256), lists the
+// slice's key changes in LDS (voxel heads in order, then possibly the start of
+// the "none" items), and its lanes then take the heads in turn: head h's
+// voxel is [list[h], list[h + 1]), the last one running past the slice to the
+// next key change (found by a wave-wide ballot walk).  Its rank is the
+// tile's rank base plus the heads before it; the sum is the same in-order
+// float chain as k_vg_centroid, voxels over VG_SHORT points go to k_vg_long.
+#ifndef SLO_VG_FUSED
+#define SLO_VG_FUSED 1
+#endif
+__global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride, const unsigned int* keys,
+                                                    const unsigned int* vals, const int32_t* off, const VgParams* prm,
+                                                    const int* hcnt, int maxT, int32_t* meta, int4* longv,
+                                                    int nlong_cap, VgOut o) {
+    constexpr int SL = VG_TILE / VG_W;   // items per wave slice
+    __shared__ int lst[VG_W][SL + 1];
+    __shared__ int wsum[VG_W];
+    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base;
+    const unsigned int none = vg_none(p);
+    const unsigned int* k = keys + base;
+    const unsigned int* v = vals + base;
+    const float4* src = srcv.pts() + (size_t)s * in_stride;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    int* L = lst[w];
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        const int j0 = w * SL, i0 = a + j0;                 // this wave's slice: items [i0, i0 + ms)
+        const int ms = max(0, min(SL, m - j0));
+        int nh = 0, nc = 0, lasth = 0;                      // heads / key changes listed so far, the last head
+        for (int q = 0; q < SL / 64; ++q) {
+            const int j = q * 64 + lane, i = i0 + j;
+            bool chg = false, head = false;
+            if (j < ms) {
+                const unsigned int x = k[i];
+                chg = i == 0 || k[i - 1] != x;
+                head = chg && x != none;
+            }
+            const unsigned long long cm = __ballot(chg);
+            if (chg) L[nc + __popcll(cm & lt)] = i;
+            const unsigned long long hb = __ballot(head);
+            if (hb) lasth = i0 + q * 64 + 63 - __clzll((long long)hb);
+            nh += __popcll(hb);
+            nc += __popcll(cm);
+        }
+        // the end of the slice's last run: the next key change at or after the slice end
+        int eend = i0 + ms;
+        if (nh > 0 && nh == nc) {   // the last change listed is a head (not the "none" start)
+            const unsigned int x = k[lasth];
+            for (;;) {
+                const int i = eend + lane;
+                const bool stop = i >= n || k[i] != x;
+                const unsigned long long sb = __ballot(stop);
+                if (sb) { eend += __ffsll((long long)sb) - 1; break; }
+                eend += 64;
+            }
+        }
+        if (lane == 0) wsum[w] = nh;
+        __syncthreads();
+        int r0 = hcnt[(size_t)s * maxT + t];
+        for (int q = 0; q < w; ++q) r0 += wsum[q];
+        for (int h = lane; h < nh; h += 64) {
+            const int r = r0 + h;
+            if (r >= o.cap) break;
+            const int j = L[h], e = h + 1 < nc ? L[h + 1] : eend;
+            if (e - j > VG_SHORT) {
+                const int li = atomicAdd(&meta[2], 1);
+                if (li < nlong_cap) longv[li] = make_int4(s, j, r, e);
+                continue;
+            }
+            float sx = 0, sy = 0, sz = 0, si = 0;
+            for (int i = j; i < e; i += 4) {
+                float4 q4[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) q4[u] = i + u < e ? src[v[i + u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (i + u < e) { sx += q4[u].x; sy += q4[u].y; sz += q4[u].z; si += q4[u].w; }
+            }
+            vg_store(o, s, r, sx, sy, sz, si, e - j);
+        }
+        __syncthreads();   // wsum and the lists are reused by the next tile
+    }
+}
+
 // workspace for S streams of up to `stride` items: allocated on the host from
 // the strides alone (never from a device count), grown geometrically
 static int ensure_ws(slo_ctx* ctx, size_t stride) {
@@ -663,9 +751,15 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT);
     SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, w.prm, w.hcnt, maxT, w.nvox, d_nout, nout_stride,
                out_cap, w.errflag);
-    SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
-    SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid, dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S),
-               dim3(VG_T), 0, src, in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
+    if (SLO_VG_FUSED) {
+        SLO_LAUNCH(ctx, "vg_reduce", k_vg_reduce, grid, dim3(VG_T), 0, src, in_stride, k0, v0, w.off, w.prm, w.hcnt,
+                   maxT, w.meta, w.longv, (int)w.nlong_cap, o);
+    } else {
+        SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
+        SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid,
+                   dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src,
+                   in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
+    }
     SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, in_stride, v0, w.off, w.meta, w.longv,
                (int)w.nlong_cap, o);
     SLO_CHECK(hipGetLastError());
