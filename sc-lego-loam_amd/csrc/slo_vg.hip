@@ -128,6 +128,23 @@ struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbit
 static_assert(VG_PASSES * VG_DMAX >= 32 && (VG_NB % VG_T == 0 || VG_T % VG_NB == 0), "VoxelGrid digit layout");
 #define VG_PAD(j) ((j) + ((j) >> 4))  // LDS index padded against 16-way bank conflicts (blocked reads)
 
+// Tile kernels run on a (GX, S8) grid, S8 = S rounded up to 8.  With VG_XCD
+// the linear workgroup id is split XCD-aware (xcd_stream_chunk): all GX
+// workgroups of a stream land on one XCD, so a stream's tiles share that
+// XCD's L2 (its scatter runs, its sorted keys, the points its voxels gather).
+#ifndef VG_XCD
+#define VG_XCD 1
+#endif
+__device__ inline bool vg_block(int S, int& s, int& chunk) {
+#if VG_XCD
+    xcd_stream_chunk(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x, s, chunk);
+#else
+    s = blockIdx.y; chunk = blockIdx.x;
+#endif
+    return s < S;
+}
+static inline dim3 vg_tile_grid(int GX, int S) { return dim3(GX, (S + 7) / 8 * 8); }
+
 __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
@@ -238,17 +255,19 @@ __device__ inline void vg_load(const float4* in, size_t in_stride, const VgParam
 template <bool FIRST>
 __global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, const int32_t* off,
                                                   const VgParams* prm, int pass, const unsigned int* ka,
-                                                  const unsigned int* kb, int* cnt, int maxT) {
+                                                  const unsigned int* kb, int* cnt, int maxT, int S) {
     const float4* in = FIRST ? src.pts() : nullptr;
     __shared__ int h[VG_NB];
-    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int s, chunk;
+    if (!vg_block(S, s, chunk)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     if (pass >= p.npass) return;
     const unsigned int* kin = vg_out_b(p, pass - 1) ? kb : ka;
     const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
     const unsigned int mask = (unsigned int)nb - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+    for (int t = chunk; t < p.ntiles; t += gridDim.x) {
         for (int d = tid; d < nb; d += VG_T) h[d] = 0;
         __syncthreads();
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
@@ -300,13 +319,15 @@ template <bool FIRST>
 __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
                                                      const VgParams* prm, int pass, unsigned int* ka,
                                                      unsigned int* va, unsigned int* kb, unsigned int* vb,
-                                                     const int* cnt, int maxT) {
+                                                     const int* cnt, int maxT, int S) {
     __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
     __shared__ int wc[VG_W][VG_NB];   // per wave slice: running digit counts, then the slice's digit offsets
     __shared__ int lb[VG_NB];         // global base of each digit minus its first position in the tile
     __shared__ int wsum[VG_W];
     const float4* in = FIRST ? src.pts() : nullptr;
-    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int s, chunk;
+    if (!vg_block(S, s, chunk)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     if (pass >= p.npass) return;
     const bool ob = vg_out_b(p, pass);
@@ -317,7 +338,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
     const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
     const unsigned int mask = (unsigned int)nb - 1u;
     const unsigned long long lt = (1ull << lane) - 1ull;
-    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+    for (int t = chunk; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         for (int d = tid; d < VG_W * VG_NB; d += VG_T) (&wc[0][0])[d] = 0;
         __syncthreads();
@@ -399,14 +420,16 @@ __device__ inline bool vg_head(const unsigned int* k, int j, unsigned int none) 
 }
 
 __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, const int32_t* off, const VgParams* prm,
-                                                   int* hcnt, int maxT) {
+                                                   int* hcnt, int maxT, int S) {
     __shared__ int wsum[VG_W];
-    const int s = blockIdx.y, tid = threadIdx.x;
+    int s, chunk;
+    if (!vg_block(S, s, chunk)) return;
+    const int tid = threadIdx.x;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base;
     const unsigned int none = vg_none(p);
     const unsigned int* k = keys + base;
-    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+    for (int t = chunk; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         int c = 0;
 #pragma unroll 4
@@ -577,11 +600,13 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
 __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride, const unsigned int* keys,
                                                     const unsigned int* vals, const int32_t* off, const VgParams* prm,
                                                     const int* hcnt, int maxT, int32_t* meta, int4* longv,
-                                                    int nlong_cap, VgOut o) {
+                                                    int nlong_cap, VgOut o, int S) {
     constexpr int SL = VG_TILE / VG_W;   // items per wave slice
     __shared__ int lst[VG_W][SL + 1];
     __shared__ int wsum[VG_W];
-    const int s = blockIdx.y, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int s, chunk;
+    if (!vg_block(S, s, chunk)) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base;
     const unsigned int none = vg_none(p);
@@ -590,7 +615,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
     const float4* src = srcv.pts() + (size_t)s * in_stride;
     const unsigned long long lt = (1ull << lane) - 1ull;
     int* L = lst[w];
-    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+    for (int t = chunk; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         const int j0 = w * SL, i0 = a + j0;                 // this wave's slice: items [i0, i0 + ms)
         const int ms = max(0, min(SL, m - j0));
@@ -695,7 +720,7 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     const int bx = std::max(1, std::min(64, (int)((in_stride + 255) / 256)));
-    const dim3 grid(GX, S);
+    const dim3 grid = vg_tile_grid(GX, S);
     const VgSrc src{in, d_n, ctx->v.io};
     SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta);
     SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, in_stride, w.off, w.bounds);
@@ -709,18 +734,18 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     for (int pass = 0; pass < VG_PASSES; ++pass) {
         if (pass == 0) {
             SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
-                       kb, w.cnt, maxT);
+                       kb, w.cnt, maxT, S);
         } else {
             SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
-                       kb, w.cnt, maxT);
+                       kb, w.cnt, maxT, S);
         }
         SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, pass, w.cnt, maxT);
         if (pass == 0) {
             SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       ka, va, kb, vb, w.cnt, maxT);
+                       ka, va, kb, vb, w.cnt, maxT, S);
         } else {
             SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       ka, va, kb, vb, w.cnt, maxT);
+                       ka, va, kb, vb, w.cnt, maxT, S);
         }
     }
     if (tm) timing_end(ctx, sort_name.c_str(), ev);
@@ -742,20 +767,20 @@ int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, co
     if (int r = vg_sort(ctx, tag, in, in_stride, d_n, n_stride, leaf, &k0, &v0, &k1, &v1)) return r;
     const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
-    const dim3 grid(GX, S);
+    const dim3 grid = vg_tile_grid(GX, S);
     const VgOut o{out, out_stride, out_cap};
     const VgSrc src{in, d_n, ctx->v.io};
     // the ping-pong buffers the sort is done with hold the voxel ranges
     int* starts = (int*)k1;
     int* ends = (int*)v1;
-    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT);
+    SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, S);
     SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, w.prm, w.hcnt, maxT, w.nvox, d_nout, nout_stride,
                out_cap, w.errflag);
     if (SLO_VG_FUSED) {
         SLO_LAUNCH(ctx, "vg_reduce", k_vg_reduce, grid, dim3(VG_T), 0, src, in_stride, k0, v0, w.off, w.prm, w.hcnt,
-                   maxT, w.meta, w.longv, (int)w.nlong_cap, o);
+                   maxT, w.meta, w.longv, (int)w.nlong_cap, o, S);
     } else {
-        SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
+        SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, dim3(GX, S), dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
         SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid,
                    dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src,
                    in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
