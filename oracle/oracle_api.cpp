@@ -262,12 +262,6 @@ int oracle_umeyama(const float* src, const float* dst, int n, float* T) {
 }
 // JacobiSVD<Matrix3d> of a row-major 3x3
 int oracle_svd3(const double* A, double* U, double* S, double* V) { return jacobi_svd3(A, U, S, V) ? 0 : -1; }
-// slo_libm_d.h elementwise: which = 0 sin, 1 cos, 2 atan2(a, b), 3 asin
-void oracle_libm_d(int which, const double* a, const double* b, double* out, int n) {
-    for (int i = 0; i < n; ++i)
-        out[i] = which == 0 ? slo_libm::sin_d(a[i]) : which == 1 ? slo_libm::cos_d(a[i])
-               : which == 2 ? slo_libm::atan2_d(a[i], b[i]) : slo_libm::asin_d(a[i]);
-}
 // the mapping node's angle round trips (oracle_tf.h): which = 0 tf hand-off, 1 keyframe estimate
 void oracle_pose_roundtrip(int which, const float* in, float* out) {
     if (which == 0) odom_handoff(in, out);
@@ -445,26 +439,6 @@ float oracle_ddsum(const float* a, const float* b, int n, int mode) {
         v.swap(w);
     }
     return to_float(v[0]);
-}
-
-// ---- libm self-test against the host glibc (tests/test_libm.py)
-long oracle_libm_selftest(long n, unsigned long seed) {
-    uint64_t st = seed * 0x9E3779B97F4A7C15ULL + 1;
-    auto nx = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
-    long bad = 0;
-    for (long i = 0; i < n; ++i) {
-        uint64_t r = nx();
-        float y = slo_libm::u2f((uint32_t)r), x = slo_libm::u2f((uint32_t)(r >> 32));
-        if (i & 1) { y = (float)((int32_t)(r & 0xffffff) - 0x800000) * 1e-5f; x = (float)((int32_t)((r >> 24) & 0xffffff) - 0x800000) * 1e-5f; }
-        auto same = [](float a, float b) { return slo_libm::f2u(a) == slo_libm::f2u(b) || (std::isnan(a) && std::isnan(b)); };
-        if (!same(slo_libm::atan2f_(y, x), atan2f(y, x))) bad++;
-        if (!same(slo_libm::sinf_(y), sinf(y))) bad++;
-        if (!same(slo_libm::cosf_(y), cosf(y))) bad++;
-        if (!same(slo_libm::atanf_(y), atanf(y))) bad++;
-        float u = fmodf(y, 1.0f);
-        if (!same(slo_libm::asinf_(u), asinf(u))) bad++;
-    }
-    return bad;
 }
 
 // ---- generator passthrough (same header the product library uses)

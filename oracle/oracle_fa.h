@@ -92,7 +92,7 @@ struct FeatureAssociation {
 
     // ------------------------------------------------------------ IMU
     void updateImuRollPitchYawStartSinCos() {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         cosImuRollStart = cosf_(imuRollStart); cosImuPitchStart = cosf_(imuPitchStart); cosImuYawStart = cosf_(imuYawStart);
         sinImuRollStart = sinf_(imuRollStart); sinImuPitchStart = sinf_(imuPitchStart); sinImuYawStart = sinf_(imuYawStart);
     }
@@ -113,7 +113,7 @@ struct FeatureAssociation {
     }
 
     void TransformToStartIMU(Pt* p) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float x1 = cosf_(imuRollCur) * p->x - sinf_(imuRollCur) * p->y;
         float y1 = sinf_(imuRollCur) * p->x + cosf_(imuRollCur) * p->y;
         float z1 = p->z;
@@ -135,7 +135,7 @@ struct FeatureAssociation {
     }
 
     void AccumulateIMUShiftAndRotation() {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float roll = imuRoll[imuPointerLast];
         float pitch = imuPitch[imuPointerLast];
         float yaw = imuYaw[imuPointerLast];
@@ -167,7 +167,7 @@ struct FeatureAssociation {
     }
 
     void imuHandler(const ImuMsg& imuIn) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         double roll, pitch, yaw;
         tf_get_rpy(TfQuat{imuIn.qx, imuIn.qy, imuIn.qz, imuIn.qw}, roll, pitch, yaw);
         float accX = imuIn.ay - sin_d(roll) * cos_d(pitch) * 9.81;
@@ -196,7 +196,7 @@ struct FeatureAssociation {
             point.x = segmentedCloud[i].y;
             point.y = segmentedCloud[i].z;
             point.z = segmentedCloud[i].x;
-            float ori = -slo_libm::atan2f_(point.x, point.z);
+            float ori = -oracle_libm::atan2f_(point.x, point.z);
             if (!halfPassed) {
                 if (ori < segInfo.startOrientation - M_PI / 2) ori = (float)(ori + 2 * M_PI);
                 else if (ori > segInfo.startOrientation + M_PI * 3 / 2) ori = (float)(ori - 2 * M_PI);
@@ -399,7 +399,7 @@ struct FeatureAssociation {
 
     // ------------------------------------------------------------ transforms
     void TransformToStart(const Pt& pi, Pt& po) const {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float s = 10 * (pi.intensity - (float)(int)pi.intensity);
         float rx = s * transformCur[0], ry = s * transformCur[1], rz = s * transformCur[2];
         float tx = s * transformCur[3], ty = s * transformCur[4], tz = s * transformCur[5];
@@ -416,7 +416,7 @@ struct FeatureAssociation {
     }
 
     void TransformToEnd(const Pt& pi, Pt& po) const {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float s = 10 * (pi.intensity - (float)(int)pi.intensity);
         float rx = s * transformCur[0], ry = s * transformCur[1], rz = s * transformCur[2];
         float tx = s * transformCur[3], ty = s * transformCur[4], tz = s * transformCur[5];
@@ -463,7 +463,7 @@ struct FeatureAssociation {
 
     static void PluginIMURotation(float bcx, float bcy, float bcz, float blx, float bly, float blz,
                                   float alx, float aly, float alz, float& acx, float& acy, float& acz) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float sbcx = sinf_(bcx), cbcx = cosf_(bcx), sbcy = sinf_(bcy), cbcy = cosf_(bcy);
         float sbcz = sinf_(bcz), cbcz = cosf_(bcz);
         float sblx = sinf_(blx), cblx = cosf_(blx), sbly = sinf_(bly), cbly = cosf_(bly);
@@ -512,7 +512,7 @@ struct FeatureAssociation {
 
     static void AccumulateRotation(float cx, float cy, float cz, float lx, float ly, float lz,
                                    float& ox, float& oy, float& oz) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float srx = cosf_(lx) * cosf_(cx) * sinf_(ly) * sinf_(cz) - cosf_(cx) * cosf_(cz) * sinf_(lx) -
                     cosf_(lx) * cosf_(ly) * sinf_(cx);
         ox = -asinf_(srx);
@@ -685,7 +685,7 @@ struct FeatureAssociation {
     }
 
     bool calculateTransformationSurf(int iterCount) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         int pointSelNum = (int)laserCloudOri.size();
         std::vector<float> A(pointSelNum * 3), B(pointSelNum);
         float srx = sinf_(transformCur[0]), crx = cosf_(transformCur[0]);
@@ -724,7 +724,7 @@ struct FeatureAssociation {
     }
 
     bool calculateTransformationCorner(int iterCount) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         int pointSelNum = (int)laserCloudOri.size();
         std::vector<float> A(pointSelNum * 3), B(pointSelNum);
         float srx = sinf_(transformCur[0]), crx = cosf_(transformCur[0]);
@@ -777,7 +777,7 @@ struct FeatureAssociation {
     }
 
     void integrateTransformation() {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float rx, ry, rz, tx, ty, tz;
         AccumulateRotation(transformSum[0], transformSum[1], transformSum[2], -transformCur[0], -transformCur[1],
                            -transformCur[2], rx, ry, rz);

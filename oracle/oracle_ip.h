@@ -3,13 +3,13 @@
 // publishing).  Follows the reference line by line, including the quirks of
 // Q1 (float -> size_t row truncation), Q2 (last point
 // wins), Q3 (BFS row count excludes the seed), Q15 (ground overwrite order).
-// Math goes through slo_libm (bit-identical to glibc float atan2f/sinf/cosf,
-// which is what `using namespace std` resolves to in the reference).
+// Math is the host glibc's own atan2f / sinf / cosf (oracle_libm.h), which is
+// what `using namespace std` resolves to in the reference.
 #pragma once
 
 #include "oracle_common.h"
 #include "../sc-lego-loam_amd/csrc/slo_config.h"
-#include "../sc-lego-loam_amd/csrc/slo_libm.h"
+#include "oracle_libm.h"
 
 namespace oracle {
 
@@ -76,8 +76,8 @@ struct ImageProjection {
     void findStartEndAngle() {  // IP:199-209
         const Pt& f = laserCloudIn.front();
         const Pt& l = laserCloudIn.back();
-        segMsg.startOrientation = -slo_libm::atan2f_(f.y, f.x);
-        segMsg.endOrientation = (float)(-slo_libm::atan2f_(l.y, l.x) + 2 * M_PI);
+        segMsg.startOrientation = -oracle_libm::atan2f_(f.y, f.x);
+        segMsg.endOrientation = (float)(-oracle_libm::atan2f_(l.y, l.x) + 2 * M_PI);
         if (segMsg.endOrientation - segMsg.startOrientation > 3 * M_PI)
             segMsg.endOrientation = (float)(segMsg.endOrientation - 2 * M_PI);
         else if (segMsg.endOrientation - segMsg.startOrientation < M_PI)
@@ -96,7 +96,7 @@ struct ImageProjection {
                 // reference requires is_dense clouds, IP:174-177)
                 rowIdn = i < rings.size() ? (int64_t)rings[i] : 0;
             } else {
-                float verticalAngle = (float)((double)(slo_libm::atan2f_(thisPoint.z,
+                float verticalAngle = (float)((double)(oracle_libm::atan2f_(thisPoint.z,
                     sqrtf(thisPoint.x * thisPoint.x + thisPoint.y * thisPoint.y)) * 180) / M_PI);
                 float rowf = (verticalAngle + cfg.ang_bottom) / cfg.ang_res_y;
                 // Q1: float -> size_t; negative values in (-1, 0) truncate to 0,
@@ -104,7 +104,7 @@ struct ImageProjection {
                 rowIdn = (int64_t)rowf;  // truncation toward zero
             }
             if (rowIdn < 0 || rowIdn >= R) continue;
-            float horizonAngle = (float)((double)(slo_libm::atan2f_(thisPoint.x, thisPoint.y) * 180) / M_PI);
+            float horizonAngle = (float)((double)(oracle_libm::atan2f_(thisPoint.x, thisPoint.y) * 180) / M_PI);
             double colD = -round(((double)horizonAngle - 90.0) / (double)cfg.ang_res_x) + (double)(C / 2);
             int64_t columnIdn = (int64_t)colD;
             if (columnIdn >= C) columnIdn -= C;
@@ -133,7 +133,7 @@ struct ImageProjection {
                 float diffX = fullCloud[upperInd].x - fullCloud[lowerInd].x;
                 float diffY = fullCloud[upperInd].y - fullCloud[lowerInd].y;
                 float diffZ = fullCloud[upperInd].z - fullCloud[lowerInd].z;
-                float angle = (float)((double)(slo_libm::atan2f_(diffZ, sqrtf(diffX * diffX + diffY * diffY)) * 180) / M_PI);
+                float angle = (float)((double)(oracle_libm::atan2f_(diffZ, sqrtf(diffX * diffX + diffY * diffY)) * 180) / M_PI);
                 if (fabsf(angle - cfg.sensor_mount_angle) <= 10) {
                     groundMat[i * C + j] = 1;
                     groundMat[(i + 1) * C + j] = 1;
@@ -169,7 +169,7 @@ struct ImageProjection {
                 float sa, ca;
                 if (nb[it][0] == 0) { sa = cfg.sin_alpha_x; ca = cfg.cos_alpha_x; }
                 else { sa = cfg.sin_alpha_y; ca = cfg.cos_alpha_y; }
-                float angle = slo_libm::atan2f_(d2 * sa, (d1 - d2 * ca));
+                float angle = oracle_libm::atan2f_(d2 * sa, (d1 - d2 * ca));
                 if (angle > cfg.segment_theta) {
                     queueIndX[queueEndInd] = thisIndX; queueIndY[queueEndInd] = thisIndY;
                     ++queueSize; ++queueEndInd;

@@ -270,9 +270,9 @@ inline void icp_align(const slo_config& cfg, const Cloud& src, const Cloud& tgt,
     r.fitness = nr > 0 ? (fs.hi + fs.lo) / (double)nr : DBL_MAX;
     r.accepted = r.converged && !(r.fitness > (double)cfg.history_keyframe_fitness_score);
     r.xyzrpy[0] = r.T[3]; r.xyzrpy[1] = r.T[7]; r.xyzrpy[2] = r.T[11];
-    r.xyzrpy[3] = slo_libm::atan2f_(r.T[9], r.T[10]);   // roll = atan2(t(2,1), t(2,2))
-    r.xyzrpy[4] = slo_libm::asinf_(-r.T[8]);           // pitch = asin(-t(2,0))
-    r.xyzrpy[5] = slo_libm::atan2f_(r.T[4], r.T[0]);    // yaw = atan2(t(1,0), t(0,0))
+    r.xyzrpy[3] = oracle_libm::atan2f_(r.T[9], r.T[10]);   // roll = atan2(t(2,1), t(2,2))
+    r.xyzrpy[4] = oracle_libm::asinf_(-r.T[8]);           // pitch = asin(-t(2,0))
+    r.xyzrpy[5] = oracle_libm::atan2f_(r.T[4], r.T[0]);    // yaw = atan2(t(1,0), t(0,0))
 }
 
 // (int)intensity >= 0 (MO:884-889, 931-936) with x86's cvttss2si semantics

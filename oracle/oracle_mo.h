@@ -79,7 +79,7 @@ struct MapOptimization {
     static void associate_to_map(const float* transformSum, const float* transformBefMapped,
                                  const float* transformAftMapped, float* transformIncre,
                                  float* transformTobeMapped) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float x1 = cosf_(transformSum[1]) * (transformBefMapped[3] - transformSum[3]) -
                    sinf_(transformSum[1]) * (transformBefMapped[5] - transformSum[5]);
         float y1 = transformBefMapped[4] - transformSum[4];
@@ -161,7 +161,7 @@ struct MapOptimization {
     }
 
     void updatePointAssociateToMapSinCos() {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         cRoll = cosf_(transformTobeMapped[0]); sRoll = sinf_(transformTobeMapped[0]);
         cPitch = cosf_(transformTobeMapped[1]); sPitch = sinf_(transformTobeMapped[1]);
         cYaw = cosf_(transformTobeMapped[2]); sYaw = sinf_(transformTobeMapped[2]);
@@ -177,7 +177,7 @@ struct MapOptimization {
         return {cPitch * x2 + sPitch * z2 + tX, y2 + tY, -sPitch * x2 + cPitch * z2 + tZ, pi.intensity};
     }
     static Cloud transformPointCloud(const Cloud& in, const Pose6& t) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float ctRoll = cosf_(t.roll), stRoll = sinf_(t.roll);
         float ctPitch = cosf_(t.pitch), stPitch = sinf_(t.pitch);
         float ctYaw = cosf_(t.yaw), stYaw = sinf_(t.yaw);
@@ -375,7 +375,7 @@ struct MapOptimization {
     }
 
     bool LMOptimization(int iterCount) {
-        using namespace slo_libm;
+        using namespace oracle_libm;
         float srx = sinf_(transformTobeMapped[0]), crx = cosf_(transformTobeMapped[0]);
         float sry = sinf_(transformTobeMapped[1]), cry = cosf_(transformTobeMapped[1]);
         float srz = sinf_(transformTobeMapped[2]), crz = cosf_(transformTobeMapped[2]);

@@ -71,8 +71,6 @@ def lib():
         L.oracle_get.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_config_preset.argtypes = [ctypes.c_int, ctypes.POINTER(SloConfig)]
         L.oracle_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-        L.oracle_libm_selftest.restype = ctypes.c_long
-        L.oracle_libm_selftest.argtypes = [ctypes.c_long, ctypes.c_ulong]
         L.oracle_bench.restype = ctypes.c_double
         L.oracle_bench.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_sc_distance.restype = ctypes.c_double
@@ -109,7 +107,6 @@ def lib():
                                        ctypes.c_void_p]
         L.oracle_ddsum.restype = ctypes.c_float
         L.oracle_ddsum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-        L.oracle_libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         _LIB = L
     return _LIB
 

@@ -17,7 +17,7 @@
 
 #include "oracle_common.h"
 #include "../sc-lego-loam_amd/csrc/slo_config.h"
-#include "../sc-lego-loam_amd/csrc/slo_libm.h"
+#include "oracle_libm.h"
 
 namespace oracle {
 
@@ -55,7 +55,7 @@ struct SCManager {
     float xy2theta(float x, float y) const {
         // atan(float) resolves to atanf (default) or ::atan(double) (Q12b)
         auto at = [&](float v) -> double {
-            return cfg.sc_atan_float ? (double)slo_libm::atanf_(v) : atan((double)v);
+            return cfg.sc_atan_float ? (double)oracle_libm::atanf_(v) : atan((double)v);
         };
         if ((x >= 0) & (y >= 0)) return (float)((180 / M_PI) * at(y / x));
         if ((x < 0) & (y >= 0)) return (float)(180 - ((180 / M_PI) * at(y / (-x))));

@@ -20,12 +20,13 @@
 // Inside (-pi, pi] (pitch inside [-pi/2, pi/2]) both round trips give back
 // the input float; outside they wrap, which is why they matter: the heading
 // of a vehicle driving a loop leaves (-pi, pi] and the reference's mapping
-// then sees the wrapped angle.  The double sin/cos/atan2/asin are the shared
-// fdlibm restatement (slo_libm_d.h, within 1 ulp of glibc's) so that the
-// float casts agree with the device bit for bit even for tiny angles.
+// then sees the wrapped angle.  The double sin/cos/atan2/asin are the host
+// glibc's (oracle_libm.h), as tf's are in the reference; the device uses the
+// fdlibm restatement (slo_libm_d.h, within 1 ulp of glibc), and the float casts
+// are where the two must agree.
 #pragma once
 #include <cmath>
-#include "../sc-lego-loam_amd/csrc/slo_libm_d.h"
+#include "oracle_libm.h"
 
 namespace oracle {
 
@@ -34,9 +35,9 @@ struct TfQuat { double x, y, z, w; };
 // tf::Quaternion::setRPY
 inline TfQuat tf_set_rpy(double roll, double pitch, double yaw) {
     const double hy = yaw * 0.5, hp = pitch * 0.5, hr = roll * 0.5;
-    const double cy = slo_libm::cos_d(hy), sy = slo_libm::sin_d(hy);
-    const double cp = slo_libm::cos_d(hp), sp = slo_libm::sin_d(hp);
-    const double cr = slo_libm::cos_d(hr), sr = slo_libm::sin_d(hr);
+    const double cy = oracle_libm::cos_d(hy), sy = oracle_libm::sin_d(hy);
+    const double cp = oracle_libm::cos_d(hp), sp = oracle_libm::sin_d(hp);
+    const double cr = oracle_libm::cos_d(hr), sr = oracle_libm::sin_d(hr);
     return {sr * cp * cy - cr * sp * sy, cr * sp * cy + sr * cp * sy, cr * cp * sy - sr * sp * cy,
             cr * cp * cy + sr * sp * sy};
 }
@@ -54,7 +55,7 @@ inline void tf_get_rpy(const TfQuat& q, double& roll, double& pitch, double& yaw
     const double m20 = xz - wy, m21 = yz + wx, m22 = 1.0 - (xx + yy);
     if (std::fabs(m20) >= 1) {   // gimbal lock (pitch = +-90 deg; unreachable for a ground vehicle, unpinned)
         yaw = 0;
-        const double delta = slo_libm::atan2_d(m01, m02);
+        const double delta = oracle_libm::atan2_d(m01, m02);
         if (m20 > 0) { pitch = M_PI / 2.0; roll = pitch + delta; }
         else { pitch = -M_PI / 2.0; roll = -pitch + delta; }
         return;
@@ -62,10 +63,10 @@ inline void tf_get_rpy(const TfQuat& q, double& roll, double& pitch, double& yaw
     double a = m20;
     if (a < -1) a = -1;
     if (a > 1) a = 1;   // tfAsin clamps
-    pitch = -slo_libm::asin_d(a);
-    const double c = slo_libm::cos_d(pitch);
-    roll = slo_libm::atan2_d(m21 / c, m22 / c);
-    yaw = slo_libm::atan2_d(m10 / c, m00 / c);
+    pitch = -oracle_libm::asin_d(a);
+    const double c = oracle_libm::cos_d(pitch);
+    roll = oracle_libm::atan2_d(m21 / c, m22 / c);
+    yaw = oracle_libm::atan2_d(m10 / c, m00 / c);
 }
 
 // publishOdometry (FA:1728-1734) -> laserOdometryHandler (MO:658-666)
@@ -85,9 +86,9 @@ inline void odom_handoff(const float ts[6], float out[6]) {
 
 // Rot3::RzRyRx(x, y, z) = Rz(z) Ry(y) Rx(x), row-major
 inline void gtsam_rzryrx(double x, double y, double z, double R[9]) {
-    const double cx = slo_libm::cos_d(x), sx = slo_libm::sin_d(x);
-    const double cy = slo_libm::cos_d(y), sy = slo_libm::sin_d(y);
-    const double cz = slo_libm::cos_d(z), sz = slo_libm::sin_d(z);
+    const double cx = oracle_libm::cos_d(x), sx = oracle_libm::sin_d(x);
+    const double cy = oracle_libm::cos_d(y), sy = oracle_libm::sin_d(y);
+    const double cz = oracle_libm::cos_d(z), sz = oracle_libm::sin_d(z);
     const double ss_ = sx * sy, cs_ = cx * sy, sc_ = sx * cy, cc_ = cx * cy;
     const double c_s = cx * sz, s_s = sx * sz, _cs = cy * sz, _cc = cy * cz;
     const double s_c = sx * cz, c_c = cx * cz;
@@ -105,17 +106,17 @@ inline void mul33(const double A[9], const double B[9], double C[9]) {
 
 // Rot3::xyz() through RQ(A) (Rot3.cpp): x = roll(), y = pitch(), z = yaw()
 inline void gtsam_xyz(const double A[9], double& x, double& y, double& z) {
-    x = -slo_libm::atan2_d(-A[7], A[8]);
-    const double c1 = slo_libm::cos_d(-x), s1 = slo_libm::sin_d(-x);
+    x = -oracle_libm::atan2_d(-A[7], A[8]);
+    const double c1 = oracle_libm::cos_d(-x), s1 = oracle_libm::sin_d(-x);
     const double Qx[9] = {1, 0, 0, 0, c1, -s1, 0, s1, c1};
     double B[9];
     mul33(A, Qx, B);
-    y = -slo_libm::atan2_d(B[6], B[8]);
-    const double c2 = slo_libm::cos_d(-y), s2 = slo_libm::sin_d(-y);
+    y = -oracle_libm::atan2_d(B[6], B[8]);
+    const double c2 = oracle_libm::cos_d(-y), s2 = oracle_libm::sin_d(-y);
     const double Qy[9] = {c2, 0, s2, 0, 1, 0, -s2, 0, c2};
     double C[9];
     mul33(B, Qy, C);
-    z = -slo_libm::atan2_d(-C[3], C[4]);
+    z = -oracle_libm::atan2_d(-C[3], C[4]);
 }
 
 // the new keyframe's iSAM2 estimate read back (MO:1545-1548/1555-1556, 1588-1601)

@@ -1,5 +1,6 @@
-"""CPU tests of the oracle (test infrastructure): the restated glibc libm and
-libstdc++ introsort against the host's, the Scan Context K-NN against the
+"""CPU tests of the oracle (test infrastructure) and of the product's host-side
+restatements: the restated glibc libm and libstdc++ introsort against the
+host's, the Scan Context K-NN against the
 reference's own nanoflann tree (committed fixture), and the oracle against
 its committed stage fingerprints (tests/golden/make_golden.py)."""
 import json
@@ -15,23 +16,37 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 GOLD = os.path.join(HERE, "golden")
 
 
-def test_libm_restatement_matches_glibc():
+@pytest.fixture(scope="module")
+def libm_check(tmp_path_factory):
+    """tests/cpp/libm_check.cpp: the product's libm restatements (slo_libm.h,
+    slo_libm_d.h), compiled with the product's -ffp-contract=off rule"""
+    import ctypes
+    so = tmp_path_factory.mktemp("libm") / "libm_check.so"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared", "-o", str(so),
+                    os.path.join(HERE, "cpp", "libm_check.cpp")], check=True)
+    L = ctypes.CDLL(str(so))
+    L.libm_selftest.restype = ctypes.c_long
+    L.libm_selftest.argtypes = [ctypes.c_long, ctypes.c_ulong]
+    L.libm_d.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    return L
+
+
+def test_libm_restatement_matches_glibc(libm_check):
     # atan2f, sinf, cosf, atanf, asinf bit-for-bit vs the host glibc
     for seed in (1, 7, 12345):
-        assert O.lib().oracle_libm_selftest(300000, seed) == 0
+        assert libm_check.libm_selftest(300000, seed) == 0
 
 
-def _libm_d(which, a, b=None):
-    import ctypes  # noqa: F401
+def _libm_d(L, which, a, b=None):
     a = np.ascontiguousarray(a, np.float64)
     b = np.ascontiguousarray(a if b is None else b, np.float64)
     out = np.zeros_like(a)
-    O.lib().oracle_libm_d(which, a.ctypes.data, b.ctypes.data, out.ctypes.data, len(a))
+    L.libm_d(which, a.ctypes.data, b.ctypes.data, out.ctypes.data, len(a))
     return out
 
 
-def test_double_libm_within_one_ulp_of_glibc():
-    # slo_libm_d.h (fdlibm sin/cos/atan2/asin, shared by the oracle and the
+def test_double_libm_within_one_ulp_of_glibc(libm_check):
+    # slo_libm_d.h (fdlibm sin/cos/atan2/asin, the
     # device for the Q18 round trips) against the host glibc via Python's math
     import math
     rng = np.random.default_rng(3)
@@ -42,7 +57,7 @@ def test_double_libm_within_one_ulp_of_glibc():
              (3, np.concatenate([rng.uniform(-1, 1, n), rng.uniform(-1e-4, 1e-4, n)]), None, math.asin),
              (2, rng.normal(size=n) * 10.0 ** rng.integers(-8, 3, n), rng.normal(size=n), math.atan2)]
     for which, a, b, f in cases:
-        got = _libm_d(which, a, b)
+        got = _libm_d(libm_check, which, a, b)
         want = np.array([f(*v) for v in (zip(a, b) if b is not None else ((x,) for x in a))])
         ulp = np.abs(got.view(np.int64) - want.view(np.int64))
         assert ulp.max() <= 1, (which, int(ulp.max()))
