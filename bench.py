@@ -140,6 +140,11 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
     if name == "vg_scatter":      # the mapping step's 7 VoxelGrid sorts, 4 radix passes each: pass 0 reads the
         # point (16 B) and writes (key, index) 8 B, passes 1-3 read and write 8 B
         return map_steps * int(c["vg_in"].sum()) * (16 + 8 + 3 * 16)
+    if name == "vg_onesweep":     # the same four passes as single-pass scatters (the look-back posts are
+        # 256 x 8 B per 4096-item tile, not priced)
+        return map_steps * int(c["vg_in"].sum()) * (16 + 8 + 3 * 16)
+    if name == "vg_ghist":        # every pass's digit counts from one read of the points
+        return map_steps * int(c["vg_in"].sum()) * 16
     if name == "vg_hist":         # pass 0 reads the point, passes 1-3 the 4 B key
         return map_steps * int(c["vg_in"].sum()) * (16 + 3 * 4)
     if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out

@@ -157,6 +157,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
         std::ceil(std::sqrt(cfg->nearest_feature_search_sq_dist) / SLO_ODO_SURF_CELL) > SLO_ODO_SURF_R)
         return SLO_E_ARG;   // the odometry surf search box (SLO_ODO_SURF_R cells) must cover the gate
     slo_ctx* ctx = new slo_ctx();
+    if (const char* e = getenv("SLO_VG_ONESWEEP")) ctx->vg_onesweep = e[0] == '1';   // experiment switch (slo_vg.hip)
     ctx->cfg = *cfg;
     ctx->dev = hip_device;
     ctx->S = n_streams;

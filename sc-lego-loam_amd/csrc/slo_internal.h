@@ -454,6 +454,12 @@ struct MapWs {  // VoxelGrid workspace (slo_vg.hip), sized on the host from the 
     unsigned int* bounds = nullptr;
     VgParams* prm = nullptr;
     int32_t* errflag = nullptr;
+    // single-pass scatter (ctx->vg_onesweep): per-stream digit histograms of every
+    // pass and their bases, tile tickets / per-XCD tile offsets, look-back status
+    int32_t* gh = nullptr;        // [S][4][256] digit counts (zeroed again by their scan)
+    int32_t* gbase = nullptr;     // [S][4][256] first output position of each digit
+    int32_t* osw = nullptr;       // [32] tickets (pass, XCD), [8] tiles per XCD, [S] XCD tile offsets
+    unsigned long long* lbk = nullptr;   // [tiles][256] (tag, inclusive flag, count)
 };
 struct HashGrid {
     int T = 0;
@@ -527,6 +533,7 @@ struct slo_ctx {
     unsigned int graph_ws[4] = {0, 0, 0, 0};
     unsigned int ws_gen = 0;            // bumped whenever a workspace behind a captured pointer moves
     const float4* pp_corner0 = nullptr; // corner_last of layout 0
+    bool vg_onesweep = false;           // VoxelGrid sort by single-pass scatters (env SLO_VG_ONESWEEP=1 at creation)
 };
 
 // launch helpers with optional per-kernel HIP-event timing

@@ -44,7 +44,7 @@ __device__ inline float ord2f(unsigned int u) {
 // stream offsets of the concatenated input (block scan), bounds init, and the
 // meta words [total, max cell count, long-voxel count]
 __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int S, int32_t* off,
-                                                    unsigned int* bounds, int32_t* meta) {
+                                                    unsigned int* bounds, int32_t* meta, int32_t* osw, int tile) {
     const int32_t* n = src.cnt();
     __shared__ int wsum[16];
     __shared__ int carry;
@@ -68,9 +68,21 @@ __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int
         if (tid == 1023) carry = before + incl;
         __syncthreads();
     }
-    if (tid == 0) { off[S] = carry; meta[0] = carry; meta[1] = 0; meta[2] = 0; }
+    if (tid == 0) { off[S] = carry; meta[0] = carry; meta[1] = 0; meta[2] = 0; meta[3] += 1; }
     for (int s = tid; s < S; s += 1024)
         for (int k = 0; k < 3; ++k) { bounds[6 * s + k] = 0xffffffffu; bounds[6 * s + 3 + k] = 0u; }
+    if (osw) {   // single-pass scatter: tickets reset, stream s's tiles dealt to XCD s & 7 in stream order
+        __syncthreads();   // off[] of this block visible
+        if (tid < 32) osw[tid] = 0;
+        if (tid < 8) {
+            int run = 0;
+            for (int s = tid; s < S; s += 8) {
+                osw[40 + s] = run;
+                run += (off[s + 1] - off[s] + tile - 1) / tile;
+            }
+            osw[32 + tid] = run;
+        }
+    }
 }
 
 __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, const int32_t* off,
@@ -301,17 +313,27 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
     if (pass >= p.npass) return;
     const int nt = p.ntiles, F = (1 << p.dbits) * nt;
     if (F == 0) return;
-    const int L = (F + 1023) / 1024, f0 = min(F, tid * L), f1 = min(F, f0 + L);
     int* c = cnt + (size_t)s * VG_NB * maxT;
-    int sum = 0;
-    for (int f = f0; f < f1; ++f) sum += c[(size_t)(f / nt) * maxT + f % nt];
-    int total;
-    int run = off[s] + vg_block_scan<16>(sum, wsum, &total);
-    for (int f = f0; f < f1; ++f) {
-        const size_t i = (size_t)(f / nt) * maxT + f % nt;
-        const int x = c[i];
-        c[i] = run;
-        run += x;
+    // chunks of 4 096 (digit, tile) counts, 4 consecutive per thread: a wave
+    // reads 256 consecutive counts of a digit row (coalesced), the block scan
+    // carries the running base from chunk to chunk
+    int run = off[s];
+    for (int f0 = 0; f0 < F; f0 += 4096) {
+        int x[4], sum = 0;
+        size_t idx[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int f = f0 + tid * 4 + k;
+            idx[k] = (size_t)(f / nt) * maxT + f % nt;
+            x[k] = f < F ? c[idx[k]] : 0;
+            sum += x[k];
+        }
+        int total;
+        int ex = run + vg_block_scan<16>(sum, wsum, &total);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            if (f0 + tid * 4 + k < F) { c[idx[k]] = ex; ex += x[k]; }
+        run += total;
     }
 }
 
@@ -404,6 +426,196 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
             }
         }
         __syncthreads();   // LDS reused by the next tile
+    }
+}
+
+// ---- Single-pass scatter (env SLO_VG_ONESWEEP=1 at context creation; Merrill & Garland's decoupled
+// look-back as in "Onesweep"): the digit counts of every pass are taken in
+// one read of the points (k_vg_ghist: the per-stream histograms do not depend
+// on the order the items are in), k_vg_gscan turns them into each digit's
+// first output position, and each pass is then one kernel: a workgroup takes
+// the next tile of its XCD's streams by ticket, ranks the tile's items, posts
+// its digit counts, adds up its predecessors' posts walking back until one
+// carries an inclusive prefix, posts its own inclusive prefix and scatters.
+// Tickets are taken in order, so every tile a workgroup waits on is held by a
+// running workgroup: no deadlock.  Posts are 64-bit words (tag, inclusive
+// flag, count); the tag names the sort call (an epoch k_vg_prefix counts in
+// meta[3]) and the pass, so no clearing pass is needed.
+#define VG_OSW_G 1024   // persistent single-pass workgroups (128 per XCD)
+static_assert(VG_NB <= VG_T, "one look-back thread per digit");
+
+template <bool FIRST>
+__global__ void __launch_bounds__(VG_T) k_vg_ghist(VgSrc src, size_t in_stride, const int32_t* off,
+                                                   const VgParams* prm, int32_t* gh, int S) {
+    const float4* in = src.pts();
+    __shared__ int h[VG_PASSES][VG_NB];
+    int s, chunk;
+    if (!vg_block(S, s, chunk)) return;
+    const int tid = threadIdx.x;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base, nb = 1 << p.dbits;
+    const unsigned int mask = (unsigned int)nb - 1u;
+    for (int d = tid; d < VG_PASSES * VG_NB; d += VG_T) (&h[0][0])[d] = 0;
+    __syncthreads();
+    for (int t = chunk; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        unsigned int key[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = k * VG_T + tid;
+            key[k] = j < m ? vg_key(in[(size_t)s * in_stride + a + j], p, a + j) : 0u;
+        }
+        const unsigned long long lt = (1ull << (tid & 63)) - 1ull;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const bool ok = k * VG_T + tid < m;
+            const unsigned long long act = __ballot(ok);
+            for (int q = 0; q < p.npass; ++q) {   // one LDS add per digit per wave (neighbouring points share digits)
+                const unsigned int d = (key[k] >> (q * p.dbits)) & mask;
+                const unsigned long long pe = vg_peers(d, p.dbits, act);
+                if (ok && (pe & lt) == 0) atomicAdd(&h[q][d], __popcll(pe));
+            }
+        }
+    }
+    __syncthreads();
+    for (int q = 0; q < p.npass; ++q)
+        for (int d = tid; d < nb; d += VG_T)
+            if (h[q][d]) atomicAdd(&gh[((size_t)s * VG_PASSES + q) * VG_NB + d], h[q][d]);
+}
+
+__global__ void __launch_bounds__(VG_T) k_vg_gscan(const int32_t* off, const VgParams* prm, int32_t* gh,
+                                                   int32_t* gbase) {
+    __shared__ int wsum[VG_W];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const VgParams p = prm[s];
+    for (int q = 0; q < p.npass; ++q) {
+        const size_t i = ((size_t)s * VG_PASSES + q) * VG_NB + tid;
+        const int x = tid < VG_NB ? gh[i] : 0;
+        int total;
+        const int ex = vg_block_scan<VG_W>(x, wsum, &total);
+        if (tid < VG_NB) { gbase[i] = off[s] + ex; gh[i] = 0; }
+    }
+}
+
+__device__ inline unsigned long long vg_post(unsigned int tag, bool incl, int c) {
+    return ((unsigned long long)tag << 32) | (incl ? 0x80000000ull : 0ull) | (unsigned int)c;
+}
+
+template <bool FIRST>
+__global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_onesweep(
+        VgSrc src, size_t in_stride, const int32_t* off, const VgParams* prm, int pass, unsigned int* ka,
+        unsigned int* va, unsigned int* kb, unsigned int* vb, const int32_t* gbase, int32_t* osw,
+        unsigned long long* lbk, const int32_t* meta, int maxT, int S, int32_t* errflag) {
+    __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
+    __shared__ int wc[VG_W][VG_NB];
+    __shared__ int lb[VG_NB];
+    __shared__ int wsum[VG_W];
+    __shared__ int tk_s;
+    const float4* in = FIRST ? src.pts() : nullptr;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int x = blockIdx.x & 7;                 // the XCD this workgroup runs on (round-robin dispatch)
+    const int ntx = osw[32 + x], J = (S - x + 7) >> 3;
+    const unsigned int tag = ((unsigned int)meta[3] << 2 | (unsigned int)pass) + 1u;
+    const unsigned long long lt = (1ull << lane) - 1ull;
+    for (;;) {
+        if (tid == 0) tk_s = atomicAdd(&osw[pass * 8 + x], 1);
+        __syncthreads();
+        const int tk = tk_s;
+        if (tk >= ntx) break;
+        int lo = 0, hi = J - 1;                   // the last stream of this XCD whose tiles start at or before tk
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (osw[40 + x + 8 * mid] <= tk) lo = mid; else hi = mid - 1;
+        }
+        const int s = x + 8 * lo, t = tk - osw[40 + s];
+        const VgParams p = prm[s];
+        if (pass >= p.npass) { __syncthreads(); continue; }
+        const bool ob = vg_out_b(p, pass);
+        const unsigned int* kin = ob ? ka : kb;
+        const unsigned int* vin = ob ? va : vb;
+        unsigned int* kout = ob ? kb : ka;
+        unsigned int* vout = ob ? vb : va;
+        const int base = off[s], n = off[s + 1] - base, shift = pass * p.dbits, nb = 1 << p.dbits;
+        const unsigned int mask = (unsigned int)nb - 1u;
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        for (int d = tid; d < VG_W * VG_NB; d += VG_T) (&wc[0][0])[d] = 0;
+        __syncthreads();
+        unsigned int key[VG_IPT], val[VG_IPT];
+        int rk[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
+            const bool ok = j < m;
+            key[k] = 0;
+            val[k] = 0;
+            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, vin, key[k], val[k]);
+            const unsigned int d = (key[k] >> shift) & mask;
+            const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
+            int before = 0;
+            if (ok) before = wc[w][d];
+            rk[k] = before + __popcll(pe & lt);
+            if (ok && (pe & lt) == 0) wc[w][d] = before + __popcll(pe);
+        }
+        __syncthreads();
+        {
+            const int d = tid;   // one digit per thread (VG_NB <= VG_T)
+            int c[VG_W], tot = 0;
+#pragma unroll
+            for (int q = 0; q < VG_W; ++q) { c[q] = d < nb ? wc[q][d] : 0; tot += c[q]; }
+            int total;
+            int run = vg_block_scan<VG_W>(tot, wsum, &total);
+            const int start = run;
+            if (d < nb) {
+#pragma unroll
+                for (int q = 0; q < VG_W; ++q) { wc[q][d] = run; run += c[q]; }
+                // post this tile's count, then walk back over the stream's earlier tiles
+                unsigned long long* L = lbk + ((size_t)s * maxT) * VG_NB + d;
+                int excl = 0;
+                if (t > 0) {
+                    __hip_atomic_store(L + (size_t)t * VG_NB, vg_post(tag, false, tot), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    int tt = t - 1;
+                    long spins = 0;
+                    for (;;) {
+                        const unsigned long long v =
+                            __hip_atomic_load(L + (size_t)tt * VG_NB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        if ((unsigned int)(v >> 32) != tag) {
+                            if (++spins > (1l << 22)) { atomicOr(errflag, 2); break; }   // never: a bound, not a hang
+                            __builtin_amdgcn_s_sleep(1);
+                            continue;
+                        }
+                        excl += (int)(v & 0x7fffffffull);
+                        if (v & 0x80000000ull) break;
+                        if (--tt < 0) break;
+                    }
+                }
+                __hip_atomic_store(L + (size_t)t * VG_NB, vg_post(tag, true, excl + tot), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                lb[d] = gbase[((size_t)s * VG_PASSES + pass) * VG_NB + d] + excl - start;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
+            if (j < m) {
+                const int pos = wc[w][(key[k] >> shift) & mask] + rk[k];
+                lk[pos] = key[k];
+                lv[pos] = val[k];
+            }
+        }
+        __syncthreads();
+#pragma unroll 4
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = k * VG_T + tid;
+            if (j < m) {
+                const unsigned int key2 = lk[j];
+                const int o = lb[(key2 >> shift) & mask] + j;
+                kout[o] = key2;
+                vout[o] = lv[j];
+            }
+        }
+        __syncthreads();   // LDS and tk_s reused by the next tile
     }
 }
 
@@ -698,10 +910,14 @@ static int ensure_ws(slo_ctx* ctx, size_t stride) {
         const size_t tt = std::max(tiles, w.tiles + w.tiles / 2);
         if (w.cnt) hipFree(w.cnt);
         if (w.hcnt) hipFree(w.hcnt);
+        if (w.lbk) hipFree(w.lbk);
         w.tiles = tt;
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.cnt, sizeof(int) * VG_NB * tt));
         SLO_CHECK(hipMalloc(&w.hcnt, sizeof(int) * tt));
+        // look-back posts: zero is no sort call's tag (tags start at 1)
+        SLO_CHECK(hipMalloc(&w.lbk, sizeof(unsigned long long) * VG_NB * tt));
+        SLO_CHECK(hipMemsetAsync(w.lbk, 0, sizeof(unsigned long long) * VG_NB * tt, ctx->stream));
     }
     return 0;
 }
@@ -722,7 +938,8 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     const int bx = std::max(1, std::min(64, (int)((in_stride + 255) / 256)));
     const dim3 grid = vg_tile_grid(GX, S);
     const VgSrc src{in, d_n, ctx->v.io};
-    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta);
+    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta,
+               ctx->vg_onesweep ? w.osw : nullptr, VG_TILE);
     SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, in_stride, w.off, w.bounds);
     SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
     hipEvent_t ev = nullptr;
@@ -731,6 +948,22 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
     // pair A = keys2/vals2, pair B = keys/vals (every stream's last pass writes B)
     unsigned int *ka = w.keys2, *va = w.vals2, *kb = w.keys, *vb = w.vals;
+    if (ctx->vg_onesweep) {
+        SLO_LAUNCH(ctx, "vg_ghist", k_vg_ghist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, w.gh, S);
+        SLO_LAUNCH(ctx, "vg_gscan", k_vg_gscan, dim3(S), dim3(VG_T), 0, w.off, w.prm, w.gh, w.gbase);
+        for (int pass = 0; pass < VG_PASSES; ++pass) {
+            if (pass == 0) {
+                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<true>, dim3(VG_OSW_G), dim3(VG_T), 0, src, in_stride,
+                           w.off, w.prm, pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
+            } else {
+                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<false>, dim3(VG_OSW_G), dim3(VG_T), 0, src, in_stride,
+                           w.off, w.prm, pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
+            }
+        }
+        if (tm) timing_end(ctx, sort_name.c_str(), ev);
+        *keys = kb; *vals = vb; *spare_k = ka; *spare_v = va;
+        return 0;
+    }
     for (int pass = 0; pass < VG_PASSES; ++pass) {
         if (pass == 0) {
             SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
@@ -1014,13 +1247,19 @@ int vg_alloc(slo_ctx* ctx) {
     SLO_CHECK(hipMalloc(&w.errflag, sizeof(int32_t)));
     SLO_CHECK(hipMemset(w.errflag, 0, sizeof(int32_t)));
     SLO_CHECK(hipMalloc(&w.meta, 4 * sizeof(int32_t)));
+    SLO_CHECK(hipMemset(w.meta, 0, 4 * sizeof(int32_t)));
     SLO_CHECK(hipMalloc(&w.nvox, sizeof(int32_t) * S));
+    SLO_CHECK(hipMalloc(&w.gh, sizeof(int32_t) * S * VG_PASSES * VG_NB));
+    SLO_CHECK(hipMemset(w.gh, 0, sizeof(int32_t) * S * VG_PASSES * VG_NB));
+    SLO_CHECK(hipMalloc(&w.gbase, sizeof(int32_t) * S * VG_PASSES * VG_NB));
+    SLO_CHECK(hipMalloc(&w.osw, sizeof(int32_t) * (40 + S)));
     return 0;
 }
 
 void vg_free(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
-    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta, w.nvox};
+    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta,
+                  w.nvox, w.gh, w.gbase, w.osw, w.lbk};
     for (void* p : ps) if (p) hipFree(p);
     w = MapWs();
 }

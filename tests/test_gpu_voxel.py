@@ -1,7 +1,8 @@
 """VoxelGrid over many wide streams: (stream << voxel bits) needs more than
 32 bits, so the batched sort runs on 64-bit keys (csrc/slo_vg.hip), with
 empty streams in between.  Every stream's downsampled cloud must equal the
-oracle's PCL VoxelGrid restatement (stable in-voxel order) bit for bit."""
+oracle's PCL VoxelGrid restatement (stable in-voxel order) bit for bit, with
+the default LSD passes and with the single-pass scatters."""
 import numpy as np
 import pytest
 
@@ -12,7 +13,11 @@ from parity_util import mismatch
 pytestmark = pytest.mark.gpu
 
 
-def test_wide_streams_voxel_grid_matches_oracle():
+@pytest.mark.parametrize("onesweep", ["0", "1"])
+def test_wide_streams_voxel_grid_matches_oracle(onesweep, monkeypatch):
+    # onesweep = 1: the single-pass scatter sort (decoupled look-back,
+    # SLO_VG_ONESWEEP, read when the context is created)
+    monkeypatch.setenv("SLO_VG_ONESWEEP", onesweep)
     import torch
     assert torch.cuda.is_available(), "no HIP device"
     pid, S = 0, 64
@@ -81,3 +86,19 @@ def test_voxel_grid_int32_overflow_returns_the_input():
             assert mismatch(got, want) == 0, s
     finally:
         ctx.close()
+
+
+def test_pipeline_with_single_pass_sort(monkeypatch):
+    """C3 (hdl64_1800) pipeline, two mapping rounds per stream, every
+    VoxelGrid sorted by the single-pass scatters: bit-exact vs the oracle."""
+    import os
+    import sys
+    monkeypatch.setenv("SLO_VG_ONESWEEP", "1")
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import parity_report
+    rep, worst, counts = parity_report.run(6, 3, 2, 14, verbose=False)
+    bad = [r for r in rep if any(isinstance(v, int) and v != 0 and k not in
+                                 ("scan", "stream", "flags_cpu", "flags_gpu") for k, v in r.items())]
+    assert not bad and not counts["flag_mismatch"] and not counts["detect_mismatch"], (bad[:2], counts)
+    assert not any(worst.values()), worst
+    assert sum(1 for r in rep if r["flags_cpu"] & 2) >= 1
