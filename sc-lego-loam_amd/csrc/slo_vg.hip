@@ -126,7 +126,10 @@ struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbit
 #endif
 #define VG_W (VG_T / 64)              // waves per tile workgroup (each owns a slice of the tile)
 #ifndef VG_SCATTER_OCC
-#define VG_SCATTER_OCC (VG_W == 4 ? 4 : 6)   // vg_scatter waves per SIMD the register budget keeps
+// vg_scatter waves per SIMD: 3 leaves room (<= 168 VGPRs) for all of a tile's
+// key and value loads in flight at once; at 4 the same code spills (measured
+// 28.5 k against 27.9 k scans/s, and 26.8 k for 4 waves with one load in flight)
+#define VG_SCATTER_OCC (VG_W == 4 ? 3 : 6)
 #endif
 #ifndef VG_IPT
 #define VG_IPT 16                     // items per thread
@@ -196,7 +199,7 @@ __device__ inline unsigned int vg_none(const VgParams& p) { return p.vbits >= 32
 
 // the PCL voxel index of point i of a stream (positions on overflow)
 __device__ inline unsigned int vg_key(const float4& q, const VgParams& p, int i) {
-    if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return vg_none(p);
+    if (!(isfinite(q.x) & isfinite(q.y) & isfinite(q.z))) return vg_none(p);   // no short-circuit: one load
     if (p.overflow) return (unsigned int)i;
     const int ijk0 = (int)(floorf(q.x * p.inv) - (float)p.minb[0]);
     const int ijk1 = (int)(floorf(q.y * p.inv) - (float)p.minb[1]);
@@ -252,15 +255,57 @@ __device__ inline unsigned long long vg_peers(unsigned int d, int dbits, unsigne
     return pe;
 }
 
+// A tile's items of one pass: item k of this thread is j = j0 + 64 k (its wave
+// slice).  Every load is issued before the first use: pass 0 loads the points
+// VG_LB at a time (their keys need the whole point) and keeps only the keys;
+// later passes load all keys at once (their values: vg_tile_vals).
+#define VG_LB 8
 template <bool FIRST>
-__device__ inline void vg_load(const float4* in, size_t in_stride, const VgParams& p, int s, int base, int i,
-                               const unsigned int* kin, const unsigned int* vin, unsigned int& key, unsigned int& val) {
+__device__ inline void vg_tile_load(const float4* in, size_t in_stride, const VgParams& p, int s, int base, int a,
+                                    int m, int j0, const unsigned int* kin, const unsigned int* vin,
+                                    unsigned int (&key)[VG_IPT], unsigned int (&val)[VG_IPT]) {
     if (FIRST) {
-        key = vg_key(in[(size_t)s * in_stride + i], p, i);
-        val = (unsigned int)i;
+        const float4* src = in + (size_t)s * in_stride + a;
+#pragma unroll
+        for (int h = 0; h < VG_IPT; h += VG_LB) {
+            float4 q[VG_LB];
+#pragma unroll
+            for (int u = 0; u < VG_LB; ++u) {
+                const int j = j0 + (h + u) * 64;
+                q[u] = j < m ? src[j] : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < VG_LB; ++u) {
+                const int j = j0 + (h + u) * 64;
+                key[h + u] = j < m ? vg_key(q[u], p, a + j) : 0u;
+                val[h + u] = (unsigned int)(a + j);
+            }
+        }
+    } else if (m == VG_TILE) {   // a full tile: straight-line loads at immediate offsets
+        const unsigned int* src = kin + base + a + j0;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) key[k] = src[k * 64];
     } else {
-        key = kin[base + i];
-        val = vin ? vin[base + i] : 0u;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            const int j = j0 + k * 64;
+            key[k] = j < m ? kin[base + a + j] : 0u;
+        }
+    }
+}
+// the values of a later pass, loaded once the keys are ranked (fewer live registers while ranking)
+__device__ inline void vg_tile_vals(int base, int a, int m, int j0, const unsigned int* vin,
+                                    unsigned int (&val)[VG_IPT]) {
+    if (m == VG_TILE) {
+        const unsigned int* src = vin + base + a + j0;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) val[k] = src[k * 64];
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < VG_IPT; ++k) {
+        const int j = j0 + k * 64;
+        val[k] = j < m ? vin[base + a + j] : 0u;
     }
 }
 
@@ -283,14 +328,8 @@ __global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, c
         for (int d = tid; d < nb; d += VG_T) h[d] = 0;
         __syncthreads();
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
-        unsigned int key[VG_IPT];
-#pragma unroll
-        for (int k = 0; k < VG_IPT; ++k) {   // all of the tile's loads in flight before the first use
-            const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
-            unsigned int val;
-            key[k] = 0;
-            if (j < m) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, nullptr, key[k], val);
-        }
+        unsigned int key[VG_IPT], val[VG_IPT];
+        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, nullptr, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
@@ -366,13 +405,11 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
+        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             const bool ok = j < m;
-            key[k] = 0;
-            val[k] = 0;
-            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, vin, key[k], val[k]);
             const unsigned int d = (key[k] >> shift) & mask;
             const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
             int before = 0;
@@ -380,6 +417,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
             rk[k] = before + __popcll(pe & lt);
             if (ok && (pe & lt) == 0) wc[w][d] = before + __popcll(pe);
         }
+        if (!FIRST) vg_tile_vals(base, a, m, w * (VG_TILE / VG_W) + lane, vin, val);   // in flight over the scan
         __syncthreads();
         // digit-major, slice-minor exclusive scan of the counts: the tile-local
         // position of each (digit, slice) run
@@ -542,13 +580,11 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
+        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
             const bool ok = j < m;
-            key[k] = 0;
-            val[k] = 0;
-            if (ok) vg_load<FIRST>(in, in_stride, p, s, base, a + j, kin, vin, key[k], val[k]);
             const unsigned int d = (key[k] >> shift) & mask;
             const unsigned long long pe = vg_peers(d, p.dbits, __ballot(ok));
             int before = 0;
@@ -556,6 +592,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
             rk[k] = before + __popcll(pe & lt);
             if (ok && (pe & lt) == 0) wc[w][d] = before + __popcll(pe);
         }
+        if (!FIRST) vg_tile_vals(base, a, m, w * (VG_TILE / VG_W) + lane, vin, val);   // in flight over the scan
         __syncthreads();
         {
             const int d = tid;   // one digit per thread (VG_NB <= VG_T)
@@ -643,12 +680,16 @@ __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, con
     const unsigned int* k = keys + base;
     for (int t = chunk; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
-        int c = 0;
-#pragma unroll 4
+        unsigned int cur[VG_IPT], prv[VG_IPT];   // every load in flight before the first compare
+#pragma unroll
         for (int q = 0; q < VG_IPT; ++q) {
-            const int j = q * VG_T + tid;
-            if (j < m) c += vg_head(k, a + j, none);
+            const int j = q * VG_T + tid, i = a + j;
+            cur[q] = j < m ? k[i] : none;
+            prv[q] = (j < m && i > 0) ? k[i - 1] : ~cur[q];
         }
+        int c = 0;
+#pragma unroll
+        for (int q = 0; q < VG_IPT; ++q) c += cur[q] != none && prv[q] != cur[q];
         int total;
         vg_block_scan<VG_W>(c, wsum, &total);
         if (tid == 0) hcnt[(size_t)s * maxT + t] = total;
@@ -832,12 +873,28 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
         const int j0 = w * SL, i0 = a + j0;                 // this wave's slice: items [i0, i0 + ms)
         const int ms = max(0, min(SL, m - j0));
         int nh = 0, nc = 0, lasth = 0;                      // heads / key changes listed so far, the last head
+        // the slice's keys, all loads in flight at once; each item's predecessor
+        // comes from the lane below (lane 0: the previous row's lane 63, or the
+        // item before the slice)
+        unsigned int kk[SL / 64];
+        if (ms == SL) {
+#pragma unroll
+            for (int q = 0; q < SL / 64; ++q) kk[q] = k[i0 + q * 64 + lane];
+        } else {
+#pragma unroll
+            for (int q = 0; q < SL / 64; ++q) kk[q] = q * 64 + lane < ms ? k[i0 + q * 64 + lane] : 0u;
+        }
+        unsigned int before = (ms > 0 && i0 > 0) ? k[i0 - 1] : 0u;
+#pragma unroll
         for (int q = 0; q < SL / 64; ++q) {
             const int j = q * 64 + lane, i = i0 + j;
+            const unsigned int x = kk[q];
+            const unsigned int up = __shfl_up(x, 1, 64);
+            const unsigned int pv = lane == 0 ? before : up;
+            before = __shfl(x, 63, 64);
             bool chg = false, head = false;
             if (j < ms) {
-                const unsigned int x = k[i];
-                chg = i == 0 || k[i - 1] != x;
+                chg = i == 0 || pv != x;
                 head = chg && x != none;
             }
             const unsigned long long cm = __ballot(chg);
