@@ -856,6 +856,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
                                                     int nlong_cap, VgOut o, int S) {
     constexpr int SL = VG_TILE / VG_W;   // items per wave slice
     __shared__ int lst[VG_W][SL + 1];
+    __shared__ unsigned int lvv[VG_W][SL];   // the slice's point indices (the gathers read them from LDS)
     __shared__ int wsum[VG_W];
     int s, chunk;
     if (!vg_block(S, s, chunk)) return;
@@ -877,12 +878,18 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
         // comes from the lane below (lane 0: the previous row's lane 63, or the
         // item before the slice)
         unsigned int kk[SL / 64];
+        unsigned int* LV = lvv[w];
         if (ms == SL) {
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q) kk[q] = k[i0 + q * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < SL / 64; ++q) LV[q * 64 + lane] = v[i0 + q * 64 + lane];
         } else {
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q) kk[q] = q * 64 + lane < ms ? k[i0 + q * 64 + lane] : 0u;
+#pragma unroll
+            for (int q = 0; q < SL / 64; ++q)
+                if (q * 64 + lane < ms) LV[q * 64 + lane] = v[i0 + q * 64 + lane];
         }
         unsigned int before = (ms > 0 && i0 > 0) ? k[i0 - 1] : 0u;
 #pragma unroll
@@ -933,7 +940,10 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
             for (int i = j; i < e; i += 4) {
                 float4 q4[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) q4[u] = i + u < e ? src[v[i + u]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int u = 0; u < 4; ++u) {   // indices inside the slice from LDS, past its end from HBM
+                    const int ii = i + u;
+                    q4[u] = ii < e ? src[ii - i0 < ms ? LV[ii - i0] : v[ii]] : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
                     if (i + u < e) { sx += q4[u].x; sy += q4[u].y; sz += q4[u].z; si += q4[u].w; }
