@@ -723,10 +723,19 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const float leaf = v.cfg.leaf_less_flat;
     const float inv = 1.0f / leaf;
     float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) {
-        float4 p = in[i];
-        mnx = fminf(mnx, p.x); mny = fminf(mny, p.y); mnz = fminf(mnz, p.z);
-        mxx = fmaxf(mxx, p.x); mxy = fmaxf(mxy, p.y); mxz = fmaxf(mxz, p.z);
+    for (int b = 0; b < n; b += 8 * 256) {   // eight loads in flight per thread
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = b + u * 256 + threadIdx.x;
+            pp[u] = in[i < n ? i : n - 1];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float4 p = pp[u];
+            mnx = fminf(mnx, p.x); mny = fminf(mny, p.y); mnz = fminf(mnz, p.z);
+            mxx = fmaxf(mxx, p.x); mxy = fmaxf(mxy, p.y); mxz = fmaxf(mxz, p.z);
+        }
     }
     block_minmax(mnx, mny, mnz, mxx, mxy, mxz, sh);
     if (n == 0) {
@@ -744,14 +753,13 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
     const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
     const int mul1 = divx, mul2 = divx * divy;
-    auto key_of = [&](int i) -> unsigned long long {
-        if (i >= n) return ~0ull;
-        const float4 p = in[i];
+    auto key_of = [&](int i) -> unsigned long long {   // branch-free (n >= 1): the sort's loads all in flight
+        const float4 p = in[min(i, n - 1)];
         const int ijk0 = (int)(floorf(p.x * inv) - (float)minbx);
         const int ijk1 = (int)(floorf(p.y * inv) - (float)minby);
         const int ijk2 = (int)(floorf(p.z * inv) - (float)minbz);
         const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
-        return ((unsigned long long)idx << 32) | (unsigned int)i;
+        return (((unsigned long long)idx << 32) | (unsigned int)i) | (0ull - (unsigned long long)(i >= n));
     };
     if (n <= 256) ring_sort_regs<1>(keys, key_of);
     else if (n <= 512) ring_sort_regs<2>(keys, key_of);
@@ -790,6 +798,45 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
         __syncthreads();
     }
     int rank = scan[threadIdx.x] - heads;
+    if (chunk <= 8) {   // rings of <= 2048 points: the chunk's points gathered at once, voxels summed in order
+        float4 pp[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int i = i0 + c;
+            pp[c] = i < i1 ? in[(unsigned int)keys[i]] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+        bool have = false;   // a voxel started in this chunk is open
+        unsigned int vid = 0;
+        int cv = 0;
+        float sx = 0, sy = 0, sz = 0, si = 0;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            const int i = i0 + c;
+            if (i < i1) {
+                const unsigned int kv = (unsigned int)(keys[i] >> 32);
+                if (i == 0 || kv != (unsigned int)(keys[i - 1] >> 32)) {
+                    if (have) {
+                        const float cnt = (float)cv;
+                        out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+                    }
+                    have = true; vid = kv; cv = 0;
+                    sx = 0; sy = 0; sz = 0; si = 0;
+                }
+                if (have) { sx += pp[c].x; sy += pp[c].y; sz += pp[c].z; si += pp[c].w; ++cv; }
+            }
+        }
+        if (have) {   // the last voxel runs on past the chunk
+            for (int e = i1; e < n && (unsigned int)(keys[e] >> 32) == vid; ++e) {
+                const float4 p = in[(unsigned int)keys[e]];
+                sx += p.x; sy += p.y; sz += p.z; si += p.w;
+                ++cv;
+            }
+            const float cnt = (float)cv;
+            out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+        }
+        if (threadIdx.x == T - 1) v.ring_cnt[rr * 4 + 3] = scan[T - 1];
+        return;
+    }
     for (int i = i0; i < i1; ++i) {
         if (!(i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32))) continue;
         unsigned int vid = (unsigned int)(keys[i] >> 32);

@@ -100,10 +100,18 @@ __global__ void k_ip_project(DevView v) {
     const int n = v.io->npts[s];
     const int R = v.cfg.n_scan;
     int fmin = INT_MAX, fmax = -1;
+    if ((int)blockIdx.x * IP_PTS_PER_WG >= n) return;   // no point of this stream here
+    // every point of the thread loaded before the first is projected
+    const float4* P = v.io->pts + (size_t)s * v.P;
+    float4 pp[IP_PTS_PER_WG / 256];
+#pragma unroll
+    for (int k = 0; k < IP_PTS_PER_WG / 256; ++k)
+        pp[k] = P[min((int)blockIdx.x * IP_PTS_PER_WG + k * 256 + (int)threadIdx.x, n - 1)];
+#pragma unroll
     for (int k = 0; k < IP_PTS_PER_WG / 256; ++k) {
         const int i = blockIdx.x * IP_PTS_PER_WG + k * 256 + threadIdx.x;
         if (i >= n) break;
-        float4 p = v.io->pts[(size_t)s * v.P + i];
+        const float4 p = pp[k];
         if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
             fmin = min(fmin, i); fmax = max(fmax, i);
             int row, col; float rg;
