@@ -349,7 +349,7 @@ __device__ inline void grid_ball_rows(const GridView& g, int s, float qx, float 
         for (int e = p0; e < p1; e += U) {
             float4 p[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) p[u] = e + u < p1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int u = 0; u < U; ++u) p[u] = E[min(e + u, p1 - 1)];   // unconditional: all U loads in flight
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 if (e + u >= p1) break;
@@ -379,8 +379,7 @@ __device__ inline void grid_ball_rows(const GridView& g, int s, float qx, float 
             for (int e = e0; e < e1; e += U) {
                 float4 p[U];
 #pragma unroll
-                for (int u = 0; u < U; ++u)
-                    p[u] = e + u < e1 ? E[e + u] : make_float4(0.f, 0.f, 0.f, 0.f);
+                for (int u = 0; u < U; ++u) p[u] = E[min(e + u, e1 - 1)];   // unconditional: all U loads in flight
 #pragma unroll
                 for (int u = 0; u < U; ++u) {
                     if (e + u >= e1) break;

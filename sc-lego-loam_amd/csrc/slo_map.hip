@@ -263,12 +263,22 @@ __global__ void k_mo_assemble(DevView v) {
         const float x2 = x1, y2 = ctRoll * y1 - stRoll * z1, z2 = stRoll * y1 + ctRoll * z1;
         return make_float4(ctPitch * x2 + stPitch * z2 + tr[6], y2 + tr[7], -stPitch * x2 + ctPitch * z2 + tr[8], p.w);
     };
-    for (int i = threadIdx.x; i < kn[0]; i += blockDim.x)
-        if (oc + i < v.cap_mc) v.map_c[(size_t)s * v.cap_mc + oc + i] = xf(v.kf_corner[ks * v.cap_kc + i]);
-    for (int i = threadIdx.x; i < kn[1]; i += blockDim.x)
-        if (os + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + i] = xf(v.kf_surf[ks * v.cap_kfs + i]);
-    for (int i = threadIdx.x; i < kn[2]; i += blockDim.x)
-        if (os + kn[1] + i < v.cap_ms) v.map_s[(size_t)s * v.cap_ms + os + kn[1] + i] = xf(v.kf_outl[ks * v.cap_kfo + i]);
+    // eight points per thread (256-thread launch) loaded before the first is transformed
+    auto copy = [&](const float4* src, int n, float4* dst, int room) {
+        for (int i0 = threadIdx.x; i0 < n; i0 += 8 * 256) {
+            float4 q[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) q[u] = src[min(i0 + u * 256, n - 1)];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u * 256;
+                if (i < n && i < room) dst[i] = xf(q[u]);
+            }
+        }
+    };
+    copy(v.kf_corner + ks * v.cap_kc, kn[0], v.map_c + (size_t)s * v.cap_mc + oc, v.cap_mc - oc);
+    copy(v.kf_surf + ks * v.cap_kfs, kn[1], v.map_s + (size_t)s * v.cap_ms + os, v.cap_ms - os);
+    copy(v.kf_outl + ks * v.cap_kfo, kn[2], v.map_s + (size_t)s * v.cap_ms + os + kn[1], v.cap_ms - os - kn[1]);
 }
 
 __global__ void k_mo_concat(DevView v) {
