@@ -84,12 +84,22 @@ __global__ void k_fa_imu_start(DevView v) {
 }
 
 // deskew + curvature + occlusion marks, one thread per position
-__global__ void k_fa_points(DevView v) {
+__global__ void __launch_bounds__(256) k_fa_points(DevView v) {
     const int s = blockIdx.y;
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
+    const int p0 = blockIdx.x * 256, p = p0 + threadIdx.x;
     const int S = v.st[s].seg_count;
-    if (p >= S) return;
+    if (p0 >= S) return;
     const size_t base = (size_t)s * v.H;
+    // the block's ranges and columns with a 6-point halo each side, staged in
+    // LDS (coalesced): the smoothness and occlusion windows read them there
+    __shared__ float lr[256 + 12];
+    __shared__ uint32_t lcol[256 + 12];
+    for (int k = threadIdx.x; k < 256 + 12; k += 256) {
+        const int i = p0 - 6 + k;
+        if (i >= 0 && i < S) { lr[k] = v.seg_range[base + i]; lcol[k] = v.seg_col[base + i]; }
+    }
+    __syncthreads();
+    if (p >= S) return;
     // ---- adjustDistortion (non-IMU)
     {
         float4 q = v.seg[base + p];
@@ -120,13 +130,13 @@ __global__ void k_fa_points(DevView v) {
         }
         v.fpts[base + p] = make_float4(px, py, pz, intensity);
     }
-    const float* r = v.seg_range + base;
-    const uint32_t* col = v.seg_col + base;
+    auto r = [&](int i) { return lr[6 - p0 + i]; };      // seg_range[i], i in [p0 - 6, p0 + 262)
+    auto col = [&](int i) { return lcol[6 - p0 + i]; };  // seg_col[i]
     // ---- calculateSmoothness
     const bool inner = p >= 5 && p < S - 5;
     if (inner) {
-        float d = r[p - 5] + r[p - 4] + r[p - 3] + r[p - 2] + r[p - 1] - r[p] * 10 + r[p + 1] + r[p + 2] +
-                  r[p + 3] + r[p + 4] + r[p + 5];
+        float d = r(p - 5) + r(p - 4) + r(p - 3) + r(p - 2) + r(p - 1) - r(p) * 10 + r(p + 1) + r(p + 2) +
+                  r(p + 3) + r(p + 4) + r(p + 5);
         float c = d * d;
         v.curv[base + p] = c;
         v.clabel[base + p] = 0;
@@ -136,17 +146,17 @@ __global__ void k_fa_points(DevView v) {
     int pk = inner ? 0 : v.picked[base + p];
     const int ilo = 5, ihi = S - 7;
     for (int i = max(ilo, p); i <= min(ihi, p + 5) && !pk; ++i) {  // case A marks [i-5, i]
-        int cd = abs((int)(col[i + 1] - col[i]));
-        if (cd < 10 && r[i] - r[i + 1] > 0.3) pk = 1;
+        int cd = abs((int)(col(i + 1) - col(i)));
+        if (cd < 10 && r(i) - r(i + 1) > 0.3) pk = 1;
     }
     for (int i = max(ilo, p - 6); i <= min(ihi, p - 1) && !pk; ++i) {  // case B marks [i+1, i+6]
-        int cd = abs((int)(col[i + 1] - col[i]));
-        if (cd < 10 && !(r[i] - r[i + 1] > 0.3) && r[i + 1] - r[i] > 0.3) pk = 1;
+        int cd = abs((int)(col(i + 1) - col(i)));
+        if (cd < 10 && !(r(i) - r(i + 1) > 0.3) && r(i + 1) - r(i) > 0.3) pk = 1;
     }
     if (!pk && p >= ilo && p <= ihi) {
-        float diff1 = fabsf((float)(r[p - 1] - r[p]));
-        float diff2 = fabsf((float)(r[p + 1] - r[p]));
-        if (diff1 > 0.02 * r[p] && diff2 > 0.02 * r[p]) pk = 1;
+        float diff1 = fabsf((float)(r(p - 1) - r(p)));
+        float diff2 = fabsf((float)(r(p + 1) - r(p)));
+        if (diff1 > 0.02 * r(p) && diff2 > 0.02 * r(p)) pk = 1;
     }
     v.picked[base + p] = pk;
 }

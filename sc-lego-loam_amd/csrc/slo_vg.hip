@@ -91,11 +91,19 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
     const int s = blockIdx.y;
     const int n = off[s + 1] - off[s];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        float4 p = in[(size_t)s * in_stride + i];
-        if (!(isfinite(p.x) && isfinite(p.y) && isfinite(p.z))) continue;
-        unsigned int q[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
-        for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], q[k]); mx[k] = max(mx[k], q[k]); }
+    const float4* pts = in + (size_t)s * in_stride;
+    const int step = gridDim.x * blockDim.x;
+    for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 8 * step) {   // eight loads in flight
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = pts[min(i0 + u * step, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const float4 p = pp[u];
+            if (i0 + u * step >= n || !(isfinite(p.x) & isfinite(p.y) & isfinite(p.z))) continue;
+            const unsigned int q[3] = {f2ord(p.x), f2ord(p.y), f2ord(p.z)};
+            for (int k = 0; k < 3; ++k) { mn[k] = min(mn[k], q[k]); mx[k] = max(mx[k], q[k]); }
+        }
     }
     for (int o = 32; o > 0; o >>= 1)
         for (int k = 0; k < 3; ++k) {
@@ -819,11 +827,15 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
         float acc = 0.0f;
         for (int c0 = a; c0 < e; c0 += 256) {
             const int m = min(256, e - c0);
+            unsigned int ix[4];
+            float4 pt[4];
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const int q = u * 64 + lane;
-                if (q < m) b[q] = src[v[c0 + q]];
-            }
+            for (int u = 0; u < 4; ++u) ix[u] = v[c0 + min(u * 64 + lane, m - 1)];   // all loads in flight
+#pragma unroll
+            for (int u = 0; u < 4; ++u) pt[u] = src[ix[u]];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (u * 64 + lane < m) b[u * 64 + lane] = pt[u];
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
             __builtin_amdgcn_wave_barrier();
             if (lane < 4) {
