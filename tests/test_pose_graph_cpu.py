@@ -6,6 +6,13 @@ Host-only code: it runs here without a GPU.  Parity is unpinned against GTSAM
 (absent from the image, no fixtures in the reference); the oracle and the
 product solve the same graph independently.  Tolerances: outputs are float32,
 so the north-star bound 1e-4 m / 1e-4 rad (tighter: 2e-5 rad) between solver and oracle.
+
+No gradient (stationarity) check is made at the product's estimate: the ABI
+returns float32 key poses, and their rounding (~1e-6 m at 20 m) is 1 % of the
+reference's odometry sigma (1e-4 m, MO:366), so the whitened gradient at the
+rounded poses is dominated by the rounding.  Optimality is instead checked as
+agreement of cost and poses with the independent numpy solver, a fixed point
+on re-optimisation, and the drift reduction a loop must give.
 """
 import os
 import sys
