@@ -76,7 +76,7 @@ def parse():
     ap.add_argument("--history", type=int, default=0,
                     help="extra Scan Context history per stream (scans before scan 0); the pre-roll builds the real one")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="mo_knn",
+    ap.add_argument("--roofline-also", default="mo_knn,fa_search_corner",
                     help="further kernels timed live the same way, reported under roofline_also (comma list)")
     ap.add_argument("--roofline-kernel", default="vg_scatter",
                     help="kernel timed with HIP events inside the timed region (the roofline's kernel)")

@@ -532,10 +532,22 @@ __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
     __shared__ int p_sh[12], p_ls[120], p_fl[24];
     const int16_t* g_sh = v.ex_list + (size_t)s * v.H * 2;
     const int16_t* g_fl = g_sh + v.H;
-    for (int k = lane; k < hi - lo; k += 64) {
-        lpk[k] = (int8_t)picked[lo + k];
-        llab[k] = (int8_t)lab[lo + k];
-        lcol[k] = (uint16_t)v.seg_col[base + lo + k];
+    const int nw = hi - lo;
+    for (int k0 = 0; k0 < nw; k0 += 8 * 64) {   // eight points per lane loaded before they are staged
+        int a[8], b[8];
+        uint32_t c[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = min(k0 + u * 64 + lane, nw - 1);
+            a[u] = picked[lo + k];
+            b[u] = lab[lo + k];
+            c[u] = v.seg_col[base + lo + k];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int k = k0 + u * 64 + lane;
+            if (k < nw) { lpk[k] = (int8_t)a[u]; llab[k] = (int8_t)b[u]; lcol[k] = (uint16_t)c[u]; }
+        }
     }
     __syncthreads();
     // FA:719-731 / 752-764 on lanes 1..10: lanes 1..5 test the column gaps
@@ -610,20 +622,27 @@ __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
     // reference's `continue`
     float4* o_lf = v.r_lf_scan + rr * C;
     int n_lf = 0;
-    for (int kb = rs; kb < re; kb += 64) {
-        const int k = kb + lane;
-        bool take = false;
-        if (k < re) {
-            for (int j = 0; j < 6; ++j) {
-                const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
-                if (k >= sp && k <= ep) { take = sp < ep; break; }
+    for (int kb0 = rs; kb0 < re; kb0 += 4 * 64) {
+        // four points per lane loaded before any is written (named, so they stay in registers)
+        const float4 q0 = fp[min(kb0 + lane, re - 1)], q1 = fp[min(kb0 + 64 + lane, re - 1)];
+        const float4 q2 = fp[min(kb0 + 128 + lane, re - 1)], q3 = fp[min(kb0 + 192 + lane, re - 1)];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const float4 qu = u == 0 ? q0 : u == 1 ? q1 : u == 2 ? q2 : q3;
+            const int k = kb0 + u * 64 + lane;
+            bool take = false;
+            if (k < re) {
+                for (int j = 0; j < 6; ++j) {
+                    const int sp = sec_sp(rs, re, j), ep = sec_ep(rs, re, j);
+                    if (k >= sp && k <= ep) { take = sp < ep; break; }
+                }
+                take = take && llab[k - lo] <= 0;
             }
-            take = take && llab[k - lo] <= 0;
+            const unsigned long long m = __ballot(take);
+            const int pos = n_lf + __popcll(m & ((1ull << lane) - 1));
+            if (take && pos < C) o_lf[pos] = qu;
+            n_lf += __popcll(m);
         }
-        const unsigned long long m = __ballot(take);
-        const int pos = n_lf + __popcll(m & ((1ull << lane) - 1));
-        if (take && pos < C) o_lf[pos] = fp[k];
-        n_lf += __popcll(m);
     }
     if (lane == 0) {
         int* rc = v.ring_cnt + rr * 4;
