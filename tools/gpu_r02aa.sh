@@ -1,0 +1,11 @@
+# hash-grid walks fetch the next row's bucket offsets while the current row's entries load (variant p):
+# parity on p, then A/B against the final build m
+set -euo pipefail
+OUT=gpurun_out/${1:-r02aa}
+mkdir -p $OUT
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export SLO_LIB=sc-lego-loam_amd/variants/libslo_p.so
+timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_loop.py tests/test_gpu_posegraph.py tests/test_gpu_imu.py -x -q --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/t_par.log 2>&1
+tail -1 $OUT/t_par.log
+unset SLO_LIB
+bash tools/gpu_variants.sh ${1:-r02aa}/v sc-lego-loam_amd/variants/libslo_m.so sc-lego-loam_amd/variants/libslo_p.so sc-lego-loam_amd/variants/libslo_m.so sc-lego-loam_amd/variants/libslo_p.so
