@@ -158,6 +158,18 @@ int slo_sc_make_and_save(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
  * (used to seed the Scan Context history, e.g. from a previous session) */
 int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
 
+/* pcl::VoxelGrid<PointXYZI> setLeafSize(leaf) + filter (PCL 1.8 applyFilter,
+ * the reference's downsize filters: featureAssociation.cpp:779-780,
+ * mapOptmization.cpp:1224-1262) on every stream's device cloud at once:
+ * stream s's d_n[s] float4 points (x, y, z, intensity; non-finite ones
+ * skipped) at d_in + s * in_stride points; its centroids, in voxel-index
+ * order, to d_out + s * out_stride, at most out_cap (more are clipped and
+ * flagged in slo_get(.., "vg_stats")[1]), their count to d_nout[s].  The
+ * order inside a voxel follows cfg.voxel_order (SLO_VOXEL_PCL: std::sort's,
+ * as PCL).  Asynchronous on slo_stream(ctx). */
+int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,
+                         void* d_out, size_t out_stride, int32_t* d_nout, int out_cap);
+
 /* ---------------------------------------------------------------- loop-closure verification
  * mapOptmization.cpp:841-1110 (detectLoopClosure + performLoopClosure, minus
  * the GTSAM factors).  Needs cfg.loop_verify = 1 and

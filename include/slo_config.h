@@ -120,7 +120,16 @@ typedef struct slo_config {
        0 = off (the keyframe estimate is its initial value, as in the
        reference while no loop is closed) */
     int32_t pose_graph;
+    /* the order of the points inside a voxel, which fixes every VoxelGrid
+       centroid's float sum (PCL VoxelGrid, FA:779-780, MO:1224-1262):
+         SLO_VOXEL_PCL (0, default)  std::sort's order, as the reference's PCL
+                                     (slo_vgpcl.hip, slo_pclsort.h);
+         SLO_VOXEL_STABLE (1)        input order (a stable radix sort; faster,
+                                     centroids differ from PCL's by rounding) */
+    int32_t voxel_order;
 } slo_config;
+
+enum { SLO_VOXEL_PCL = 0, SLO_VOXEL_STABLE = 1 };
 
 /* preset ids */
 enum {

@@ -201,6 +201,9 @@ int oracle_get(void* h, const char* name_c, void* out, int cap) {
     if (name == "surf_total_ds") return copy_cloud(s->mo.laserCloudSurfTotalLastDS, (float*)out, cap);
     if (name == "map_corner_ds") return copy_cloud(s->mo.lastCornerMapDS, (float*)out, cap);
     if (name == "map_surf_ds") return copy_cloud(s->mo.lastSurfMapDS, (float*)out, cap);
+    // the local maps before their VoxelGrid (MO:1224-1230), as last assembled
+    if (name == "map_corner_raw") return copy_cloud(s->mo.lastCornerMapRaw, (float*)out, cap);
+    if (name == "map_surf_raw") return copy_cloud(s->mo.lastSurfMapRaw, (float*)out, cap);
     if (name == "sc_desc") {
         if (s->mo.sc.polarcontexts_.empty()) return 0;
         auto& d = s->mo.sc.polarcontexts_.back();

@@ -43,6 +43,7 @@ struct MapOptimization {
     Cloud laserCloudSurfTotalLast, laserCloudSurfTotalLastDS;
     Cloud laserCloudCornerFromMap, laserCloudSurfFromMap, laserCloudCornerFromMapDS, laserCloudSurfFromMapDS;
     Cloud lastCornerMapDS, lastSurfMapDS;   // the last run's DS maps (parity checks only)
+    Cloud lastCornerMapRaw, lastSurfMapRaw; // and the maps before their VoxelGrid (parity checks only)
     Cloud laserCloudOri, coeffSel;
     KdTree kdtreeCornerFromMap, kdtreeSurfFromMap;
     bool isDegenerate = false;
@@ -512,6 +513,7 @@ struct MapOptimization {
         // clearCloud (MO:1640): the DS maps are kept aside for parity checks
         lastCornerMapDS.swap(laserCloudCornerFromMapDS);
         lastSurfMapDS.swap(laserCloudSurfFromMapDS);
+        lastCornerMapRaw.swap(laserCloudCornerFromMap); lastSurfMapRaw.swap(laserCloudSurfFromMap);
         laserCloudCornerFromMap.clear(); laserCloudSurfFromMap.clear();
         laserCloudCornerFromMapDS.clear(); laserCloudSurfFromMapDS.clear();
         return true;

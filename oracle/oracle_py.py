@@ -48,7 +48,7 @@ class SloConfig(ctypes.Structure):
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
         ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
-        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32), ("voxel_order", ctypes.c_int32),
     ]
 
 
@@ -144,7 +144,8 @@ assert LOOP_DTYPE.itemsize == 128
 _DTYPES["loop"] = LOOP_DTYPE
 _DTYPES["imu"] = np.float64
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
-           "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds"}
+           "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds",
+           "map_corner_raw", "map_surf_raw"}
 
 
 def voxel_grid(pts, leaf, stable=False):

@@ -108,6 +108,7 @@ inline int slo_config_preset_impl(int preset, slo_config* c) {
     c->map_keyframes = 0;
     c->keyframe_ring = 0;
     c->pose_graph = 0;
+    c->voxel_order = 0;   /* SLO_VOXEL_PCL */
     return 0;
 }
 #endif

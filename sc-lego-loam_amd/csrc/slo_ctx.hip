@@ -344,6 +344,7 @@ void slo_destroy(slo_ctx* ctx) {
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
     slo::graphs_drop(ctx);
     slo::vg_free(ctx);
+    slo::pcl_free(ctx);
     slo::grid_free(ctx->grid_c);
     slo::grid_free(ctx->grid_s);
     slo::grid_free(ctx->grid_oc);
@@ -674,6 +675,12 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "tobe_mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformTobeMapped, 24); count = 6; esz = 4; }
     else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
+    else if (name == "vg_stats") {   // [0] PCL-order finish ranges over the LDS capacity (slo_vgpcl.hip), [1] clipped outputs
+        int32_t a[2] = {0, 0};
+        if (ctx->pws.cstat) SLO_CHECK(hipMemcpy(&a[0], ctx->pws.cstat, 4, hipMemcpyDeviceToHost));
+        SLO_CHECK(hipMemcpy(&a[1], ctx->mws.errflag, 4, hipMemcpyDeviceToHost));
+        tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
+    }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "imu") {   // FA's IMU scalars (slo::ImuState), as float64
         slo::ImuState m;
@@ -965,6 +972,15 @@ int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_count
                         &v.st->n_raw_ds, SS, v.P);
     if (r) return r;
     return slo::sc_make_run(ctx, v.cur_raw_ds, v.P, &v.st->n_raw_ds, SS, ctx->S);
+}
+
+int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,
+                         void* d_out, size_t out_stride, int32_t* d_nout, int out_cap) {
+    if (!ctx || !d_in || !d_n || !d_out || !d_nout || in_stride == 0 || out_cap < 0 || !(leaf > 0.0f))
+        return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::vg_run(ctx, "user", (const float4*)d_in, in_stride, d_n, 1, leaf, (float4*)d_out, out_stride, d_nout,
+                       1, out_cap);
 }
 
 int slo_pack_records(slo_ctx* ctx, void* d_out) {

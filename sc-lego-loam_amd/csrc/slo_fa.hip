@@ -20,6 +20,7 @@
 //     of (voxel idx, position) keys in LDS, centroid of each voxel summed in
 //     position order (DESIGN.md "VoxelGrid order").
 #include "slo_internal.h"
+#include "slo_pclsort.h"
 #include "slo_libm.h"
 #include "slo_introsort.h"
 #include "slo_imu.h"
@@ -790,7 +791,17 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
         const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
         return (((unsigned long long)idx << 32) | (unsigned int)i) | (0ull - (unsigned long long)(i >= n));
     };
-    if (n <= 256) ring_sort_regs<1>(keys, key_of);
+    if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // std::sort's order, as PCL (slo_pclsort.h)
+        __shared__ slo_pcl::BlockSmem<256, 2048, 64> psm;
+        for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = key_of(i);
+        __syncthreads();
+        if (n <= 2048) {
+            slo_pcl::pcl_block_sort<256, 2048, 64>(keys, n, 2 * slo_pcl::lg2(n), psm);
+        } else {   // rings over 2048 points: one lane (no preset has them)
+            if (threadIdx.x == 0) slo_sort::introsort_range(keys, n, 2 * slo_pcl::lg2(n), slo_pcl::Less());
+            __syncthreads();
+        }
+    } else if (n <= 256) ring_sort_regs<1>(keys, key_of);
     else if (n <= 512) ring_sort_regs<2>(keys, key_of);
     else if (n <= 1024) ring_sort_regs<4>(keys, key_of);
     else if (n <= 2048) ring_sort_regs<8>(keys, key_of);

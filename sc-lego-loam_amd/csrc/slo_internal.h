@@ -460,6 +460,22 @@ struct MapWs {  // VoxelGrid workspace (slo_vg.hip), sized on the host from the 
     int32_t* osw = nullptr;       // [32] tickets (pass, XCD), [8] tiles per XCD, [S] XCD tile offsets
     unsigned long long* lbk = nullptr;   // [tiles][256] (tag, inclusive flag, count)
 };
+struct PSeg;
+struct PRes;
+struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the input strides only
+    size_t items = 0, tiles = 0;
+    int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries, pair chunks)
+    int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
+    int32_t* nfin = nullptr;      // [S] finite points per stream
+    unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
+    PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level
+    PRes* res = nullptr;          // per range of the current level: pivot, m, cuts, pair chunks
+    int* cseg[2] = {nullptr, nullptr};     // chunk -> range
+    int2* ccnt = nullptr;         // per chunk stopper counts -> prefixes
+    int* pseg = nullptr;          // pair chunk -> range
+    int4* wl = nullptr;           // finish entries (f, l, depth)
+    int* tcnt = nullptr;          // [S][maxT] finite points per tile -> prefixes
+};
 struct HashGrid {
     int T = 0;
     float cell = 1.0f;
@@ -508,6 +524,7 @@ struct slo_ctx {
     int32_t* d_cnt = nullptr;
     // mapping workspaces
     slo::MapWs mws;
+    slo::PclWs pws;
     slo::HashGrid grid_c, grid_s, grid_oc, grid_os;
     bool map_ready = false;
     // loop-closure verification (cfg.loop_verify)
@@ -551,6 +568,7 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan);
 void fa_swap_last(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
+void pcl_free(slo_ctx* ctx);
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);
 int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell);

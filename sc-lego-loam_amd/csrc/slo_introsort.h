@@ -164,4 +164,41 @@ SLO_SORT_HD void std_sort(T* first, int n, Less less) {
     }
 }
 
+// What std::sort still does to one sub-range [first, first+n) that its
+// introsort loop reaches with `depth` levels of budget left: the rest of the
+// loop on it, then the final insertion sort restricted to it.  The global
+// final insertion sort never moves an element across a partition boundary
+// (everything left of a cut is <= everything right of it, and an element
+// only passes strictly greater ones), so restricting it to the sub-range —
+// and making it guarded — changes nothing.  Used by the PCL-order VoxelGrid
+// (slo_pclsort.h) for the sub-ranges one lane finishes.
+template <class T, class Less>
+SLO_SORT_HD void introsort_range(T* first, int n, int depth, Less less) {
+    if (n <= 1) return;
+    const int threshold = 16;
+    int st_lo[64], st_hi[64], st_d[64];
+    int sp = 0;
+    st_lo[sp] = 0; st_hi[sp] = n; st_d[sp] = depth; sp++;
+    while (sp > 0) {
+        sp--;
+        int lo = st_lo[sp], hi = st_hi[sp], dep = st_d[sp];
+        while (hi - lo > threshold) {
+            if (dep == 0) {
+                heap_sort_(first + lo, hi - lo, less);
+                break;
+            }
+            --dep;
+            T* f = first + lo;
+            T* l = first + hi;
+            T* mid = f + (hi - lo) / 2;
+            move_median_to_first_(f, f + 1, mid, l - 1, less);
+            T* cut = unguarded_partition_(f + 1, l, f, less);
+            int c = (int)(cut - first);
+            st_lo[sp] = c; st_hi[sp] = hi; st_d[sp] = dep; sp++;
+            hi = c;
+        }
+    }
+    insertion_sort_(first, first + n, less);
+}
+
 }  // namespace slo_sort

@@ -17,29 +17,11 @@
 // buckets [S][T + 1] (the last bucket of each stream stays empty, so a run of
 // consecutive buckets ends at off[h + 1]); queried by grid_ball
 // (slo_internal.h).
-#include "slo_internal.h"
+#include "slo_vgcommon.h"
 #include <float.h>
 #include <string>
 
 namespace slo {
-
-// a VoxelGrid input: a cloud [S][stride] with counts n[s * n_stride], or
-// (in == nullptr) the context's input scan through its io slot
-struct VgSrc {
-    const float4* in;
-    const int32_t* n;
-    const SloIo* io;
-    __device__ const float4* pts() const { return in ? in : io->pts; }
-    __device__ const int32_t* cnt() const { return in ? n : io->npts; }
-};
-
-__device__ inline unsigned int f2ord(float f) {
-    unsigned int u = __float_as_uint(f);
-    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
-}
-__device__ inline float ord2f(unsigned int u) {
-    return __uint_as_float((u & 0x80000000u) ? (u & 0x7fffffffu) : ~u);
-}
 
 // stream offsets of the concatenated input (block scan), bounds init, and the
 // meta words [total, max cell count, long-voxel count]
@@ -124,33 +106,6 @@ __global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, 
     }
 }
 
-// voxel-index parameters (PCL applyFilter) per stream, and the stream's key
-// width: vbits (every voxel index < 2^vbits - 1, the all-ones key marks a
-// non-finite point), split into npass digits of dbits <= VG_DMAX each
-struct VgParams { int minb[3]; int mul1, mul2; int overflow; float inv; int vbits, dbits, npass, ntiles; };
-
-#ifndef VG_T
-#define VG_T 256                      // threads per tile workgroup
-#endif
-#define VG_W (VG_T / 64)              // waves per tile workgroup (each owns a slice of the tile)
-#ifndef VG_SCATTER_OCC
-// vg_scatter waves per SIMD: 3 leaves room (<= 168 VGPRs) for all of a tile's
-// key and value loads in flight at once; at 4 the same code spills (measured
-// 28.5 k against 27.9 k scans/s, and 26.8 k for 4 waves with one load in flight)
-#define VG_SCATTER_OCC (VG_W == 4 ? 3 : 6)
-#endif
-#ifndef VG_IPT
-#define VG_IPT 16                     // items per thread
-#endif
-#define VG_TILE (VG_T * VG_IPT)       // items per tile
-#define VG_PASSES 4                   // LSD radix passes launched (a stream runs npass <= VG_PASSES of them)
-#ifndef VG_DMAX
-#define VG_DMAX 8                     // digit bits per pass at most; VG_PASSES * VG_DMAX >= 32
-#endif
-#define VG_NB (1 << VG_DMAX)          // digit bins
-static_assert(VG_PASSES * VG_DMAX >= 32 && (VG_NB % VG_T == 0 || VG_T % VG_NB == 0), "VoxelGrid digit layout");
-#define VG_PAD(j) ((j) + ((j) >> 4))  // LDS index padded against 16-way bank conflicts (blocked reads)
-
 // Tile kernels run on a (GX, S8) grid, S8 = S rounded up to 8.  With VG_XCD
 // the linear workgroup id is split XCD-aware (xcd_stream_chunk): all GX
 // workgroups of a stream land on one XCD, so a stream's tiles share that
@@ -201,39 +156,6 @@ __global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int 
     p.npass = (vb + VG_DMAX - 1) / VG_DMAX;
     p.dbits = (vb + p.npass - 1) / p.npass;
     prm[s] = p;
-}
-
-__device__ inline unsigned int vg_none(const VgParams& p) { return p.vbits >= 32 ? 0xffffffffu : (1u << p.vbits) - 1u; }
-
-// the PCL voxel index of point i of a stream (positions on overflow)
-__device__ inline unsigned int vg_key(const float4& q, const VgParams& p, int i) {
-    if (!(isfinite(q.x) & isfinite(q.y) & isfinite(q.z))) return vg_none(p);   // no short-circuit: one load
-    if (p.overflow) return (unsigned int)i;
-    const int ijk0 = (int)(floorf(q.x * p.inv) - (float)p.minb[0]);
-    const int ijk1 = (int)(floorf(q.y * p.inv) - (float)p.minb[1]);
-    const int ijk2 = (int)(floorf(q.z * p.inv) - (float)p.minb[2]);
-    return (unsigned int)(ijk0 + ijk1 * p.mul1 + ijk2 * p.mul2);
-}
-
-// exclusive scan over the workgroup (NW waves of 64); *total = the sum
-template <int NW, class T>
-__device__ inline T vg_block_scan(T x, T* wsum, T* total) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    T incl = x;
-    for (int o = 1; o < 64; o <<= 1) {
-        const T y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    T before = 0, all = 0;
-    for (int k = 0; k < NW; ++k) {
-        if (k < w) before += wsum[k];
-        all += wsum[k];
-    }
-    __syncthreads();   // wsum reusable
-    *total = all;
-    return before + incl - x;
 }
 
 // ---- LSD radix passes.  The items of stream s occupy [off[s], off[s+1]) of
@@ -1025,6 +947,12 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
     const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
+    if (ctx->cfg.voxel_order == SLO_VOXEL_PCL) {   // the reference's order (slo_vgpcl.hip)
+        if (int r = vg_pcl_sort(ctx, src, in_stride, w.prm, w.off, w.keys, w.vals)) return r;
+        if (tm) timing_end(ctx, sort_name.c_str(), ev);
+        *keys = w.keys; *vals = w.vals; *spare_k = w.keys2; *spare_v = w.vals2;
+        return 0;
+    }
     // pair A = keys2/vals2, pair B = keys/vals (every stream's last pass writes B)
     unsigned int *ka = w.keys2, *va = w.vals2, *kb = w.keys, *vb = w.vals;
     if (ctx->vg_onesweep) {

@@ -1,0 +1,550 @@
+// slo_vgpcl.hip — the batched VoxelGrid sort in PCL's own order
+// (cfg.voxel_order == SLO_VOXEL_PCL, the default).
+//
+// PCL's VoxelGrid::applyFilter (featureAssociation.cpp:779-780,
+// mapOptmization.cpp:1224-1262) collects (voxel index, point index) pairs of
+// the finite points in input order and sorts them with std::sort by voxel
+// index; each voxel's centroid is summed in the resulting order.  This file
+// produces that order exactly (slo_pclsort.h states the formulation) for S
+// streams at once; the voxel heads and centroid sums of slo_vg.hip then read
+// it as they read the radix sort's.
+//
+// Pipeline per call (all sizes from the input strides, counts on the device):
+//   k_pc_count, k_pc_scan, k_pc_write: the finite points' items, compacted in
+//     input order (the raw cloud is not dense, MO:1236; the other clouds are
+//     finite), the non-finite ones after them with the "none" key; each
+//     stream's range becomes the first introsort range: a global range
+//     (> PC_T items) or a finish entry;
+//   G global levels, one introsort step of every global range per level:
+//     k_pc_lcount  per chunk of PC_CH positions: stopper counts (the median of
+//                  three is taken virtually: every chunk derives it alone);
+//     k_pc_lscan   per range: chunk prefixes, m from the chunk where the
+//                  left / right counts cross, the pair chunks;
+//     k_pc_lrank   per chunk: the positions of the left stoppers of rank < m
+//                  and of the right stoppers of rank < m (from the right), the
+//                  cut candidates; chunk 0 makes the median swap real;
+//     k_pc_lpairs  the swaps;
+//     k_pc_lsplit  per range: the halves — over PC_T items back to the next
+//                  level, otherwise (or at the last level) a finish entry;
+//   k_pc_finish: one workgroup per finish entry (<= PC_T items) sorts it in
+//     LDS to the end (pcl_block_sort); an entry still over PC_T after the G
+//     levels (never seen on the configs; counted in meta) is finished by one
+//     lane in global memory.
+#include "slo_vgcommon.h"
+#include "slo_pclsort.h"
+
+namespace slo {
+
+using slo_pcl::u64;
+
+#define PC_CH 4096        // positions per chunk of the global levels (256 threads x 16)
+#define PC_CT 256
+#define PC_PCH 4096       // pairs per pair chunk
+#define PC_T 8192         // a range of at most PC_T items is finished in LDS
+#define PC_FT 1024        // threads of the big finish workgroup
+#define PC_BT 64          // ranges of <= PC_BT items are finished by one lane
+#define PC_ST 2048        // small finish entries (<= PC_ST items): 256-thread workgroups
+#define PC_G 2048         // workgroups of the grid-stride level kernels
+
+struct PSeg { int f, l, d, c0; };
+struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB, pc0; };
+
+// counters (PclWs::ctr)
+enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 4, PCC_NPC = 5 };
+
+// libstdc++ __move_median_to_first on the keys at f+1, mid, l-1: which of
+// them (0, 1, 2) is swapped to f
+__device__ inline int median3(unsigned int a, unsigned int b, unsigned int c) {
+    if (a < b) {
+        if (b < c) return 1;
+        if (a < c) return 2;
+        return 0;
+    }
+    if (a < c) return 0;
+    if (b < c) return 2;
+    return 1;
+}
+// the pivot of range [f, l), the position swapped with f, and the key that
+// lands there (the one at f)
+__device__ inline void pc_median(const unsigned int* K, int f, int l, unsigned int& piv, int& med, unsigned int& vmed) {
+    const int pos[3] = {f + 1, f + (l - f) / 2, l - 1};
+    const unsigned int k0 = K[pos[0]], k1 = K[pos[1]], k2 = K[pos[2]], kf = K[f];
+    const int w = median3(k0, k1, k2);
+    med = pos[w];
+    piv = w == 0 ? k0 : (w == 1 ? k1 : k2);
+    vmed = kf;
+}
+
+// ---- items: finite points first, in input order
+__global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, const int32_t* off,
+                                                    const VgParams* prm, int* tcnt, int maxT, int S, int* ctr) {
+    __shared__ unsigned int wsum[VG_W];
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 16) ctr[threadIdx.x] = 0;
+    const int s = blockIdx.y;
+    if (s >= S) return;
+    const VgParams p = prm[s];
+    const int n = off[s + 1] - off[s];
+    const float4* in = src.pts() + (size_t)s * in_stride;
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        float4 q[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) q[k] = in[a + min(k * VG_T + (int)threadIdx.x, m - 1)];
+        unsigned int c = 0;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k)
+            c += (k * VG_T + (int)threadIdx.x < m) & isfinite(q[k].x) & isfinite(q[k].y) & isfinite(q[k].z);
+        unsigned int total;
+        vg_block_scan<VG_W>(c, wsum, &total);
+        if (threadIdx.x == 0) tcnt[(size_t)s * maxT + t] = (int)total;
+    }
+}
+
+// per stream: tile prefix of the finite counts, and the stream's first range
+__global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
+                                                  PSeg* seg0, int* cseg0, int4* wl, int* ctr, int32_t* nfin) {
+    __shared__ int wsum[16];
+    __shared__ int slot_c0[2];
+    const int s = blockIdx.x, tid = threadIdx.x;
+    const VgParams p = prm[s];
+    const int nt = p.ntiles;
+    int* h = tcnt + (size_t)s * maxT;
+    const int L = (nt + 1023) / 1024, t0 = min(nt, tid * L), t1 = min(nt, t0 + L);
+    int sum = 0;
+    for (int t = t0; t < t1; ++t) sum += h[t];
+    int total;
+    int run = vg_block_scan<16>(sum, wsum, &total);
+    for (int t = t0; t < t1; ++t) {
+        const int x = h[t];
+        h[t] = run;
+        run += x;
+    }
+    const int f = off[s], n = total;
+    if (tid == 0) {
+        nfin[s] = n;
+        slot_c0[0] = -1;
+        // overflow keys are the positions: already in order
+        if (!p.overflow && n >= 2) {
+            const int d = 2 * slo_pcl::lg2(n);
+            if (n > PC_T) {
+                const int nch = (n - 1 + PC_CH - 1) / PC_CH;
+                const int slot = atomicAdd(&ctr[PCC_NSEG], 1);
+                const int c0 = atomicAdd(&ctr[PCC_NCH], nch);
+                seg0[slot] = PSeg{f, f + n, d, c0};
+                slot_c0[0] = slot; slot_c0[1] = c0;
+            } else {
+                const int w = atomicAdd(&ctr[PCC_NW], 1);
+                wl[w] = make_int4(f, f + n, d, 0);
+            }
+        }
+    }
+    __syncthreads();
+    if (slot_c0[0] >= 0) {
+        const int nch = (n - 1 + PC_CH - 1) / PC_CH;
+        for (int c = tid; c < nch; c += 1024) cseg0[slot_c0[1] + c] = slot_c0[0];
+    }
+}
+
+__global__ void __launch_bounds__(VG_T) k_pc_write(VgSrc src, size_t in_stride, const int32_t* off,
+                                                    const VgParams* prm, const int* tcnt, const int32_t* nfin,
+                                                    int maxT, unsigned int* K, unsigned int* V, int S) {
+    __shared__ unsigned int wsum[VG_W];
+    const int s = blockIdx.y;
+    if (s >= S) return;
+    const VgParams p = prm[s];
+    const int base = off[s], n = off[s + 1] - base, nf = nfin[s];
+    const float4* in = src.pts() + (size_t)s * in_stride;
+    for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
+        const int a = t * VG_TILE, m = min(VG_TILE, n - a);
+        // blocked: thread tid holds items a + tid*VG_IPT + k, so the block scan keeps input order
+        const int j0 = threadIdx.x * VG_IPT;
+        float4 q[VG_IPT];
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) q[k] = in[a + min(j0 + k, m - 1)];
+        unsigned int key[VG_IPT], fin = 0, c = 0;
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            key[k] = vg_key(q[k], p, a + j0 + k);
+            const bool ok = j0 + k < m && key[k] != vg_none(p);
+            fin |= (unsigned int)ok << k;
+            c += ok;
+        }
+        unsigned int total;
+        const unsigned int ex = vg_block_scan<VG_W>(c, wsum, &total);
+        int r = tcnt[(size_t)s * maxT + t] + (int)ex;        // finite items before this thread's first
+        int rn = nf + (a + j0) - r;                            // non-finite items before it
+#pragma unroll
+        for (int k = 0; k < VG_IPT; ++k) {
+            if (j0 + k >= m) break;
+            const int o = ((fin >> k) & 1) ? r++ : rn++;
+            K[base + o] = key[k];
+            V[base + o] = (unsigned int)(a + j0 + k);
+        }
+    }
+}
+
+// ---- global levels
+__device__ inline void pc_chunk(const PSeg& g, int c, int& a, int& b) {
+    a = g.f + 1 + (c - g.c0) * PC_CH;
+    b = min(g.l, a + PC_CH);
+}
+
+__global__ void __launch_bounds__(PC_CT) k_pc_lcount(const unsigned int* K, const PSeg* seg, const int* cseg,
+                                                      int2* ccnt, int* ctr, int cur) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[PCC_NPC] = 0;   // pair chunks of this level (k_pc_lscan)
+    __shared__ unsigned int wsum[PC_CT / 64];
+    const int nch = ctr[PCC_NCH + cur];
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        const PSeg g = seg[cseg[c]];
+        unsigned int piv, vmed;
+        int med;
+        pc_median(K, g.f, g.l, piv, med, vmed);
+        int a, b;
+        pc_chunk(g, c, a, b);
+        unsigned int kk[PC_CH / PC_CT];
+#pragma unroll
+        for (int q = 0; q < PC_CH / PC_CT; ++q) kk[q] = K[min(a + q * PC_CT + (int)threadIdx.x, b - 1)];
+        unsigned int cl = 0, cr = 0;
+#pragma unroll
+        for (int q = 0; q < PC_CH / PC_CT; ++q) {
+            const int x = a + q * PC_CT + (int)threadIdx.x;
+            const unsigned int k = x == med ? vmed : kk[q];
+            const bool in = x < b;
+            cl += in & !(k < piv);
+            cr += in & !(piv < k);
+        }
+        unsigned int total;
+        vg_block_scan<PC_CT / 64>(cl | (cr << 16), wsum, &total);
+        if (threadIdx.x == 0) ccnt[c] = make_int2((int)(total & 0xffffu), (int)(total >> 16));
+    }
+}
+
+// per range: pivot record, chunk prefixes, m, pair chunks
+__global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const PSeg* seg, int2* ccnt, PRes* res,
+                                                     int* pseg, int* ctr, int cur) {
+    __shared__ unsigned int wsum[PC_CT / 64];
+    __shared__ int cstar_s, mx_s, pc0_s;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { ctr[PCC_NSEG + (cur ^ 1)] = 0; ctr[PCC_NCH + (cur ^ 1)] = 0; }
+    const int ns = ctr[PCC_NSEG + cur];
+    const int tid = threadIdx.x;
+    for (int s = blockIdx.x; s < ns; s += gridDim.x) {
+        const PSeg g = seg[s];
+        unsigned int piv, vmed;
+        int med;
+        pc_median(K, g.f, g.l, piv, med, vmed);
+        const int nch = (g.l - g.f - 1 + PC_CH - 1) / PC_CH;
+        // exclusive prefix of the chunk counts, in place (chunks in rounds of PC_CT)
+        int runL = 0, runR = 0;
+        for (int c0 = 0; c0 < nch; c0 += PC_CT) {
+            const int c = c0 + tid;
+            const int2 x = c < nch ? ccnt[g.c0 + c] : make_int2(0, 0);
+            int totL, totR;
+            const int exL = vg_block_scan<PC_CT / 64>(x.x, (int*)wsum, &totL);
+            const int exR = vg_block_scan<PC_CT / 64>(x.y, (int*)wsum, &totR);
+            if (c < nch) ccnt[g.c0 + c] = make_int2(runL + exL, runR + exR);
+            runL += totL;
+            runR += totR;
+        }
+        const int TR = runR;
+        __syncthreads();   // the prefixes are visible to the block
+        // the crossing chunk: the first whose end boundary has left >= right-at-or-after
+        if (tid == 0) cstar_s = nch - 1;
+        __syncthreads();
+        for (int c = tid; c < nch; c += PC_CT) {
+            const int2 pre = ccnt[g.c0 + c];
+            const int2 nxt = c + 1 < nch ? ccnt[g.c0 + c + 1] : make_int2(runL, runR);
+            (void)pre;
+            if (nxt.x >= TR - nxt.y) atomicMin(&cstar_s, c);
+        }
+        __syncthreads();
+        const int cs = cstar_s;
+        // exact m over the boundaries of the crossing chunk (its end included)
+        int a, b;
+        pc_chunk(g, g.c0 + cs, a, b);
+        const int2 pre = ccnt[g.c0 + cs];
+        constexpr int Q = PC_CH / PC_CT;
+        const int j0 = tid * Q;   // blocked positions a + j0 ..
+        unsigned int kk[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) kk[q] = K[min(a + j0 + q, b - 1)];
+        unsigned int fl = 0, fr = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int x = a + j0 + q;
+            const unsigned int k = x == med ? vmed : kk[q];
+            if (x < b) {
+                fl |= (unsigned int)!(k < piv) << q;
+                fr |= (unsigned int)!(piv < k) << q;
+            }
+        }
+        unsigned int tot;
+        const unsigned int ex = vg_block_scan<PC_CT / 64>((unsigned int)__popc(fl) | ((unsigned int)__popc(fr) << 16),
+                                                          wsum, &tot);
+        int rl = pre.x + (int)(ex & 0xffffu), rr = pre.y + (int)(ex >> 16);
+        int g_best = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int x = a + j0 + q;
+            if (x < b) g_best = max(g_best, min(rl, TR - rr));
+            rl += (fl >> q) & 1;
+            rr += (fr >> q) & 1;
+        }
+        if (a + j0 < b && a + j0 + Q >= b) g_best = max(g_best, min(rl, TR - rr));   // the end boundary b
+        if (tid == 0) mx_s = 0;
+        __syncthreads();
+        atomicMax(&mx_s, g_best);
+        __syncthreads();
+        const int m = mx_s;
+        if (tid == 0) {
+            const int npc = (m + PC_PCH - 1) / PC_PCH;
+            pc0_s = npc ? atomicAdd(&ctr[PCC_NPC], npc) : 0;
+            res[s] = PRes{piv, vmed, med, m, TR, 0x7fffffff, 0x7fffffff, pc0_s};
+        }
+        __syncthreads();
+        const int npc = (m + PC_PCH - 1) / PC_PCH;
+        for (int i = tid; i < npc; i += PC_CT) pseg[pc0_s + i] = s;
+        __syncthreads();   // shared scalars reused by the next range
+    }
+}
+
+__global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
+                                                     const int2* ccnt, PRes* res, unsigned int* PA, unsigned int* PB,
+                                                     const int* ctr, int cur) {
+    __shared__ unsigned int wsum[PC_CT / 64];
+    const int nch = ctr[PCC_NCH + cur];
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
+        const int si = cseg[c];
+        const PSeg g = seg[si];
+        const PRes r = res[si];
+        int a, b;
+        pc_chunk(g, c, a, b);
+        constexpr int Q = PC_CH / PC_CT;
+        const int j0 = threadIdx.x * Q;
+        unsigned int kk[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) kk[q] = K[min(a + j0 + q, b - 1)];
+        unsigned int fl = 0, fr = 0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int x = a + j0 + q;
+            const unsigned int k = x == r.med ? r.vmed : kk[q];
+            if (x < b) {
+                fl |= (unsigned int)!(k < r.piv) << q;
+                fr |= (unsigned int)!(r.piv < k) << q;
+            }
+        }
+        unsigned int tot;
+        const unsigned int ex = vg_block_scan<PC_CT / 64>((unsigned int)__popc(fl) | ((unsigned int)__popc(fr) << 16),
+                                                          wsum, &tot);
+        const int2 pre = ccnt[c];
+        int rl = pre.x + (int)(ex & 0xffffu), rr = pre.y + (int)(ex >> 16);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const int x = a + j0 + q;
+            if ((fl >> q) & 1) {
+                if (rl < r.m) PA[g.f + rl] = (unsigned int)x;
+                else if (rl == r.m) res[si].cutA = x;          // i_{m+1}
+                ++rl;
+            }
+            if ((fr >> q) & 1) {
+                const int kr = r.TR - 1 - rr;                   // rank from the right
+                if (kr < r.m) PB[g.f + kr] = (unsigned int)x;
+                if (kr == r.m - 1) res[si].cutB = x;            // j_m
+                ++rr;
+            }
+        }
+        if (c == g.c0 && threadIdx.x == 0 && r.med != g.f) {    // the median swap, made real
+            const unsigned int kf = K[g.f], vf = V[g.f], km = K[r.med], vm = V[r.med];
+            K[g.f] = km; V[g.f] = vm; K[r.med] = kf; V[r.med] = vf;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int* V, const PSeg* seg, const PRes* res,
+                                                    const int* pseg, const unsigned int* PA, const unsigned int* PB,
+                                                    const int* ctr) {
+    const int npc = ctr[PCC_NPC];
+    for (int pc = blockIdx.x; pc < npc; pc += gridDim.x) {
+        const int si = pseg[pc];
+        const PSeg g = seg[si];
+        const PRes r = res[si];
+        const int k0 = (pc - r.pc0) * PC_PCH, k1 = min(r.m, k0 + PC_PCH);
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += 256) {
+            const unsigned int x = PA[g.f + k], y = PB[g.f + k];
+            const unsigned int kx = K[x], vx = V[x], ky = K[y], vy = V[y];
+            K[x] = ky; V[x] = vy; K[y] = kx; V[y] = vx;
+        }
+    }
+}
+
+__global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* res, PSeg* nseg, int* ncseg,
+                                                    int4* wl, int* ctr, int cur, int last) {
+    __shared__ int slot_s[2], c0_s[2], nch_s[2];
+    const int ns = ctr[PCC_NSEG + cur];
+    for (int s = blockIdx.x; s < ns; s += gridDim.x) {
+        const PSeg g = seg[s];
+        const PRes r = res[s];
+        if (threadIdx.x == 0) {
+            const int cut = min(r.cutA, r.m > 0 ? r.cutB : 0x7fffffff);
+            const int D = g.d - 1;
+            const int lo[2] = {g.f, cut}, hi[2] = {cut, g.l};
+            for (int h = 0; h < 2; ++h) {
+                slot_s[h] = -1;
+                const int n = hi[h] - lo[h];
+                if (n <= 1) continue;
+                if (n > PC_T && D > 0 && !last) {
+                    const int nch = (n - 1 + PC_CH - 1) / PC_CH;
+                    slot_s[h] = atomicAdd(&ctr[PCC_NSEG + (cur ^ 1)], 1);
+                    c0_s[h] = atomicAdd(&ctr[PCC_NCH + (cur ^ 1)], nch);
+                    nch_s[h] = nch;
+                    nseg[slot_s[h]] = PSeg{lo[h], hi[h], D, c0_s[h]};
+                } else {
+                    const int w = atomicAdd(&ctr[PCC_NW], 1);
+                    wl[w] = make_int4(lo[h], hi[h], D, 0);
+                }
+            }
+        }
+        __syncthreads();
+        for (int h = 0; h < 2; ++h)
+            if (slot_s[h] >= 0)
+                for (int i = threadIdx.x; i < nch_s[h]; i += 256) ncseg[c0_s[h] + i] = slot_s[h];
+        __syncthreads();
+    }
+}
+
+// ---- finish: one workgroup per entry
+template <int NT, int NMAX>
+__global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int* V, const int4* wl, const int* ctr,
+                                                  int* cstat, u64* scratch, int lo_excl, int hi_incl) {
+    __shared__ u64 items[NMAX];
+    __shared__ slo_pcl::BlockSmem<NT, NMAX, PC_BT> sm;
+    const int nw = ctr[PCC_NW];
+    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
+        const int4 w = wl[e];
+        const int f = w.x, n = w.y - w.x, d = w.z;
+        if (n <= lo_excl || n > hi_incl) continue;   // another finish kernel's entry
+        if (n <= NMAX) {
+            for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
+            __syncthreads();
+            slo_pcl::pcl_block_sort<NT, NMAX, PC_BT>(items, n, d, sm);
+            for (int i = threadIdx.x; i < n; i += NT) {
+                const u64 it = items[i];
+                K[f + i] = (unsigned int)(it >> 32);
+                V[f + i] = (unsigned int)it;
+            }
+            __syncthreads();
+        } else {   // over the LDS capacity after the global levels: one lane, in global memory
+            for (int i = threadIdx.x; i < n; i += NT) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                atomicAdd(&cstat[0], 1);
+                slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());
+            }
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += NT) {
+                const u64 it = scratch[f + i];
+                K[f + i] = (unsigned int)(it >> 32);
+                V[f + i] = (unsigned int)it;
+            }
+            __syncthreads();
+        }
+    }
+}
+
+// ---- workspace and driver
+static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
+    PclWs& w = ctx->pws;
+    const size_t S = (size_t)ctx->S;
+    if (!w.ctr) {
+        SLO_CHECK(hipMalloc(&w.ctr, 16 * sizeof(int)));
+        SLO_CHECK(hipMemset(w.ctr, 0, 16 * sizeof(int)));
+        SLO_CHECK(hipMalloc(&w.nfin, S * sizeof(int32_t)));
+        SLO_CHECK(hipMalloc(&w.cstat, 16 * sizeof(int)));
+        SLO_CHECK(hipMemset(w.cstat, 0, 16 * sizeof(int)));
+    }
+    if (items > w.items) {
+        const size_t it = std::max(items, w.items + w.items / 2);
+        void* old[] = {w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg, w.wl};
+        for (void* q : old) if (q) hipFree(q);
+        w.items = it;
+        const size_t segcap = S + it / PC_T + 2;
+        const size_t chcap = it / PC_CH + segcap;
+        const size_t pccap = it / 2 / PC_PCH + segcap;
+        const size_t wcap = it / 2 + S + 2;
+        ++ctx->ws_gen;
+        SLO_CHECK(hipMalloc(&w.pairs, sizeof(u64) * it));
+        SLO_CHECK(hipMalloc(&w.seg[0], sizeof(PSeg) * segcap));
+        SLO_CHECK(hipMalloc(&w.seg[1], sizeof(PSeg) * segcap));
+        SLO_CHECK(hipMalloc(&w.res, sizeof(PRes) * segcap));
+        SLO_CHECK(hipMalloc(&w.cseg[0], sizeof(int) * chcap));
+        SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
+        SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
+        SLO_CHECK(hipMalloc(&w.pseg, sizeof(int) * pccap));
+        SLO_CHECK(hipMalloc(&w.wl, sizeof(int4) * wcap));
+    }
+    if (S * maxT > w.tiles) {
+        if (w.tcnt) hipFree(w.tcnt);
+        w.tiles = std::max(S * maxT, w.tiles + w.tiles / 2);
+        ++ctx->ws_gen;
+        SLO_CHECK(hipMalloc(&w.tcnt, sizeof(int) * w.tiles));
+    }
+    return 0;
+}
+
+// global levels for ranges of up to `stride` items: enough that what is left
+// fits the LDS finish (measured on the C3 / C5 maps: a 600 k-item surf map
+// leaves its last range over PC_T after 15 levels; 2 * log2(stride / PC_T) + 4)
+static int pcl_levels(size_t stride) {
+    int g = 0;
+    size_t x = PC_T;
+    while (x < stride) { x <<= 1; g += 2; }
+    return g ? std::min(40, g + 4) : 0;
+}
+
+int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
+                unsigned int* K, unsigned int* V) {
+    const int S = ctx->S;
+    const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
+    if (int r = pcl_ws(ctx, (size_t)S * in_stride, (size_t)maxT)) return r;
+    PclWs& w = ctx->pws;
+    const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
+    unsigned int* PA = (unsigned int*)w.pairs;
+    unsigned int* PB = PA + w.items;
+    SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
+               w.ctr);
+    SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], w.wl,
+               w.ctr, w.nfin);
+    SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
+               maxT, K, V, S);
+    const int G = pcl_levels(in_stride);
+    for (int lv = 0; lv < G; ++lv) {
+        const int cur = lv & 1;
+        SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(PC_G), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
+                   w.ctr, cur);
+        SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(PC_G / 4), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.pseg,
+                   w.ctr, cur);
+        SLO_LAUNCH(ctx, "pc_lrank", k_pc_lrank, dim3(PC_G), dim3(PC_CT), 0, K, V, w.seg[cur], w.cseg[cur], w.ccnt,
+                   w.res, PA, PB, w.ctr, cur);
+        SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(PC_G), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,
+                   w.ctr);
+        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(PC_G / 4), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
+                   w.cseg[cur ^ 1], w.wl, w.ctr, cur, (int)(lv == G - 1));
+    }
+    const int FG = std::max(64, std::min(4096, S * 8));
+    SLO_LAUNCH(ctx, "pc_finish", (k_pc_finish<256, PC_ST>), dim3(FG), dim3(256), 0, K, V, w.wl, w.ctr, w.cstat, w.pairs, 1,
+               PC_ST);
+    SLO_LAUNCH(ctx, "pc_finish", (k_pc_finish<PC_FT, PC_T>), dim3(FG), dim3(PC_FT), 0, K, V, w.wl, w.ctr, w.cstat, w.pairs,
+               PC_ST, 0x7fffffff);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+void pcl_free(slo_ctx* ctx) {
+    PclWs& w = ctx->pws;
+    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg,
+                  w.wl, w.tcnt};
+    for (void* p : ps) if (p) hipFree(p);
+    w = PclWs();
+}
+
+}  // namespace slo

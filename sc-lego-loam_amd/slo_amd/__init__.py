@@ -43,6 +43,7 @@ assert LOOP_DTYPE.itemsize == 128
 _DT["loop"] = LOOP_DTYPE
 _DT["imu"] = np.float64
 _DT["vg_in"] = np.int32
+_DT["vg_stats"] = np.int32
 
 
 class SloError(RuntimeError):
@@ -187,6 +188,11 @@ class Context:
 
     def batch_sc_make(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_sc_make(self.h, d_pts, d_cnt), "slo_batch_sc_make")
+
+    def batch_voxel_grid(self, d_in, in_stride, d_n, leaf, d_out, out_stride, d_nout, out_cap):
+        """pcl::VoxelGrid filter of every stream's device cloud (slo_batch_voxel_grid); asynchronous"""
+        self._ok(self.L.slo_batch_voxel_grid(self.h, d_in, int(in_stride), d_n, float(leaf), d_out, int(out_stride),
+                                             d_nout, int(out_cap)), "slo_batch_voxel_grid")
 
     def batch_loop_closure(self):
         """RS + SC loop verification (MO:841-1110) for every stream whose SC detect ran."""

@@ -49,7 +49,7 @@ class SloConfig(ctypes.Structure):
         ("icp_fitness_epsilon", ctypes.c_double),
         ("use_cloud_ring", ctypes.c_int32),
         ("surrounding_keyframe_search_radius", ctypes.c_float), ("leaf_surrounding_key_poses", ctypes.c_float),
-        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32),
+        ("map_keyframes", ctypes.c_int32), ("keyframe_ring", ctypes.c_int32), ("pose_graph", ctypes.c_int32), ("voxel_order", ctypes.c_int32),
     ]
 
 
@@ -115,7 +115,7 @@ EXPORTS = [
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
     "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_batch_imu", "slo_batch_scan_time",
     "slo_imu_handler", "slo_image_projection", "slo_feature_association",
-    "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_pack_records",
+    "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_batch_voxel_grid", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
     "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
@@ -196,6 +196,7 @@ def lib():
     L.slo_icp_align_batch.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_size_t, P, P]
     L.slo_sc_make_and_save.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
     L.slo_batch_sc_make.argtypes = [P, P, P]
+    L.slo_batch_voxel_grid.argtypes = [P, P, ctypes.c_size_t, P, ctypes.c_float, P, ctypes.c_size_t, P, ctypes.c_int]
     L.slo_pack_records.argtypes = [P, P]
     L.slo_pc2_layout_of.argtypes = [ctypes.POINTER(Pc2), ctypes.POINTER(Pc2Layout)]
     L.slo_pc2_to_xyzi.argtypes = [ctypes.POINTER(Pc2), P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]

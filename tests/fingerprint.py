@@ -36,7 +36,7 @@ def row(k, flags, get):
 
 
 def oracle_rows(O, pid, config, n_scans, stream=0):
-    st = O.OracleStream(O.preset(pid), stable_voxel=True)
+    st = O.OracleStream(O.preset(pid), stable_voxel=False)
     rows = []
     for k in range(n_scans):
         flags = st.step(O.gen_scan(pid, config, stream, k), 0.1 * k)

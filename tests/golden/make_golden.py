@@ -8,7 +8,8 @@ build container, where /root/reference exists):
    stream 0) is sampled every 3rd scan for 240 keyframes (> one 606 m lap,
    so loops close).  Each keyframe goes through the oracle's
    VoxelGrid(0.5) + makeAndSaveScancontextAndKeys + detectLoopClosureID
-   (stable in-voxel order, the order the GPU VoxelGrid produces).  For every
+   (PCL's std::sort in-voxel order, the reference's, which the GPU VoxelGrid
+   reproduces by default).  For every
    detect the tree snapshot and query are also fed to oracle/_ref/nanoflann_pin
    — the reference's KDTreeVectorOfVectorsAdaptor + nanoflann.hpp, compiled
    from /root/reference by `make -C oracle ref` — for K = 10 (C3) and K = 50
@@ -64,7 +65,7 @@ def nanoflann(queries, dim, K):
 def make_sc():
     cfg = O.preset(SC_PRESET)
     NR, EXC, PER = cfg.sc_num_ring, cfg.sc_num_exclude_recent, cfg.sc_tree_making_period
-    ses = O.SCSession(cfg, stable_voxel=True)
+    ses = O.SCSession(cfg, stable_voxel=False)
     keys, n_ds, det = [], [], []
     snaps, counter = None, 0
     queries = []
@@ -105,7 +106,7 @@ def make_sc():
 def make_front(name, pid, config, n_scans):
     rows = F.oracle_rows(O, pid, config, n_scans)
     with open(os.path.join(HERE, f"front_{name}.json"), "w") as f:
-        json.dump({"preset": pid, "config": config, "stream": 0, "stable_voxel": True, "scans": rows}, f, indent=1)
+        json.dump({"preset": pid, "config": config, "stream": 0, "stable_voxel": False, "scans": rows}, f, indent=1)
     print(f"front_{name}: {n_scans} scans")
 
 

@@ -37,7 +37,7 @@ def loop_config(pid=LOOP_PRESET):
 
 def run_oracle(n_scans=LOOP_SCANS):
     cfg = loop_config()
-    st = O.OracleStream(cfg, stable_voxel=True)
+    st = O.OracleStream(cfg, stable_voxel=False)
     scans, nkf, det, loops = [], [], [], []
     for k in range(n_scans):
         pts = O.gen_scan(LOOP_PRESET, LOOP_CONFIG, LOOP_STREAM, k * LOOP_STRIDE)

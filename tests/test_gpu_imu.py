@@ -61,7 +61,7 @@ def test_imu_single_scan_api():
     cfg = slo_amd.preset(pid)
     ctx = slo_amd.Context(cfg, 0, 1)
     ip, fa = slo_amd.ImageProjection(ctx), slo_amd.FeatureAssociation(ctx)
-    orc = O.OracleStream(O.preset(pid), stable_voxel=True)
+    orc = O.OracleStream(O.preset(pid), stable_voxel=False)
     try:
         for k in range(12):
             msgs = imu_synth.scan_messages(0, k, wrap=True)

@@ -169,7 +169,7 @@ def test_node_mirrors_match_oracle():
     ctx = slo_amd.Context(cfg, 0, 1)
     ip, fa, mo = slo_amd.ImageProjection(ctx), slo_amd.FeatureAssociation(ctx), slo_amd.MapOptimization(ctx)
     tf = slo_amd.TransformFusion(ctx)
-    orc = O.OracleStream(O.preset(pid), stable_voxel=True)
+    orc = O.OracleStream(O.preset(pid), stable_voxel=False)
     try:
         for k in range(10):
             pts = O.gen_scan(pid, cid, 0, k)

@@ -76,7 +76,7 @@ def test_pose_graph_pipeline():
     gcfg.pose_graph = 1
     ctx = slo_amd.Context(gcfg, 0, 1)
     pgraph = ProductGraph()
-    orc = PG.PipelineWithGraph(O.OracleStream(ocfg, stable_voxel=True), pgraph)
+    orc = PG.PipelineWithGraph(O.OracleStream(ocfg, stable_voxel=False), pgraph)
     cnt = torch.full((1,), gcfg.max_points, dtype=torch.int32, device="cuda")
     loops_gpu, corrected = 0, 0
     try:

@@ -45,7 +45,7 @@ def test_message_rings_follow_the_reference_indexing():
     cfg = _cfg(slo_amd, pid)
     ctx = slo_amd.Context(cfg, 0, 1)
     ip = slo_amd.ImageProjection(ctx)
-    orc = O.OracleStream(_cfg(O, pid), stable_voxel=True)
+    orc = O.OracleStream(_cfg(O, pid), stable_voxel=False)
     try:
         for k in range(3):
             pts = O.gen_scan(pid, cid, 0, k)
@@ -70,7 +70,7 @@ def test_batched_rings_through_the_pipeline():
     cfg = _cfg(slo_amd, pid)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, S)
-    orcs = [O.OracleStream(_cfg(O, pid), stable_voxel=True) for _ in range(S)]
+    orcs = [O.OracleStream(_cfg(O, pid), stable_voxel=False) for _ in range(S)]
     d_cnt = torch.full((S,), P, dtype=torch.int32, device="cuda")
     try:
         for k in range(K):

@@ -1,0 +1,129 @@
+"""The VoxelGrid in PCL's own order (cfg.voxel_order = SLO_VOXEL_PCL, the
+default; csrc/slo_vgpcl.hip + csrc/slo_pclsort.h) against the oracle's
+reference-faithful restatement — PCL's applyFilter with the host libstdc++
+std::sort (oracle_common.h voxel_grid, stable=False; FA:779-780,
+MO:1224-1262) — bit for bit, through slo_batch_voxel_grid.
+
+The clouds cover the sort's regimes: a 570 k-point map-like cloud (global
+introsort levels, then the LDS finish), a raw scan with NaNs (compaction),
+McIlroy's killer sequences (introsort's depth limit and heapsort, in the LDS
+finish and past the global levels), one voxel holding 20 000 points, tiny,
+single-point and empty clouds.  Points inside a voxel are jittered, so a
+wrong in-voxel order changes the centroid's float sums."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_py as O
+import slo_amd
+from parity_util import mismatch
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "no HIP device"
+    return torch
+
+
+@pytest.fixture(scope="module")
+def model(tmp_path_factory):
+    exe = tmp_path_factory.mktemp("pclsort") / "pcl_sort_model"
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", str(exe), os.path.join(HERE, "cpp", "pcl_sort_model.cpp")],
+                   check=True)
+    return exe
+
+
+def killer_keys(model, n, tmp):
+    out = tmp / f"killer{n}.u32"
+    r = subprocess.run([str(model), "--killer", str(n), str(out)], capture_output=True, text=True)
+    assert r.returncode == 0 and "heapsorts=1" in r.stdout and "OK" in r.stdout, r.stdout
+    return np.fromfile(out, np.uint32)
+
+
+def cloud_from_keys(keys, rng):
+    """points whose voxel index at leaf 1 is the key (x voxel = key, y = z = 0),
+    jittered inside the voxel, random intensities"""
+    n = len(keys)
+    p = np.empty((n, 4), np.float32)
+    p[:, 0] = keys.astype(np.float32) + rng.uniform(0.05, 0.95, n).astype(np.float32)
+    p[:, 1] = rng.uniform(0.05, 0.95, n).astype(np.float32)
+    p[:, 2] = rng.uniform(0.05, 0.95, n).astype(np.float32)
+    p[:, 3] = rng.uniform(0, 1, n).astype(np.float32)
+    return p
+
+
+def run_batch(clouds, leaf, voxel_order=0):
+    torch = _torch()
+    cfg = slo_amd.preset(0)
+    cfg.voxel_order = voxel_order
+    S = len(clouds)
+    stride = max(1, max(len(c) for c in clouds))
+    host = np.zeros((S, stride, 4), np.float32)
+    for s, c in enumerate(clouds):
+        host[s, :len(c)] = c
+    ctx = slo_amd.Context(cfg, 0, S)
+    try:
+        d_in = torch.from_numpy(host).cuda()
+        d_n = torch.tensor([len(c) for c in clouds], dtype=torch.int32, device="cuda")
+        d_out = torch.zeros((S, stride, 4), dtype=torch.float32, device="cuda")
+        d_nout = torch.zeros(S, dtype=torch.int32, device="cuda")
+        ctx.batch_voxel_grid(d_in.data_ptr(), stride, d_n.data_ptr(), leaf, d_out.data_ptr(), stride,
+                             d_nout.data_ptr(), stride)
+        ctx.synchronize()
+        nout = d_nout.cpu().numpy()
+        out = d_out.cpu().numpy()
+        stats = ctx.get(0, "vg_stats")
+        return [out[s, :nout[s]] for s in range(S)], stats
+    finally:
+        ctx.close()
+
+
+def test_pcl_order_map_and_raw_clouds():
+    rng = np.random.default_rng(11)
+    parts = []
+    for k in range(5):
+        p = O.gen_scan(6, 3, 0, 4 * k)
+        p = p[np.isfinite(p[:, :3]).all(1)].copy()
+        p[:, 0] += np.float32(2.0 * k)
+        parts.append(p)
+    big = np.concatenate(parts)                       # ~570 k points, 0.3 m voxels
+    raw = O.gen_scan(6, 3, 1, 7)                      # with NaNs (dropouts)
+    small = big[rng.choice(len(big), 3000, replace=False)]
+    clouds = [big, raw, small, big[:1], big[:0], raw[:20000]]
+    for leaf in (0.3, 0.5):
+        got, stats = run_batch(clouds, leaf)
+        for s, c in enumerate(clouds):
+            want = O.voxel_grid(c[np.isfinite(c[:, :3]).all(1)], leaf, stable=False)
+            assert len(got[s]) == len(want) and mismatch(got[s], want) == 0, (leaf, s)
+        assert stats[0] == 0   # every range fit the LDS finish after the global levels
+    # the test has teeth: the stable order gives different centroids on the big cloud
+    stable = O.voxel_grid(big, 0.3, stable=True)
+    assert mismatch(stable, O.voxel_grid(big, 0.3, stable=False)) != 0
+
+
+def test_pcl_order_killer_sequences_and_one_voxel(model, tmp_path):
+    rng = np.random.default_rng(12)
+    k5 = killer_keys(model, 5000, tmp_path)           # heapsort inside the LDS finish
+    k100 = killer_keys(model, 100000, tmp_path)       # depth limit past the global levels
+    one = np.zeros(20000, np.uint32)                  # every point in one voxel
+    few = rng.integers(0, 50, 3000).astype(np.uint32)
+    runs = np.concatenate([np.arange(4000, dtype=np.uint32) // 7, (np.arange(4000, dtype=np.uint32) // 5)[::-1]])
+    clouds = [cloud_from_keys(k, rng) for k in (k5, k100, one, few, runs)]
+    got, stats = run_batch(clouds, 1.0)
+    for s, c in enumerate(clouds):
+        want = O.voxel_grid(c, 1.0, stable=False)
+        assert len(got[s]) == len(want) and mismatch(got[s], want) == 0, s
+    print("finish ranges over the LDS capacity:", int(stats[0]))
+
+
+def test_stable_order_switch():
+    """cfg.voxel_order = SLO_VOXEL_STABLE keeps the radix sort: input order in a voxel"""
+    big = O.gen_scan(6, 3, 0, 3)
+    big = big[np.isfinite(big[:, :3]).all(1)]
+    got, _ = run_batch([big], 0.3, voxel_order=1)
+    assert mismatch(got[0], O.voxel_grid(big, 0.3, stable=True)) == 0

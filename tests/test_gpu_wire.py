@@ -27,7 +27,7 @@ def test_cloud_handler_takes_pointcloud2():
     pid, cid = 0, 1
     ctx = slo_amd.Context(slo_amd.preset(pid), 0, 1)
     ip = slo_amd.ImageProjection(ctx)
-    orc = O.OracleStream(O.preset(pid), stable_voxel=True)
+    orc = O.OracleStream(O.preset(pid), stable_voxel=False)
     try:
         for k in range(3):
             pts = O.gen_scan(pid, cid, 0, k)

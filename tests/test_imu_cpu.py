@@ -16,7 +16,7 @@ PID, CID = 0, 1   # VLP-16: small and fast
 
 
 def _run(n_scans, imu_fn=None, stream=0):
-    o = O.OracleStream(O.preset(PID), stable_voxel=True)
+    o = O.OracleStream(O.preset(PID), stable_voxel=False)
     out = []
     for k in range(n_scans):
         if imu_fn is not None:
@@ -49,7 +49,7 @@ def test_imu_ring_pointers_and_dropout():
     """imuPointerLast advances one slot per message modulo imuQueLength = 200;
     imuPointerLastIteration follows it after each scan (FA:616), also across a
     dropout where a scan receives no message"""
-    o = O.OracleStream(O.preset(PID), stable_voxel=True)
+    o = O.OracleStream(O.preset(PID), stable_voxel=False)
     total = 0
     for k in range(30):
         m = imu_synth.scan_messages(1, k, every=3)

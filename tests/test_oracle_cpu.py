@@ -103,7 +103,7 @@ def test_sc_session_reproduces_fixture_prefix(sc_gold):
     """First 60 keyframes: ring keys and detect results are bit-identical."""
     pid, cid, sid, step = (int(sc_gold[k]) for k in ("preset", "config", "stream", "step"))
     cfg = O.preset(pid)
-    ses = O.SCSession(cfg, stable_voxel=True)
+    ses = O.SCSession(cfg, stable_voxel=False)
     for j in range(60):
         n, key = ses.add(O.gen_scan(pid, cid, sid, j * step))
         assert n == sc_gold["n_ds"][j]
@@ -172,7 +172,7 @@ def test_radius_branch_keeps_the_keyframes_near_the_robot():
     keyframes that fell out of range leave it."""
     cfg = O.preset(0)
     cfg.loop_closure_enable = 0
-    o = O.OracleStream(cfg, stable_voxel=True)
+    o = O.OracleStream(cfg, stable_voxel=False)
     last = None
     dropped = False
     for k in range(120):

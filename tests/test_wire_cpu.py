@@ -112,7 +112,7 @@ def test_oracle_cloud_ring_rows():
     cfg = O.preset(0)
     cfg.use_cloud_ring = 1
     R, C = cfg.n_scan, cfg.horizon_scan
-    orc = O.OracleStream(cfg, stable_voxel=True)
+    orc = O.OracleStream(cfg, stable_voxel=False)
     n_fin = int(np.isfinite(SCAN[:, :3]).all(axis=1).sum())
     rings = np.full(len(SCAN), 3, np.uint16)
     rings[n_fin // 2:] = R + 1   # the second half of the finite points: out of range

@@ -43,7 +43,7 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
         cfg_edit(ocfg)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, n_streams)
-    ors = [O.OracleStream(ocfg, stable_voxel=True) for _ in range(n_streams)]
+    ors = [O.OracleStream(ocfg, stable_voxel=cfg.voxel_order == 1) for _ in range(n_streams)]
     report = []
     worst = {"odom": 0.0, "map": 0.0, "keypose": 0.0}
     counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0, "flag_mismatch": 0}
