@@ -73,6 +73,8 @@ def parse():
                     help="slo_config.keyframe_cloud_cap: points per keyframe surf/outlier cloud (0 = worst case); "
                          "an overflow sets the stream's error bit, reported as stream_errors")
     ap.add_argument("--config-id", type=int, default=3)
+    ap.add_argument("--voxel-order", type=int, default=0,
+                    help="0: PCL's std::sort order inside a voxel (the reference's; default), 1: stable (radix sort)")
     ap.add_argument("--history", type=int, default=0,
                     help="extra Scan Context history per stream (scans before scan 0); the pre-roll builds the real one")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
@@ -353,6 +355,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     cfg = slo_amd.preset(a.preset)
     cfg.keyframe_cloud_cap = a.keyframe_cap
+    cfg.voxel_order = a.voxel_order
     pid = slo_amd.PRESETS[a.preset]
     P = cfg.max_points
     S = a.streams

@@ -188,7 +188,9 @@ class PipelineWithGraph:
                 use_rs = rs["ran"] and rs["accepted"] and rs["id"] >= 0
                 use_sc = sc["ran"] and sc["accepted"] and sc["id"] >= 0
                 latest = len(self.g.est) - 1
-                if (use_rs or use_sc) and latest >= 0:
+                # aLoopIsClosed = true once performLoopClosure got past
+                # detection, accepted or not (MO:1107-1108)
+                if (rs["ran"] or sc["ran"]) and latest >= 0:
                     self.snap = self.g.key_poses().astype(np.float32)
                     kp = self.st.get("keyposes").reshape(-1, 6)
                     if use_rs:
@@ -200,7 +202,8 @@ class PipelineWithGraph:
                         x = np.asarray(sc["xyzrpy"], np.float32)
                         self.g.add_loop(latest, int(sc["id"]), np.array([x[3], x[4], x[5], x[0], x[1], x[2]], np.float32),
                                         np.zeros(6, np.float32))
-                    self.g.optimize()
+                    if use_rs or use_sc:
+                        self.g.optimize()
+                        self.loops += 1
                     self.pending = True
-                    self.loops += 1
         return f

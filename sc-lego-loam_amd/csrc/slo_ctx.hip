@@ -54,6 +54,8 @@ static void timing_flush(slo_ctx* ctx) {
         hipStreamSynchronize(ctx->stream);
         hipMemcpy(h.data(), ctx->d_stamp, sizeof(unsigned long long) * (2 * SLO_STAMP_CAP + 1), hipMemcpyDeviceToHost);
         const unsigned int n = std::min((unsigned int)h[2 * SLO_STAMP_CAP], (unsigned int)SLO_STAMP_CAP);
+        if (h[2 * SLO_STAMP_CAP] > SLO_STAMP_CAP)   // the ring wrapped since the last flush: stamps were lost
+            ctx->ktimes["!stamps_lost"].n += (long long)(h[2 * SLO_STAMP_CAP] - SLO_STAMP_CAP);
         for (unsigned int i = 0; i + 1 < n; i += 2) {
             const int id = (int)h[2 * i + 1];
             if (id < 0 || id >= (int)ctx->stamp_names.size() || (int)h[2 * i + 3] != id) continue;
@@ -528,27 +530,36 @@ static int step_graph(slo_ctx* ctx, const void* d_points, const int32_t* d_count
         }
         memcpy(&ctx->graph_v[key], &ctx->v, sizeof(DevView));
         const unsigned int ws0 = ctx->ws_gen;
+        // a capture that cannot become a graph: undo what the captured launches
+        // did to the host state (the ping-pong swap) and run this step eagerly,
+        // with graphs off from now on, so the stream stays in step
+        auto eager_instead = [&](const std::string& why) {
+            memcpy(&ctx->v, &ctx->graph_v[key], sizeof(DevView));
+            ctx->graphs = false;
+            ctx->err = why;
+            const int r2 = step_launches(ctx, map);
+            if (!r2 && map) ctx->mapped_now = true;
+            return r2;
+        };
         SLO_CHECK(hipStreamBeginCapture(ctx->stream, hipStreamCaptureModeThreadLocal));
         const int r = step_launches(ctx, map);   // swaps the ping-pong halves, as a replay does below
         hipGraph_t g = nullptr;
         const hipError_t e = hipStreamEndCapture(ctx->stream, &g);
         if (r || e != hipSuccess) {
             if (g) hipGraphDestroy(g);
-            if (!r) ctx->err = std::string("hipStreamEndCapture: ") + hipGetErrorString(e);
-            return r ? r : SLO_E_HIP;
+            if (r) return r;   // a launch failed: a real error
+            return eager_instead(std::string("hipStreamEndCapture: ") + hipGetErrorString(e));
         }
         if (ctx->ws_gen != ws0) {   // a workspace moved while capturing (not expected): no graph
             hipGraphDestroy(g);
-            ctx->err = "a workspace was reallocated during graph capture";
-            return SLO_E_STATE;
+            return eager_instead("a workspace was reallocated during graph capture");
         }
         ctx->graph_ws[key] = ws0;
         const hipError_t ei = hipGraphInstantiate(&ctx->graph_exec[key], g, nullptr, nullptr, 0);
         hipGraphDestroy(g);
         if (ei != hipSuccess) {
             ctx->graph_exec[key] = nullptr;
-            ctx->err = std::string("hipGraphInstantiate: ") + hipGetErrorString(ei);
-            return SLO_E_HIP;
+            return eager_instead(std::string("hipGraphInstantiate: ") + hipGetErrorString(ei));
         }
     } else {
         fa_swap_last(ctx);   // what the captured fa_odometry_run did on the host

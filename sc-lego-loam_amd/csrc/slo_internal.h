@@ -103,6 +103,7 @@ struct StreamState {
     float kf_pre[6];
     // scan context
     int32_t sc_count, sc_tree_n, sc_counter;
+    int32_t sc_wrote;   // the last makeAndSave stored its descriptor (0: the history was full)
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];
     float det_yaw;
     double det_min_dist;

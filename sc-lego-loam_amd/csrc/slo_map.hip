@@ -778,7 +778,7 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
     __syncthreads();
     const int kfid = hid;
     if (kfid >= v.KFMAX) {
-        if (threadIdx.x == 0) st.err |= SLO_ERR_SC_HISTORY;
+        if (threadIdx.x == 0) { st.err |= SLO_ERR_SC_HISTORY; st.sc_wrote = 0; }
         return;
     }
     for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
@@ -811,7 +811,7 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
         const int c = threadIdx.x - 64;
         v.sc_sect[((size_t)s * v.KFMAX + kfid) * NS + c] = eigen_sum(desc + c, NR, NS) / (double)NR;
     }
-    if (threadIdx.x == 0) st.sc_count = kfid + 1;
+    if (threadIdx.x == 0) { st.sc_count = kfid + 1; st.sc_wrote = 1; }
 }
 
 int map_run(slo_ctx* ctx) {

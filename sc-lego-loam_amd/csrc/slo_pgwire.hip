@@ -146,7 +146,10 @@ int pg_after_loops(slo_ctx* ctx) {
         const slo_loop_result& rs = res[2 * s];
         const slo_loop_result& sc = res[2 * s + 1];
         const bool use_rs = rs.ran && rs.accepted && rs.id >= 0, use_sc = sc.ran && sc.accepted && sc.id >= 0;
-        if (!use_rs && !use_sc) continue;
+        // performLoopClosure got past detectLoopClosure: aLoopIsClosed is set
+        // whether or not an ICP was accepted (MO:1107-1108), so correctPoses
+        // runs at the next mapping step either way
+        if (!rs.ran && !sc.ran) continue;
         slo_pg* g = ctx->pg[s];
         const int latest = st.n_keyframes - 1;   // latestFrameIDLoopCloure (MO:849)
         if (latest < 0 || latest >= slo_pg_size(g)) continue;
@@ -170,7 +173,10 @@ int pg_after_loops(slo_ctx* ctx) {
             const float to[6] = {0, 0, 0, 0, 0, 0};
             if (slo_pg_add_loop(g, latest, sc.id, from, to) != SLO_OK) { ctx->err = slo_pg_last_error(g); return SLO_E_STATE; }
         }
-        if (slo_pg_optimize(g, 0, nullptr, nullptr) < 0) { ctx->err = slo_pg_last_error(g); return SLO_E_STATE; }
+        if ((use_rs || use_sc) && slo_pg_optimize(g, 0, nullptr, nullptr) < 0) {   // isam->update (MO:1045, 1090)
+            ctx->err = slo_pg_last_error(g);
+            return SLO_E_STATE;
+        }
         ctx->pg_pending[s] = 1;   // aLoopIsClosed = true (MO:1107)
     }
     return 0;

@@ -123,7 +123,9 @@ __global__ void __launch_bounds__(256) k_pack_records(DevView v, float* out) {
     float* o = out + (size_t)s * SLO_RECORD_FLOATS;
     const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
     const int kf = st.sc_count - 1;
-    const bool saved = st.kf_saved && kf >= 0;
+    // a keyframe whose descriptor did not fit the history sends none (the
+    // newest stored one is an older keyframe's)
+    const bool saved = st.kf_saved && st.sc_wrote && kf >= 0;
     const double* d = saved ? v.sc_desc + ((size_t)s * v.KFMAX + kf) * NR * NS : nullptr;
     for (int i = threadIdx.x; i < SLO_SC_MAX_CELLS; i += blockDim.x)
         o[SLO_REC_DESC + i] = (saved && i < NR * NS) ? (float)d[i] : 0.0f;

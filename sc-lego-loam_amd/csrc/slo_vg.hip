@@ -25,8 +25,12 @@ namespace slo {
 
 // stream offsets of the concatenated input (block scan), bounds init, and the
 // meta words [total, max cell count, long-voxel count]
+// A count above the stream's input stride (a caller's io->npts: nothing else
+// bounds it) is clamped to the stride — the workspace is sized from the
+// strides — and flagged (errflag bit 4, slo_get "vg_stats").
 __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int S, int32_t* off,
-                                                    unsigned int* bounds, int32_t* meta, int32_t* osw, int tile) {
+                                                    unsigned int* bounds, int32_t* meta, int32_t* osw, int tile,
+                                                    int in_stride, int32_t* errflag) {
     const int32_t* n = src.cnt();
     __shared__ int wsum[16];
     __shared__ int carry;
@@ -35,7 +39,9 @@ __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int
     __syncthreads();
     for (int b0 = 0; b0 < S; b0 += 1024) {
         const int s = b0 + tid;
-        const int x = s < S ? n[(size_t)s * n_stride] : 0;
+        const int x0 = s < S ? n[(size_t)s * n_stride] : 0;
+        const int x = max(0, min(x0, in_stride));
+        if (x != x0) atomicOr(errflag, 4);
         int incl = x;   // inclusive wave scan
         for (int o = 1; o < 64; o <<= 1) {
             const int y = __shfl_up(incl, o, 64);
@@ -940,7 +946,7 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     const dim3 grid = vg_tile_grid(GX, S);
     const VgSrc src{in, d_n, ctx->v.io};
     SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta,
-               ctx->vg_onesweep ? w.osw : nullptr, VG_TILE);
+               ctx->vg_onesweep ? w.osw : nullptr, VG_TILE, (int)std::min<size_t>(in_stride, 0x7fffffff), w.errflag);
     SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, in_stride, w.off, w.bounds);
     SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
     hipEvent_t ev = nullptr;

@@ -89,15 +89,22 @@ def test_voxel_grid_int32_overflow_returns_the_input():
         ctx.close()
 
 
-def test_pipeline_with_single_pass_sort(monkeypatch):
+def _stable(cfg):
+    cfg.voxel_order = 1   # SLO_VOXEL_STABLE: the radix sort, input order inside a voxel
+
+
+@pytest.mark.parametrize("onesweep", ["0", "1"])
+def test_pipeline_with_stable_voxel_order(monkeypatch, onesweep):
     """C3 (hdl64_1800) pipeline, two mapping rounds per stream, every
-    VoxelGrid sorted by the single-pass scatters: bit-exact vs the oracle."""
+    VoxelGrid in the stable order (cfg.voxel_order = 1) by the LSD radix
+    passes or by the single-pass scatters: bit-exact vs the oracle in its
+    stable mode."""
     import os
     import sys
-    monkeypatch.setenv("SLO_VG_ONESWEEP", "1")
+    monkeypatch.setenv("SLO_VG_ONESWEEP", onesweep)
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import parity_report
-    rep, worst, counts = parity_report.run(6, 3, 2, 14, verbose=False)
+    rep, worst, counts = parity_report.run(6, 3, 2, 14, verbose=False, cfg_edit=_stable)
     bad = [r for r in rep if any(isinstance(v, int) and v != 0 and k not in
                                  ("scan", "stream", "flags_cpu", "flags_gpu") for k, v in r.items())]
     assert not bad and not counts["flag_mismatch"] and not counts["detect_mismatch"], (bad[:2], counts)
