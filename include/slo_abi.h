@@ -158,6 +158,31 @@ int slo_sc_make_and_save(slo_ctx* ctx, const void* pts, size_t n, size_t stride_
  * (used to seed the Scan Context history, e.g. from a previous session) */
 int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_counts);
 
+/* The public SCManager helpers (Scancontext.h:63-69), computed on the device
+ * in the reference's evaluation order (Eigen 3.3 packet sums).  A descriptor
+ * is NR x NS doubles, row-major (ring r, sector c at [r * NS + c]; Eigen's
+ * MatrixXd is column-major, so bind it through a RowMajor Map); a ring key is
+ * NR doubles, a sector key NS doubles (cfg.sc_num_ring / sc_num_sector).
+ * Host pointers; synchronous. */
+/* makeScancontext (SCc:151-195): n points of stride_bytes with x, y, z floats at off_xyz */
+int slo_sc_make_scancontext(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                            double* desc);
+/* makeRingkeyFromScancontext (SCc:198-211): the row means */
+int slo_sc_ring_key(slo_ctx* ctx, const double* desc, double* ring_key);
+/* makeSectorkeyFromScancontext (SCc:214-227): the column means */
+int slo_sc_sector_key(slo_ctx* ctx, const double* desc, double* sector_key);
+/* fastAlignUsingVkey (SCc:93-113): the shift of least |vkey1 - circshift(vkey2, shift)| */
+int slo_sc_fast_align(slo_ctx* ctx, const double* vkey1, const double* vkey2, int32_t* shift);
+/* distDirectSC (SCc:69-90): 1 - mean cosine of the columns non-zero in both */
+int slo_sc_dist_direct(slo_ctx* ctx, const double* sc1, const double* sc2, double* dist);
+/* distanceBtnScanContext (SCc:116-148): (min distance over the aligned shift
+ * window, its shift) */
+int slo_sc_distance(slo_ctx* ctx, const double* sc1, const double* sc2, double* dist, int32_t* shift);
+/* batched distanceBtnScanContext on device arrays: n pairs (d_sc1[i], d_sc2[i]),
+ * each NR x NS; asynchronous on slo_stream(ctx) */
+int slo_batch_sc_distance(slo_ctx* ctx, const double* d_sc1, const double* d_sc2, int n, double* d_dist,
+                          int32_t* d_shift);
+
 /* pcl::VoxelGrid<PointXYZI> setLeafSize(leaf) + filter (PCL 1.8 applyFilter,
  * the reference's downsize filters: featureAssociation.cpp:779-780,
  * mapOptmization.cpp:1224-1262) on every stream's device cloud at once:

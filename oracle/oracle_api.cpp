@@ -280,6 +280,17 @@ double oracle_sc_distance(const slo_config* cfg, const double* sc1, const double
     *shift = r.second;
     return r.first;
 }
+double oracle_sc_dist_direct(const slo_config* cfg, const double* sc1, const double* sc2) {
+    SCManager m(*cfg);
+    std::vector<double> a(sc1, sc1 + cfg->sc_num_ring * cfg->sc_num_sector);
+    std::vector<double> b(sc2, sc2 + cfg->sc_num_ring * cfg->sc_num_sector);
+    return m.distDirectSC(a, b, 0);
+}
+int oracle_sc_fast_align(const slo_config* cfg, const double* vk1, const double* vk2) {
+    SCManager m(*cfg);
+    std::vector<double> a(vk1, vk1 + cfg->sc_num_sector), b(vk2, vk2 + cfg->sc_num_sector);
+    return m.fastAlignUsingVkey(a, b);
+}
 void oracle_sc_make(const slo_config* cfg, const float* pts, int n, double* desc, double* ring, double* sector) {
     SCManager m(*cfg);
     Cloud c(n);

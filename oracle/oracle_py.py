@@ -76,6 +76,9 @@ def lib():
         L.oracle_sc_distance.restype = ctypes.c_double
         L.oracle_sc_distance.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_int)]
+        L.oracle_sc_dist_direct.restype = ctypes.c_double
+        L.oracle_sc_dist_direct.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_sc_fast_align.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_sc_make.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_voxel_grid.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_float, ctypes.c_int,
@@ -146,6 +149,35 @@ _DTYPES["imu"] = np.float64
 _CLOUDS = {"full_cloud", "seg_pts", "outlier", "fa_seg_pts", "sharp", "flat", "less_sharp", "less_flat",
            "corner_last", "surf_last", "raw_ds", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds",
            "map_corner_raw", "map_surf_raw"}
+
+
+def sc_make(cfg, pts):
+    """makeScancontext + ring / sector keys of an already downsampled cloud (SCc:151-227)"""
+    pts = np.ascontiguousarray(pts, np.float32)
+    NR, NS = cfg.sc_num_ring, cfg.sc_num_sector
+    d, r, s = np.zeros(NR * NS), np.zeros(NR), np.zeros(NS)
+    lib().oracle_sc_make(ctypes.byref(cfg), pts.ctypes.data, len(pts), d.ctypes.data, r.ctypes.data, s.ctypes.data)
+    return d.reshape(NR, NS), r, s
+
+
+def sc_distance(cfg, sc1, sc2):
+    """distanceBtnScanContext (SCc:116-148) -> (dist, shift)"""
+    a, b = (np.ascontiguousarray(x, np.float64) for x in (sc1, sc2))
+    sh = ctypes.c_int(0)
+    d = lib().oracle_sc_distance(ctypes.byref(cfg), a.ctypes.data, b.ctypes.data, ctypes.byref(sh))
+    return d, sh.value
+
+
+def sc_dist_direct(cfg, sc1, sc2):
+    """distDirectSC (SCc:69-90)"""
+    a, b = (np.ascontiguousarray(x, np.float64) for x in (sc1, sc2))
+    return lib().oracle_sc_dist_direct(ctypes.byref(cfg), a.ctypes.data, b.ctypes.data)
+
+
+def sc_fast_align(cfg, vk1, vk2):
+    """fastAlignUsingVkey (SCc:93-113)"""
+    a, b = (np.ascontiguousarray(x, np.float64) for x in (vk1, vk2))
+    return lib().oracle_sc_fast_align(ctypes.byref(cfg), a.ctypes.data, b.ctypes.data)
 
 
 def voxel_grid(pts, leaf, stable=False):

@@ -692,6 +692,11 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         SLO_CHECK(hipMemcpy(&a[1], ctx->mws.errflag, 4, hipMemcpyDeviceToHost));
         tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
     }
+    else if (name == "pcl_stats") {   // SLO_PCL_STATS builds: wave tier (ranges, items, levels), 2 block tiers the same
+        unsigned long long a[9] = {0};
+        if (ctx->pws.pstat) SLO_CHECK(hipMemcpy(a, ctx->pws.pstat, sizeof(a), hipMemcpyDeviceToHost));
+        tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 9; esz = 8;
+    }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "imu") {   // FA's IMU scalars (slo::ImuState), as float64
         slo::ImuState m;
@@ -983,6 +988,85 @@ int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_count
                         &v.st->n_raw_ds, SS, v.P);
     if (r) return r;
     return slo::sc_make_run(ctx, v.cur_raw_ds, v.P, &v.st->n_raw_ds, SS, ctx->S);
+}
+
+// the SCManager helpers on host data: stage the inputs, one launch, read back
+static int sc_api_host(slo_ctx* ctx, int op, const void* a, size_t na, const void* b, size_t nb, const int32_t* n,
+                       size_t stride, void* o1, size_t no1, void* o2, size_t no2, void* o3, size_t no3) {
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    const size_t al = 256, sz[6] = {na, nb, (size_t)(n ? 4 : 0), no1, no2, no3};
+    size_t off[7] = {0};
+    for (int i = 0; i < 6; ++i) off[i + 1] = off[i] + (sz[i] + al - 1) / al * al;
+    char* d = nullptr;
+    SLO_CHECK(hipMalloc(&d, std::max<size_t>(off[6], al)));
+    auto dp = [&](int i) -> void* { return sz[i] ? d + off[i] : nullptr; };
+    hipError_t e = hipSuccess;
+    if (na) e = hipMemcpyAsync(dp(0), a, na, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && nb) e = hipMemcpyAsync(dp(1), b, nb, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess && n) e = hipMemcpyAsync(dp(2), n, 4, hipMemcpyHostToDevice, ctx->stream);
+    int r = e == hipSuccess ? slo::sc_api_run(ctx, op, 1, dp(0), dp(1), stride, (const int32_t*)dp(2), dp(3), dp(4),
+                                               dp(5))
+                            : SLO_E_HIP;
+    void* outs[3] = {o1, o2, o3};
+    for (int i = 0; i < 3 && !r; ++i)
+        if (sz[3 + i] && outs[i] && hipMemcpyAsync(outs[i], dp(3 + i), sz[3 + i], hipMemcpyDeviceToHost, ctx->stream))
+            r = SLO_E_HIP;
+    if (hipStreamSynchronize(ctx->stream) != hipSuccess && !r) r = SLO_E_HIP;
+    hipFree(d);
+    if (r == SLO_E_HIP) ctx->err = "SCManager helper: HIP copy / launch failed";
+    return r;
+}
+
+int slo_sc_make_scancontext(slo_ctx* ctx, const void* pts, size_t n, size_t stride_bytes, size_t off_xyz,
+                            double* desc) {
+    if (!ctx || (!pts && n) || !desc || (n && stride_bytes < off_xyz + 12)) return SLO_E_ARG;
+    const int NR = ctx->cfg.sc_num_ring, NS = ctx->cfg.sc_num_sector;
+    std::vector<float> p4(4 * std::max<size_t>(n, 1), 0.0f);
+    for (size_t i = 0; i < n; ++i) memcpy(&p4[4 * i], (const char*)pts + i * stride_bytes + off_xyz, 12);
+    const int32_t cnt = (int32_t)n;
+    return sc_api_host(ctx, 0, p4.data(), p4.size() * 4, nullptr, 0, &cnt, std::max<size_t>(n, 1), desc,
+                       sizeof(double) * NR * NS, nullptr, sizeof(double) * NR, nullptr, sizeof(double) * NS);
+}
+
+int slo_sc_ring_key(slo_ctx* ctx, const double* desc, double* ring_key) {
+    if (!ctx || !desc || !ring_key) return SLO_E_ARG;
+    const int NR = ctx->cfg.sc_num_ring, NS = ctx->cfg.sc_num_sector;
+    return sc_api_host(ctx, 1, desc, sizeof(double) * NR * NS, nullptr, 0, nullptr, 0, ring_key, sizeof(double) * NR,
+                       nullptr, sizeof(double) * NS, nullptr, 0);
+}
+
+int slo_sc_sector_key(slo_ctx* ctx, const double* desc, double* sector_key) {
+    if (!ctx || !desc || !sector_key) return SLO_E_ARG;
+    const int NR = ctx->cfg.sc_num_ring, NS = ctx->cfg.sc_num_sector;
+    return sc_api_host(ctx, 1, desc, sizeof(double) * NR * NS, nullptr, 0, nullptr, 0, nullptr, sizeof(double) * NR,
+                       sector_key, sizeof(double) * NS, nullptr, 0);
+}
+
+int slo_sc_fast_align(slo_ctx* ctx, const double* vkey1, const double* vkey2, int32_t* shift) {
+    if (!ctx || !vkey1 || !vkey2 || !shift) return SLO_E_ARG;
+    const int NS = ctx->cfg.sc_num_sector;
+    return sc_api_host(ctx, 2, vkey1, sizeof(double) * NS, vkey2, sizeof(double) * NS, nullptr, 0, shift, 4, nullptr,
+                       0, nullptr, 0);
+}
+
+int slo_sc_dist_direct(slo_ctx* ctx, const double* sc1, const double* sc2, double* dist) {
+    if (!ctx || !sc1 || !sc2 || !dist) return SLO_E_ARG;
+    const size_t nb = sizeof(double) * ctx->cfg.sc_num_ring * ctx->cfg.sc_num_sector;
+    return sc_api_host(ctx, 3, sc1, nb, sc2, nb, nullptr, 0, dist, 8, nullptr, 0, nullptr, 0);
+}
+
+int slo_sc_distance(slo_ctx* ctx, const double* sc1, const double* sc2, double* dist, int32_t* shift) {
+    if (!ctx || !sc1 || !sc2 || !dist || !shift) return SLO_E_ARG;
+    const size_t nb = sizeof(double) * ctx->cfg.sc_num_ring * ctx->cfg.sc_num_sector;
+    return sc_api_host(ctx, 4, sc1, nb, sc2, nb, nullptr, 0, dist, 8, shift, 4, nullptr, 0);
+}
+
+int slo_batch_sc_distance(slo_ctx* ctx, const double* d_sc1, const double* d_sc2, int n, double* d_dist,
+                          int32_t* d_shift) {
+    if (!ctx || !d_sc1 || !d_sc2 || !d_dist || !d_shift || n < 0) return SLO_E_ARG;
+    if (n == 0) return SLO_OK;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    return slo::sc_api_run(ctx, 4, n, d_sc1, d_sc2, 0, nullptr, d_dist, d_shift, nullptr);
 }
 
 int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,

@@ -792,11 +792,16 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
         return (((unsigned long long)idx << 32) | (unsigned int)i) | (0ull - (unsigned long long)(i >= n));
     };
     if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // std::sort's order, as PCL (slo_pclsort.h)
-        __shared__ slo_pcl::BlockSmem<256, 2048, 64> psm;
+        __shared__ slo_pcl::BlockSmem<256, 2048> psm;
+        __shared__ slo_pcl::WaveSmem pws[4];
         for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = key_of(i);
         __syncthreads();
         if (n <= 2048) {
-            slo_pcl::pcl_block_sort<256, 2048, 64>(keys, n, 2 * slo_pcl::lg2(n), psm);
+            slo_pcl::pcl_block_sort<256, 2048>(keys, n, 2 * slo_pcl::lg2(n), psm);
+            const int w = threadIdx.x >> 6;
+            for (int q = w; q < psm.nw; q += 4)
+                slo_pcl::pcl_wave_sort(keys, psm.wf[q], psm.wl[q] - psm.wf[q], psm.wd[q], pws[w]);
+            __syncthreads();
         } else {   // rings over 2048 points: one lane (no preset has them)
             if (threadIdx.x == 0) slo_sort::introsort_range(keys, n, 2 * slo_pcl::lg2(n), slo_pcl::Less());
             __syncthreads();

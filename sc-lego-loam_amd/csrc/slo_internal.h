@@ -467,6 +467,7 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
     size_t items = 0, tiles = 0;
     int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries, pair chunks)
     int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
+    unsigned long long* pstat = nullptr;   // [16] SLO_PCL_STATS builds: finish ranges / items / levels per tier
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
     PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level
@@ -474,7 +475,8 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
     int* cseg[2] = {nullptr, nullptr};     // chunk -> range
     int2* ccnt = nullptr;         // per chunk stopper counts -> prefixes
     int* pseg = nullptr;          // pair chunk -> range
-    int4* wl = nullptr;           // finish entries (f, l, depth)
+    int2* wl = nullptr;           // finish entries (f, size | depth << 24): four lists by size
+    size_t wcap0 = 0, wcapk = 0;  // capacity of list 0 and of lists 1..3
     int* tcnt = nullptr;          // [S][maxT] finite points per tile -> prefixes
 };
 struct HashGrid {
@@ -580,6 +582,11 @@ int map_run(slo_ctx* ctx);
 void graphs_drop(slo_ctx* ctx);
 int imu_init(slo_ctx* ctx);
 int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams);
+// the SCManager helpers on device data (slo_map.hip): op 0 make (pts, stride, n -> desc, ring, sector),
+// 1 keys (desc -> ring, sector), 2 align (vkey1, vkey2 -> shift), 3 direct (sc1, sc2 -> dist),
+// 4 distance (sc1, sc2 -> dist, shift); nitems descriptors / pairs, contiguous
+int sc_api_run(slo_ctx* ctx, int op, int nitems, const void* in1, const void* in2, size_t stride, const int32_t* n,
+               void* out1, void* out2, void* out3);
 int sc_detect_run(slo_ctx* ctx);
 int sc_detect_run_one(slo_ctx* ctx);
 int pack_records_run(slo_ctx* ctx, float* d_out);

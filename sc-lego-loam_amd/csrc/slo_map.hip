@@ -678,6 +678,7 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
 
 // ---------------------------------------------------------------- keyframe + Scan Context make
 __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
+__device__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc);
 
 
 __device__ inline float sc_xy2theta(float x, float y, int atan_float) {
@@ -759,10 +760,162 @@ __global__ void __launch_bounds__(256) k_sc_make(DevView v, const float4* pts, s
     sc_make_block(v, s, pts + (size_t)s * stride, n[(size_t)s * n_stride]);
 }
 
+// ---- the public SCManager helpers (Scancontext.h:63-69), batched: item b of
+// each launch is one descriptor / pair (slo_sc_* in include/slo_abi.h).
+// Descriptors are row-major NR x NS doubles, sector keys NS, ring keys NR.
+__device__ inline void sc_keys_block(const slo_config& cfg, const double* desc, double* ring, double* sect) {
+    const int NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
+    for (int r = threadIdx.x; r < NR; r += blockDim.x) ring[r] = eigen_sum(desc + r * NS, NS, 1) / (double)NS;   // SCc:198-211
+    for (int c = threadIdx.x; c < NS; c += blockDim.x) sect[c] = eigen_sum(desc + c, NR, NS) / (double)NR;       // SCc:214-227
+}
+
+__global__ void __launch_bounds__(256) k_sc_api_make(slo_config cfg, const float4* pts, size_t stride, const int32_t* n,
+                                                     double* desc, double* ring, double* sect) {
+    __shared__ unsigned int cell[20 * 60];
+    __shared__ double d[20 * 60];
+    const int b = blockIdx.x, NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
+    sc_desc_block(cfg, pts + (size_t)b * stride, n[b], cell, d);
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) desc[(size_t)b * NR * NS + i] = d[i];
+    sc_keys_block(cfg, d, ring + (size_t)b * NR, sect + (size_t)b * NS);
+}
+
+__global__ void __launch_bounds__(64) k_sc_api_keys(slo_config cfg, const double* desc, double* ring, double* sect) {
+    const int b = blockIdx.x, NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
+    sc_keys_block(cfg, desc + (size_t)b * NR * NS, ring + (size_t)b * NR, sect + (size_t)b * NS);
+}
+
+// fastAlignUsingVkey (SCc:93-113): the first shift of least |vkey1 - circshift(vkey2, shift)|
+__global__ void __launch_bounds__(64) k_sc_api_align(slo_config cfg, const double* vk1, const double* vk2,
+                                                     int32_t* shift) {
+    __shared__ double nrm[SC_NS];
+    const int b = blockIdx.x, NS = cfg.sc_num_sector, tid = threadIdx.x;
+    const double* a = vk1 + (size_t)b * NS;
+    const double* c = vk2 + (size_t)b * NS;
+    if (tid < NS) {
+        ESum e;
+        for (int j = 0; j < NS; ++j) {
+            const double d = a[j] - c[((j - tid) % NS + NS) % NS];
+            e.add(d * d);
+        }
+        nrm[tid] = sqrt(e.get());
+    }
+    __syncthreads();
+    if (tid == 0) {
+        int am = 0;
+        double mn = 10000000;
+        for (int sh = 0; sh < NS; ++sh)
+            if (nrm[sh] < mn) { am = sh; mn = nrm[sh]; }
+        shift[b] = am;
+    }
+}
+
+// distDirectSC (SCc:69-90): 1 - the mean column cosine over the columns non-zero in both
+__global__ void __launch_bounds__(64) k_sc_api_direct(slo_config cfg, const double* sc1, const double* sc2,
+                                                      double* dist) {
+    __shared__ double sim[SC_NS];
+    __shared__ int ok[SC_NS];
+    const int b = blockIdx.x, NR = cfg.sc_num_ring, NS = cfg.sc_num_sector, j = threadIdx.x;
+    const double* a = sc1 + (size_t)b * NR * NS;
+    const double* c = sc2 + (size_t)b * NR * NS;
+    if (j < NS) {
+        ESum n1, n2, dt;
+        for (int r = 0; r < NR; ++r) {
+            const double x = a[r * NS + j], y = c[r * NS + j];
+            n1.add(x * x); n2.add(y * y); dt.add(x * y);
+        }
+        const double nn1 = sqrt(n1.get()), nn2 = sqrt(n2.get());
+        ok[j] = !((nn1 == 0) | (nn2 == 0));
+        sim[j] = ok[j] ? dt.get() / (nn1 * nn2) : 0.0;
+    }
+    __syncthreads();
+    if (j == 0) {
+        double sum = 0;
+        int ne = 0;
+        for (int k = 0; k < NS; ++k)
+            if (ok[k]) { sum = sum + sim[k]; ne = ne + 1; }
+        dist[b] = 1.0 - sum / ne;
+    }
+}
+
+// distanceBtnScanContext (SCc:116-148): sector keys, then the shared pair distance
+__global__ void __launch_bounds__(256) k_sc_api_dist(slo_config cfg, const double* sc1, const double* sc2,
+                                                     double* dist, int32_t* shift) {
+    __shared__ double vk[2][SC_NS];
+    __shared__ double rk[2][20];
+    __shared__ ScPairLds L;
+    const int b = blockIdx.x, NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
+    const double* a = sc1 + (size_t)b * NR * NS;
+    const double* c = sc2 + (size_t)b * NR * NS;
+    sc_keys_block(cfg, a, rk[0], vk[0]);
+    sc_keys_block(cfg, c, rk[1], vk[1]);
+    __syncthreads();
+    double d;
+    int al;
+    sc_pair_distance(a, vk[0], c, vk[1], NR, NS, cfg.sc_search_ratio, L, &d, &al);
+    if (threadIdx.x == 0) { dist[b] = d; shift[b] = al; }
+}
+
+int sc_api_run(slo_ctx* ctx, int op, int nitems, const void* in1, const void* in2, size_t stride, const int32_t* n,
+               void* out1, void* out2, void* out3) {
+    const slo_config& cfg = ctx->cfg;
+    if (cfg.sc_num_ring > 20 || cfg.sc_num_sector > SC_NS || nitems <= 0) return SLO_E_ARG;
+    switch (op) {
+    case 0:
+        SLO_LAUNCH(ctx, "sc_api_make", k_sc_api_make, dim3(nitems), dim3(256), 0, cfg, (const float4*)in1, stride, n,
+                   (double*)out1, (double*)out2, (double*)out3);
+        break;
+    case 1:
+        SLO_LAUNCH(ctx, "sc_api_keys", k_sc_api_keys, dim3(nitems), dim3(64), 0, cfg, (const double*)in1,
+                   (double*)out1, (double*)out2);
+        break;
+    case 2:
+        SLO_LAUNCH(ctx, "sc_api_align", k_sc_api_align, dim3(nitems), dim3(64), 0, cfg, (const double*)in1,
+                   (const double*)in2, (int32_t*)out1);
+        break;
+    case 3:
+        SLO_LAUNCH(ctx, "sc_api_direct", k_sc_api_direct, dim3(nitems), dim3(64), 0, cfg, (const double*)in1,
+                   (const double*)in2, (double*)out1);
+        break;
+    default:
+        SLO_LAUNCH(ctx, "sc_api_dist", k_sc_api_dist, dim3(nitems), dim3(256), 0, cfg, (const double*)in1,
+                   (const double*)in2, (double*)out1, (int32_t*)out2);
+    }
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
 int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams) {
     SLO_LAUNCH(ctx, "sc_make", k_sc_make, dim3(n_streams), dim3(256), 0, ctx->v, pts, stride, n, n_stride);
     SLO_CHECK(hipGetLastError());
     return 0;
+}
+
+// SCManager::makeScancontext (Scancontext.cpp:151-195) of nraw points into
+// desc[NR * NS] (LDS, row-major: ring, sector), one workgroup; cell is LDS
+// scratch of the same size
+__device__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc) {
+    const int NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
+    __syncthreads();
+    for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
+        float4 p0 = raw[i];
+        float px = p0.x, py = p0.y;
+        float pz = (float)(p0.z + cfg.sc_lidar_height);
+        float azim_range = sqrtf(px * px + py * py);
+        float azim_angle = sc_xy2theta(px, py, cfg.sc_atan_float);
+        if (azim_range > cfg.sc_max_radius) continue;
+        int ring_idx = max(min(NR, (int)ceil((azim_range / cfg.sc_max_radius) * NR)), 1);
+        double sc = ceil((azim_angle / 360.0) * NS);
+        int sraw = isnan(sc) ? INT_MIN : (int)sc;
+        int sctor_idx = max(min(NS, sraw), 1);
+        atomicMax(&cell[(ring_idx - 1) * NS + (sctor_idx - 1)], ford(pz));
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) {
+        float f = unord(cell[i]);
+        desc[i] = (f == -1000.0f) ? 0.0 : (double)f;
+    }
+    __syncthreads();
 }
 
 // SCManager::makeScancontext + makeRingkey/SectorkeyFromScancontext +
@@ -774,34 +927,15 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
     __shared__ double desc[20 * 60];
     __shared__ int hid;
     if (threadIdx.x == 0) hid = st.sc_count;
-    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
     __syncthreads();
     const int kfid = hid;
     if (kfid >= v.KFMAX) {
         if (threadIdx.x == 0) { st.err |= SLO_ERR_SC_HISTORY; st.sc_wrote = 0; }
         return;
     }
-    for (int i = threadIdx.x; i < nraw; i += blockDim.x) {
-        float4 p0 = raw[i];
-        float px = p0.x, py = p0.y;
-        float pz = (float)(p0.z + v.cfg.sc_lidar_height);
-        float azim_range = sqrtf(px * px + py * py);
-        float azim_angle = sc_xy2theta(px, py, v.cfg.sc_atan_float);
-        if (azim_range > v.cfg.sc_max_radius) continue;
-        int ring_idx = max(min(NR, (int)ceil((azim_range / v.cfg.sc_max_radius) * NR)), 1);
-        double sc = ceil((azim_angle / 360.0) * NS);
-        int sraw = isnan(sc) ? INT_MIN : (int)sc;
-        int sctor_idx = max(min(NS, sraw), 1);
-        atomicMax(&cell[(ring_idx - 1) * NS + (sctor_idx - 1)], ford(pz));
-    }
-    __syncthreads();
+    sc_desc_block(v.cfg, raw, nraw, cell, desc);
     double* hd = v.sc_desc + ((size_t)s * v.KFMAX + kfid) * NR * NS;
-    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) {
-        float f = unord(cell[i]);
-        double d = (f == -1000.0f) ? 0.0 : (double)f;
-        desc[i] = d;
-        hd[i] = d;
-    }
+    for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) hd[i] = desc[i];
     __syncthreads();
     if (threadIdx.x < NR) {
         double rk = eigen_sum(desc + threadIdx.x * NS, NS, 1) / (double)NS;

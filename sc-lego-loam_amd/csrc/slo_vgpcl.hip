@@ -40,17 +40,29 @@ using slo_pcl::u64;
 #define PC_CH 4096        // positions per chunk of the global levels (256 threads x 16)
 #define PC_CT 256
 #define PC_PCH 4096       // pairs per pair chunk
-#define PC_T 8192         // a range of at most PC_T items is finished in LDS
-#define PC_FT 1024        // threads of the big finish workgroup
-#define PC_BT 64          // ranges of <= PC_BT items are finished by one lane
+#define PC_T 4096         // a range of at most PC_T items is finished in LDS
+#define PC_FT 512         // threads of the big finish workgroup
 #define PC_ST 2048        // small finish entries (<= PC_ST items): 256-thread workgroups
 #define PC_G 2048         // workgroups of the grid-stride level kernels
+#ifndef SLO_PCL_STATS
+#define SLO_PCL_STATS 0   // 1: count finish ranges, items and levels (PclWs::pstat, slo_get "pcl_stats")
+#endif
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB, pc0; };
 
 // counters (PclWs::ctr)
-enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 4, PCC_NPC = 5 };
+enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NPC = 4, PCC_NW = 5 };   // PCC_NW + k: entries of finish list k
+
+// Finish entries by size class: list 0 <= kWT items (k_pc_finish_w), 1 <=
+// PC_ST (k_pc_finish<256>), 2 <= PC_T (k_pc_finish<PC_FT>), 3 larger (the
+// global fallback).  An entry is (first position, size | depth << 24).
+struct PcLists { int2* l[4]; };
+__device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) {
+    const int k = n <= slo_pcl::kWT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
+    const int i = atomicAdd(&ctr[PCC_NW + k], 1);
+    L.l[k][i] = make_int2(f, n | (d << 24));
+}
 
 // libstdc++ __move_median_to_first on the keys at f+1, mid, l-1: which of
 // them (0, 1, 2) is swapped to f
@@ -102,7 +114,7 @@ __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, 
 
 // per stream: tile prefix of the finite counts, and the stream's first range
 __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
-                                                  PSeg* seg0, int* cseg0, int4* wl, int* ctr, int32_t* nfin) {
+                                                  PSeg* seg0, int* cseg0, PcLists wl, int* ctr, int32_t* nfin) {
     __shared__ int wsum[16];
     __shared__ int slot_c0[2];
     const int s = blockIdx.x, tid = threadIdx.x;
@@ -133,8 +145,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgPa
                 seg0[slot] = PSeg{f, f + n, d, c0};
                 slot_c0[0] = slot; slot_c0[1] = c0;
             } else {
-                const int w = atomicAdd(&ctr[PCC_NW], 1);
-                wl[w] = make_int4(f, f + n, d, 0);
+                pc_push(wl, ctr, f, n, d);
             }
         }
     }
@@ -307,56 +318,70 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const
     }
 }
 
+// ranks by ballots on striped rows: position a + q * PC_CT + tid is row q,
+// wave w, lane t; the stoppers before it are the chunk's prefix + the
+// (row, wave) pairs before (q, w) + the lanes below t
 __global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
                                                      const int2* ccnt, PRes* res, unsigned int* PA, unsigned int* PB,
                                                      const int* ctr, int cur) {
-    __shared__ unsigned int wsum[PC_CT / 64];
+    constexpr int Q = PC_CH / PC_CT, NWV = PC_CT / 64;
+    static_assert(Q * NWV <= 64, "one lane per (row, wave) pair");
+    __shared__ unsigned int rc[Q * NWV];   // packed left | right << 16 counts per (row, wave), then their prefixes
     const int nch = ctr[PCC_NCH + cur];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const unsigned long long lt = (1ull << lane) - 1ull;
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
         const int si = cseg[c];
         const PSeg g = seg[si];
         const PRes r = res[si];
         int a, b;
         pc_chunk(g, c, a, b);
-        constexpr int Q = PC_CH / PC_CT;
-        const int j0 = threadIdx.x * Q;
         unsigned int kk[Q];
 #pragma unroll
-        for (int q = 0; q < Q; ++q) kk[q] = K[min(a + j0 + q, b - 1)];
-        unsigned int fl = 0, fr = 0;
+        for (int q = 0; q < Q; ++q) kk[q] = K[min(a + q * PC_CT + (int)threadIdx.x, b - 1)];
+        unsigned long long bl[Q], br[Q];
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int x = a + j0 + q;
+            const int x = a + q * PC_CT + (int)threadIdx.x;
             const unsigned int k = x == r.med ? r.vmed : kk[q];
-            if (x < b) {
-                fl |= (unsigned int)!(k < r.piv) << q;
-                fr |= (unsigned int)!(r.piv < k) << q;
-            }
+            bl[q] = __ballot(x < b && !(k < r.piv));
+            br[q] = __ballot(x < b && !(r.piv < k));
+            if (lane == 0) rc[q * NWV + w] = (unsigned int)__popcll(bl[q]) | ((unsigned int)__popcll(br[q]) << 16);
         }
-        unsigned int tot;
-        const unsigned int ex = vg_block_scan<PC_CT / 64>((unsigned int)__popc(fl) | ((unsigned int)__popc(fr) << 16),
-                                                          wsum, &tot);
+        __syncthreads();
+        if (w == 0) {   // exclusive scan of the (row, wave) counts in position order
+            const unsigned int v = lane < Q * NWV ? rc[lane] : 0u;
+            unsigned int incl = v;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const unsigned int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            if (lane < Q * NWV) rc[lane] = incl - v;
+        }
+        __syncthreads();
         const int2 pre = ccnt[c];
-        int rl = pre.x + (int)(ex & 0xffffu), rr = pre.y + (int)(ex >> 16);
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int x = a + j0 + q;
-            if ((fl >> q) & 1) {
+            const int x = a + q * PC_CT + (int)threadIdx.x;
+            const unsigned int p = rc[q * NWV + w];
+            if ((bl[q] >> lane) & 1) {
+                const int rl = pre.x + (int)(p & 0xffffu) + __popcll(bl[q] & lt);
                 if (rl < r.m) PA[g.f + rl] = (unsigned int)x;
                 else if (rl == r.m) res[si].cutA = x;          // i_{m+1}
-                ++rl;
             }
-            if ((fr >> q) & 1) {
+            if ((br[q] >> lane) & 1) {
+                const int rr = pre.y + (int)(p >> 16) + __popcll(br[q] & lt);
                 const int kr = r.TR - 1 - rr;                   // rank from the right
                 if (kr < r.m) PB[g.f + kr] = (unsigned int)x;
                 if (kr == r.m - 1) res[si].cutB = x;            // j_m
-                ++rr;
             }
         }
         if (c == g.c0 && threadIdx.x == 0 && r.med != g.f) {    // the median swap, made real
             const unsigned int kf = K[g.f], vf = V[g.f], km = K[r.med], vm = V[r.med];
             K[g.f] = km; V[g.f] = vm; K[r.med] = kf; V[r.med] = vf;
         }
+        __syncthreads();   // rc reused by the next chunk
     }
 }
 
@@ -378,7 +403,7 @@ __global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int
 }
 
 __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* res, PSeg* nseg, int* ncseg,
-                                                    int4* wl, int* ctr, int cur, int last) {
+                                                    PcLists wl, int* ctr, int cur, int last) {
     __shared__ int slot_s[2], c0_s[2], nch_s[2];
     const int ns = ctr[PCC_NSEG + cur];
     for (int s = blockIdx.x; s < ns; s += gridDim.x) {
@@ -399,8 +424,7 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
                     nch_s[h] = nch;
                     nseg[slot_s[h]] = PSeg{lo[h], hi[h], D, c0_s[h]};
                 } else {
-                    const int w = atomicAdd(&ctr[PCC_NW], 1);
-                    wl[w] = make_int4(lo[h], hi[h], D, 0);
+                    pc_push(wl, ctr, lo[h], n, D);
                 }
             }
         }
@@ -412,42 +436,84 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
     }
 }
 
-// ---- finish: one workgroup per entry
-template <int NT, int NMAX>
-__global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int* V, const int4* wl, const int* ctr,
-                                                  int* cstat, u64* scratch, int lo_excl, int hi_incl) {
-    __shared__ u64 items[NMAX];
-    __shared__ slo_pcl::BlockSmem<NT, NMAX, PC_BT> sm;
+// ---- finish, small entries (<= kWT items): one wave per entry, no workgroup barrier
+__global__ void __launch_bounds__(256) k_pc_finish_w(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
+                                                      unsigned long long* pst) {
+    __shared__ u64 items[4][slo_pcl::kWT];
+    __shared__ slo_pcl::WaveSmem ws[4];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int nw = ctr[PCC_NW];
-    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
-        const int4 w = wl[e];
-        const int f = w.x, n = w.y - w.x, d = w.z;
-        if (n <= lo_excl || n > hi_incl) continue;   // another finish kernel's entry
-        if (n <= NMAX) {
-            for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
-            __syncthreads();
-            slo_pcl::pcl_block_sort<NT, NMAX, PC_BT>(items, n, d, sm);
-            for (int i = threadIdx.x; i < n; i += NT) {
-                const u64 it = items[i];
-                K[f + i] = (unsigned int)(it >> 32);
-                V[f + i] = (unsigned int)it;
-            }
-            __syncthreads();
-        } else {   // over the LDS capacity after the global levels: one lane, in global memory
-            for (int i = threadIdx.x; i < n; i += NT) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
-            __syncthreads();
-            if (threadIdx.x == 0) {
-                atomicAdd(&cstat[0], 1);
-                slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());
-            }
-            __syncthreads();
-            for (int i = threadIdx.x; i < n; i += NT) {
-                const u64 it = scratch[f + i];
-                K[f + i] = (unsigned int)(it >> 32);
-                V[f + i] = (unsigned int)it;
-            }
-            __syncthreads();
+    for (int e = blockIdx.x * 4 + w; e < nw; e += gridDim.x * 4) {
+        const int2 q = wl[e];
+        const int f = q.x, n = q.y & 0xffffff, d = q.y >> 24;
+        for (int i = lane; i < n; i += 64) items[w][i] = ((u64)K[f + i] << 32) | V[f + i];
+        slo_pcl::wave_sync();
+        const int lv = slo_pcl::pcl_wave_sort(items[w], 0, n, d, ws[w]);
+#if SLO_PCL_STATS
+        if (lane == 0) { atomicAdd(&pst[0], 1ull); atomicAdd(&pst[1], (unsigned long long)n); atomicAdd(&pst[2], (unsigned long long)lv); }
+#endif
+        for (int i = lane; i < n; i += 64) {
+            const u64 it = items[w][i];
+            K[f + i] = (unsigned int)(it >> 32);
+            V[f + i] = (unsigned int)it;
         }
+        slo_pcl::wave_sync();
+    }
+}
+
+// ---- finish: one workgroup per entry
+// (the block tier; the ranges of <= kWT items it leaves are appended to the
+// entry list for k_pc_finish_w, which runs after it)
+template <int NT, int NMAX>
+__global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
+                                                  unsigned long long* pst) {
+    __shared__ u64 items[NMAX];
+    __shared__ slo_pcl::BlockSmem<NT, NMAX> sm;
+    __shared__ int base_s;
+    const int nw = ctr[PCC_NW + list];
+    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
+        const int2 w = wl.l[list][e];
+        const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
+        for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
+        __syncthreads();
+        const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm);
+#if SLO_PCL_STATS
+        if (threadIdx.x == 0) { atomicAdd(&pst[3 + 3 * (list - 1)], 1ull); atomicAdd(&pst[4 + 3 * (list - 1)], (unsigned long long)n); atomicAdd(&pst[5 + 3 * (list - 1)], (unsigned long long)lv); }
+#endif
+        if (threadIdx.x == 0) base_s = atomicAdd(&ctr[PCC_NW], sm.nw);
+        __syncthreads();
+        for (int q = threadIdx.x; q < sm.nw; q += NT)
+            wl.l[0][base_s + q] = make_int2(f + sm.wf[q], (sm.wl[q] - sm.wf[q]) | ((int)sm.wd[q] << 24));
+        for (int i = threadIdx.x; i < n; i += NT) {
+            const u64 it = items[i];
+            K[f + i] = (unsigned int)(it >> 32);
+            V[f + i] = (unsigned int)it;
+        }
+        __syncthreads();
+    }
+}
+
+// an entry still over PC_T after the global levels (adversarial inputs only):
+// one lane finishes it in global memory with the sequential restatement
+__global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
+                                                      int* cstat, u64* scratch) {
+    const int nw = ctr[PCC_NW + 3];
+    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
+        const int2 w = wl[e];
+        const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
+        for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            atomicAdd(&cstat[0], 1);
+            slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += 256) {
+            const u64 it = scratch[f + i];
+            K[f + i] = (unsigned int)(it >> 32);
+            V[f + i] = (unsigned int)it;
+        }
+        __syncthreads();
     }
 }
 
@@ -461,6 +527,8 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.nfin, S * sizeof(int32_t)));
         SLO_CHECK(hipMalloc(&w.cstat, 16 * sizeof(int)));
         SLO_CHECK(hipMemset(w.cstat, 0, 16 * sizeof(int)));
+        SLO_CHECK(hipMalloc(&w.pstat, 16 * sizeof(unsigned long long)));
+        SLO_CHECK(hipMemset(w.pstat, 0, 16 * sizeof(unsigned long long)));
     }
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
@@ -470,7 +538,7 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         const size_t segcap = S + it / PC_T + 2;
         const size_t chcap = it / PC_CH + segcap;
         const size_t pccap = it / 2 / PC_PCH + segcap;
-        const size_t wcap = it / 2 + S + 2;
+        const size_t wcap0 = it / 2 + S + 2, wcapk = it / slo_pcl::kWT + S + 2;   // disjoint entries of >= 2 / > kWT items
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.pairs, sizeof(u64) * it));
         SLO_CHECK(hipMalloc(&w.seg[0], sizeof(PSeg) * segcap));
@@ -480,7 +548,9 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
         SLO_CHECK(hipMalloc(&w.pseg, sizeof(int) * pccap));
-        SLO_CHECK(hipMalloc(&w.wl, sizeof(int4) * wcap));
+        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 3 * wcapk)));
+        w.wcap0 = wcap0;
+        w.wcapk = wcapk;
     }
     if (S * maxT > w.tiles) {
         if (w.tcnt) hipFree(w.tcnt);
@@ -508,11 +578,14 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     if (int r = pcl_ws(ctx, (size_t)S * in_stride, (size_t)maxT)) return r;
     PclWs& w = ctx->pws;
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
+    PcLists L;
+    L.l[0] = w.wl;
+    for (int k = 1; k < 4; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
     unsigned int* PA = (unsigned int*)w.pairs;
     unsigned int* PB = PA + w.items;
     SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
                w.ctr);
-    SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], w.wl,
+    SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
                w.ctr, w.nfin);
     SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
@@ -528,20 +601,20 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
         SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(PC_G), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,
                    w.ctr);
         SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(PC_G / 4), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
-                   w.cseg[cur ^ 1], w.wl, w.ctr, cur, (int)(lv == G - 1));
+                   w.cseg[cur ^ 1], L, w.ctr, cur, (int)(lv == G - 1));
     }
     const int FG = std::max(64, std::min(4096, S * 8));
-    SLO_LAUNCH(ctx, "pc_finish", (k_pc_finish<256, PC_ST>), dim3(FG), dim3(256), 0, K, V, w.wl, w.ctr, w.cstat, w.pairs, 1,
-               PC_ST);
-    SLO_LAUNCH(ctx, "pc_finish", (k_pc_finish<PC_FT, PC_T>), dim3(FG), dim3(PC_FT), 0, K, V, w.wl, w.ctr, w.cstat, w.pairs,
-               PC_ST, 0x7fffffff);
+    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[3], w.ctr, w.cstat, w.pairs);
+    SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_FT, PC_T>), dim3(FG), dim3(PC_FT), 0, K, V, L, w.ctr, 2, w.pstat);
+    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<256, PC_ST>), dim3(FG), dim3(256), 0, K, V, L, w.ctr, 1, w.pstat);
+    SLO_LAUNCH(ctx, "pc_finish_w", k_pc_finish_w, dim3(FG), dim3(256), 0, K, V, L.l[0], w.ctr, w.pstat);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
 
 void pcl_free(slo_ctx* ctx) {
     PclWs& w = ctx->pws;
-    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg,
+    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg,
                   w.wl, w.tcnt};
     for (void* p : ps) if (p) hipFree(p);
     w = PclWs();

@@ -44,6 +44,7 @@ _DT["loop"] = LOOP_DTYPE
 _DT["imu"] = np.float64
 _DT["vg_in"] = np.int32
 _DT["vg_stats"] = np.int32
+_DT["pcl_stats"] = np.uint64
 
 
 class SloError(RuntimeError):
@@ -365,10 +366,60 @@ class MapOptimization(_Node):
 
 class SCManager:
     """Mirror of the public SCManager API (Scancontext.h:63-73) on stream 0 of
-    a Context: makeAndSaveScancontextAndKeys / detectLoopClosureID."""
+    a Context: makeAndSaveScancontextAndKeys / detectLoopClosureID, and the
+    public helpers makeScancontext, makeRingkeyFromScancontext,
+    makeSectorkeyFromScancontext, fastAlignUsingVkey, distDirectSC,
+    distanceBtnScanContext (slo_sc_* in include/slo_abi.h).  Descriptors are
+    (NR, NS) float64 arrays (ring, sector), as the reference's MatrixXd."""
 
     def __init__(self, ctx):
         self.ctx = ctx
+        self.NR, self.NS = ctx.cfg.sc_num_ring, ctx.cfg.sc_num_sector
+
+    def _desc(self, d):
+        d = np.ascontiguousarray(d, np.float64)
+        if d.shape != (self.NR, self.NS):
+            raise SloError(f"a descriptor is ({self.NR}, {self.NS}), got {d.shape}")
+        return d
+
+    def makeScancontext(self, scan_down_xyzi):
+        p = np.ascontiguousarray(scan_down_xyzi, np.float32).reshape(-1, 4)
+        d = np.zeros((self.NR, self.NS), np.float64)
+        self.ctx._ok(self.ctx.L.slo_sc_make_scancontext(self.ctx.h, p.ctypes.data, len(p), 16, 0, d.ctypes.data),
+                     "slo_sc_make_scancontext")
+        return d
+
+    def makeRingkeyFromScancontext(self, desc):
+        d, k = self._desc(desc), np.zeros(self.NR, np.float64)
+        self.ctx._ok(self.ctx.L.slo_sc_ring_key(self.ctx.h, d.ctypes.data, k.ctypes.data), "slo_sc_ring_key")
+        return k
+
+    def makeSectorkeyFromScancontext(self, desc):
+        d, k = self._desc(desc), np.zeros(self.NS, np.float64)
+        self.ctx._ok(self.ctx.L.slo_sc_sector_key(self.ctx.h, d.ctypes.data, k.ctypes.data), "slo_sc_sector_key")
+        return k
+
+    def fastAlignUsingVkey(self, vkey1, vkey2):
+        a, b = (np.ascontiguousarray(v, np.float64).reshape(self.NS) for v in (vkey1, vkey2))
+        sh = ctypes.c_int32(0)
+        self.ctx._ok(self.ctx.L.slo_sc_fast_align(self.ctx.h, a.ctypes.data, b.ctypes.data, ctypes.byref(sh)),
+                     "slo_sc_fast_align")
+        return sh.value
+
+    def distDirectSC(self, sc1, sc2):
+        a, b = self._desc(sc1), self._desc(sc2)
+        d = ctypes.c_double(0)
+        self.ctx._ok(self.ctx.L.slo_sc_dist_direct(self.ctx.h, a.ctypes.data, b.ctypes.data, ctypes.byref(d)),
+                     "slo_sc_dist_direct")
+        return d.value
+
+    def distanceBtnScanContext(self, sc1, sc2):
+        """-> (min distance, shift) like the reference's std::pair<double, int>"""
+        a, b = self._desc(sc1), self._desc(sc2)
+        d, sh = ctypes.c_double(0), ctypes.c_int32(0)
+        self.ctx._ok(self.ctx.L.slo_sc_distance(self.ctx.h, a.ctypes.data, b.ctypes.data, ctypes.byref(d),
+                                                ctypes.byref(sh)), "slo_sc_distance")
+        return d.value, sh.value
 
     def makeAndSaveScancontextAndKeys(self, scan_down_xyzi):
         self.ctx.sc_make_and_save(scan_down_xyzi)

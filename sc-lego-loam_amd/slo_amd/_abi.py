@@ -115,7 +115,8 @@ EXPORTS = [
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
     "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_batch_imu", "slo_batch_scan_time",
     "slo_imu_handler", "slo_image_projection", "slo_feature_association",
-    "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_batch_voxel_grid", "slo_pack_records",
+    "slo_map_optimization", "slo_sc_detect", "slo_sc_make_and_save", "slo_batch_sc_make", "slo_batch_voxel_grid", "slo_sc_make_scancontext", "slo_sc_ring_key",
+    "slo_sc_sector_key", "slo_sc_fast_align", "slo_sc_dist_direct", "slo_sc_distance", "slo_batch_sc_distance", "slo_pack_records",
     "slo_record_floats", "slo_get", "slo_timing_enable", "slo_timing_read", "slo_timing_reset", "slo_gen_scan",
     "slo_gen_batch", "slo_batch_loop_closure", "slo_loop_closure", "slo_icp_align_batch",
     "slo_timing_filter", "slo_image_projection_ring", "slo_batch_set_rings", "slo_pc2_layout_of", "slo_pc2_to_xyzi", "slo_image_projection_pc2", "slo_batch_pc2_unpack",
@@ -196,6 +197,13 @@ def lib():
     L.slo_icp_align_batch.argtypes = [P, P, ctypes.c_size_t, P, P, ctypes.c_size_t, P, P]
     L.slo_sc_make_and_save.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t]
     L.slo_batch_sc_make.argtypes = [P, P, P]
+    L.slo_sc_make_scancontext.argtypes = [P, P, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, P]
+    L.slo_sc_ring_key.argtypes = [P, P, P]
+    L.slo_sc_sector_key.argtypes = [P, P, P]
+    L.slo_sc_fast_align.argtypes = [P, P, P, P]
+    L.slo_sc_dist_direct.argtypes = [P, P, P, P]
+    L.slo_sc_distance.argtypes = [P, P, P, P, P]
+    L.slo_batch_sc_distance.argtypes = [P, P, P, ctypes.c_int, P, P]
     L.slo_batch_voxel_grid.argtypes = [P, P, ctypes.c_size_t, P, ctypes.c_float, P, ctypes.c_size_t, P, ctypes.c_int]
     L.slo_pack_records.argtypes = [P, P]
     L.slo_pc2_layout_of.argtypes = [ctypes.POINTER(Pc2), ctypes.POINTER(Pc2Layout)]

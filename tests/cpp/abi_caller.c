@@ -23,6 +23,20 @@ int main(void) {
     CHECK(slo_batch_process(NULL, NULL, NULL, 0.0) == SLO_E_ARG);
     CHECK(slo_graph_mode(NULL, 1) == SLO_E_ARG);
     CHECK(slo_record_floats() == SLO_RECORD_FLOATS);
+    /* argument checks of the SCManager helpers and the batched VoxelGrid (no GPU call) */
+    {
+        double d[1200] = {0}, k[60] = {0}, dist = 0;
+        int32_t sh = 0;
+        CHECK(slo_sc_make_scancontext(NULL, NULL, 0, 16, 0, d) == SLO_E_ARG);
+        CHECK(slo_sc_ring_key(NULL, d, k) == SLO_E_ARG);
+        CHECK(slo_sc_sector_key(NULL, d, k) == SLO_E_ARG);
+        CHECK(slo_sc_fast_align(NULL, k, k, &sh) == SLO_E_ARG);
+        CHECK(slo_sc_dist_direct(NULL, d, d, &dist) == SLO_E_ARG);
+        CHECK(slo_sc_distance(NULL, d, d, &dist, &sh) == SLO_E_ARG);
+        CHECK(slo_batch_sc_distance(NULL, d, d, 1, &dist, &sh) == SLO_E_ARG);
+        CHECK(slo_batch_voxel_grid(NULL, d, 1, NULL, 0.5f, d, 1, NULL, 1) == SLO_E_ARG);
+        CHECK(cfg.voxel_order == SLO_VOXEL_PCL);
+    }
     CHECK(SLO_REC_DESC + 20 * 60 <= SLO_RECORD_FLOATS);
 
     /* the synthetic stream generator (host) */
