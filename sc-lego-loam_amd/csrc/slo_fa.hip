@@ -740,6 +740,8 @@ __device__ inline void ring_sort_regs(unsigned long long* lds, KF&& key_of) {
     __syncthreads();
 }
 
+// PMAX: the largest ring the PCL-order sort takes (the horizon_scan bound)
+template <int PMAX>
 __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int s = blockIdx.y, ring = blockIdx.x;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
@@ -792,20 +794,16 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
         return (((unsigned long long)idx << 32) | (unsigned int)i) | (0ull - (unsigned long long)(i >= n));
     };
     if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // std::sort's order, as PCL (slo_pclsort.h)
-        __shared__ slo_pcl::BlockSmem<256, 2048> psm;
-        __shared__ slo_pcl::WaveSmem pws[4];
+        // one LDS area for the instance the ring's size picks (each a smaller struct than the largest)
+        __shared__ __attribute__((aligned(16))) char pbuf[sizeof(slo_pcl::BlockSmem<256, PMAX>)];
         for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = key_of(i);
         __syncthreads();
-        if (n <= 2048) {
-            slo_pcl::pcl_block_sort<256, 2048>(keys, n, 2 * slo_pcl::lg2(n), psm);
-            const int w = threadIdx.x >> 6;
-            for (int q = w; q < psm.nw; q += 4)
-                slo_pcl::pcl_wave_sort(keys, psm.wf[q], psm.wl[q] - psm.wf[q], psm.wd[q], pws[w]);
-            __syncthreads();
-        } else {   // rings over 2048 points: one lane (no preset has them)
-            if (threadIdx.x == 0) slo_sort::introsort_range(keys, n, 2 * slo_pcl::lg2(n), slo_pcl::Less());
-            __syncthreads();
-        }
+        const int d = 2 * slo_pcl::lg2(n);
+        if (n <= 256) slo_pcl::pcl_block_sort<256, 256>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 256>*>(pbuf));
+        else if (n <= 512) slo_pcl::pcl_block_sort<256, 512>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 512>*>(pbuf));
+        else if (n <= 1024) slo_pcl::pcl_block_sort<256, 1024>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 1024>*>(pbuf));
+        else if (n <= 2048 || PMAX == 2048) slo_pcl::pcl_block_sort<256, 2048>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 2048>*>(pbuf));
+        else slo_pcl::pcl_block_sort<256, PMAX>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, PMAX>*>(pbuf));
     } else if (n <= 256) ring_sort_regs<1>(keys, key_of);
     else if (n <= 512) ring_sort_regs<2>(keys, key_of);
     else if (n <= 1024) ring_sort_regs<4>(keys, key_of);
@@ -953,7 +951,11 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
     while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
-    SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
+    if (v.cfg.horizon_scan <= 2048) {
+        SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds<2048>, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
+    } else {   // the PCL-order ring sort holds up to 4096 points (slo_create refuses wider rings)
+        SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds<4096>, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
+    }
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());
     return 0;

@@ -25,7 +25,10 @@
 //                  cut candidates; chunk 0 makes the median swap real;
 //     k_pc_lpairs  the swaps;
 //     k_pc_lsplit  per range: the halves — over PC_T items back to the next
-//                  level, otherwise (or at the last level) a finish entry;
+//                  level, otherwise (or at the last level) a finish entry.
+//   (Folding the per-range steps into the last chunk's workgroup, by a
+//   done counter, measured 20x slower: the device-scope fence each chunk
+//   then needs writes the XCD's L2 back.)
 //   k_pc_finish: one workgroup per finish entry (<= PC_T items) sorts it in
 //     LDS to the end (pcl_block_sort); an entry still over PC_T after the G
 //     levels (never seen on the configs; counted in meta) is finished by one
@@ -41,8 +44,9 @@ using slo_pcl::u64;
 #define PC_CT 256
 #define PC_PCH 4096       // pairs per pair chunk
 #define PC_T 4096         // a range of at most PC_T items is finished in LDS
-#define PC_FT 512         // threads of the big finish workgroup
-#define PC_ST 2048        // small finish entries (<= PC_ST items): 256-thread workgroups
+#define PC_FT 1024        // threads of the big finish workgroup (4 positions each)
+#define PC_ST 2048        // small finish entries (<= PC_ST items): 512-thread workgroups
+#define PC_WT 512         // smallest finish entries (<= PC_WT items): 128-thread workgroups
 #define PC_G 2048         // workgroups of the grid-stride level kernels
 #ifndef SLO_PCL_STATS
 #define SLO_PCL_STATS 0   // 1: count finish ranges, items and levels (PclWs::pstat, slo_get "pcl_stats")
@@ -52,14 +56,13 @@ struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB, pc0; };
 
 // counters (PclWs::ctr)
-enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NPC = 4, PCC_NW = 5 };   // PCC_NW + k: entries of finish list k
+enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NPC = 4, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: finish list k
 
-// Finish entries by size class: list 0 <= kWT items (k_pc_finish_w), 1 <=
-// PC_ST (k_pc_finish<256>), 2 <= PC_T (k_pc_finish<PC_FT>), 3 larger (the
-// global fallback).  An entry is (first position, size | depth << 24).
+// Finish entries by size class: list 0 <= PC_WT items (k_pc_finish<128>), 1 <= PC_ST (k_pc_finish<512>), 2 <= PC_T (k_pc_finish<PC_FT>), 3
+// larger (the global fallback).  An entry is (first position, size | depth << 24).
 struct PcLists { int2* l[4]; };
 __device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) {
-    const int k = n <= slo_pcl::kWT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
+    const int k = n <= PC_WT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
     const int i = atomicAdd(&ctr[PCC_NW + k], 1);
     L.l[k][i] = make_int2(f, n | (d << 24));
 }
@@ -202,7 +205,7 @@ __device__ inline void pc_chunk(const PSeg& g, int c, int& a, int& b) {
 
 __global__ void __launch_bounds__(PC_CT) k_pc_lcount(const unsigned int* K, const PSeg* seg, const int* cseg,
                                                       int2* ccnt, int* ctr, int cur) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[PCC_NPC] = 0;   // pair chunks of this level (k_pc_lscan)
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[PCC_NPC + cur] = 0;   // pair chunks of this level (k_pc_lscan)
     __shared__ unsigned int wsum[PC_CT / 64];
     const int nch = ctr[PCC_NCH + cur];
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
@@ -308,7 +311,7 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const
         const int m = mx_s;
         if (tid == 0) {
             const int npc = (m + PC_PCH - 1) / PC_PCH;
-            pc0_s = npc ? atomicAdd(&ctr[PCC_NPC], npc) : 0;
+            pc0_s = npc ? atomicAdd(&ctr[PCC_NPC + cur], npc) : 0;
             res[s] = PRes{piv, vmed, med, m, TR, 0x7fffffff, 0x7fffffff, pc0_s};
         }
         __syncthreads();
@@ -387,8 +390,8 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned in
 
 __global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int* V, const PSeg* seg, const PRes* res,
                                                     const int* pseg, const unsigned int* PA, const unsigned int* PB,
-                                                    const int* ctr) {
-    const int npc = ctr[PCC_NPC];
+                                                    const int* ctr, int cur) {
+    const int npc = ctr[PCC_NPC + cur];
     for (int pc = blockIdx.x; pc < npc; pc += gridDim.x) {
         const int si = pseg[pc];
         const PSeg g = seg[si];
@@ -436,40 +439,12 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
     }
 }
 
-// ---- finish, small entries (<= kWT items): one wave per entry, no workgroup barrier
-__global__ void __launch_bounds__(256) k_pc_finish_w(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
-                                                      unsigned long long* pst) {
-    __shared__ u64 items[4][slo_pcl::kWT];
-    __shared__ slo_pcl::WaveSmem ws[4];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int nw = ctr[PCC_NW];
-    for (int e = blockIdx.x * 4 + w; e < nw; e += gridDim.x * 4) {
-        const int2 q = wl[e];
-        const int f = q.x, n = q.y & 0xffffff, d = q.y >> 24;
-        for (int i = lane; i < n; i += 64) items[w][i] = ((u64)K[f + i] << 32) | V[f + i];
-        slo_pcl::wave_sync();
-        const int lv = slo_pcl::pcl_wave_sort(items[w], 0, n, d, ws[w]);
-#if SLO_PCL_STATS
-        if (lane == 0) { atomicAdd(&pst[0], 1ull); atomicAdd(&pst[1], (unsigned long long)n); atomicAdd(&pst[2], (unsigned long long)lv); }
-#endif
-        for (int i = lane; i < n; i += 64) {
-            const u64 it = items[w][i];
-            K[f + i] = (unsigned int)(it >> 32);
-            V[f + i] = (unsigned int)it;
-        }
-        slo_pcl::wave_sync();
-    }
-}
-
 // ---- finish: one workgroup per entry
-// (the block tier; the ranges of <= kWT items it leaves are appended to the
-// entry list for k_pc_finish_w, which runs after it)
 template <int NT, int NMAX>
 __global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
                                                   unsigned long long* pst) {
     __shared__ u64 items[NMAX];
     __shared__ slo_pcl::BlockSmem<NT, NMAX> sm;
-    __shared__ int base_s;
     const int nw = ctr[PCC_NW + list];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
@@ -478,12 +453,8 @@ __global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int*
         __syncthreads();
         const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm);
 #if SLO_PCL_STATS
-        if (threadIdx.x == 0) { atomicAdd(&pst[3 + 3 * (list - 1)], 1ull); atomicAdd(&pst[4 + 3 * (list - 1)], (unsigned long long)n); atomicAdd(&pst[5 + 3 * (list - 1)], (unsigned long long)lv); }
+        if (threadIdx.x == 0) { atomicAdd(&pst[3 * list], 1ull); atomicAdd(&pst[1 + 3 * list], (unsigned long long)n); atomicAdd(&pst[2 + 3 * list], (unsigned long long)lv); }
 #endif
-        if (threadIdx.x == 0) base_s = atomicAdd(&ctr[PCC_NW], sm.nw);
-        __syncthreads();
-        for (int q = threadIdx.x; q < sm.nw; q += NT)
-            wl.l[0][base_s + q] = make_int2(f + sm.wf[q], (sm.wl[q] - sm.wf[q]) | ((int)sm.wd[q] << 24));
         for (int i = threadIdx.x; i < n; i += NT) {
             const u64 it = items[i];
             K[f + i] = (unsigned int)(it >> 32);
@@ -538,7 +509,7 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         const size_t segcap = S + it / PC_T + 2;
         const size_t chcap = it / PC_CH + segcap;
         const size_t pccap = it / 2 / PC_PCH + segcap;
-        const size_t wcap0 = it / 2 + S + 2, wcapk = it / slo_pcl::kWT + S + 2;   // disjoint entries of >= 2 / > kWT items
+        const size_t wcap0 = it / 2 + S + 2, wcapk = it / PC_WT + S + 2;   // disjoint entries of >= 2 / > PC_WT items
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.pairs, sizeof(u64) * it));
         SLO_CHECK(hipMalloc(&w.seg[0], sizeof(PSeg) * segcap));
@@ -562,13 +533,16 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
 }
 
 // global levels for ranges of up to `stride` items: enough that what is left
-// fits the LDS finish (measured on the C3 / C5 maps: a 600 k-item surf map
-// leaves its last range over PC_T after 15 levels; 2 * log2(stride / PC_T) + 4)
+// fits the LDS finish.  Measured with tests/cpp/pcl_sort_model.cpp at PC_T =
+// 4096: a C3 raw scan (110 k points, 0.5 m) leaves a range over PC_T for up to
+// 13 levels, the 600 k-point surf map for 16; 2 log2(stride / PC_T) + 10
+// covers both with room (an empty level costs only its five launches).
+// Whatever is still over PC_T then is finished by k_pc_fallback (one lane).
 static int pcl_levels(size_t stride) {
     int g = 0;
     size_t x = PC_T;
     while (x < stride) { x <<= 1; g += 2; }
-    return g ? std::min(40, g + 4) : 0;
+    return g ? std::min(48, g + 10) : 0;
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
@@ -592,22 +566,25 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     const int G = pcl_levels(in_stride);
     for (int lv = 0; lv < G; ++lv) {
         const int cur = lv & 1;
-        SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(PC_G), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
+        // the grid-stride kernels take whatever the level holds; past the first
+        // levels most items have left for the finish lists: smaller grids
+        const int GG = lv < 8 ? PC_G : PC_G / 4, GS = PC_G / 4;
+        SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(GG), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(PC_G / 4), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.pseg,
+        SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(GS), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.pseg,
                    w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lrank", k_pc_lrank, dim3(PC_G), dim3(PC_CT), 0, K, V, w.seg[cur], w.cseg[cur], w.ccnt,
+        SLO_LAUNCH(ctx, "pc_lrank", k_pc_lrank, dim3(GG), dim3(PC_CT), 0, K, V, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.res, PA, PB, w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(PC_G), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,
-                   w.ctr);
-        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(PC_G / 4), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
+        SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(GG), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,
+                   w.ctr, cur);
+        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(GS), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
                    w.cseg[cur ^ 1], L, w.ctr, cur, (int)(lv == G - 1));
     }
     const int FG = std::max(64, std::min(4096, S * 8));
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[3], w.ctr, w.cstat, w.pairs);
     SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_FT, PC_T>), dim3(FG), dim3(PC_FT), 0, K, V, L, w.ctr, 2, w.pstat);
-    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<256, PC_ST>), dim3(FG), dim3(256), 0, K, V, L, w.ctr, 1, w.pstat);
-    SLO_LAUNCH(ctx, "pc_finish_w", k_pc_finish_w, dim3(FG), dim3(256), 0, K, V, L.l[0], w.ctr, w.pstat);
+    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<512, PC_ST>), dim3(FG), dim3(512), 0, K, V, L, w.ctr, 1, w.pstat);
+    SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<128, PC_WT>), dim3(2 * FG), dim3(128), 0, K, V, L, w.ctr, 0, w.pstat);
     SLO_CHECK(hipGetLastError());
     return 0;
 }

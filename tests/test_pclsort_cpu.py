@@ -34,29 +34,3 @@ def test_killer_sequences_reach_heapsort(model, tmp_path, n):
     assert r.returncode == 0 and "OK" in r.stdout, r.stdout
     assert "heapsorts=0" not in r.stdout
 
-
-def test_wave_tier_emulation_matches_std_sort(model, tmp_path):
-    """The wave tier's lane-level steps (ballots, prefix / select, m by
-    binary search, cuts, swap partners, child tables, leaf ranks), emulated in
-    Python (tests/pclsort_emul.py), give std::sort's order — random ties,
-    runs, all-equal keys, and a killer sequence (depth limit, heapsort)."""
-    import random
-    import sys
-    import numpy as np
-    sys.path.insert(0, HERE)
-    import pclsort_emul as P
-    rng = random.Random(5)
-    cases = []
-    for n in (2, 16, 17, 40, 64, 65, 200, 511, 512):
-        for nk in (1, 3, 50, 1000):
-            cases.append([(rng.randrange(nk), i) for i in range(n)])
-    cases.append([(i // 3, i) for i in range(300)])
-    cases.append([(300 - i, i) for i in range(300)])
-    subprocess.run([str(model), "--killer", "500", str(tmp_path / "k.u32")], check=True, capture_output=True)
-    cases.append([(int(k), i) for i, k in enumerate(np.fromfile(tmp_path / "k.u32", np.uint32))])
-    for keys in cases:
-        n = len(keys)
-        want = P.std_sort(keys)
-        buf = [(7, -1)] * 3 + list(keys) + [(7, -1)] * 2
-        P.wave_sort(buf, 3, n, 2 * (n.bit_length() - 1))
-        assert buf[3:3 + n] == want, n
