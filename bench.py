@@ -75,13 +75,15 @@ def parse():
     ap.add_argument("--config-id", type=int, default=3)
     ap.add_argument("--voxel-order", type=int, default=0,
                     help="0: PCL's std::sort order inside a voxel (the reference's; default), 1: stable (radix sort)")
-    ap.add_argument("--history", type=int, default=0,
-                    help="extra Scan Context history per stream (scans before scan 0); the pre-roll builds the real one")
+    ap.add_argument("--history", type=int, default=1000,
+                    help="extra Scan Context history per stream (scans before scan 0, a KITTI-00 mid-drive history: "
+                         "detects search ~1000 keyframes, SCc:264-289); the pre-roll builds the recent part")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="mo_knn,fa_search_corner",
+    ap.add_argument("--roofline-also", default="mo_knn,vg_scatter,pc_lpairs,fa_search_corner",
                     help="further kernels timed live the same way, reported under roofline_also (comma list)")
-    ap.add_argument("--roofline-kernel", default="vg_scatter",
-                    help="kernel timed with HIP events inside the timed region (the roofline's kernel)")
+    ap.add_argument("--roofline-kernel", default="auto",
+                    help="kernel timed inside the timed region (the roofline's kernel); auto = the largest kernel by "
+                         "device time in the instrumented pass, which runs before the timed window")
     ap.add_argument("--cpu-scans", type=int, default=8, help="timed scans per CPU stream in the baseline (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core in sched_getaffinity")
     ap.add_argument("--cpu-distinct", type=int, default=8,
@@ -112,7 +114,31 @@ def stream_counts(ctx, S):
     c["fa_iters"] = np.array([ctx.get(s, "fa_iters") for s in range(S)], np.int64)
     c["vg_in"] = np.array([ctx.get(s, "vg_in") for s in range(S)], np.int64)   # [S][7] VoxelGrid items
     c["mo_iters"] = np.array([int(ctx.get(s, "mo_iters")[0]) for s in range(S)], np.int64)
+    c["raw_ds"] = np.array([ctx.get(s, "raw_ds").shape[0] for s in range(S)], np.int64)
+    c["map_raw_n"] = np.array([ctx.get(s, "map_raw_n") for s in range(S)], np.int64)   # [S][2] before the VoxelGrids
+    c["n_keyframes"] = np.array([int(ctx.get(s, "n_keyframes")[0]) for s in range(S)], np.int64)
     return c
+
+
+def path_bytes(c, cfg, history):
+    """SURVEY §8(d)'s algorithmic bytes of the whole path, from the logged
+    per-stream counts: (every scan, summed over streams; a mapping step adds,
+    summed over streams) — projection 16P + 24H, ground + labels 32 C gsi +
+    9H, components 20H, compaction 25H + 25S, deskew / curvature / occlusion
+    48S, feature selection + DS 25S + 16 (F_s + F_ls + F_f + F_lf), odometry
+    LM 64 per query-iteration; map build 16 M_raw + 16 M, mapping LM 96 per
+    query-iteration, Scan Context 16 P_ds + 9.6 KB + the detect 80 L + K 10.1 KB."""
+    P, H, C = cfg.max_points, cfg.n_scan * cfg.horizon_scan, cfg.horizon_scan
+    gsi = cfg.ground_scan_ind + 1
+    seg = c["seg_pts"]
+    front = (16 * P + 24 * H + 32 * C * gsi + 9 * H + 20 * H + 25 * H + 25 * seg + 48 * seg + 25 * seg
+             + 16 * (c["sharp"] + c["corner_last"] + c["flat"] + c["surf_last"])
+             + 64 * (c["fa_iters"][:, 0] * c["flat"] + c["fa_iters"][:, 1] * c["sharp"]))
+    L = np.maximum(c["n_keyframes"] + history - cfg.sc_num_exclude_recent, 0)
+    mapping = (16 * c["map_raw_n"].sum(axis=1) + 16 * (c["map_corner_ds"] + c["map_surf_ds"])
+               + 96 * c["mo_iters"] * (c["corner_ds"] + c["surf_total_ds"])
+               + 16 * c["raw_ds"] + 9600 + 80 * L + cfg.sc_num_candidates * 10100)
+    return int(front.sum()), int(mapping.sum())
 
 
 def algo_bytes(name, c, cfg, S, steps, map_steps):
@@ -149,6 +175,22 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
         return map_steps * int(c["vg_in"].sum()) * 16
     if name == "vg_hist":         # pass 0 reads the point, passes 1-3 the 4 B key
         return map_steps * int(c["vg_in"].sum()) * (16 + 3 * 4)
+    pw = c.get("pcl_work")        # PCL-order sort work counters over the instrumented pass (slo_vgpcl.hip PW_*)
+    if pw is not None:
+        if name == "pc_lcount":   # the keys of every stepped range
+            return int(4 * pw[0])
+        if name == "pc_lrank":    # the keys again, the pair positions out
+            return int(4 * pw[0] + 8 * pw[1])
+        if name == "pc_lpairs":   # per pair: both positions in, both items (key + index) read and written
+            return int(40 * pw[1])
+        if name in ("pc_finish_w", "pc_finish_s", "pc_finish_b"):   # a finish entry's items in and out
+            return int(16 * pw[2 + ("pc_finish_w", "pc_finish_s", "pc_finish_b").index(name)])
+        if name == "pc_count":    # the points
+            return int(16 * pw[5])
+        if name == "pc_write":    # the points in, (key, index) out
+            return int(24 * pw[5])
+    if name == "vg_reduce":       # sorted (key, index) in, the point gathered, per item
+        return map_steps * int(c["vg_in"].sum()) * (8 + 16)
     if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
         return steps * int(c["seg_pts"].sum()) * (8 + 8 + 4 + 1 + 2)
     if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
@@ -261,16 +303,21 @@ def host_info():
     return info
 
 
-def cpu_baseline(a, pid, ncpu):
-    """SURVEY §8(d) CPU baselines on the oracle (C++ restatement, g++ -O2), same window as the GPU"""
+def cpu_baseline(a, pid, ncpu, start):
+    """SURVEY §8(d) CPU baselines on the oracle (C++ restatement, g++ -O2), same window as the GPU
+    (scans from `start`); (B) runs one stream per core this process can actually use: min(affinity, the
+    cgroup CPU quota)"""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ctypes
     import oracle_py as O
-    th = a.cpu_threads or ncpu
+    info = host_info()
+    quota = info.get("cgroup_cpu_quota")
+    eff = max(1, min(ncpu, int(quota))) if quota else ncpu
+    th = a.cpu_threads or eff
     stage = (ctypes.c_double * 4)()
     one = (ctypes.c_double * 4)()
     t0 = time.time()
-    secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, a.preroll + a.warmup, a.history,
+    secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, start, a.history,
                                 min(a.cpu_distinct, th), stage, one)
     wall = time.time() - t0
     n = a.cpu_scans
@@ -278,10 +325,10 @@ def cpu_baseline(a, pid, ncpu):
     # runs at the pace of its slowest stage (mapOptimization includes SC)
     per = {"ip": one[0] / n, "fa": one[1] / n, "mo_sc": (one[2] + one[3]) / n}
     a_val = 1.0 / max(per.values())
-    info = host_info()
-    return {"value": round(th * n / secs, 3), "unit": "scans/s", "cores": th, "kind": "port",
-            "sample": f"(B) {th} independent {a.preset} streams, one per core in sched_getaffinity, each timed over "
-                      f"scans {a.preroll + a.warmup}..{a.preroll + a.warmup + n - 1} after an untimed pre-roll "
+    return {"value": round(th * n / secs, 3), "unit": "scans/s", "cores": th, "affinity_cores": ncpu, "kind": "port",
+            "sample": f"(B) {th} independent {a.preset} streams, one per usable core (min of sched_getaffinity "
+                      f"{ncpu} and the cgroup CPU quota {quota}), each timed over "
+                      f"scans {start}..{start + n - 1} after an untimed pre-roll "
                       f"(the GPU's steady-state window); {min(a.cpu_distinct, th)} streams pre-rolled, the rest "
                       f"continue from copies; oracle/ C++ restatement g++ -O2",
             "seconds": round(secs, 2), "wall_seconds_incl_preroll": round(wall, 1),
@@ -379,7 +426,7 @@ def main():
     # contexts as the mapping period the contexts map on different steps
     lag = (lambda g: g) if a.stagger else (lambda g: 0)
     maxlag = max(lag(g) for g in range(len(groups)))
-    nwin = a.warmup + a.steps + a.profile_steps + maxlag
+    nwin = a.profile_steps + a.warmup + a.steps + maxlag
     dev = torch.empty((max(nwin, a.chunk), S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
     gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
@@ -431,9 +478,15 @@ def main():
     gen.close()
     t_gen += time.time() - t1
 
-    def step(k):   # k = index into the resident window; context g processes scan base + lag(g) + k
-        each(lambda g, c, o, n: c.batch_process(dev[k + lag(g), o].data_ptr(), cnt[o].data_ptr(),
-                                                0.1 * (base + lag(g) + k)))
+    def step(k, serial=False):   # k = index into the resident window; context g processes scan base + lag(g) + k
+        if serial:   # instrumented pass: one context at a time, so its kernels have the device alone
+            for g, c in enumerate(ctxs):
+                c.batch_process(dev[k + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
+                                0.1 * (base + lag(g) + k))
+                c.synchronize()
+        else:
+            each(lambda g, c, o, n: c.batch_process(dev[k + lag(g), o].data_ptr(), cnt[o].data_ptr(),
+                                                    0.1 * (base + lag(g) + k)))
         if gather:   # records of every group, then one all-gather after all of them
             evs = []
             for g, c in enumerate(ctxs):
@@ -453,7 +506,38 @@ def main():
             for e in exts[1:]:
                 e.wait_event(done)   # next step's records overwrite rec
 
-    for k in range(a.warmup):
+    # ---- instrumented pass first (scans [0, profile) of the window): per-kernel
+    # HIP-event times on each context's stream, the contexts one after the other
+    # so the events time each kernel alone; it names the dominant kernel, which
+    # is then timed live inside the timed region
+    roof, roof_also, kt, workload, gbs, path = None, None, {}, None, {}, None
+    counts, map_steps = None, 0
+    P0 = a.profile_steps
+    if P0 > 0:
+        for c in ctxs:
+            c.timing(True)
+            c.timing_reset()
+        pw0 = [c.get(0, "pcl_work").astype(np.int64) for c in ctxs]
+        for k in range(P0):
+            step(k, serial=True)
+            sync_all()
+            map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
+        for c in ctxs:
+            for kn, (kms, kcalls) in c.timing_read().items():
+                m0, c0 = kt.get(kn, (0.0, 0))
+                kt[kn] = (m0 + kms, c0 + kcalls)
+            c.timing(False)
+        parts = [stream_counts(c, c.n_streams) for c in ctxs]
+        counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+        counts["pcl_work"] = sum(c.get(0, "pcl_work").astype(np.int64) - w0 for c, w0 in zip(ctxs, pw0))
+        workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1 and k != "pcl_work"}
+    # the largest single kernel by device time (vg_sort:<filter> entries time groups of launches)
+    dominant = max(((kn, v) for kn, v in kt.items() if not kn.startswith("vg_sort:")),
+                   key=lambda kv: kv[1][0])[0] if kt else None
+    rk0 = dominant if a.roofline_kernel == "auto" else a.roofline_kernel
+    rks = ([rk0] if rk0 else []) + [k for k in a.roofline_also.split(",") if k and k != rk0]
+
+    for k in range(P0, P0 + a.warmup):
         step(k)
     sync_all()
     torch.cuda.synchronize()
@@ -462,7 +546,6 @@ def main():
     # the roofline kernels alone are timed inside the timed region: two
     # in-stream device timestamps per launch on its context's stream (captured
     # into the step graphs), nothing else
-    rks = [a.roofline_kernel] + [k for k in a.roofline_also.split(",") if k and k != a.roofline_kernel]
     for c in ctxs:
         c.timing(True)
         c.timing_filter(",".join(rks))
@@ -471,7 +554,7 @@ def main():
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k in range(a.warmup, a.warmup + a.steps):
+    for k in range(P0 + a.warmup, P0 + a.warmup + a.steps):
         step(k)
     sync_all()
     torch.cuda.synchronize()
@@ -489,46 +572,23 @@ def main():
                 live[kn][1] += kcalls
         c.timing(False)
         c.timing_filter(None)
-    live_ms, live_n = live[a.roofline_kernel]
     value = S * a.steps * world / el
     errs = sum(int(c.get(s, "err")[0]) != 0 for c in ctxs for s in range(c.n_streams))
     kfs = np.array([int(c.get(s, "n_keyframes")[0]) for c in ctxs for s in range(c.n_streams)])
 
-    # ---- instrumented pass: per-kernel HIP-event times on each context's
-    # stream, groups run one after the other so the events time each kernel alone
-    roof, roof_also, kt, workload, gbs = None, None, {}, None, {}
-    if a.profile_steps > 0:
-        for c in ctxs:
-            c.timing(True)
-            c.timing_reset()
-        k0 = a.warmup + a.steps
-        map_steps = 0
-        for k in range(k0, k0 + a.profile_steps):
-            for g, c in enumerate(ctxs):
-                c.batch_process(dev[k + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
-                                0.1 * (base + lag(g) + k))
-                c.synchronize()
-            map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
-        for c in ctxs:
-            for kn, (kms, kcalls) in c.timing_read().items():
-                m0, c0 = kt.get(kn, (0.0, 0))
-                kt[kn] = (m0 + kms, c0 + kcalls)
-            c.timing(False)
-        parts = [stream_counts(c, c.n_streams) for c in ctxs]
-        counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
-        workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1}
+    if counts is not None:
         total_ms = sum(v[0] for kn, v in kt.items() if not kn.startswith("vg_sort:"))   # groups double count
-        name, (ms, n) = max(kt.items(), key=lambda kv: kv[1][0])
         for kn, (kms, kcalls) in kt.items():
-            kb = algo_bytes(kn, counts, cfg, S, a.profile_steps, map_steps)
+            kb = algo_bytes(kn, counts, cfg, S, P0, map_steps)
             if kb is not None and kms > 0:
                 gbs[kn] = round(kb / (kms / 1e3) / 1e9, 1)
+
         # achieved = algorithmic bytes per launch (instrumented pass, same
         # launch mix) / the average launch time inside the timed region,
         # where the contexts' kernels share the device
         def roof_of(rk):
             rms, rn = kt.get(rk, (0.0, 0))
-            rb = algo_bytes(rk, counts, cfg, S, a.profile_steps, map_steps)
+            rb = algo_bytes(rk, counts, cfg, S, P0, map_steps)
             bpl = rb / rn if (rb is not None and rn) else None
             lms, ln = live.get(rk, (0.0, 0))
             live_s = lms / 1e3 / ln if ln else None
@@ -546,16 +606,23 @@ def main():
                                  "note": "instrumented steps, contexts one after the other"},
                     "share_of_device_time": round(rms / total_ms, 4) if total_ms else None}
 
-        # the largest single kernel (vg_sort:<filter> entries time groups of launches)
-        name = max(((kn, v) for kn, v in kt.items() if not kn.startswith("vg_sort:")), key=lambda kv: kv[1][0])[0]
-        roof = roof_of(a.roofline_kernel)
-        roof["largest_kernel"] = name
-        roof_also = {rk: roof_of(rk) for rk in rks[1:]}
-
-    elif live_n:   # no instrumented pass: the live launch time alone (no byte counts)
+        roof = roof_of(rks[0])
+        roof["largest_kernel"] = dominant
+        roof_also = {rk: roof_of(rk) for rk in rks[1:] if rk in kt}
+        # the whole path: per-scan algorithmic bytes from the
+        # logged counts, the mapping share from the instrumented pass, over the
+        # timed window's wall time
+        fb, mb = path_bytes(counts, cfg, a.history)
+        per_step = fb + mb * map_steps / P0
+        ach = per_step * a.steps * world / el / 1e9
+        roof["path"] = {"achieved": round(ach, 2), "unit": "GB/s", "bytes_per_step": int(per_step),
+                        "frac_of_measured_copy_6290": round(ach / 6290.0, 5),
+                        "frac_of_spec_8000": round(ach / 8000.0, 5), "mapping_share": round(map_steps / P0, 3),
+                        "note": "SURVEY §8(d) per-scan formula on the logged counts (last instrumented step's sizes)"}
+    elif rks and live.get(rks[0], [0, 0])[1]:   # no instrumented pass: the live launch time alone (no byte counts)
+        lms, ln = live[rks[0]]
         roof = {"bound": "hbm", "achieved": None, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "kernel": a.roofline_kernel,
-                "avg_launch_us": round(live_ms / live_n * 1e3, 2), "launches_timed": live_n}
+                "traffic": None, "kernel": rks[0], "avg_launch_us": round(lms / ln * 1e3, 2), "launches_timed": ln}
     for c in ctxs:
         c.close()
     ctxs = []
@@ -579,7 +646,7 @@ def main():
     # ---- CPU baseline (oracle = C++ restatement of the reference), rank 0, N = 1
     cpu = None
     if rank == 0 and world == 1 and a.cpu_scans > 0:
-        cpu = cpu_baseline(a, pid, ncpu)
+        cpu = cpu_baseline(a, pid, ncpu, a.preroll + P0 + a.warmup)
 
     if rank == 0:
         out = {
@@ -591,7 +658,8 @@ def main():
                        "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
                        "scans_per_step": S * world, "preroll_scans": a.preroll,
                        "context_phase_lag": [lag(g) for g in range(n_ctx)],
-                       "timed_scans": [base + a.warmup, base + a.warmup + a.steps - 1],
+                       "timed_scans": [base + P0 + a.warmup, base + P0 + a.warmup + a.steps - 1],
+                       "voxel_order": "pcl std::sort (reference)" if a.voxel_order == 0 else "stable",
                        "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
                        "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),
                        "sc_history_seed": a.history,

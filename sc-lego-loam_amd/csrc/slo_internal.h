@@ -467,7 +467,7 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
     size_t items = 0, tiles = 0;
     int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries, pair chunks)
     int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
-    unsigned long long* pstat = nullptr;   // [16] SLO_PCL_STATS builds: finish ranges / items / levels per tier
+    unsigned long long* pstat = nullptr;   // [16] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
     PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level

@@ -48,9 +48,12 @@ using slo_pcl::u64;
 #define PC_ST 2048        // small finish entries (<= PC_ST items): 512-thread workgroups
 #define PC_WT 512         // smallest finish entries (<= PC_WT items): 128-thread workgroups
 #define PC_G 2048         // workgroups of the grid-stride level kernels
-#ifndef SLO_PCL_STATS
-#define SLO_PCL_STATS 0   // 1: count finish ranges, items and levels (PclWs::pstat, slo_get "pcl_stats")
-#endif
+// PclWs::pstat, cumulative work counters (slo_get "pcl_work"; the bench
+// prices the kernels' algorithmic bytes with them): [0] items of the ranges
+// stepped by the global levels, [1] pairs they swapped, [2..4] items of
+// finish lists 0..2, [5] VoxelGrid input points, [6] finish entries, [7]
+// block-tier levels they ran
+enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_LEVELS = 7 };
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB, pc0; };
@@ -117,7 +120,8 @@ __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, 
 
 // per stream: tile prefix of the finite counts, and the stream's first range
 __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
-                                                  PSeg* seg0, int* cseg0, PcLists wl, int* ctr, int32_t* nfin) {
+                                                  PSeg* seg0, int* cseg0, PcLists wl, int* ctr, int32_t* nfin,
+                                                  unsigned long long* pst) {
     __shared__ int wsum[16];
     __shared__ int slot_c0[2];
     const int s = blockIdx.x, tid = threadIdx.x;
@@ -137,6 +141,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgPa
     const int f = off[s], n = total;
     if (tid == 0) {
         nfin[s] = n;
+        atomicAdd(&pst[PW_INPUT], (unsigned long long)(off[s + 1] - off[s]));
         slot_c0[0] = -1;
         // overflow keys are the positions: already in order
         if (!p.overflow && n >= 2) {
@@ -235,7 +240,7 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lcount(const unsigned int* K, cons
 
 // per range: pivot record, chunk prefixes, m, pair chunks
 __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const PSeg* seg, int2* ccnt, PRes* res,
-                                                     int* pseg, int* ctr, int cur) {
+                                                     int* pseg, int* ctr, int cur, unsigned long long* pst) {
     __shared__ unsigned int wsum[PC_CT / 64];
     __shared__ int cstar_s, mx_s, pc0_s;
     if (blockIdx.x == 0 && threadIdx.x == 0) { ctr[PCC_NSEG + (cur ^ 1)] = 0; ctr[PCC_NCH + (cur ^ 1)] = 0; }
@@ -313,6 +318,8 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const
             const int npc = (m + PC_PCH - 1) / PC_PCH;
             pc0_s = npc ? atomicAdd(&ctr[PCC_NPC + cur], npc) : 0;
             res[s] = PRes{piv, vmed, med, m, TR, 0x7fffffff, 0x7fffffff, pc0_s};
+            atomicAdd(&pst[PW_ACTIVE], (unsigned long long)(g.l - g.f));
+            atomicAdd(&pst[PW_PAIRS], (unsigned long long)m);
         }
         __syncthreads();
         const int npc = (m + PC_PCH - 1) / PC_PCH;
@@ -452,9 +459,11 @@ __global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int*
         for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
         const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm);
-#if SLO_PCL_STATS
-        if (threadIdx.x == 0) { atomicAdd(&pst[3 * list], 1ull); atomicAdd(&pst[1 + 3 * list], (unsigned long long)n); atomicAdd(&pst[2 + 3 * list], (unsigned long long)lv); }
-#endif
+        if (threadIdx.x == 0) {
+            atomicAdd(&pst[PW_FIN + list], (unsigned long long)n);
+            atomicAdd(&pst[PW_ENTRIES], 1ull);
+            atomicAdd(&pst[PW_LEVELS], (unsigned long long)lv);
+        }
         for (int i = threadIdx.x; i < n; i += NT) {
             const u64 it = items[i];
             K[f + i] = (unsigned int)(it >> 32);
@@ -560,7 +569,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
                w.ctr);
     SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
-               w.ctr, w.nfin);
+               w.ctr, w.nfin, w.pstat);
     SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
     const int G = pcl_levels(in_stride);
@@ -572,7 +581,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
         SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(GG), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.ctr, cur);
         SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(GS), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.pseg,
-                   w.ctr, cur);
+                   w.ctr, cur, w.pstat);
         SLO_LAUNCH(ctx, "pc_lrank", k_pc_lrank, dim3(GG), dim3(PC_CT), 0, K, V, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.res, PA, PB, w.ctr, cur);
         SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(GG), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,

@@ -44,7 +44,7 @@ _DT["loop"] = LOOP_DTYPE
 _DT["imu"] = np.float64
 _DT["vg_in"] = np.int32
 _DT["vg_stats"] = np.int32
-_DT["pcl_stats"] = np.uint64
+_DT["pcl_work"] = np.uint64
 
 
 class SloError(RuntimeError):

@@ -59,12 +59,12 @@ def main():
                 run()
             ctx.synchronize()
             t = ctx.timing_read()
-            st = ctx.get(0, "pcl_stats").tolist()
+            st = ctx.get(0, "pcl_work").tolist()
             ctx.close()
             res[f"{name}_vo{vo}"] = {"wall_ms": round(wall, 3), "items": S * n,
                                      "kernels_ms": {k: round(v[0] / a.reps, 3) for k, v in
                                                     sorted(t.items(), key=lambda kv: -kv[1][0])[:12]},
-                                     "pcl_stats": st}
+                                     "pcl_work": st}
             print(name, vo, json.dumps(res[f"{name}_vo{vo}"]), flush=True)
     print(json.dumps(res))
 
