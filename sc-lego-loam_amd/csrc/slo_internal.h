@@ -465,16 +465,15 @@ struct PSeg;
 struct PRes;
 struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the input strides only
     size_t items = 0, tiles = 0;
-    int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries, pair chunks)
+    int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries)
     int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
     unsigned long long* pstat = nullptr;   // [16] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
     PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level
-    PRes* res = nullptr;          // per range of the current level: pivot, m, cuts, pair chunks
+    PRes* res = nullptr;          // per range of the current level: pivot, m, cuts
     int* cseg[2] = {nullptr, nullptr};     // chunk -> range
     int2* ccnt = nullptr;         // per chunk stopper counts -> prefixes
-    int* pseg = nullptr;          // pair chunk -> range
     int2* wl = nullptr;           // finish entries (f, size | depth << 24): four lists by size
     size_t wcap0 = 0, wcapk = 0;  // capacity of list 0 and of lists 1..3
     int* tcnt = nullptr;          // [S][maxT] finite points per tile -> prefixes

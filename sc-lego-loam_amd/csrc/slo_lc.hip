@@ -30,7 +30,6 @@
 // transforms bit for bit.
 #include "slo_internal.h"
 #include "slo_libm.h"
-#include <hipcub/hipcub.hpp>
 #include <float.h>
 #include <limits.h>
 

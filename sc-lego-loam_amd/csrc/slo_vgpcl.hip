@@ -19,7 +19,7 @@
 //     k_pc_lcount  per chunk of PC_CH positions: stopper counts (the median of
 //                  three is taken virtually: every chunk derives it alone);
 //     k_pc_lscan   per range: chunk prefixes, m from the chunk where the
-//                  left / right counts cross, the pair chunks;
+//                  left / right counts cross;
 //     k_pc_lrank   per chunk: the positions of the left stoppers of rank < m
 //                  and of the right stoppers of rank < m (from the right), the
 //                  cut candidates; chunk 0 makes the median swap real;
@@ -42,7 +42,6 @@ using slo_pcl::u64;
 
 #define PC_CH 4096        // positions per chunk of the global levels (256 threads x 16)
 #define PC_CT 256
-#define PC_PCH 4096       // pairs per pair chunk
 #define PC_T 4096         // a range of at most PC_T items is finished in LDS
 #define PC_FT 1024        // threads of the big finish workgroup (4 positions each)
 #define PC_ST 2048        // small finish entries (<= PC_ST items): 512-thread workgroups
@@ -52,14 +51,14 @@ using slo_pcl::u64;
 // prices the kernels' algorithmic bytes with them): [0] items of the ranges
 // stepped by the global levels, [1] pairs they swapped, [2..4] items of
 // finish lists 0..2, [5] VoxelGrid input points, [6] finish entries, [7]
-// block-tier levels they ran
+// block-tier levels they ran; [8..15] finish phase cycles (k_pc_finish)
 enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_LEVELS = 7 };
 
 struct PSeg { int f, l, d, c0; };
-struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB, pc0; };
+struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
 
 // counters (PclWs::ctr)
-enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NPC = 4, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: finish list k
+enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: finish list k
 
 // Finish entries by size class: list 0 <= PC_WT items (k_pc_finish<128>), 1 <= PC_ST (k_pc_finish<512>), 2 <= PC_T (k_pc_finish<PC_FT>), 3
 // larger (the global fallback).  An entry is (first position, size | depth << 24).
@@ -70,24 +69,12 @@ __device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) 
     L.l[k][i] = make_int2(f, n | (d << 24));
 }
 
-// libstdc++ __move_median_to_first on the keys at f+1, mid, l-1: which of
-// them (0, 1, 2) is swapped to f
-__device__ inline int median3(unsigned int a, unsigned int b, unsigned int c) {
-    if (a < b) {
-        if (b < c) return 1;
-        if (a < c) return 2;
-        return 0;
-    }
-    if (a < c) return 0;
-    if (b < c) return 2;
-    return 1;
-}
 // the pivot of range [f, l), the position swapped with f, and the key that
 // lands there (the one at f)
 __device__ inline void pc_median(const unsigned int* K, int f, int l, unsigned int& piv, int& med, unsigned int& vmed) {
     const int pos[3] = {f + 1, f + (l - f) / 2, l - 1};
     const unsigned int k0 = K[pos[0]], k1 = K[pos[1]], k2 = K[pos[2]], kf = K[f];
-    const int w = median3(k0, k1, k2);
+    const int w = slo_pcl::median3(k0, k1, k2);
     med = pos[w];
     piv = w == 0 ? k0 : (w == 1 ? k1 : k2);
     vmed = kf;
@@ -210,7 +197,6 @@ __device__ inline void pc_chunk(const PSeg& g, int c, int& a, int& b) {
 
 __global__ void __launch_bounds__(PC_CT) k_pc_lcount(const unsigned int* K, const PSeg* seg, const int* cseg,
                                                       int2* ccnt, int* ctr, int cur) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr[PCC_NPC + cur] = 0;   // pair chunks of this level (k_pc_lscan)
     __shared__ unsigned int wsum[PC_CT / 64];
     const int nch = ctr[PCC_NCH + cur];
     for (int c = blockIdx.x; c < nch; c += gridDim.x) {
@@ -238,11 +224,12 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lcount(const unsigned int* K, cons
     }
 }
 
-// per range: pivot record, chunk prefixes, m, pair chunks
+// per range: pivot record, chunk prefixes, m
 __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const PSeg* seg, int2* ccnt, PRes* res,
-                                                     int* pseg, int* ctr, int cur, unsigned long long* pst) {
+                                                     int* ctr, int cur, unsigned long long* pst) {
     __shared__ unsigned int wsum[PC_CT / 64];
-    __shared__ int cstar_s, mx_s, pc0_s;
+    __shared__ int cstar_s, mx_s;
+    unsigned long long wact = 0, wpairs = 0;   // work counters, one atomic per block
     if (blockIdx.x == 0 && threadIdx.x == 0) { ctr[PCC_NSEG + (cur ^ 1)] = 0; ctr[PCC_NCH + (cur ^ 1)] = 0; }
     const int ns = ctr[PCC_NSEG + cur];
     const int tid = threadIdx.x;
@@ -315,16 +302,15 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const
         __syncthreads();
         const int m = mx_s;
         if (tid == 0) {
-            const int npc = (m + PC_PCH - 1) / PC_PCH;
-            pc0_s = npc ? atomicAdd(&ctr[PCC_NPC + cur], npc) : 0;
-            res[s] = PRes{piv, vmed, med, m, TR, 0x7fffffff, 0x7fffffff, pc0_s};
-            atomicAdd(&pst[PW_ACTIVE], (unsigned long long)(g.l - g.f));
-            atomicAdd(&pst[PW_PAIRS], (unsigned long long)m);
+            res[s] = PRes{piv, vmed, med, m, TR, 0x7fffffff, 0x7fffffff};
+            wact += (unsigned long long)(g.l - g.f);
+            wpairs += (unsigned long long)m;
         }
-        __syncthreads();
-        const int npc = (m + PC_PCH - 1) / PC_PCH;
-        for (int i = tid; i < npc; i += PC_CT) pseg[pc0_s + i] = s;
         __syncthreads();   // shared scalars reused by the next range
+    }
+    if (tid == 0 && wact) {
+        atomicAdd(&pst[PW_ACTIVE], wact);
+        atomicAdd(&pst[PW_PAIRS], wpairs);
     }
 }
 
@@ -395,81 +381,147 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned in
     }
 }
 
-__global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int* V, const PSeg* seg, const PRes* res,
-                                                    const int* pseg, const unsigned int* PA, const unsigned int* PB,
+// the swaps: chunk c of a range takes the pair ranks [(c - c0) PC_CH, + PC_CH)
+// (m < the range's size); a wave per chunk, each lane's four pairs loaded
+// before any is written (the pairs are disjoint)
+__global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
+                                                    const PRes* res, const unsigned int* PA, const unsigned int* PB,
                                                     const int* ctr, int cur) {
-    const int npc = ctr[PCC_NPC + cur];
-    for (int pc = blockIdx.x; pc < npc; pc += gridDim.x) {
-        const int si = pseg[pc];
-        const PSeg g = seg[si];
-        const PRes r = res[si];
-        const int k0 = (pc - r.pc0) * PC_PCH, k1 = min(r.m, k0 + PC_PCH);
-        for (int k = k0 + (int)threadIdx.x; k < k1; k += 256) {
-            const unsigned int x = PA[g.f + k], y = PB[g.f + k];
-            const unsigned int kx = K[x], vx = V[x], ky = K[y], vy = V[y];
-            K[x] = ky; V[x] = vy; K[y] = kx; V[y] = vx;
+    const int nch = ctr[PCC_NCH + cur];
+    const int lane = threadIdx.x & 63;
+    const int nwv = gridDim.x * 4;
+    for (int c = blockIdx.x * 4 + (int)(threadIdx.x >> 6); c < nch; c += nwv) {
+        const int si = cseg[c];
+        const int f = seg[si].f, c0 = seg[si].c0;
+        const int m = res[si].m;
+        const int k0 = (c - c0) * PC_CH, k1 = min(m, k0 + PC_CH);
+        for (int k = k0 + lane; k < k1; k += 256) {
+            unsigned int x[4], y[4], kx[4], vx[4], ky[4], vy[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int kk = f + min(k + 64 * u, k1 - 1);
+                x[u] = PA[kk];
+                y[u] = PB[kk];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                kx[u] = K[x[u]]; vx[u] = V[x[u]];
+                ky[u] = K[y[u]]; vy[u] = V[y[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (k + 64 * u < k1) {
+                    K[x[u]] = ky[u]; V[x[u]] = vy[u];
+                    K[y[u]] = kx[u]; V[y[u]] = vx[u];
+                }
         }
     }
 }
 
+// the halves of every range, a thread per range: the block's new ranges,
+// chunks and finish entries are counted by block scans and claimed with one
+// atomic per counter (the device-wide counters live in memory shared by all
+// XCDs: an atomic per range serialises there)
 __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* res, PSeg* nseg, int* ncseg,
                                                     PcLists wl, int* ctr, int cur, int last) {
-    __shared__ int slot_s[2], c0_s[2], nch_s[2];
+    __shared__ unsigned int wsum[4];
+    __shared__ int base_s[6];
     const int ns = ctr[PCC_NSEG + cur];
-    for (int s = blockIdx.x; s < ns; s += gridDim.x) {
-        const PSeg g = seg[s];
-        const PRes r = res[s];
-        if (threadIdx.x == 0) {
+    for (int s0 = blockIdx.x * 256; s0 < ns; s0 += gridDim.x * 256) {
+        const int s = s0 + (int)threadIdx.x;
+        int lo[2] = {0, 0}, hi[2] = {0, 0}, kind[2] = {-1, -1}, nch[2] = {0, 0}, D = 0;
+        if (s < ns) {
+            const PSeg g = seg[s];
+            const PRes r = res[s];
             const int cut = min(r.cutA, r.m > 0 ? r.cutB : 0x7fffffff);
-            const int D = g.d - 1;
-            const int lo[2] = {g.f, cut}, hi[2] = {cut, g.l};
+            D = g.d - 1;
+            lo[0] = g.f; hi[0] = cut; lo[1] = cut; hi[1] = g.l;
+#pragma unroll
             for (int h = 0; h < 2; ++h) {
-                slot_s[h] = -1;
                 const int n = hi[h] - lo[h];
                 if (n <= 1) continue;
                 if (n > PC_T && D > 0 && !last) {
-                    const int nch = (n - 1 + PC_CH - 1) / PC_CH;
-                    slot_s[h] = atomicAdd(&ctr[PCC_NSEG + (cur ^ 1)], 1);
-                    c0_s[h] = atomicAdd(&ctr[PCC_NCH + (cur ^ 1)], nch);
-                    nch_s[h] = nch;
-                    nseg[slot_s[h]] = PSeg{lo[h], hi[h], D, c0_s[h]};
+                    kind[h] = 4;
+                    nch[h] = (n - 1 + PC_CH - 1) / PC_CH;
                 } else {
-                    pc_push(wl, ctr, lo[h], n, D);
+                    kind[h] = n <= PC_WT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
                 }
             }
         }
+        // counts: new ranges | list 0 << 10 | list 1 << 20, list 2 | list 3 << 10, chunks
+        unsigned int ca = 0, cb = 0, cc = (unsigned int)(nch[0] + nch[1]);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (kind[h] == 4) ca += 1u;
+            if (kind[h] == 0) ca += 1u << 10;
+            if (kind[h] == 1) ca += 1u << 20;
+            if (kind[h] == 2) cb += 1u;
+            if (kind[h] == 3) cb += 1u << 10;
+        }
+        unsigned int ta, tb, tc;
+        const unsigned int ea = vg_block_scan<4>(ca, wsum, &ta);
+        const unsigned int eb = vg_block_scan<4>(cb, wsum, &tb);
+        const unsigned int ec = vg_block_scan<4>(cc, wsum, &tc);
+        if (threadIdx.x == 0) {
+            const int tot[6] = {(int)(ta & 1023u), (int)((ta >> 10) & 1023u), (int)(ta >> 20), (int)(tb & 1023u),
+                                (int)(tb >> 10), (int)tc};
+            int* dst[6] = {&ctr[PCC_NSEG + (cur ^ 1)], &ctr[PCC_NW + 0], &ctr[PCC_NW + 1], &ctr[PCC_NW + 2],
+                           &ctr[PCC_NW + 3], &ctr[PCC_NCH + (cur ^ 1)]};
+#pragma unroll
+            for (int q = 0; q < 6; ++q) base_s[q] = tot[q] ? atomicAdd(dst[q], tot[q]) : 0;
+        }
         __syncthreads();
-        for (int h = 0; h < 2; ++h)
-            if (slot_s[h] >= 0)
-                for (int i = threadIdx.x; i < nch_s[h]; i += 256) ncseg[c0_s[h] + i] = slot_s[h];
-        __syncthreads();
+        int o[6] = {base_s[0] + (int)(ea & 1023u), base_s[1] + (int)((ea >> 10) & 1023u), base_s[2] + (int)(ea >> 20),
+                    base_s[3] + (int)(eb & 1023u), base_s[4] + (int)(eb >> 10), base_s[5] + (int)ec};
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int n = hi[h] - lo[h];
+            if (kind[h] == 4) {
+                const int slot = o[0]++, c0 = o[5];
+                o[5] += nch[h];
+                nseg[slot] = PSeg{lo[h], hi[h], D, c0};
+                for (int i = 0; i < nch[h]; ++i) ncseg[c0 + i] = slot;
+            } else if (kind[h] >= 0) {
+                const int i = o[1 + kind[h]]++;
+                wl.l[kind[h]][i] = make_int2(lo[h], n | (D << 24));
+            }
+        }
+        __syncthreads();   // base_s reused
     }
 }
 
 // ---- finish: one workgroup per entry
 template <int NT, int NMAX>
-__global__ void __launch_bounds__(NT) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
+__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
                                                   unsigned long long* pst) {
     __shared__ u64 items[NMAX];
     __shared__ slo_pcl::BlockSmem<NT, NMAX> sm;
     const int nw = ctr[PCC_NW + list];
+    unsigned long long wn = 0, we = 0, wlv = 0, ph[4] = {0, 0, 0, 0};   // work counters, one atomic per block
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
         for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
-        const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm);
-        if (threadIdx.x == 0) {
-            atomicAdd(&pst[PW_FIN + list], (unsigned long long)n);
-            atomicAdd(&pst[PW_ENTRIES], 1ull);
-            atomicAdd(&pst[PW_LEVELS], (unsigned long long)lv);
-        }
+        const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm, ph);
+        wn += (unsigned long long)n;
+        we += 1ull;
+        wlv += (unsigned long long)lv;
         for (int i = threadIdx.x; i < n; i += NT) {
             const u64 it = items[i];
             K[f + i] = (unsigned int)(it >> 32);
             V[f + i] = (unsigned int)it;
         }
         __syncthreads();
+    }
+    if (threadIdx.x == 0 && we) {
+        atomicAdd(&pst[PW_FIN + list], wn);
+        atomicAdd(&pst[PW_ENTRIES], we);
+        atomicAdd(&pst[PW_LEVELS], wlv);
+        if (list) {   // [8..11] list 1, [12..15] list 2: block-tier, wave-tier and leaf cycles, wave ranges
+#pragma unroll
+            for (int q = 0; q < 4; ++q) atomicAdd(&pst[8 + 4 * (list - 1) + q], ph[q]);
+        }
     }
 }
 
@@ -512,12 +564,11 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
     }
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
-        void* old[] = {w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg, w.wl};
+        void* old[] = {w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl};
         for (void* q : old) if (q) hipFree(q);
         w.items = it;
         const size_t segcap = S + it / PC_T + 2;
         const size_t chcap = it / PC_CH + segcap;
-        const size_t pccap = it / 2 / PC_PCH + segcap;
         const size_t wcap0 = it / 2 + S + 2, wcapk = it / PC_WT + S + 2;   // disjoint entries of >= 2 / > PC_WT items
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.pairs, sizeof(u64) * it));
@@ -527,7 +578,6 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.cseg[0], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
-        SLO_CHECK(hipMalloc(&w.pseg, sizeof(int) * pccap));
         SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 3 * wcapk)));
         w.wcap0 = wcap0;
         w.wcapk = wcapk;
@@ -580,13 +630,13 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
         const int GG = lv < 8 ? PC_G : PC_G / 4, GS = PC_G / 4;
         SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(GG), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(GS), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.pseg,
-                   w.ctr, cur, w.pstat);
+        SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(GS), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.ctr, cur,
+                   w.pstat);
         SLO_LAUNCH(ctx, "pc_lrank", k_pc_lrank, dim3(GG), dim3(PC_CT), 0, K, V, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.res, PA, PB, w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(GG), dim3(256), 0, K, V, w.seg[cur], w.res, w.pseg, PA, PB,
+        SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(GG), dim3(256), 0, K, V, w.seg[cur], w.cseg[cur], w.res, PA, PB,
                    w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(GS), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
+        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(std::max(1, GS / 4)), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
                    w.cseg[cur ^ 1], L, w.ctr, cur, (int)(lv == G - 1));
     }
     const int FG = std::max(64, std::min(4096, S * 8));
@@ -600,8 +650,8 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
 
 void pcl_free(slo_ctx* ctx) {
     PclWs& w = ctx->pws;
-    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.pseg,
-                  w.wl, w.tcnt};
+    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl,
+                  w.tcnt};
     for (void* p : ps) if (p) hipFree(p);
     w = PclWs();
 }
