@@ -382,24 +382,22 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned in
 }
 
 // the swaps: chunk c of a range takes the pair ranks [(c - c0) PC_CH, + PC_CH)
-// (m < the range's size); a wave per chunk, each lane's four pairs loaded
-// before any is written (the pairs are disjoint)
+// (m < the range's size); each thread's four pairs are loaded before any is
+// written (the pairs are disjoint)
 __global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
                                                     const PRes* res, const unsigned int* PA, const unsigned int* PB,
                                                     const int* ctr, int cur) {
     const int nch = ctr[PCC_NCH + cur];
-    const int lane = threadIdx.x & 63;
-    const int nwv = gridDim.x * 4;
-    for (int c = blockIdx.x * 4 + (int)(threadIdx.x >> 6); c < nch; c += nwv) {
+    for (int c = blockIdx.x; c < nch; c += gridDim.x) {
         const int si = cseg[c];
         const int f = seg[si].f, c0 = seg[si].c0;
         const int m = res[si].m;
         const int k0 = (c - c0) * PC_CH, k1 = min(m, k0 + PC_CH);
-        for (int k = k0 + lane; k < k1; k += 256) {
+        for (int k = k0 + (int)threadIdx.x; k < k1; k += 1024) {
             unsigned int x[4], y[4], kx[4], vx[4], ky[4], vy[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
-                const int kk = f + min(k + 64 * u, k1 - 1);
+                const int kk = f + min(k + 256 * u, k1 - 1);
                 x[u] = PA[kk];
                 y[u] = PB[kk];
             }
@@ -410,7 +408,7 @@ __global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int
             }
 #pragma unroll
             for (int u = 0; u < 4; ++u)
-                if (k + 64 * u < k1) {
+                if (k + 256 * u < k1) {
                     K[x[u]] = ky[u]; V[x[u]] = vy[u];
                     K[y[u]] = kx[u]; V[y[u]] = vx[u];
                 }
@@ -594,9 +592,13 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
 // global levels for ranges of up to `stride` items: enough that what is left
 // fits the LDS finish.  Measured with tests/cpp/pcl_sort_model.cpp at PC_T =
 // 4096: a C3 raw scan (110 k points, 0.5 m) leaves a range over PC_T for up to
-// 13 levels, the 600 k-point surf map for 16; 2 log2(stride / PC_T) + 10
-// covers both with room (an empty level costs only its five launches).
-// Whatever is still over PC_T then is finished by k_pc_fallback (one lane).
+// 13 levels, the 600 k-point surf map for 16, i.e. median-of-three
+// quicksort's depth runs to ~2 log2(n / PC_T); 2 log2(stride / PC_T) + 10
+// covers both with room (+6 measured too few on the bench's raw scans: the
+// fallback then cost more than the bench's whole sort).  An empty level
+// still costs its five launches.
+// Whatever is still over PC_T then (adversarial inputs) is finished by
+// k_pc_fallback (one lane, correct but slow).
 static int pcl_levels(size_t stride) {
     int g = 0;
     size_t x = PC_T;

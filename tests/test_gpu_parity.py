@@ -78,6 +78,21 @@ def test_c3_steady_state_parity():
     assert len(full) >= 5                                         # detects that searched the tree snapshot
 
 
+def test_c4_os1_64_steady_state():
+    """C4's sensor (OS1-64, 64 x 1024, preset 4) for 240 scans with Scan
+    Context on: the 50-keyframe deque filled and rolling, detects searching
+    the tree snapshot.  Mapping results compared at every mapping step, the
+    front end every 10th scan."""
+    _torch()
+    rep, worst, counts = _run(4, 4, 1, 240, every=10)
+    _assert_clean(rep, worst, counts)
+    kf = [r["n_kf"][1] for r in rep if "n_kf" in r]
+    print(f"C4 OS1-64: {kf[-1]} keyframes, {counts}")
+    assert kf[-1] >= 55                                           # deque full and rolling
+    full = [r for r in rep if "detect_cpu" in r and len(r["detect_cpu"]) >= 3 and r["detect_cpu"][2] == 10]
+    assert len(full) >= 3                                         # detects that searched the tree snapshot
+
+
 def _k50(cfg):
     cfg.sc_num_candidates = 50
 

@@ -3,7 +3,8 @@ oracle's record (bit for bit, descriptor included), the RCCL all-gather of the
 records (a one-rank NCCL group: the N > 1 code path), and the cross-stream
 Scan Context store (slo_xsc) against its oracle restatement — candidate
 stream / keyframe, distance and yaw bit for bit — on two sessions of one
-world (stream 0's first lap and, 590 scans later, its second lap)."""
+world (stream 0's first lap and, 590 scans later, its second lap) — on the
+VLP-16 preset and on C4's OS1-64 64x1024."""
 import os
 import socket
 
@@ -18,7 +19,8 @@ pytestmark = pytest.mark.gpu
 LAG = 590
 
 
-def test_records_allgather_and_cross_session_match():
+@pytest.mark.parametrize("pid,nscans,min_loops", [(0, 64, 3), (4, 64, 3)], ids=["vlp16", "os1_64"])
+def test_records_allgather_and_cross_session_match(pid, nscans, min_loops):
     import torch
     import torch.distributed as dist
     from slo_amd import dist as sdist
@@ -28,7 +30,6 @@ def test_records_allgather_and_cross_session_match():
         port = sk.getsockname()[1]
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
-    pid = 0
     cfg = slo_amd.preset(pid)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, 2)
@@ -42,7 +43,7 @@ def test_records_allgather_and_cross_session_match():
     cnt = torch.full((2,), P, dtype=torch.int32, device="cuda")
     loops = 0
     try:
-        for k in range(64):
+        for k in range(nscans):
             scans = [O.gen_scan(pid, 1, 0, k), O.gen_scan(pid, 1, 0, k + LAG)]
             pts = torch.from_numpy(np.stack(scans)).cuda()
             ctx.batch_process(pts.data_ptr(), cnt.data_ptr(), 0.1 * k)
@@ -65,7 +66,7 @@ def test_records_allgather_and_cross_session_match():
                     assert np.float32(m[q]["yaw"]) == np.float32(of[q, 0]) and \
                         np.float64(m[q]["min_dist"]).tobytes() == of[q, 1].tobytes(), k
             loops += int(oi[1, 4])
-        assert loops >= 3   # session B closes loops against session A
+        assert loops >= min_loops   # session B closes loops against session A
     finally:
         xs.close()
         ctx.close()
