@@ -693,9 +693,9 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
     }
     else if (name == "pcl_work") {   // PCL-order sort work counters, cumulative (slo_vgpcl.hip PW_*)
-        unsigned long long a[16] = {0};
+        unsigned long long a[32] = {0};
         if (ctx->pws.pstat) SLO_CHECK(hipMemcpy(a, ctx->pws.pstat, sizeof(a), hipMemcpyDeviceToHost));
-        tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 16; esz = 8;
+        tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 32; esz = 8;
     }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
     else if (name == "imu") {   // FA's IMU scalars (slo::ImuState), as float64

@@ -740,8 +740,8 @@ __device__ inline void ring_sort_regs(unsigned long long* lds, KF&& key_of) {
     __syncthreads();
 }
 
-// PMAX: the largest ring the PCL-order sort takes (the horizon_scan bound)
-template <int PMAX>
+// the stable in-voxel order (cfg.voxel_order == SLO_VOXEL_STABLE): one
+// workgroup per ring, a bitonic sort of (voxel, index) keys
 __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     const int s = blockIdx.y, ring = blockIdx.x;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
@@ -793,18 +793,7 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
         const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
         return (((unsigned long long)idx << 32) | (unsigned int)i) | (0ull - (unsigned long long)(i >= n));
     };
-    if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // std::sort's order, as PCL (slo_pclsort.h)
-        // one LDS area for the instance the ring's size picks (each a smaller struct than the largest)
-        __shared__ __attribute__((aligned(16))) char pbuf[sizeof(slo_pcl::BlockSmem<256, PMAX>)];
-        for (int i = threadIdx.x; i < n; i += blockDim.x) keys[i] = key_of(i);
-        __syncthreads();
-        const int d = 2 * slo_pcl::lg2(n);
-        if (n <= 256) slo_pcl::pcl_block_sort<256, 256>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 256>*>(pbuf));
-        else if (n <= 512) slo_pcl::pcl_block_sort<256, 512>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 512>*>(pbuf));
-        else if (n <= 1024) slo_pcl::pcl_block_sort<256, 1024>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 1024>*>(pbuf));
-        else if (n <= 2048 || PMAX == 2048) slo_pcl::pcl_block_sort<256, 2048>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, 2048>*>(pbuf));
-        else slo_pcl::pcl_block_sort<256, PMAX>(keys, n, d, *reinterpret_cast<slo_pcl::BlockSmem<256, PMAX>*>(pbuf));
-    } else if (n <= 256) ring_sort_regs<1>(keys, key_of);
+    if (n <= 256) ring_sort_regs<1>(keys, key_of);
     else if (n <= 512) ring_sort_regs<2>(keys, key_of);
     else if (n <= 1024) ring_sort_regs<4>(keys, key_of);
     else if (n <= 2048) ring_sort_regs<8>(keys, key_of);
@@ -896,6 +885,104 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
     if (threadIdx.x == T - 1) v.ring_cnt[rr * 4 + 3] = scan[T - 1];
 }
 
+// PCL's own in-voxel order (cfg.voxel_order == SLO_VOXEL_PCL, the default):
+// one wave per ring (FA:779-780).  The bounds, the (voxel, index) keys in
+// LDS, std::sort's order by slo_pcl::wave_sort, then the voxel heads and the
+// centroids summed in that order.  PMAX: the longest ring (horizon_scan bound).
+#ifndef RING_TLANE
+#define RING_TLANE 64
+#endif
+template <int PMAX>
+__global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
+    const int s = blockIdx.y, ring = blockIdx.x, lane = threadIdx.x;
+    const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
+    const size_t rr = (size_t)s * R + ring;
+    const int n = v.r_lf_n[rr];
+    const float4* in = v.r_lf_scan + rr * C;
+    float4* out = v.r_lf_ds + rr * C;
+    __shared__ unsigned long long keys[PMAX];
+    __shared__ unsigned short tbl[PMAX];
+    __shared__ slo_pcl::WaveSmem ws;
+    __shared__ int serr;
+    if (n == 0) {
+        if (lane == 0) v.ring_cnt[rr * 4 + 3] = 0;
+        return;
+    }
+    const float inv = 1.0f / v.cfg.leaf_less_flat;
+    float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
+    for (int b = 0; b < n; b += 8 * 64) {   // eight loads in flight per lane
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * 64 + lane, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            mnx = fminf(mnx, pp[u].x); mny = fminf(mny, pp[u].y); mnz = fminf(mnz, pp[u].z);
+            mxx = fmaxf(mxx, pp[u].x); mxy = fmaxf(mxy, pp[u].y); mxz = fmaxf(mxz, pp[u].z);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        mnx = fminf(mnx, __shfl_xor(mnx, o, 64)); mny = fminf(mny, __shfl_xor(mny, o, 64));
+        mnz = fminf(mnz, __shfl_xor(mnz, o, 64)); mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
+        mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64)); mxz = fmaxf(mxz, __shfl_xor(mxz, o, 64));
+    }
+    const long long dx = (long long)((mxx - mnx) * inv) + 1, dy = (long long)((mxy - mny) * inv) + 1,
+                    dz = (long long)((mxz - mnz) * inv) + 1;
+    if (dx * dy * dz > 2147483647LL) {  // PCL: integer indices would overflow -> output = input
+        for (int i = lane; i < n; i += 64) out[i] = in[i];
+        if (lane == 0) v.ring_cnt[rr * 4 + 3] = n;
+        return;
+    }
+    const int minbx = (int)floorf(mnx * inv), minby = (int)floorf(mny * inv), minbz = (int)floorf(mnz * inv);
+    const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
+    const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
+    const int mul1 = divx, mul2 = divx * divy;
+    for (int b = 0; b < n; b += 8 * 64) {
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * 64 + lane, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = b + u * 64 + lane;
+            const int ijk0 = (int)(floorf(pp[u].x * inv) - (float)minbx);
+            const int ijk1 = (int)(floorf(pp[u].y * inv) - (float)minby);
+            const int ijk2 = (int)(floorf(pp[u].z * inv) - (float)minbz);
+            const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
+            if (i < n) keys[i] = ((unsigned long long)idx << 32) | (unsigned int)i;
+        }
+    }
+    if (lane == 0) serr = 0;
+    slo_pcl::wave_fence();
+    slo_pcl::wave_sort<RING_TLANE>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, &serr);
+    if (lane == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
+    // voxel heads: a lane per contiguous chunk, ranks by a wave scan
+    const int chunk = (n + 63) / 64;
+    const int i0 = min(n, lane * chunk), i1 = min(n, i0 + chunk);
+    int heads = 0;
+    for (int i = i0; i < i1; ++i) heads += (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32));
+    int incl = heads;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    int rank = incl - heads;
+    for (int i = i0; i < i1; ++i) {   // each voxel that starts in the chunk, summed in the sorted order
+        if (!(i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32))) continue;
+        const unsigned int vid = (unsigned int)(keys[i] >> 32);
+        float sx = 0, sy = 0, sz = 0, si = 0;
+        int e = i;
+        while (e < n && (unsigned int)(keys[e] >> 32) == vid) {
+            const float4 p = in[(unsigned int)keys[e]];
+            sx += p.x; sy += p.y; sz += p.z; si += p.w;
+            ++e;
+        }
+        const float cnt = (float)(e - i);
+        out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+    }
+    if (lane == 63) v.ring_cnt[rr * 4 + 3] = incl;
+}
+
 // concatenate per-ring outputs in ring order: one block per (ring, stream),
 // each summing the counts of the rings before its own
 __global__ void __launch_bounds__(256) k_fa_gather(DevView v) {
@@ -949,12 +1036,15 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
-    int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
-    while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
-    if (v.cfg.horizon_scan <= 2048) {
-        SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds<2048>, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
-    } else {   // the PCL-order ring sort holds up to 4096 points (slo_create refuses wider rings)
-        SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds<4096>, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
+    if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // one wave per ring; slo_create refuses rings over 4096 points
+        if (v.cfg.horizon_scan <= 2048)
+            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<2048>, dim3(R, S), dim3(64), 0, v);
+        else
+            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<4096>, dim3(R, S), dim3(64), 0, v);
+    } else {
+        int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
+        while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
+        SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
     }
     SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());

@@ -256,6 +256,7 @@ struct DevView {
 #define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
 #define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud
 #define SLO_ERR_INPUT 8         // slo_batch_pc2_unpack: a message exceeded max_points
+#define SLO_ERR_SORT 16         // PCL-order ring sort: an inconsistent step (slo_pclsort.h wave_sort; never expected)
 
 // Locality-preserving bucket of cell (x, y, z): x-adjacent cells get adjacent
 // buckets, so a ring walk reads each row of cells' bucket words from one cache
@@ -467,7 +468,7 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
     size_t items = 0, tiles = 0;
     int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries)
     int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
-    unsigned long long* pstat = nullptr;   // [16] cumulative work counters (slo_vgpcl.hip PW_*)
+    unsigned long long* pstat = nullptr;   // [32] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
     PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level

@@ -6,8 +6,8 @@
 // voxel index only, and sums each voxel's points in the order that leaves.
 // std::sort is not stable, so that order — and with it every centroid's
 // float sum — is whatever libstdc++'s introsort makes of the input order.
-// This header computes exactly that order with a workgroup instead of one
-// thread.
+// This header computes exactly that order for a range of up to 4097 items
+// with one wave (wave_sort) or a few (block_sort).
 //
 // The formulation (checked against the host std::sort by
 // tests/cpp/pcl_sort_model.cpp).  One introsort step on [f, l), size > 16,
@@ -23,16 +23,29 @@
 // the final insertion sort.  Every quantity depends only on the flags of the
 // range as it stood before the step: a step is two scans and one swap pass.
 //
-// Here (pcl_block_sort): the items of one range sit in LDS as 64-bit words
-// (voxel index << 32 | point index); all ranges of a level over 16 items are
-// stepped together by the whole workgroup (ballot prefixes of the left /
-// right stoppers, per-range prefixes at the range ends, m where the left
-// and right counts cross, a position table of the right stoppers by rank,
-// the swaps).  A range of <= 16 items is a leaf: the final insertion sort makes it the
-// stable order of its items, so every item's place is its rank in the leaf by
-// (key, position) — one lane per item.  A range whose depth budget is spent
-// (only adversarial inputs) is heapsorted by one lane (slo_sort::heap_sort_,
-// the restated libstdc++ heap).
+// wave_sort: the items of the range sit in LDS as 64-bit words (voxel index
+// << 32 | point index).  The wave walks the introsort recursion depth first
+// (an explicit stack of right halves; disjoint ranges are independent, so the
+// order of the walk does not change the result) and takes each step with all
+// 64 lanes:
+//   * a range of more than 129 items: stream_step — rows of 64 positions are
+//     streamed from LDS three times (stopper counts per row, kept one per lane
+//     of a register; the right stoppers that swap, by rank, into a table; the
+//     left stoppers' swaps), about 30 instructions per row and step;
+//   * 17..129 items (when TLANE is below that): wave_step, the rows held in
+//     registers across the step;
+//   * at most TLANE items, or a spent depth budget: a lane task.  Tasks queue
+//     up and 64 of them run at once, one per lane, through the sequential
+//     libstdc++ restatement (slo_sort::introsort_range: the rest of the
+//     introsort loop, heapsort when the budget is spent, and the final
+//     insertion sort restricted to the range, which is all the global final
+//     insertion sort does to it).  That replaces the many small steps at the
+//     bottom of the recursion, where a wave-wide step would leave most lanes
+//     idle.
+// A full stack hands the range to a lane task (exact), a step whose cut falls
+// outside (f, l) — impossible for a correct step — as well (then sorted but not
+// necessarily in std::sort's order, instead of a hang); both count in *err,
+// which the callers report and the tests require to stay 0.
 #pragma once
 
 #include "slo_introsort.h"
@@ -52,28 +65,19 @@ __host__ __device__ inline int lg2(int n) {
     return r;
 }
 
-constexpr unsigned short kNone = 0xffff;
+constexpr int kQ = 64;        // lane tasks per flush
+constexpr int kStack = 64;    // wave stack entries (the depth budget, <= 62, bounds the stack)
 
-constexpr unsigned char kDone = 0xff;
-constexpr unsigned char kHeap = 0xff;
-constexpr unsigned char kWave = 0xfe;   // the position's range went to the wave tier
-constexpr int kWaveMax = 128;           // ranges of at most this many items go to the wave tier
+// per-wave LDS besides the items: the stack and the lane-task queue
+struct WaveSmem {
+    unsigned int stk[kStack];
+    unsigned int q[kQ];
+};
 
-// ---- wave tier: one wave takes a range of at most kWaveMax items to the
-// end (its introsort steps, heapsorts and leaves) with no workgroup barrier.
-// Control flow is wave-uniform throughout (every lane runs every step), so
-// the cross-lane reductions see all 64 lanes.  LDS operations of one wave
-// complete in order; the fences keep the compiler from reordering them.
 __device__ __forceinline__ void wave_fence() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-}
-
-__device__ __forceinline__ int wave_max(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
-    return v;
 }
 
 __device__ __forceinline__ int lane_prefix(unsigned long long b) {   // set bits of b below this lane
@@ -93,12 +97,17 @@ __host__ __device__ inline int median3(unsigned int a, unsigned int b, unsigned 
     return 1;
 }
 
-// one introsort step of [f, l) (l - f - 1 <= 64 R): the formulation of the
-// header comment with the range's positions f + 1 + 64 r + lane in R rows.
-// The median swap is taken virtually while the rows are read (one LDS round
-// trip), m comes from the ballot of the crossing and two lane reads, and the
-// LDS sees the median swap, the right-stopper table, its reads, the partner
-// reads and the swaps: five dependent steps.  Returns the cut.
+// range encoding of the stack and the queue: first | end << 13 | depth << 26
+__device__ __forceinline__ unsigned int renc(int f, int l, int d) {
+    return (unsigned int)f | ((unsigned int)l << 13) | ((unsigned int)d << 26);
+}
+
+// one introsort step of [f, l) (l - f - 1 <= 64 R) with the range's positions
+// f + 1 + 64 r + lane held in R rows of registers.  The median swap is taken
+// virtually while the rows are read (one LDS round trip), m comes from the
+// ballot of the crossing and two lane reads, and the LDS sees the median
+// swap, the right-stopper table (tbl[f + rank]), its reads, the partner reads and
+// the swaps.  Returns the cut.
 template <int R>
 __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f, int l) {
     const int lane = threadIdx.x & 63;
@@ -114,7 +123,6 @@ __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f,
     const unsigned int p = vkey(pit);
     bool iL[R], iR[R];
     int pl[R], pr[R];
-    unsigned long long bl[R], br[R];
     int cl = 0, cr = 0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -124,12 +132,11 @@ __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f,
         const unsigned int k = vkey(it[r]);
         iL[r] = act && !(k < p);
         iR[r] = act && !(p < k);
-        bl[r] = __ballot(iL[r]);
-        br[r] = __ballot(iR[r]);
-        pl[r] = cl + lane_prefix(bl[r]);
-        pr[r] = cr + lane_prefix(br[r]);
-        cl += __popcll(bl[r]);
-        cr += __popcll(br[r]);
+        const unsigned long long bl = __ballot(iL[r]), br = __ballot(iR[r]);
+        pl[r] = cl + lane_prefix(bl);
+        pr[r] = cr + lane_prefix(br);
+        cl += __popcll(bl);
+        cr += __popcll(br);
     }
     const int TR = cr;
     // m = max over boundaries b of min(Lb, Rb) (left stoppers before b, right
@@ -185,378 +192,305 @@ __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f,
     return min(cutA, m > 0 ? cutB : INF);
 }
 
-// [F, L) with `depth` levels of budget, to the end, by the calling wave
-// (every lane); stk: 32 words of this wave's LDS.  Steps go depth first; a
-// leaf (<= 16 items, which the final insertion sort leaves stably sorted)
-// only marks its positions in tbl (offset in the leaf | size << 5: a
-// position's tbl word is free once its range is a leaf), a heapsorted range
-// marks them 0xffff; one pass over [F, L) at the end ranks every leaf's
-// items at once.
-__device__ __forceinline__ void wave_range(u64* items, unsigned short* tbl, unsigned int* stk, int F, int L,
-                                           int depth) {
+// one introsort step of [f, l), l - f - 1 <= 64 * 64, rows streamed from LDS.
+// rowL / rowR hold, in lane r, the left / right stoppers before row r, so a
+// row's exclusive prefixes are one lane read and a lane count away in every
+// later pass; keys are the high words of the items.
+__device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int f, int l) {
     const int lane = threadIdx.x & 63;
-    int sp = 0, f = F, l = L;
-    for (;;) {
-        const int n = l - f;
-        bool pop = true;
-        if (n <= 16) {
-            if (lane < n) tbl[f + lane] = (unsigned short)(lane | (n << 5));
-        } else if (depth == 0) {
-            if (lane == 0) slo_sort::heap_sort_(items + f, n, Less());
-            for (int x = f + lane; x < l; x += 64) tbl[x] = 0xffff;
-        } else {
-            const int cut = n - 1 <= 64 ? wave_step<1>(items, tbl, f, l) : wave_step<kWaveMax / 64>(items, tbl, f, l);
-            if (lane == 0) stk[sp] = (unsigned int)cut | ((unsigned int)l << 13) | ((unsigned int)(depth - 1) << 26);
-            ++sp;
-            l = cut;
-            depth -= 1;
-            pop = false;
-        }
-        wave_fence();
-        if (pop) {
-            if (sp == 0) break;
-            --sp;
-            const unsigned int e = __builtin_amdgcn_readfirstlane(stk[sp]);
-            f = (int)(e & 0x1fffu);
-            l = (int)((e >> 13) & 0x1fffu);
-            depth = (int)(e >> 26);
+    constexpr int INF = 0x7fffffff;
+    constexpr int U = 4;   // rows in flight
+    const unsigned int* K = reinterpret_cast<const unsigned int*>(items);
+    const int mid = f + (l - f) / 2;
+    const u64 a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+    const int w = median3(vkey(a1), vkey(a2), vkey(a3));
+    const int med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
+    const u64 pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
+    const unsigned int p = vkey(pit), k0 = vkey(a0);
+    const int b0 = f + 1, R = (l - b0 + 63) >> 6;   // rows of [f + 1, l)
+    // (1) stopper counts per row (the median swap taken virtually)
+    int rowL = 0, rowR = 0, cl = 0, cr = 0;
+    for (int r0 = 0; r0 < R; r0 += U) {
+        unsigned int kk[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u) + lane, l - 1) + 1];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int r = r0 + u;
+            if (r < R) {
+                const int x = b0 + 64 * r + lane;
+                const unsigned int k = x == med ? k0 : kk[u];
+                const bool act = x < l;
+                const unsigned long long bl = __ballot(act && !(k < p)), br = __ballot(act && !(p < k));
+                rowL = lane == r ? cl : rowL;
+                rowR = lane == r ? cr : rowR;
+                cl += __popcll(bl);
+                cr += __popcll(br);
+            }
         }
     }
-    // every leaf at once: an item's place is its rank in the leaf by (key, position)
-    constexpr int RR = kWaveMax / 64;
-    u64 own[RR];
-    int dst[RR];
-#pragma unroll
-    for (int r = 0; r < RR; ++r) {
-        const int x = F + 64 * r + lane;
-        own[r] = items[min(x, L - 1)];
-        const unsigned int info = tbl[min(x, L - 1)];
-        dst[r] = -1;
-        if (x >= L || info == 0xffffu) continue;
-        const int o = (int)(info & 31u), sz = (int)(info >> 5), lo = x - o;
-        const unsigned int k = vkey(own[r]);
-        unsigned int ky[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) ky[t] = vkey(items[lo + min(t, sz - 1)]);
-        int rk = 0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) rk += (t < sz) & ((ky[t] < k) | ((ky[t] == k) & (t < o)));
-        dst[r] = lo + rk;
+    const int TL = cl, TR = cr;
+    // (2) m: the crossing (the first boundary X with Lb >= Rb) lies in the
+    // first row c whose end boundary qualifies — its start boundary (row c - 1's
+    // end) does not, so X is past row c's first position unless c = 0 and
+    // X = f + 1.  The last row's end (Lb = TL, Rb = 0) always qualifies.
+    int eL = __shfl_down(rowL, 1, 64), eR = __shfl_down(rowR, 1, 64);
+    if (lane == R - 1) { eL = TL; eR = TR; }
+    const int c = __builtin_ctzll(__ballot(lane < R && eL >= TR - eR));
+    // a row's stoppers with their exclusive prefixes (the median swap virtual)
+    auto row_flags = [&](int r, bool& iL, bool& iR, int& pl, int& pr) {
+        const int x = b0 + 64 * r + lane;
+        unsigned int k = K[2 * min(x, l - 1) + 1];
+        k = x == med ? k0 : k;
+        const bool act = x < l;
+        iL = act && !(k < p);
+        iR = act && !(p < k);
+        pl = __builtin_amdgcn_readlane(rowL, r) + lane_prefix(__ballot(iL));
+        pr = __builtin_amdgcn_readlane(rowR, r) + lane_prefix(__ballot(iR));
+    };
+    int m;
+    {
+        bool iL, iR;
+        int pl, pr;
+        row_flags(c, iL, iR, pl, pr);
+        const int bc = b0 + 64 * c;
+        const unsigned long long fx = __ballot(bc + lane < l && pl >= TR - pr);
+        if (fx) {
+            const int xl = __builtin_ctzll(fx);
+            m = TR - __builtin_amdgcn_readlane(pr, xl);                 // Rb(X)
+            if (xl > 0) m = max(m, __builtin_amdgcn_readlane(pl, xl - 1));   // Lb(X - 1)
+        } else {   // X = the row's end boundary
+            const int last = min(63, l - 1 - bc);
+            m = max(TR - __builtin_amdgcn_readlane(eR, c), __builtin_amdgcn_readlane(pl, last));
+        }
+    }
+    // (3) the cuts: i_{m+1} (left stopper of rank m), j_m (right stopper with
+    // TR - m right stoppers before it), each from its row
+    int cutA = INF, cutB = INF, rA = R - 1, rB = 0;
+    if (m < TL) {
+        rA = __builtin_ctzll(__ballot(lane < R && rowL <= m && m < eL));
+        bool iL, iR;
+        int pl, pr;
+        row_flags(rA, iL, iR, pl, pr);
+        cutA = b0 + 64 * rA + __builtin_ctzll(__ballot(iL && pl == m));
+    }
+    if (m > 0) {
+        const int t = TR - m;
+        rB = __builtin_ctzll(__ballot(lane < R && rowR <= t && t < eR));
+        bool iL, iR;
+        int pl, pr;
+        row_flags(rB, iL, iR, pl, pr);
+        cutB = b0 + 64 * rB + __builtin_ctzll(__ballot(iR && pr == t));
+    }
+    if (lane == 0) {   // the median swap, made real
+        items[f] = pit;
+        items[med] = a0;
     }
     wave_fence();
+    if (m > 0) {
+        // (4) the m last right stoppers (rows rB ..), by rank from the right
+        const unsigned int* Kr = K;
+        for (int r0 = rB; r0 < R; r0 += U) {
+            unsigned int kk[U];
 #pragma unroll
-    for (int r = 0; r < RR; ++r)
-        if (dst[r] >= 0) items[dst[r]] = own[r];
+            for (int u = 0; u < U; ++u) kk[u] = Kr[2 * min(b0 + 64 * (r0 + u) + lane, l - 1) + 1];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = r0 + u;
+                if (r < R) {
+                    const int x = b0 + 64 * r + lane;
+                    const bool iR = x < l && !(p < kk[u]);
+                    const int kr = TR - 1 - (__builtin_amdgcn_readlane(rowR, r) + lane_prefix(__ballot(iR)));
+                    if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
+                }
+            }
+        }
+        wave_fence();
+        // (5) the m first left stoppers (rows .. rA) swap with their partners;
+        // every swapped left stopper lies before the crossing and every
+        // partner at or after it, so a batch's loads see no earlier write
+        const int rEnd = m < TL ? rA : R - 1;
+        for (int r0 = 0; r0 <= rEnd; r0 += U) {
+            u64 it[U], py[U];
+            int y[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) it[u] = items[min(b0 + 64 * (r0 + u) + lane, l - 1)];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int r = r0 + u;
+                y[u] = -1;
+                if (r <= rEnd) {
+                    const int x = b0 + 64 * r + lane;
+                    const bool iL = x < l && !(vkey(it[u]) < p);
+                    const int pl = __builtin_amdgcn_readlane(rowL, r) + lane_prefix(__ballot(iL));
+                    if (iL && pl < m) y[u] = pl;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) y[u] = y[u] >= 0 ? (int)tbl[f + y[u]] : -1;
+#pragma unroll
+            for (int u = 0; u < U; ++u) py[u] = items[y[u] >= 0 ? y[u] : f];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (y[u] >= 0) {
+                    items[b0 + 64 * (r0 + u) + lane] = py[u];
+                    items[y[u]] = it[u];
+                }
+        }
+        wave_fence();
+    }
+    return min(cutA, m > 0 ? cutB : INF);
+}
+
+// the queued lane tasks, one per lane, through the sequential restatement
+__device__ __forceinline__ void lane_flush(u64* items, const unsigned int* q, int nq) {
+    const int lane = threadIdx.x & 63;
+    wave_fence();
+    if (lane < nq) {
+        const unsigned int e = q[lane];
+        const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
+        slo_sort::introsort_range(items + f, l - f, d, Less());
+    }
     wave_fence();
 }
 
-template <int NT, int NMAX>
-struct BlockSmem {
-    static constexpr int MAXSEG = NMAX / 17 + 2;   // disjoint ranges of > 16 items, + slack
-    unsigned short tblB[NMAX];     // right stoppers by rank from the right, at f + rank
-    unsigned short f[2][MAXSEG], l[2][MAXSEG];
-    unsigned char d[2][MAXSEG];
-    unsigned int piv[MAXSEG];
-    int sL[MAXSEG], eR[MAXSEG], m[MAXSEG], cutA[MAXSEG], cutB[MAXSEG];
-    short nidL[MAXSEG], nidR[MAXSEG];
-    unsigned short hf[MAXSEG], hl[MAXSEG];   // heapsort ranges
-    unsigned int wq[MAXSEG];                 // wave-tier ranges: first | end << 13 | depth << 26
-    unsigned int stk[NT / 64][32];           // wave-tier stacks
-    int nseg[2], nheap, nwq, wq_next;
-    unsigned int wsum[NT / 64];
+// one step of [f, l) by the calling wave, the variant its size picks
+__device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, int f, int l) {
+    const int len = l - f;
+    return len - 1 <= 64 ? wave_step<1>(items, tbl, f, l)
+         : len - 1 <= 128 ? wave_step<2>(items, tbl, f, l) : stream_step(items, tbl, f, l);
+}
+
+// Sorts items[f0, l0) (LDS, positions < 8192, l0 - f0 <= 4097) into exactly
+// std::sort's order for a range that the introsort loop reaches with `depth`
+// levels of budget (2 * lg(n) for a whole array).  Called by all 64 lanes of
+// one wave; tbl holds an entry per position (a step writes tbl[f .. f + m),
+// so waves on disjoint ranges share it).  *err (if given) counts ranges
+// handed to a lane for a reason other than their size (must stay 0).
+// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] lane tasks
+template <int TLANE>
+__device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int depth, unsigned short* tbl,
+                                                WaveSmem& ws, int* err = nullptr, long long* prof = nullptr) {
+    static_assert(TLANE >= 16, "ranges of <= 16 items are lane tasks");
+    const int lane = threadIdx.x & 63;
+    if (l0 - f0 <= 1) return;
+    int sp = 0, nq = 0, f = f0, l = l0, d = depth;
+    for (;;) {
+        const int len = l - f;
+        bool task = len <= TLANE || d == 0;
+        int cut = 0;
+        if (!task && sp == kStack) {   // cannot happen (sp <= the depth budget); exact anyway
+            task = true;
+            if (err && lane == 0) atomicAdd(err, 1);
+        }
+        if (!task) {
+            const long long t0 = prof ? clock64() : 0;
+            cut = wave_step_any(items, tbl, f, l);
+            if (prof) prof[len - 1 <= 128] += clock64() - t0;
+            if (cut <= f || cut >= l) {   // cannot happen; sorted (not std::sort's order) rather than a hang
+                task = true;
+                if (err && lane == 0) atomicAdd(err, 1);
+            }
+        }
+        if (task) {
+            if (len >= 2) {
+                if (lane == 0) ws.q[nq] = renc(f, l, d);
+                if (++nq == kQ) {
+                    const long long t0 = prof ? clock64() : 0;
+                    lane_flush(items, ws.q, nq);
+                    if (prof) prof[2] += clock64() - t0;
+                    nq = 0;
+                }
+            }
+            if (sp == 0) break;
+            wave_fence();
+            const unsigned int e = __builtin_amdgcn_readfirstlane(ws.stk[--sp]);
+            f = (int)(e & 0x1fffu);
+            l = (int)((e >> 13) & 0x1fffu);
+            d = (int)(e >> 26);
+            continue;
+        }
+        if (lane == 0) ws.stk[sp] = renc(cut, l, d - 1);
+        ++sp;
+        l = cut;
+        --d;
+    }
+    if (nq) {
+        const long long t0 = prof ? clock64() : 0;
+        lane_flush(items, ws.q, nq);
+        if (prof) prof[2] += clock64() - t0;
+    }
+}
+
+template <int TLANE>
+__device__ __forceinline__ void wave_sort(u64* items, int n, int depth, unsigned short* tbl, WaveSmem& ws,
+                                          int* err = nullptr, long long* prof = nullptr) {
+    wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws, err, prof);
+}
+
+// W waves on one range: the first levels breadth first (level k steps its
+// 2^k ranges on as many waves) until there are 2W ranges, which the waves
+// then take one at a time (an LDS counter) and finish depth first.
+template <int W>
+struct BlockQ {
+    unsigned int cur[2 * W], nxt[2 * W];
+    int ncur, take;
 };
 
-// Sorts items[0, n) (LDS, n <= NMAX) into exactly std::sort's order for a
-// range that the introsort loop reaches with `depth` levels of budget
-// (2 * lg(n) for a whole array).  All NT threads of the workgroup call it.
-//
-// Positions are wave-striped: wave w, row j, lane t owns position
-// x = w * 64 * IPT + j * 64 + t for the whole sort, so each position's state
-// (its active range, or its leaf) lives in the owner's registers, each LDS
-// access of a row is 64 consecutive words (no bank conflicts) and every
-// prefix count is a ballot.  Every step issues all of a thread's loads
-// before it uses any (indices clamped, no loads behind branches), so a step
-// costs one LDS round trip, not one per row.  Returns the levels run.
-template <int NT, int NMAX>
-__device__ __forceinline__ int pcl_block_sort(u64* items, int n, int depth, BlockSmem<NT, NMAX>& sm,
-                                              unsigned long long* prof = nullptr) {   // [4] thread 0: phase cycles, wave ranges
-    const long long pt0 = clock64();
-    static_assert(NMAX % NT == 0 && NMAX <= 4096 && NT % 64 == 0, "pcl_block_sort layout");
-    constexpr int IPT = NMAX / NT, NW = NT / 64;
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int xw = w * 64 * IPT + lane;   // position of row j: xw + 64 j
-    const unsigned long long lt = (1ull << lane) - 1ull;
-    // per position, packed: bits 0-7 the active range (kDone once finished),
-    // 8-15 its leaf's size (kHeap: a heapsort range), 16-31 its leaf's start
-    unsigned int st[IPT];
-    const bool wave0 = n > 16 && depth > 0 && n <= kWaveMax;
-    const bool act0 = n > 16 && depth > 0 && !wave0;
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-        const int x = xw + 64 * j;
-        st[j] = (unsigned int)((act0 && x < n) ? 0 : kDone) |
-                ((unsigned int)(n <= 16 ? n : wave0 ? kWave : kHeap) << 8);
+template <int TLANE, int W>
+__device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigned short* tbl, WaveSmem* ws,
+                                           BlockQ<W>& bq, int* err = nullptr, long long* prof = nullptr) {
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    if (W == 1) {
+        wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws[0], err, prof);
+        return;
     }
-    if (tid == 0) {
-        sm.nseg[0] = act0 ? 1 : 0;
-        sm.nseg[1] = 0;
-        sm.nheap = (n > 16 && depth == 0) ? 1 : 0;
-        sm.nwq = wave0 ? 1 : 0;
-        sm.wq_next = 0;
-        sm.f[0][0] = 0; sm.l[0][0] = (unsigned short)n; sm.d[0][0] = (unsigned char)depth;
-        sm.hf[0] = 0; sm.hl[0] = (unsigned short)n;
-        sm.wq[0] = (unsigned int)n << 13 | (unsigned int)depth << 26;
+    if (threadIdx.x == 0) {
+        bq.cur[0] = renc(0, n, depth);
+        bq.ncur = n >= 2 ? 1 : 0;
+        bq.take = 0;
     }
     __syncthreads();
-    int c = 0, levels = 0;
-    for (;;) {
-        const int ns = sm.nseg[c];
-        if (ns == 0) break;
-        // (1) median of three to the front; the pivot
-        for (int s = tid; s < ns; s += NT) {
-            const int F = sm.f[c][s], L = sm.l[c][s];
-            u64* a = items + F;
-            slo_sort::move_median_to_first_(a, a + 1, a + (L - F) / 2, a + (L - F - 1), Less());
-            sm.piv[s] = vkey(a[0]);
-            sm.m[s] = 0;
-            sm.cutA[s] = 0x7fffffff;
-            sm.cutB[s] = 0x7fffffff;
-        }
-        __syncthreads();
-        // (2) every row's range bounds, pivot and item (all loads first), stopper ballots
-        u64 it[IPT];
-        int rf[IPT], rl[IPT];
-        unsigned long long bL[IPT], bR[IPT];
-        {
-            unsigned int pv[IPT];
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int sc = (st[j] & 0xff) == kDone ? 0 : (int)(st[j] & 0xff);
-                rf[j] = sm.f[c][sc];
-                rl[j] = sm.l[c][sc];
-                pv[j] = sm.piv[sc];
-                it[j] = items[min(xw + 64 * j, NMAX - 1)];
-            }
-            int cL = 0, cR = 0;
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int x = xw + 64 * j;
-                const bool act = (st[j] & 0xff) != kDone && x != rf[j];
-                const unsigned int k = vkey(it[j]);
-                bL[j] = __ballot(act && !(k < pv[j]));
-                bR[j] = __ballot(act && !(pv[j] < k));
-                cL += __popcll(bL[j]);
-                cR += __popcll(bR[j]);
-            }
-            if (lane == 0) sm.wsum[w] = (unsigned int)cL | ((unsigned int)cR << 16);
-        }
-        __syncthreads();
-        int pl[IPT], pr[IPT];   // stoppers before each row's position (exclusive prefixes)
-        {
-            unsigned int ws[NW];
-#pragma unroll
-            for (int q = 0; q < NW; ++q) ws[q] = sm.wsum[q];
-            int bl = 0, br = 0;
-#pragma unroll
-            for (int q = 0; q < NW; ++q)
-                if (q < w) { bl += (int)(ws[q] & 0xffffu); br += (int)(ws[q] >> 16); }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                pl[j] = bl + __popcll(bL[j] & lt);
-                pr[j] = br + __popcll(bR[j] & lt);
-                bl += __popcll(bL[j]);
-                br += __popcll(bR[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                if ((st[j] & 0xff) == kDone) continue;
-                const int x = xw + 64 * j, s = st[j] & 0xff;
-                if (x == rf[j] + 1) sm.sL[s] = pl[j];
-                if (x == rl[j] - 1) sm.eR[s] = pr[j] + (int)((bR[j] >> lane) & 1);
-            }
-        }
-        __syncthreads();
-        // (3) m of every range: with Lb = left stoppers before a boundary and
-        // Rb = right stoppers at or after it, max(min(Lb, Rb)) sits where
-        // Lb >= Rb first holds; only the positions around that crossing post
-        // it (a wave-block edge, whose neighbour is another wave's, posts its
-        // own value: any min(Lb, Rb) is <= m)
-        int rsL[IPT], reR[IPT];
-        {
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int sc = (st[j] & 0xff) == kDone ? 0 : (int)(st[j] & 0xff);
-                rsL[j] = sm.sL[sc];
-                reR[j] = sm.eR[sc];
-            }
-            unsigned long long bF[IPT];
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int x = xw + 64 * j;
-                const bool act = (st[j] & 0xff) != kDone && x > rf[j];
-                bF[j] = __ballot(act && pl[j] - rsL[j] >= reR[j] - pr[j]);
-            }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int x = xw + 64 * j;
-                if ((st[j] & 0xff) == kDone || x <= rf[j]) continue;
-                const int s = st[j] & 0xff;
-                const int lb = pl[j] - rsL[j], rb = reR[j] - pr[j];
-                const bool fl = (bF[j] >> lane) & 1;
-                const bool prevF = lane > 0 ? (bF[j] >> (lane - 1)) & 1 : (j > 0 ? (bF[j - 1] >> 63) & 1 : 0);
-                const bool nextF = lane < 63 ? (bF[j] >> (lane + 1)) & 1 : (j + 1 < IPT ? bF[j + 1] & 1 : 1);
-                const bool first = x == rf[j] + 1, last = x == rl[j] - 1;
-                if (fl && (first || !prevF) && rb > 0) atomicMax(&sm.m[s], rb);
-                if (!fl && (last || nextF) && lb > 0) atomicMax(&sm.m[s], lb);
-            }
-        }
-        __syncthreads();
-        // (4) right stoppers by rank from the right; the cut candidates
-        int rm[IPT];
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            const int sc = (st[j] & 0xff) == kDone ? 0 : (int)(st[j] & 0xff);
-            rm[j] = sm.m[sc];
-        }
-#pragma unroll
-        for (int j = 0; j < IPT; ++j) {
-            if ((st[j] & 0xff) == kDone) continue;
-            const int x = xw + 64 * j, s = st[j] & 0xff;
-            if (((bL[j] >> lane) & 1) && pl[j] - rsL[j] == rm[j]) sm.cutA[s] = x;   // i_{m+1}
-            if ((bR[j] >> lane) & 1) {
-                const int kr = reR[j] - pr[j] - 1;                                  // right stoppers after x
-                if (kr < rm[j]) sm.tblB[rf[j] + kr] = (unsigned short)x;
-                if (kr == rm[j] - 1) sm.cutB[s] = x;                                 // j_m
-            }
-        }
-        __syncthreads();
-        // (5a) swap partners (left stopper of rank k < m <-> right stopper of rank k)
-        u64 pit[IPT];
-        int py[IPT];
-        unsigned int sw = 0;
-        {
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int k = pl[j] - rsL[j];
-                const bool swp = ((bL[j] >> lane) & 1) && k < rm[j];
-                sw |= (unsigned int)swp << j;
-                py[j] = sm.tblB[min(max(rf[j] + k, 0), NMAX - 1)];
-            }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) pit[j] = items[((sw >> j) & 1) ? py[j] : 0];
-        }
-        // (6) the halves: ranges of > 16 items with budget left stay active
-        for (int s = tid; s < ns; s += NT) {
-            const int F = sm.f[c][s], L = sm.l[c][s], D = sm.d[c][s] - 1;
-            const int cut = min(sm.cutA[s], sm.m[s] > 0 ? sm.cutB[s] : 0x7fffffff);
-            sm.cutA[s] = cut;
-            const int lo[2] = {F, cut}, hi[2] = {cut, L};
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                short id = -1;
-                if (hi[h] - lo[h] > 16) {
-                    if (D > 0 && hi[h] - lo[h] <= kWaveMax) {   // to the wave tier
-                        const int q = atomicAdd(&sm.nwq, 1);
-                        sm.wq[q] = (unsigned int)lo[h] | ((unsigned int)hi[h] << 13) | ((unsigned int)D << 26);
-                        id = -2;
-                    } else if (D > 0) {
-                        id = (short)atomicAdd(&sm.nseg[c ^ 1], 1);
-                        sm.f[c ^ 1][id] = (unsigned short)lo[h]; sm.l[c ^ 1][id] = (unsigned short)hi[h];
-                        sm.d[c ^ 1][id] = (unsigned char)D;
-                    } else {   // depth spent: heapsort
-                        const int q = atomicAdd(&sm.nheap, 1);
-                        sm.hf[q] = (unsigned short)lo[h]; sm.hl[q] = (unsigned short)hi[h];
-                    }
-                }
-                (h ? sm.nidR : sm.nidL)[s] = id;
-            }
-        }
-        __syncthreads();
-        // (5b) the swaps; (7) every position's next range or leaf (state in registers)
-#pragma unroll
-        for (int j = 0; j < IPT; ++j)
-            if ((sw >> j) & 1) {
-                items[xw + 64 * j] = pit[j];
-                items[py[j]] = it[j];
-            }
-        {
-            int ct[IPT], iL[IPT], iR[IPT];
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                const int sc = (st[j] & 0xff) == kDone ? 0 : (int)(st[j] & 0xff);
-                ct[j] = sm.cutA[sc];
-                iL[j] = sm.nidL[sc];
-                iR[j] = sm.nidR[sc];
-            }
-#pragma unroll
-            for (int j = 0; j < IPT; ++j) {
-                if ((st[j] & 0xff) == kDone) continue;
-                const int x = xw + 64 * j;
-                const bool left = x < ct[j];
-                const int id = left ? iL[j] : iR[j];
-                if (id >= 0) {
-                    st[j] = (st[j] & ~0xffu) | (unsigned int)id;
-                } else if (id == -2) {
-                    st[j] = (unsigned int)kDone | ((unsigned int)kWave << 8);
-                } else {
-                    const int lo = left ? rf[j] : ct[j], hi = left ? ct[j] : rl[j];
-                    st[j] = (unsigned int)kDone | ((unsigned int)(hi - lo <= 16 ? hi - lo : kHeap) << 8) |
-                            ((unsigned int)lo << 16);
+    for (int k = 1; k < 2 * W; k <<= 1) {
+        const int nc = bq.ncur;
+        for (int i = wv; i < nc; i += W) {
+            const unsigned int e = bq.cur[i];
+            const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
+            unsigned int a = e, b = 0;
+            if (l - f > TLANE && d > 0) {
+                const long long t0 = prof ? clock64() : 0;
+                const int cut = wave_step_any(items, tbl, f, l);
+                if (prof) prof[l - f - 1 <= 128] += clock64() - t0;
+                if (cut > f && cut < l) {
+                    a = renc(f, cut, d - 1);
+                    b = renc(cut, l, d - 1);
+                } else if (err && lane == 0) {
+                    atomicAdd(err, 1);
                 }
             }
+            if (lane == 0) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
         }
-        if (tid == 0) sm.nseg[c] = 0;
-        c ^= 1;
-        ++levels;
+        __syncthreads();
+        if (threadIdx.x == 0) {   // the next level's ranges of two or more items
+            int c = 0;
+            for (int i = 0; i < 2 * nc; ++i) {
+                const unsigned int e = bq.nxt[i];
+                if ((int)((e >> 13) & 0x1fffu) - (int)(e & 0x1fffu) >= 2) bq.cur[c++] = e;
+            }
+            bq.ncur = c;
+        }
         __syncthreads();
     }
-    const long long pt1 = clock64();
-    // heapsort ranges (depth spent), one lane each
-    for (int q = tid; q < sm.nheap; q += NT)
-        slo_sort::heap_sort_(items + sm.hf[q], sm.hl[q] - sm.hf[q], Less());
-    // wave tier: every wave takes queued ranges until none is left
     for (;;) {
         int q = 0;
-        if (lane == 0) q = atomicAdd(&sm.wq_next, 1);
+        if (lane == 0) q = atomicAdd(&bq.take, 1);
         q = __builtin_amdgcn_readfirstlane(q);
-        if (q >= sm.nwq) break;
-        const unsigned int e = __builtin_amdgcn_readfirstlane(sm.wq[q]);
-        wave_range(items, sm.tblB, sm.stk[w], (int)(e & 0x1fffu), (int)((e >> 13) & 0x1fffu), (int)(e >> 26));
+        if (q >= bq.ncur) break;
+        const unsigned int e = bq.cur[q];
+        wave_sort_range<TLANE>(items, (int)(e & 0x1fffu), (int)((e >> 13) & 0x1fffu), (int)(e >> 26), tbl, ws[wv],
+                               err, prof);
     }
     __syncthreads();
-    const long long pt2 = clock64();
-    // leaves: the final insertion sort = each item's rank in its leaf by (key, position)
-    u64 own[IPT];
-    int dst[IPT];
-#pragma unroll
-    for (int j = 0; j < IPT; ++j) {
-        const int x = xw + 64 * j;
-        own[j] = items[min(x, NMAX - 1)];
-        const int lo = (int)(st[j] >> 16), sz = (int)((st[j] >> 8) & 0xff);
-        dst[j] = -1;
-        if (x >= n || sz == kHeap || sz == kWave) continue;
-        const unsigned int k = vkey(own[j]);
-        unsigned int ky[16];
-#pragma unroll
-        for (int t = 0; t < 16; ++t) ky[t] = vkey(items[lo + min(t, sz - 1)]);
-        int r = 0;
-#pragma unroll
-        for (int t = 0; t < 16; ++t) r += (t < sz) & ((ky[t] < k) | ((ky[t] == k) & (lo + t < x)));
-        dst[j] = lo + r;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < IPT; ++j)
-        if (dst[j] >= 0) items[dst[j]] = own[j];
-    __syncthreads();
-    if (prof && tid == 0) {
-        const long long pt3 = clock64();
-        prof[0] += (unsigned long long)(pt1 - pt0);
-        prof[1] += (unsigned long long)(pt2 - pt1);
-        prof[2] += (unsigned long long)(pt3 - pt2);
-        prof[3] += (unsigned long long)sm.nwq;
-    }
-    return levels;
 }
 
 }  // namespace slo_pcl

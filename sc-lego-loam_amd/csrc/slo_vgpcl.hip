@@ -14,7 +14,7 @@
 //     input order (the raw cloud is not dense, MO:1236; the other clouds are
 //     finite), the non-finite ones after them with the "none" key; each
 //     stream's range becomes the first introsort range: a global range
-//     (> PC_T items) or a finish entry;
+//     (> PC_TAIL items) or a list entry;
 //   G global levels, one introsort step of every global range per level:
 //     k_pc_lcount  per chunk of PC_CH positions: stopper counts (the median of
 //                  three is taken virtually: every chunk derives it alone);
@@ -24,15 +24,17 @@
 //                  and of the right stoppers of rank < m (from the right), the
 //                  cut candidates; chunk 0 makes the median swap real;
 //     k_pc_lpairs  the swaps;
-//     k_pc_lsplit  per range: the halves — over PC_T items back to the next
-//                  level, otherwise (or at the last level) a finish entry.
+//     k_pc_lsplit  per range: the halves — over PC_TAIL items back to the
+//                  next level, otherwise (or at the last level) a list entry.
 //   (Folding the per-range steps into the last chunk's workgroup, by a
 //   done counter, measured 20x slower: the device-scope fence each chunk
 //   then needs writes the XCD's L2 back.)
-//   k_pc_finish: one workgroup per finish entry (<= PC_T items) sorts it in
-//     LDS to the end (pcl_block_sort); an entry still over PC_T after the G
-//     levels (never seen on the configs; counted in meta) is finished by one
-//     lane in global memory.
+//   k_pc_tail: one workgroup per range of more than PC_T items, depth first
+//     down to ranges of at most PC_T (the same step, barriers for launches);
+//   k_pc_finish: one wave per range of at most PC_T items sorts it in LDS to
+//     the end (slo_pcl::wave_sort);
+//   k_pc_fallback: a range over PC_T items with its depth budget spent
+//     (adversarial inputs only; counted in vg_stats) is heapsorted by one lane.
 #include "slo_vgcommon.h"
 #include "slo_pclsort.h"
 
@@ -43,16 +45,19 @@ using slo_pcl::u64;
 #define PC_CH 4096        // positions per chunk of the global levels (256 threads x 16)
 #define PC_CT 256
 #define PC_T 4096         // a range of at most PC_T items is finished in LDS
-#define PC_FT 1024        // threads of the big finish workgroup (4 positions each)
-#define PC_ST 2048        // small finish entries (<= PC_ST items): 512-thread workgroups
-#define PC_WT 512         // smallest finish entries (<= PC_WT items): 128-thread workgroups
+#define PC_ST 2048        // finish size classes: <= PC_WT, <= PC_ST, <= PC_T items (LDS per wave)
+#define PC_WT 512
+#ifndef PC_TAIL
+#define PC_TAIL 65536     // the global levels take ranges of more than PC_TAIL items, k_pc_tail the rest
+#endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
 // PclWs::pstat, cumulative work counters (slo_get "pcl_work"; the bench
 // prices the kernels' algorithmic bytes with them): [0] items of the ranges
 // stepped by the global levels, [1] pairs they swapped, [2..4] items of
 // finish lists 0..2, [5] VoxelGrid input points, [6] finish entries, [7]
-// block-tier levels they ran; [8..15] finish phase cycles (k_pc_finish)
-enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_LEVELS = 7 };
+// items of the ranges k_pc_tail stepped, [8] pairs it swapped, [9 + 3 list + q]
+// finish cycles of list `list` in streamed steps, register steps, lane tasks
+enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_TAIL = 7, PW_TAIL_PAIRS = 8, PW_PROF = 9 };
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
@@ -60,9 +65,10 @@ struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
 // counters (PclWs::ctr)
 enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: finish list k
 
-// Finish entries by size class: list 0 <= PC_WT items (k_pc_finish<128>), 1 <= PC_ST (k_pc_finish<512>), 2 <= PC_T (k_pc_finish<PC_FT>), 3
-// larger (the global fallback).  An entry is (first position, size | depth << 24).
-struct PcLists { int2* l[4]; };
+// Range lists: finish entries by size class, list 0 <= PC_WT items, 1 <= PC_ST,
+// 2 <= PC_T (k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
+// over PC_T items (k_pc_fallback: heapsort).  An entry is (first position, size | depth << 24).
+struct PcLists { int2* l[5]; };
 __device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) {
     const int k = n <= PC_WT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
     const int i = atomicAdd(&ctr[PCC_NW + k], 1);
@@ -133,7 +139,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgPa
         // overflow keys are the positions: already in order
         if (!p.overflow && n >= 2) {
             const int d = 2 * slo_pcl::lg2(n);
-            if (n > PC_T) {
+            if (n > PC_TAIL) {
                 const int nch = (n - 1 + PC_CH - 1) / PC_CH;
                 const int slot = atomicAdd(&ctr[PCC_NSEG], 1);
                 const int c0 = atomicAdd(&ctr[PCC_NCH], nch);
@@ -438,7 +444,7 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
             for (int h = 0; h < 2; ++h) {
                 const int n = hi[h] - lo[h];
                 if (n <= 1) continue;
-                if (n > PC_T && D > 0 && !last) {
+                if (n > PC_TAIL && D > 0 && !last) {
                     kind[h] = 4;
                     nch[h] = (n - 1 + PC_CH - 1) / PC_CH;
                 } else {
@@ -488,46 +494,326 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
     }
 }
 
-// ---- finish: one workgroup per entry
-template <int NT, int NMAX>
-__global__ void __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(4))) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
-                                                  unsigned long long* pst) {
+// ---- finish: PC_FW waves per entry (slo_pcl::block_sort; one for the
+// smallest class), the entry's items staged in LDS; lane tasks take the
+// ranges of <= PC_TLANE items
+#ifndef PC_TLANE
+#define PC_TLANE 64
+#endif
+#ifndef PC_FW
+#define PC_FW 4           // waves per entry of the two larger size classes
+#endif
+template <int NMAX, int W>
+__global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
+                                                       unsigned long long* pst, int* cstat) {
     __shared__ u64 items[NMAX];
-    __shared__ slo_pcl::BlockSmem<NT, NMAX> sm;
-    const int nw = ctr[PCC_NW + list];
-    unsigned long long wn = 0, we = 0, wlv = 0, ph[4] = {0, 0, 0, 0};   // work counters, one atomic per block
+    __shared__ unsigned short tbl[NMAX];
+    __shared__ slo_pcl::WaveSmem ws[W];
+    __shared__ slo_pcl::BlockQ<W> bq;
+    const int nw = ctr[PCC_NW + list], tid = threadIdx.x;
+    unsigned long long wn = 0, we = 0;   // work counters, one atomic per wave
+    long long prof[3] = {0, 0, 0};
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
-        for (int i = threadIdx.x; i < n; i += NT) items[i] = ((u64)K[f + i] << 32) | V[f + i];
+        for (int i0 = 0; i0 < n; i0 += 8 * 64 * W) {   // eight loads of each array in flight
+            unsigned int kk[8], vv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = min(i0 + u * 64 * W + tid, n - 1);
+                kk[u] = K[f + i];
+                vv[u] = V[f + i];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i0 + u * 64 * W + tid < n) items[i0 + u * 64 * W + tid] = ((u64)kk[u] << 32) | vv[u];
+        }
         __syncthreads();
-        const int lv = slo_pcl::pcl_block_sort<NT, NMAX>(items, n, d, sm, ph);
-        wn += (unsigned long long)n;
-        we += 1ull;
-        wlv += (unsigned long long)lv;
-        for (int i = threadIdx.x; i < n; i += NT) {
+        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, cstat + 1, prof);
+        for (int i = tid; i < n; i += 64 * W) {
             const u64 it = items[i];
             K[f + i] = (unsigned int)(it >> 32);
             V[f + i] = (unsigned int)it;
         }
         __syncthreads();
+        wn += (unsigned long long)n;
+        we += 1ull;
     }
-    if (threadIdx.x == 0 && we) {
-        atomicAdd(&pst[PW_FIN + list], wn);
-        atomicAdd(&pst[PW_ENTRIES], we);
-        atomicAdd(&pst[PW_LEVELS], wlv);
-        if (list) {   // [8..11] list 1, [12..15] list 2: block-tier, wave-tier and leaf cycles, wave ranges
-#pragma unroll
-            for (int q = 0; q < 4; ++q) atomicAdd(&pst[8 + 4 * (list - 1) + q], ph[q]);
+    if ((tid & 63) == 0 && we) {
+        if (tid == 0) {
+            atomicAdd(&pst[PW_FIN + list], wn);
+            atomicAdd(&pst[PW_ENTRIES], we);
         }
+        for (int q = 0; q < 3; ++q) atomicAdd(&pst[PW_PROF + 3 * list + q], (unsigned long long)prof[q]);
     }
 }
 
-// an entry still over PC_T after the global levels (adversarial inputs only):
-// one lane finishes it in global memory with the sequential restatement
+// ---- the tail: the ranges of more than PC_T items the global levels leave
+// (list 3: up to PC_TAIL items, or whatever is left after the G levels), one
+// workgroup per range, depth first.  A step is the global levels' step with
+// the workgroup in place of the grid: a tile of PT_TILE positions is one
+// wave's (PT_ROWS rows of 64), the tile counts and their prefixes sit in LDS,
+// and barriers separate the passes instead of launches.  Halves of at most
+// PC_T items go to the finish lists, larger ones onto the workgroup's stack;
+// a range whose depth budget is spent goes to list 4 (k_pc_fallback,
+// heapsort).  Ranges over PT_MAXT tiles go to list 4 as well (one lane
+// finishes them exactly; never seen: the map clouds' strides are ~1.6 M).
+#define PT_NT 512
+#define PT_NW (PT_NT / 64)
+#define PT_ROWS 16
+#define PT_TILE (64 * PT_ROWS)
+#define PT_MAXT 4096
+struct TailSm {
+    int tl[PT_MAXT + 1], tr[PT_MAXT + 1];   // per tile stopper counts, then exclusive prefixes (+ totals)
+    int sf[64], sl[64], sd[64];             // the stack of ranges still over PC_T
+    int f, l, d, sp;                        // the range in hand
+    unsigned int piv, k0;
+    int med, c, m, cutA, cutB, tA, tB;
+    int wsum[PT_NW];
+};
+
+__global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
+                                                    int* ctr, unsigned long long* pst) {
+    __shared__ TailSm sm;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    constexpr int INF = 0x7fffffff;
+    const int nw = ctr[PCC_NW + 3];
+    unsigned long long wact = 0, wpairs = 0;
+    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
+        if (tid == 0) {
+            const int2 w = wl.l[3][e];
+            sm.sf[0] = w.x; sm.sl[0] = w.x + (w.y & 0xffffff); sm.sd[0] = w.y >> 24;
+            sm.sp = 1;
+        }
+        __syncthreads();
+        while (sm.sp > 0) {
+            if (tid == 0) {   // pop; the pivot (median swap taken virtually until the swaps)
+                const int q = --sm.sp, f = sm.sf[q], l = sm.sl[q];
+                sm.f = f; sm.l = l; sm.d = sm.sd[q];
+                const int mid = f + (l - f) / 2;
+                const unsigned int kf = K[f], k1 = K[f + 1], k2 = K[mid], k3 = K[l - 1];
+                const int w = slo_pcl::median3(k1, k2, k3);
+                sm.med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
+                sm.piv = w == 0 ? k1 : (w == 1 ? k2 : k3);
+                sm.k0 = kf;
+                sm.c = INF;
+            }
+            __syncthreads();
+            const int f = sm.f, l = sm.l, d = sm.d, med = sm.med;
+            const unsigned int p = sm.piv, k0 = sm.k0;
+            const int b0 = f + 1, nt = (l - b0 + PT_TILE - 1) / PT_TILE;
+            if (d == 0 || nt > PT_MAXT) {   // heapsort (or too long for the tile table): list 4
+                if (tid == 0) {
+                    const int i = atomicAdd(&ctr[PCC_NW + 4], 1);
+                    wl.l[4][i] = make_int2(f, (l - f) | (d << 24));
+                }
+                __syncthreads();
+                continue;
+            }
+            // (A) stopper counts per tile, a wave per tile
+            for (int t = wv; t < nt; t += PT_NW) {
+                const int a = b0 + t * PT_TILE;
+                unsigned int kk[PT_ROWS];
+#pragma unroll
+                for (int r = 0; r < PT_ROWS; ++r) kk[r] = K[min(a + 64 * r + lane, l - 1)];
+                int cl = 0, cr = 0;
+#pragma unroll
+                for (int r = 0; r < PT_ROWS; ++r) {
+                    const int x = a + 64 * r + lane;
+                    const unsigned int k = x == med ? k0 : kk[r];
+                    cl += __popcll(__ballot(x < l && !(k < p)));
+                    cr += __popcll(__ballot(x < l && !(p < k)));
+                }
+                if (lane == 0) { sm.tl[t] = cl; sm.tr[t] = cr; }
+            }
+            __syncthreads();
+            {   // exclusive prefixes over the tiles, totals at [nt]
+                const int per = (nt + PT_NT - 1) / PT_NT, t0 = min(nt, tid * per), t1 = min(nt, t0 + per);
+                int sl_ = 0, sr_ = 0;
+                for (int t = t0; t < t1; ++t) { sl_ += sm.tl[t]; sr_ += sm.tr[t]; }
+                int totl, totr;
+                int rl = vg_block_scan<PT_NW>(sl_, sm.wsum, &totl);
+                int rr = vg_block_scan<PT_NW>(sr_, sm.wsum, &totr);
+                for (int t = t0; t < t1; ++t) {
+                    const int xl = sm.tl[t], xr = sm.tr[t];
+                    sm.tl[t] = rl; sm.tr[t] = rr;
+                    rl += xl; rr += xr;
+                }
+                if (tid == 0) { sm.tl[nt] = totl; sm.tr[nt] = totr; }
+            }
+            __syncthreads();
+            const int TL = sm.tl[nt], TR = sm.tr[nt];
+            // the crossing tile: the first whose end boundary has Lb >= Rb (the last one's always has)
+            for (int t = tid; t < nt; t += PT_NT)
+                if (sm.tl[t + 1] >= TR - sm.tr[t + 1]) atomicMin(&sm.c, t);
+            __syncthreads();
+            if (wv == 0) {   // m, then the cuts, by the first wave
+                // a tile's rows in order: per lane the exclusive prefixes; fn(r, x, act, iL, iR, pl, pr) -> stop
+                auto rows = [&](int t, auto&& fn) {
+                    const int a = b0 + t * PT_TILE;
+                    int runL = sm.tl[t], runR = sm.tr[t];
+                    for (int r = 0; r < PT_ROWS && a + 64 * r < l; ++r) {
+                        const int x = a + 64 * r + lane;
+                        unsigned int k = K[min(x, l - 1)];
+                        k = x == med ? k0 : k;
+                        const bool act = x < l, iL = act && !(k < p), iR = act && !(p < k);
+                        const unsigned long long bl = __ballot(iL), br = __ballot(iR);
+                        const int pl = runL + slo_pcl::lane_prefix(bl), pr = runR + slo_pcl::lane_prefix(br);
+                        if (fn(x, act, iL, iR, pl, pr)) return;
+                        runL += __popcll(bl);
+                        runR += __popcll(br);
+                    }
+                };
+                const int c = sm.c;
+                int m = -1, lastPl = 0;
+                rows(c, [&](int x, bool act, bool, bool, int pl, int pr) {
+                    const unsigned long long fx = __ballot(act && pl >= TR - pr);
+                    if (fx) {
+                        const int xl = __builtin_ctzll(fx);
+                        m = TR - __builtin_amdgcn_readlane(pr, xl);                          // Rb(X)
+                        if (xl > 0) m = max(m, __builtin_amdgcn_readlane(pl, xl - 1));       // Lb(X - 1)
+                        else if (x - lane > b0) m = max(m, lastPl);                          // X - 1 in the row before
+                        return true;
+                    }
+                    lastPl = __builtin_amdgcn_readlane(pl, min(63, l - 1 - (x - lane)));
+                    return false;
+                });
+                if (m < 0) m = max(TR - sm.tr[c + 1], lastPl);   // X = the tile's end boundary
+                int cutA = INF, cutB = INF, tA = nt - 1, tB = 0;
+                if (m < TL) {   // i_{m+1}: the left stopper of rank m
+                    for (int t0 = 0; t0 < nt; t0 += 64) {
+                        const int t = t0 + lane;
+                        const unsigned long long b = __ballot(t < nt && sm.tl[min(t, nt - 1)] <= m && m < sm.tl[min(t, nt - 1) + 1]);
+                        if (b) { tA = t0 + __builtin_ctzll(b); break; }
+                    }
+                    rows(tA, [&](int x, bool, bool iL, bool, int pl, int) {
+                        const unsigned long long b = __ballot(iL && pl == m);
+                        if (b) cutA = x - lane + __builtin_ctzll(b);
+                        return b != 0;
+                    });
+                }
+                if (m > 0) {    // j_m: the right stopper with TR - m right stoppers before it
+                    const int tq = TR - m;
+                    for (int t0 = 0; t0 < nt; t0 += 64) {
+                        const int t = t0 + lane;
+                        const unsigned long long b = __ballot(t < nt && sm.tr[min(t, nt - 1)] <= tq && tq < sm.tr[min(t, nt - 1) + 1]);
+                        if (b) { tB = t0 + __builtin_ctzll(b); break; }
+                    }
+                    rows(tB, [&](int x, bool, bool, bool iR, int, int pr) {
+                        const unsigned long long b = __ballot(iR && pr == tq);
+                        if (b) cutB = x - lane + __builtin_ctzll(b);
+                        return b != 0;
+                    });
+                }
+                if (lane == 0) {
+                    sm.m = m; sm.cutA = cutA; sm.cutB = cutB; sm.tA = tA; sm.tB = tB;
+                    if (med != f) {   // the median swap, made real
+                        const unsigned int vf = V[f], vm = V[med];
+                        K[f] = p; V[f] = vm;
+                        K[med] = k0; V[med] = vf;
+                    }
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+            const int m = sm.m;
+            if (m > 0) {
+                // (B) the m last right stoppers (tiles tB ..), by rank from the right
+                for (int t = sm.tB + wv; t < nt; t += PT_NW) {
+                    const int a = b0 + t * PT_TILE;
+                    unsigned int kk[PT_ROWS];
+#pragma unroll
+                    for (int r = 0; r < PT_ROWS; ++r) kk[r] = K[min(a + 64 * r + lane, l - 1)];
+                    int runR = sm.tr[t];
+#pragma unroll
+                    for (int r = 0; r < PT_ROWS; ++r) {
+                        const int x = a + 64 * r + lane;
+                        const bool iR = x < l && !(p < kk[r]);
+                        const unsigned long long br = __ballot(iR);
+                        const int kr = TR - 1 - (runR + slo_pcl::lane_prefix(br));
+                        if (iR && kr < m) PB[f + kr] = (unsigned int)x;
+                        runR += __popcll(br);
+                    }
+                }
+                __threadfence_block();
+                __syncthreads();
+                // (C) the m first left stoppers (tiles .. tA) swap with their partners:
+                // every swapped left stopper lies before the crossing and every
+                // partner at or after it, so no wave reads what another writes
+                const int tEnd = m < TL ? sm.tA : nt - 1;
+                for (int t = wv; t <= tEnd; t += PT_NW) {
+                    const int a = b0 + t * PT_TILE;
+                    int runL = sm.tl[t];
+                    for (int r0 = 0; r0 < PT_ROWS && a + 64 * r0 < l; r0 += 4) {
+                        unsigned int kx[4], vx[4], ky[4], vy[4];
+                        int y[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int x = min(a + 64 * (r0 + u) + lane, l - 1);
+                            kx[u] = K[x];
+                            vx[u] = V[x];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int x = a + 64 * (r0 + u) + lane;
+                            const bool iL = x < l && !(kx[u] < p);
+                            const unsigned long long bl = __ballot(iL);
+                            const int pl = runL + slo_pcl::lane_prefix(bl);
+                            y[u] = (iL && pl < m) ? pl : -1;
+                            runL += __popcll(bl);
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) y[u] = y[u] >= 0 ? (int)PB[f + y[u]] : -1;
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const int yy = y[u] >= 0 ? y[u] : f;
+                            ky[u] = K[yy];
+                            vy[u] = V[yy];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 4; ++u)
+                            if (y[u] >= 0) {
+                                const int x = a + 64 * (r0 + u) + lane;
+                                K[x] = ky[u]; V[x] = vy[u];
+                                K[y[u]] = kx[u]; V[y[u]] = vx[u];
+                            }
+                    }
+                }
+                __threadfence_block();
+            }
+            if (tid == 0) {   // the halves
+                const int cut = min(sm.cutA, m > 0 ? sm.cutB : INF);
+                wact += (unsigned long long)(l - f);
+                wpairs += (unsigned long long)m;
+                const int lo[2] = {f, cut}, hi[2] = {cut, l};
+                for (int h = 0; h < 2; ++h) {
+                    const int n = hi[h] - lo[h];
+                    if (n <= 1) continue;
+                    if (n <= PC_T) {
+                        pc_push(wl, ctr, lo[h], n, d - 1);
+                    } else if (sm.sp < 64) {   // the stack holds at most one range per depth level (+ 1)
+                        sm.sf[sm.sp] = lo[h]; sm.sl[sm.sp] = hi[h]; sm.sd[sm.sp] = d - 1; ++sm.sp;
+                    } else {                   // cannot happen; one lane finishes it exactly
+                        const int i = atomicAdd(&ctr[PCC_NW + 4], 1);
+                        wl.l[4][i] = make_int2(lo[h], n | ((d - 1) << 24));
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    if (tid == 0 && wact) {
+        atomicAdd(&pst[PW_TAIL], wact);
+        atomicAdd(&pst[PW_TAIL_PAIRS], wpairs);
+    }
+}
+
+// list 4 — a range over PC_T items whose depth budget is spent (adversarial
+// inputs only): one lane finishes it in global memory with the sequential
+// restatement (heapsort)
 __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
                                                       int* cstat, u64* scratch) {
-    const int nw = ctr[PCC_NW + 3];
+    const int nw = ctr[PCC_NW + 4];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl[e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
@@ -557,8 +843,8 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.nfin, S * sizeof(int32_t)));
         SLO_CHECK(hipMalloc(&w.cstat, 16 * sizeof(int)));
         SLO_CHECK(hipMemset(w.cstat, 0, 16 * sizeof(int)));
-        SLO_CHECK(hipMalloc(&w.pstat, 16 * sizeof(unsigned long long)));
-        SLO_CHECK(hipMemset(w.pstat, 0, 16 * sizeof(unsigned long long)));
+        SLO_CHECK(hipMalloc(&w.pstat, 32 * sizeof(unsigned long long)));
+        SLO_CHECK(hipMemset(w.pstat, 0, 32 * sizeof(unsigned long long)));
     }
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
@@ -576,7 +862,7 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.cseg[0], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
-        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 3 * wcapk)));
+        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 4 * wcapk)));
         w.wcap0 = wcap0;
         w.wcapk = wcapk;
     }
@@ -590,20 +876,15 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
 }
 
 // global levels for ranges of up to `stride` items: enough that what is left
-// fits the LDS finish.  Measured with tests/cpp/pcl_sort_model.cpp at PC_T =
-// 4096: a C3 raw scan (110 k points, 0.5 m) leaves a range over PC_T for up to
-// 13 levels, the 600 k-point surf map for 16, i.e. median-of-three
-// quicksort's depth runs to ~2 log2(n / PC_T); 2 log2(stride / PC_T) + 10
-// covers both with room (+6 measured too few on the bench's raw scans: the
-// fallback then cost more than the bench's whole sort).  An empty level
-// still costs its five launches.
-// Whatever is still over PC_T then (adversarial inputs) is finished by
-// k_pc_fallback (one lane, correct but slow).
+// is mostly at most PC_TAIL items (median-of-three quicksort's depth runs to
+// ~1.5 log2(n / PC_TAIL) on the configs' clouds); whatever is larger after the
+// G levels is stepped by k_pc_tail like the rest, only with one workgroup.  An
+// empty level still costs its five launches.
 static int pcl_levels(size_t stride) {
     int g = 0;
-    size_t x = PC_T;
-    while (x < stride) { x <<= 1; g += 2; }
-    return g ? std::min(48, g + 10) : 0;
+    size_t x = PC_TAIL;
+    while (x < stride) { x <<= 1; ++g; }
+    return g ? g + 3 : 0;
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
@@ -615,7 +896,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     PcLists L;
     L.l[0] = w.wl;
-    for (int k = 1; k < 4; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
+    for (int k = 1; k < 5; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
     unsigned int* PA = (unsigned int*)w.pairs;
     unsigned int* PB = PA + w.items;
     SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
@@ -641,11 +922,17 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
         SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(std::max(1, GS / 4)), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
                    w.cseg[cur ^ 1], L, w.ctr, cur, (int)(lv == G - 1));
     }
-    const int FG = std::max(64, std::min(4096, S * 8));
-    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[3], w.ctr, w.cstat, w.pairs);
-    SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_FT, PC_T>), dim3(FG), dim3(PC_FT), 0, K, V, L, w.ctr, 2, w.pstat);
-    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<512, PC_ST>), dim3(FG), dim3(512), 0, K, V, L, w.ctr, 1, w.pstat);
-    SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<128, PC_WT>), dim3(2 * FG), dim3(128), 0, K, V, L, w.ctr, 0, w.pstat);
+    // a workgroup per entry, grid-stride: enough to fill the chip at the LDS
+    // each size class takes (43 / 23 / 5.6 KB per entry)
+    const int FG = std::max(256, std::min(8192, S * 16));
+    SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
+               w.ctr, w.pstat);
+    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, w.pairs);
+    SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2, w.pstat,
+               w.cstat);
+    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
+               w.pstat, w.cstat);
+    SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat);
     SLO_CHECK(hipGetLastError());
     return 0;
 }

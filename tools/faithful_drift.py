@@ -51,7 +51,8 @@ def run(pid, cid, n_scans, cfg_edit=None, verbose=False):
             worst["map_rad"], worst["map_m"] = max(worst["map_rad"], r), max(worst["map_m"], t)
             ka, kb = a.get("keyposes"), b.get("keyposes")
             if len(ka) == len(kb):
-                r, t = pose_dev(ka, kb)
+                # keyposes are PointTypePose rows (x, y, z, roll, pitch, yaw)
+                r, t = pose_dev(ka.reshape(-1, 6)[:, [3, 4, 5, 0, 1, 2]], kb.reshape(-1, 6)[:, [3, 4, 5, 0, 1, 2]])
                 worst["key_rad"], worst["key_m"] = max(worst["key_rad"], r), max(worst["key_m"], t)
             else:
                 flags_diff += 1
