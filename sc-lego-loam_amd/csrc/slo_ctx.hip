@@ -686,11 +686,17 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "tobe_mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformTobeMapped, 24); count = 6; esz = 4; }
     else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
     else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
-    else if (name == "vg_stats") {   // [0] PCL-order finish ranges over the LDS capacity (slo_vgpcl.hip), [1] clipped outputs
-        int32_t a[2] = {0, 0};
-        if (ctx->pws.cstat) SLO_CHECK(hipMemcpy(&a[0], ctx->pws.cstat, 4, hipMemcpyDeviceToHost));
+    else if (name == "vg_stats") {   // PCL-order sort (slo_vgpcl.hip): [0] ranges the one-lane fallback took,
+                                     // [2] inconsistent wave-sort steps, [3] / [4] inconsistent tail cuts /
+                                     // partners (2-4 must stay 0); [1] clipped outputs
+        int32_t a[5] = {0, 0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
+        if (ctx->pws.cstat) SLO_CHECK(hipMemcpy(c, ctx->pws.cstat, 16, hipMemcpyDeviceToHost));
+        a[0] = c[0];
+        a[2] = c[1];
+        a[3] = c[2];
+        a[4] = c[3];
         SLO_CHECK(hipMemcpy(&a[1], ctx->mws.errflag, 4, hipMemcpyDeviceToHost));
-        tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;
+        tmp.resize(20); memcpy(tmp.data(), a, 20); count = 5; esz = 4;
     }
     else if (name == "pcl_work") {   // PCL-order sort work counters, cumulative (slo_vgpcl.hip PW_*)
         unsigned long long a[32] = {0};

@@ -467,7 +467,8 @@ struct PRes;
 struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the input strides only
     size_t items = 0, tiles = 0;
     int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries)
-    int* cstat = nullptr;         // [16] cumulative: [0] finish entries over the LDS capacity
+    int* cstat = nullptr;         // [16] cumulative: [0] ranges the one-lane fallback took, [1] inconsistent
+                                  // wave-sort steps, [2] / [3] inconsistent tail cuts / partners (1-3 must stay 0)
     unsigned long long* pstat = nullptr;   // [32] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch

@@ -34,14 +34,14 @@
 //     left stoppers' swaps), about 30 instructions per row and step;
 //   * 17..129 items (when TLANE is below that): wave_step, the rows held in
 //     registers across the step;
-//   * at most TLANE items, or a spent depth budget: a lane task.  Tasks queue
-//     up and 64 of them run at once, one per lane, through the sequential
-//     libstdc++ restatement (slo_sort::introsort_range: the rest of the
-//     introsort loop, heapsort when the budget is spent, and the final
-//     insertion sort restricted to the range, which is all the global final
-//     insertion sort does to it).  That replaces the many small steps at the
-//     bottom of the recursion, where a wave-wide step would leave most lanes
-//     idle.
+//   * at most TLANE (<= 64) items: wave_small_sort — one item per lane in
+//     registers, every segment of the range stepped at once (lane masks,
+//     lane permutes), the leaves ranked by (key, lane);
+//   * a spent depth budget: a lane task.  Tasks queue up and 64 of them run
+//     at once, one per lane, through the sequential libstdc++ restatement
+//     (slo_sort::introsort_range: heapsort, then the final insertion sort
+//     restricted to the range, which is all the global final insertion sort
+//     does to it).  Adversarial inputs only.
 // A full stack hands the range to a lane task (exact), a step whose cut falls
 // outside (f, l) — impossible for a correct step — as well (then sorted but not
 // necessarily in std::sort's order, instead of a hang); both count in *err,
@@ -72,6 +72,7 @@ constexpr int kStack = 64;    // wave stack entries (the depth budget, <= 62, bo
 struct WaveSmem {
     unsigned int stk[kStack];
     unsigned int q[kQ];
+    unsigned char tw[128];   // wave_small_sort's partner tables
 };
 
 __device__ __forceinline__ void wave_fence() {
@@ -342,6 +343,90 @@ __device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int 
     return min(cutA, m > 0 ? cutB : INF);
 }
 
+// ---- ranges of at most 64 items: one item per lane, in registers.  Every
+// segment still over 16 items with depth left takes its introsort step at
+// once (the wave holds several segments side by side: lane masks), the
+// median swap and the pair swaps are lane permutes, the partner of each
+// stopper comes from a 64-entry LDS table; a segment of <= 16 items (a leaf)
+// ends stably sorted — each lane's place is its rank in the leaf by (key,
+// lane).  A segment over 16 items with its depth spent (only adversarial
+// inputs) is left in place and returned for a lane task (heapsort).
+__device__ __forceinline__ unsigned long long lanes_below(int k) {   // bits [0, k), 0 <= k <= 64
+    return k >= 64 ? ~0ull : ((1ull << k) - 1ull);
+}
+__device__ __forceinline__ u64 shfl64(u64 v, int src) {
+    const unsigned int lo = (unsigned int)__shfl((int)(unsigned int)v, src, 64);
+    const unsigned int hi = (unsigned int)__shfl((int)(unsigned int)(v >> 32), src, 64);
+    return ((u64)hi << 32) | lo;
+}
+
+// items[f, f + n), n <= 64; tw: 128 bytes of this wave's LDS.  Returns the
+// lanes that start a spent-depth segment (bit lo), the segment's end in *hend
+// (per lane) for the caller's lane tasks.
+__device__ __forceinline__ unsigned long long wave_small_sort(u64* items, int f, int n, int depth, unsigned char* tw,
+                                                              int* hend) {
+    const int i = threadIdx.x & 63;
+    const bool live = i < n;
+    u64 it = items[f + min(i, n - 1)];
+    int lo = 0, hi = n, dd = depth;
+    for (;;) {
+        const bool act = live && hi - lo > 16 && dd > 0;
+        if (__ballot(act) == 0) break;
+        const int mid = lo + (hi - lo) / 2;
+        const unsigned int key0 = vkey(it);
+        const unsigned int ka = (unsigned int)__shfl((int)key0, act ? lo + 1 : i, 64);
+        const unsigned int kb = (unsigned int)__shfl((int)key0, act ? mid : i, 64);
+        const unsigned int kc = (unsigned int)__shfl((int)key0, act ? hi - 1 : i, 64);
+        const int w = median3(ka, kb, kc);
+        const int med = w == 0 ? lo + 1 : (w == 1 ? mid : hi - 1);
+        const unsigned int p = w == 0 ? ka : (w == 1 ? kb : kc);
+        it = shfl64(it, act ? (i == lo ? med : (i == med ? lo : i)) : i);   // the median swap
+        const unsigned int k = vkey(it);
+        const bool inr = act && i > lo;
+        const bool iL = inr && !(k < p), iR = inr && !(p < k);
+        const unsigned long long BL = __ballot(iL), BR = __ballot(iR);
+        const unsigned long long seg = lanes_below(hi) & ~lanes_below(lo + 1), below = lanes_below(i) & seg;
+        const int pl = __popcll(BL & below), pr = __popcll(BR & below);
+        const int TL = __popcll(BL & seg), TR = __popcll(BR & seg);
+        const unsigned long long Q = __ballot(inr && pl >= TR - pr) & seg;
+        const int X = Q ? __builtin_ctzll(Q) : hi;   // the first boundary with Lb >= Rb
+        const int prX = __shfl(pr, act && X < hi ? X : i, 64), plX1 = __shfl(pl, act && X - 1 > lo ? X - 1 : i, 64);
+        const int m = max(X < hi ? TR - prX : 0, X - 1 > lo ? plX1 : 0);
+        const unsigned long long A = __ballot(iL && pl == m) & seg, B = __ballot(iR && TR - 1 - pr == m - 1) & seg;
+        const int cut = min(m < TL && A ? __builtin_ctzll(A) : 64, m > 0 && B ? __builtin_ctzll(B) : 64);
+        // partners: left stopper of rank k <-> right stopper of rank k from the right
+        const bool sL = iL && pl < m, sR = iR && TR - 1 - pr < m;
+        if (sL) tw[lo + pl] = (unsigned char)i;
+        if (sR) tw[64 + lo + (TR - 1 - pr)] = (unsigned char)i;
+        wave_fence();
+        int src = i;
+        if (sL) src = tw[64 + lo + pl];
+        if (sR) src = tw[lo + (TR - 1 - pr)];
+        wave_fence();
+        it = shfl64(it, src);
+        if (act) {
+            if (i < cut) hi = cut;
+            else lo = cut;
+            --dd;
+        }
+    }
+    // leaves: an item's place is its rank in the leaf by (key, lane)
+    const unsigned int k = vkey(it);
+    const bool heap = live && hi - lo > 16;   // dd == 0
+    int rank = 0;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+        const int j = lo + t;
+        const unsigned int kj = (unsigned int)__shfl((int)k, min(j, 63), 64);
+        rank += (j < hi) & ((kj < k) | ((kj == k) & (j < i)));
+    }
+    wave_fence();
+    if (live) items[f + (heap ? i : lo + rank)] = it;
+    wave_fence();
+    *hend = hi;
+    return __ballot(heap && i == lo);
+}
+
 // the queued lane tasks, one per lane, through the sequential restatement
 __device__ __forceinline__ void lane_flush(u64* items, const unsigned int* q, int nq) {
     const int lane = threadIdx.x & 63;
@@ -367,17 +452,17 @@ __device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, in
 // one wave; tbl holds an entry per position (a step writes tbl[f .. f + m),
 // so waves on disjoint ranges share it).  *err (if given) counts ranges
 // handed to a lane for a reason other than their size (must stay 0).
-// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] lane tasks
+// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges
 template <int TLANE>
 __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int depth, unsigned short* tbl,
                                                 WaveSmem& ws, int* err = nullptr, long long* prof = nullptr) {
-    static_assert(TLANE >= 16, "ranges of <= 16 items are lane tasks");
+    static_assert(TLANE >= 16 && TLANE <= 64, "ranges of <= TLANE items go to wave_small_sort");
     const int lane = threadIdx.x & 63;
     if (l0 - f0 <= 1) return;
     int sp = 0, nq = 0, f = f0, l = l0, d = depth;
     for (;;) {
         const int len = l - f;
-        bool task = len <= TLANE || d == 0;
+        bool task = len <= TLANE || d == 0, stepped = false;
         int cut = 0;
         if (!task && sp == kStack) {   // cannot happen (sp <= the depth budget); exact anyway
             task = true;
@@ -388,17 +473,30 @@ __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int 
             cut = wave_step_any(items, tbl, f, l);
             if (prof) prof[len - 1 <= 128] += clock64() - t0;
             if (cut <= f || cut >= l) {   // cannot happen; sorted (not std::sort's order) rather than a hang
-                task = true;
+                task = stepped = true;
                 if (err && lane == 0) atomicAdd(err, 1);
             }
         }
         if (task) {
-            if (len >= 2) {
-                if (lane == 0) ws.q[nq] = renc(f, l, d);
+            // a spent depth budget (heapsort) or a step that failed: a lane task;
+            // otherwise a range of <= 64 items in registers, its spent-depth
+            // segments (if any) queued as lane tasks
+            unsigned long long hs = 0;
+            int hend = 0;
+            const long long t0 = prof ? clock64() : 0;
+            const bool small = len >= 2 && len <= 64 && d > 0 && !stepped;
+            if (small) hs = wave_small_sort(items, f, len, d, ws.tw, &hend);
+            else if (len >= 2) hs = 1ull;   // the whole range
+            if (prof) prof[2] += clock64() - t0;
+            while (hs) {
+                const int b = __builtin_ctzll(hs);
+                hs &= hs - 1;
+                const int e0 = small ? f + b : f;
+                const int e1 = small ? f + __shfl(hend, b, 64) : l;
+                const int de = small ? 0 : d;
+                if (lane == 0) ws.q[nq] = renc(e0, e1, de);
                 if (++nq == kQ) {
-                    const long long t0 = prof ? clock64() : 0;
                     lane_flush(items, ws.q, nq);
-                    if (prof) prof[2] += clock64() - t0;
                     nq = 0;
                 }
             }

@@ -63,7 +63,7 @@ struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
 
 // counters (PclWs::ctr)
-enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: finish list k
+enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: range list k
 
 // Range lists: finish entries by size class, list 0 <= PC_WT items, 1 <= PC_ST,
 // 2 <= PC_T (k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
@@ -515,7 +515,7 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
     long long prof[3] = {0, 0, 0};
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
-        const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
+        const int f = w.x, n = min(w.y & 0xffffff, NMAX), d = w.y >> 24;
         for (int i0 = 0; i0 < n; i0 += 8 * 64 * W) {   // eight loads of each array in flight
             unsigned int kk[8], vv[8];
 #pragma unroll
@@ -566,39 +566,44 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
 struct TailSm {
     int tl[PT_MAXT + 1], tr[PT_MAXT + 1];   // per tile stopper counts, then exclusive prefixes (+ totals)
     int sf[64], sl[64], sd[64];             // the stack of ranges still over PC_T
-    int f, l, d, sp;                        // the range in hand
+    int f, l, d, sp, have;                  // the range in hand (have: one is)
     unsigned int piv, k0;
     int med, c, m, cutA, cutB, tA, tB;
     int wsum[PT_NW];
 };
 
 __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
-                                                    int* ctr, unsigned long long* pst) {
+                                                    int* ctr, unsigned long long* pst, int* cstat) {
     __shared__ TailSm sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int INF = 0x7fffffff;
     const int nw = ctr[PCC_NW + 3];
     unsigned long long wact = 0, wpairs = 0;
+    // tid 0 pops the next range into sm.f / sm.l / sm.d with its pivot (the
+    // median swap taken virtually until the swaps); sm.have is read by every
+    // thread after a barrier and written again only before the next one
+    auto pop = [&]() {
+        if (sm.sp == 0) { sm.have = 0; return; }
+        const int q = --sm.sp, f = sm.sf[q], l = sm.sl[q];
+        sm.f = f; sm.l = l; sm.d = sm.sd[q];
+        const int mid = f + (l - f) / 2;
+        const unsigned int kf = K[f], k1 = K[f + 1], k2 = K[mid], k3 = K[l - 1];
+        const int w = slo_pcl::median3(k1, k2, k3);
+        sm.med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
+        sm.piv = w == 0 ? k1 : (w == 1 ? k2 : k3);
+        sm.k0 = kf;
+        sm.c = INF;
+        sm.have = 1;
+    };
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         if (tid == 0) {
             const int2 w = wl.l[3][e];
             sm.sf[0] = w.x; sm.sl[0] = w.x + (w.y & 0xffffff); sm.sd[0] = w.y >> 24;
             sm.sp = 1;
+            pop();
         }
         __syncthreads();
-        while (sm.sp > 0) {
-            if (tid == 0) {   // pop; the pivot (median swap taken virtually until the swaps)
-                const int q = --sm.sp, f = sm.sf[q], l = sm.sl[q];
-                sm.f = f; sm.l = l; sm.d = sm.sd[q];
-                const int mid = f + (l - f) / 2;
-                const unsigned int kf = K[f], k1 = K[f + 1], k2 = K[mid], k3 = K[l - 1];
-                const int w = slo_pcl::median3(k1, k2, k3);
-                sm.med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
-                sm.piv = w == 0 ? k1 : (w == 1 ? k2 : k3);
-                sm.k0 = kf;
-                sm.c = INF;
-            }
-            __syncthreads();
+        while (sm.have) {
             const int f = sm.f, l = sm.l, d = sm.d, med = sm.med;
             const unsigned int p = sm.piv, k0 = sm.k0;
             const int b0 = f + 1, nt = (l - b0 + PT_TILE - 1) / PT_TILE;
@@ -606,6 +611,7 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                 if (tid == 0) {
                     const int i = atomicAdd(&ctr[PCC_NW + 4], 1);
                     wl.l[4][i] = make_int2(f, (l - f) | (d << 24));
+                    pop();
                 }
                 __syncthreads();
                 continue;
@@ -763,7 +769,13 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                             runL += __popcll(bl);
                         }
 #pragma unroll
-                        for (int u = 0; u < 4; ++u) y[u] = y[u] >= 0 ? (int)PB[f + y[u]] : -1;
+                        for (int u = 0; u < 4; ++u) {
+                            y[u] = y[u] >= 0 ? (int)PB[f + y[u]] : -1;
+                            if (y[u] >= l || (y[u] >= 0 && y[u] <= f)) {   // cannot happen: counted, not followed
+                                atomicAdd(&cstat[3], 1);
+                                y[u] = -1;
+                            }
+                        }
 #pragma unroll
                         for (int u = 0; u < 4; ++u) {
                             const int yy = y[u] >= 0 ? y[u] : f;
@@ -781,8 +793,13 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                 }
                 __threadfence_block();
             }
+            __syncthreads();   // every swap is done before tid 0 reads the next range's pivot
             if (tid == 0) {   // the halves
-                const int cut = min(sm.cutA, m > 0 ? sm.cutB : INF);
+                int cut = min(sm.cutA, m > 0 ? sm.cutB : INF);
+                if (cut <= f || cut >= l) {   // cannot happen: counted; the range is left as it is
+                    atomicAdd(&cstat[2], 1);
+                    cut = l;
+                }
                 wact += (unsigned long long)(l - f);
                 wpairs += (unsigned long long)m;
                 const int lo[2] = {f, cut}, hi[2] = {cut, l};
@@ -798,9 +815,11 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                         wl.l[4][i] = make_int2(lo[h], n | ((d - 1) << 24));
                     }
                 }
+                pop();
             }
             __syncthreads();
         }
+        __syncthreads();   // every thread has read sm.have == 0 before the next entry is pushed
     }
     if (tid == 0 && wact) {
         atomicAdd(&pst[PW_TAIL], wact);
@@ -926,7 +945,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     // each size class takes (43 / 23 / 5.6 KB per entry)
     const int FG = std::max(256, std::min(8192, S * 16));
     SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
-               w.ctr, w.pstat);
+               w.ctr, w.pstat, w.cstat);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, w.pairs);
     SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2, w.pstat,
                w.cstat);

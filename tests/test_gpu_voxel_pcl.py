@@ -100,10 +100,35 @@ def test_pcl_order_map_and_raw_clouds():
         for s, c in enumerate(clouds):
             want = O.voxel_grid(c[np.isfinite(c[:, :3]).all(1)], leaf, stable=False)
             assert len(got[s]) == len(want) and mismatch(got[s], want) == 0, (leaf, s)
-        assert stats[0] == 0   # every range fit the LDS finish after the global levels
+        assert stats[0] == 0   # no range needed the one-lane fallback
+        assert stats[2] == 0 and stats[3] == 0 and stats[4] == 0   # no inconsistent wave-sort / tail step
     # the test has teeth: the stable order gives different centroids on the big cloud
     stable = O.voxel_grid(big, 0.3, stable=True)
     assert mismatch(stable, O.voxel_grid(big, 0.3, stable=False)) != 0
+
+
+def test_pcl_order_many_map_streams():
+    """eight map-like streams at once (the bench's batched regime: global
+    levels, the workgroup tail and the finish lists shared by the streams),
+    each shifted and thinned differently, against the oracle one by one"""
+    rng = np.random.default_rng(13)
+    parts = []
+    for k in range(5):
+        p = O.gen_scan(6, 3, 0, 4 * k)
+        p = p[np.isfinite(p[:, :3]).all(1)].copy()
+        p[:, 0] += np.float32(2.0 * k)
+        parts.append(p)
+    big = np.concatenate(parts)
+    clouds = []
+    for s in range(8):
+        c = big[rng.random(len(big)) < 0.6 + 0.05 * s].copy()
+        c[:, 1] += np.float32(0.37 * s)
+        clouds.append(c)
+    got, stats = run_batch(clouds, 0.3)
+    for s, c in enumerate(clouds):
+        want = O.voxel_grid(c, 0.3, stable=False)
+        assert len(got[s]) == len(want) and mismatch(got[s], want) == 0, s
+    assert stats[0] == 0 and stats[2] == 0 and stats[3] == 0 and stats[4] == 0
 
 
 def test_pcl_order_killer_sequences_and_one_voxel(model, tmp_path):

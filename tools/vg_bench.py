@@ -60,11 +60,12 @@ def main():
             ctx.synchronize()
             t = ctx.timing_read()
             st = ctx.get(0, "pcl_work").tolist()
+            vs = ctx.get(0, "vg_stats").tolist()
             ctx.close()
             res[f"{name}_vo{vo}"] = {"wall_ms": round(wall, 3), "items": S * n,
                                      "kernels_ms": {k: round(v[0] / a.reps, 3) for k, v in
                                                     sorted(t.items(), key=lambda kv: -kv[1][0])[:12]},
-                                     "pcl_work": st}
+                                     "pcl_work": st, "vg_stats": vs}
             print(name, vo, json.dumps(res[f"{name}_vo{vo}"]), flush=True)
     print(json.dumps(res))
 
