@@ -886,15 +886,20 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 }
 
 // PCL's own in-voxel order (cfg.voxel_order == SLO_VOXEL_PCL, the default):
-// one wave per ring (FA:779-780).  The bounds, the (voxel, index) keys in
-// LDS, std::sort's order by slo_pcl::wave_sort, then the voxel heads and the
-// centroids summed in that order.  PMAX: the longest ring (horizon_scan bound).
+// one workgroup of RW waves per ring (FA:779-780).  The bounds, the (voxel,
+// index) keys in LDS, std::sort's order by slo_pcl::block_sort, then the
+// voxel heads and the centroids summed in that order.  PMAX: the longest
+// ring (the horizon_scan bound).
 #ifndef RING_TLANE
 #define RING_TLANE 64
 #endif
+#ifndef RING_W
+#define RING_W 4
+#endif
 template <int PMAX>
-__global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
-    const int s = blockIdx.y, ring = blockIdx.x, lane = threadIdx.x;
+__global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
+    constexpr int NT = 64 * RING_W;
+    const int s = blockIdx.y, ring = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const size_t rr = (size_t)s * R + ring;
     const int n = v.r_lf_n[rr];
@@ -902,18 +907,21 @@ __global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
     float4* out = v.r_lf_ds + rr * C;
     __shared__ unsigned long long keys[PMAX];
     __shared__ unsigned short tbl[PMAX];
-    __shared__ slo_pcl::WaveSmem ws;
+    __shared__ slo_pcl::WaveSmem ws[RING_W];
+    __shared__ slo_pcl::BlockQ<RING_W> bq;
+    __shared__ float mm[RING_W][6];
+    __shared__ int wsum[RING_W];
     __shared__ int serr;
     if (n == 0) {
-        if (lane == 0) v.ring_cnt[rr * 4 + 3] = 0;
+        if (tid == 0) v.ring_cnt[rr * 4 + 3] = 0;
         return;
     }
     const float inv = 1.0f / v.cfg.leaf_less_flat;
     float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
-    for (int b = 0; b < n; b += 8 * 64) {   // eight loads in flight per lane
+    for (int b = 0; b < n; b += 8 * NT) {   // eight loads in flight per thread
         float4 pp[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * 64 + lane, n - 1)];
+        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * NT + tid, n - 1)];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             mnx = fminf(mnx, pp[u].x); mny = fminf(mny, pp[u].y); mnz = fminf(mnz, pp[u].z);
@@ -926,24 +934,33 @@ __global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
         mnz = fminf(mnz, __shfl_xor(mnz, o, 64)); mxx = fmaxf(mxx, __shfl_xor(mxx, o, 64));
         mxy = fmaxf(mxy, __shfl_xor(mxy, o, 64)); mxz = fmaxf(mxz, __shfl_xor(mxz, o, 64));
     }
+    if (lane == 0) {
+        mm[wv][0] = mnx; mm[wv][1] = mny; mm[wv][2] = mnz; mm[wv][3] = mxx; mm[wv][4] = mxy; mm[wv][5] = mxz;
+    }
+    if (tid == 0) serr = 0;
+    __syncthreads();
+    for (int w = 0; w < RING_W; ++w) {   // min / max are exact: any order gives the same bounds
+        mnx = fminf(mnx, mm[w][0]); mny = fminf(mny, mm[w][1]); mnz = fminf(mnz, mm[w][2]);
+        mxx = fmaxf(mxx, mm[w][3]); mxy = fmaxf(mxy, mm[w][4]); mxz = fmaxf(mxz, mm[w][5]);
+    }
     const long long dx = (long long)((mxx - mnx) * inv) + 1, dy = (long long)((mxy - mny) * inv) + 1,
                     dz = (long long)((mxz - mnz) * inv) + 1;
     if (dx * dy * dz > 2147483647LL) {  // PCL: integer indices would overflow -> output = input
-        for (int i = lane; i < n; i += 64) out[i] = in[i];
-        if (lane == 0) v.ring_cnt[rr * 4 + 3] = n;
+        for (int i = tid; i < n; i += NT) out[i] = in[i];
+        if (tid == 0) v.ring_cnt[rr * 4 + 3] = n;
         return;
     }
     const int minbx = (int)floorf(mnx * inv), minby = (int)floorf(mny * inv), minbz = (int)floorf(mnz * inv);
     const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
     const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
     const int mul1 = divx, mul2 = divx * divy;
-    for (int b = 0; b < n; b += 8 * 64) {
+    for (int b = 0; b < n; b += 8 * NT) {
         float4 pp[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * 64 + lane, n - 1)];
+        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * NT + tid, n - 1)];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const int i = b + u * 64 + lane;
+            const int i = b + u * NT + tid;
             const int ijk0 = (int)(floorf(pp[u].x * inv) - (float)minbx);
             const int ijk1 = (int)(floorf(pp[u].y * inv) - (float)minby);
             const int ijk2 = (int)(floorf(pp[u].z * inv) - (float)minbz);
@@ -951,13 +968,12 @@ __global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
             if (i < n) keys[i] = ((unsigned long long)idx << 32) | (unsigned int)i;
         }
     }
-    if (lane == 0) serr = 0;
-    slo_pcl::wave_fence();
-    slo_pcl::wave_sort<RING_TLANE>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, &serr);
-    if (lane == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
-    // voxel heads: a lane per contiguous chunk, ranks by a wave scan
-    const int chunk = (n + 63) / 64;
-    const int i0 = min(n, lane * chunk), i1 = min(n, i0 + chunk);
+    __syncthreads();
+    slo_pcl::block_sort<RING_TLANE, RING_W>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr);
+    if (tid == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
+    // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan
+    const int chunk = (n + NT - 1) / NT;
+    const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
     int heads = 0;
     for (int i = i0; i < i1; ++i) heads += (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32));
     int incl = heads;
@@ -966,7 +982,14 @@ __global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
         const int y = __shfl_up(incl, o, 64);
         if (lane >= o) incl += y;
     }
-    int rank = incl - heads;
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < RING_W; ++w) {
+        if (w < wv) before += wsum[w];
+        total += wsum[w];
+    }
+    int rank = before + incl - heads;
     for (int i = i0; i < i1; ++i) {   // each voxel that starts in the chunk, summed in the sorted order
         if (!(i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32))) continue;
         const unsigned int vid = (unsigned int)(keys[i] >> 32);
@@ -980,7 +1003,7 @@ __global__ void __launch_bounds__(64) k_fa_ring_ds_pcl(DevView v) {
         const float cnt = (float)(e - i);
         out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
     }
-    if (lane == 63) v.ring_cnt[rr * 4 + 3] = incl;
+    if (tid == 0) v.ring_cnt[rr * 4 + 3] = total;
 }
 
 // concatenate per-ring outputs in ring order: one block per (ring, stream),
@@ -1036,11 +1059,11 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
-    if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // one wave per ring; slo_create refuses rings over 4096 points
+    if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // RING_W waves per ring; slo_create refuses rings over 4096 points
         if (v.cfg.horizon_scan <= 2048)
-            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<2048>, dim3(R, S), dim3(64), 0, v);
+            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<2048>, dim3(R, S), dim3(64 * RING_W), 0, v);
         else
-            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<4096>, dim3(R, S), dim3(64), 0, v);
+            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<4096>, dim3(R, S), dim3(64 * RING_W), 0, v);
     } else {
         int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
         while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;

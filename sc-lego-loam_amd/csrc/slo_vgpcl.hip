@@ -44,9 +44,11 @@ using slo_pcl::u64;
 
 #define PC_CH 4096        // positions per chunk of the global levels (256 threads x 16)
 #define PC_CT 256
+#ifndef PC_T
 #define PC_T 4096         // a range of at most PC_T items is finished in LDS
-#define PC_ST 2048        // finish size classes: <= PC_WT, <= PC_ST, <= PC_T items (LDS per wave)
+#define PC_ST 2048        // finish size classes: <= PC_WT, <= PC_ST, <= PC_T items (LDS per entry)
 #define PC_WT 512
+#endif
 #ifndef PC_TAIL
 #define PC_TAIL 65536     // the global levels take ranges of more than PC_TAIL items, k_pc_tail the rest
 #endif
@@ -653,23 +655,28 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
             for (int t = tid; t < nt; t += PT_NT)
                 if (sm.tl[t + 1] >= TR - sm.tr[t + 1]) atomicMin(&sm.c, t);
             __syncthreads();
-            if (wv == 0) {   // m, then the cuts, by the first wave
-                // a tile's rows in order: per lane the exclusive prefixes; fn(r, x, act, iL, iR, pl, pr) -> stop
-                auto rows = [&](int t, auto&& fn) {
-                    const int a = b0 + t * PT_TILE;
-                    int runL = sm.tl[t], runR = sm.tr[t];
-                    for (int r = 0; r < PT_ROWS && a + 64 * r < l; ++r) {
-                        const int x = a + 64 * r + lane;
-                        unsigned int k = K[min(x, l - 1)];
-                        k = x == med ? k0 : k;
-                        const bool act = x < l, iL = act && !(k < p), iR = act && !(p < k);
-                        const unsigned long long bl = __ballot(iL), br = __ballot(iR);
-                        const int pl = runL + slo_pcl::lane_prefix(bl), pr = runR + slo_pcl::lane_prefix(br);
-                        if (fn(x, act, iL, iR, pl, pr)) return;
-                        runL += __popcll(bl);
-                        runR += __popcll(br);
-                    }
-                };
+            // a tile's rows in order, the tile's keys loaded at once: per lane the
+            // exclusive prefixes; fn(x, act, iL, iR, pl, pr) -> stop
+            auto rows = [&](int t, auto&& fn) {
+                const int a = b0 + t * PT_TILE;
+                unsigned int kk[PT_ROWS];
+#pragma unroll
+                for (int r = 0; r < PT_ROWS; ++r) kk[r] = K[min(a + 64 * r + lane, l - 1)];
+                int runL = sm.tl[t], runR = sm.tr[t];
+#pragma unroll
+                for (int r = 0; r < PT_ROWS; ++r) {
+                    if (a + 64 * r >= l) return;
+                    const int x = a + 64 * r + lane;
+                    const unsigned int k = x == med ? k0 : kk[r];
+                    const bool act = x < l, iL = act && !(k < p), iR = act && !(p < k);
+                    const unsigned long long bl = __ballot(iL), br = __ballot(iR);
+                    const int pl = runL + slo_pcl::lane_prefix(bl), pr = runR + slo_pcl::lane_prefix(br);
+                    if (fn(x, act, iL, iR, pl, pr)) return;
+                    runL += __popcll(bl);
+                    runR += __popcll(br);
+                }
+            };
+            if (wv == 0) {   // m, by the first wave, from the crossing tile
                 const int c = sm.c;
                 int m = -1, lastPl = 0;
                 rows(c, [&](int x, bool act, bool, bool, int pl, int pr) {
@@ -685,44 +692,47 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                     return false;
                 });
                 if (m < 0) m = max(TR - sm.tr[c + 1], lastPl);   // X = the tile's end boundary
-                int cutA = INF, cutB = INF, tA = nt - 1, tB = 0;
-                if (m < TL) {   // i_{m+1}: the left stopper of rank m
-                    for (int t0 = 0; t0 < nt; t0 += 64) {
-                        const int t = t0 + lane;
-                        const unsigned long long b = __ballot(t < nt && sm.tl[min(t, nt - 1)] <= m && m < sm.tl[min(t, nt - 1) + 1]);
-                        if (b) { tA = t0 + __builtin_ctzll(b); break; }
-                    }
-                    rows(tA, [&](int x, bool, bool iL, bool, int pl, int) {
-                        const unsigned long long b = __ballot(iL && pl == m);
-                        if (b) cutA = x - lane + __builtin_ctzll(b);
-                        return b != 0;
-                    });
+                if (lane == 0) { sm.m = m; sm.cutA = INF; sm.cutB = INF; sm.tA = nt - 1; sm.tB = 0; }
+            }
+            __syncthreads();
+            const int m = sm.m;
+            if (wv == 0 && m < TL) {   // i_{m+1}: the left stopper of rank m
+                int tA = nt - 1, cutA = INF;
+                for (int t0 = 0; t0 < nt; t0 += 64) {
+                    const int t = t0 + lane;
+                    const unsigned long long b = __ballot(t < nt && sm.tl[min(t, nt - 1)] <= m && m < sm.tl[min(t, nt - 1) + 1]);
+                    if (b) { tA = t0 + __builtin_ctzll(b); break; }
                 }
-                if (m > 0) {    // j_m: the right stopper with TR - m right stoppers before it
-                    const int tq = TR - m;
-                    for (int t0 = 0; t0 < nt; t0 += 64) {
-                        const int t = t0 + lane;
-                        const unsigned long long b = __ballot(t < nt && sm.tr[min(t, nt - 1)] <= tq && tq < sm.tr[min(t, nt - 1) + 1]);
-                        if (b) { tB = t0 + __builtin_ctzll(b); break; }
-                    }
-                    rows(tB, [&](int x, bool, bool, bool iR, int, int pr) {
-                        const unsigned long long b = __ballot(iR && pr == tq);
-                        if (b) cutB = x - lane + __builtin_ctzll(b);
-                        return b != 0;
-                    });
+                rows(tA, [&](int x, bool, bool iL, bool, int pl, int) {
+                    const unsigned long long b = __ballot(iL && pl == m);
+                    if (b) cutA = x - lane + __builtin_ctzll(b);
+                    return b != 0;
+                });
+                if (lane == 0) { sm.cutA = cutA; sm.tA = tA; }
+            }
+            if (wv == 1 && m > 0) {    // j_m: the right stopper with TR - m right stoppers before it
+                const int tq = TR - m;
+                int tB = 0, cutB = INF;
+                for (int t0 = 0; t0 < nt; t0 += 64) {
+                    const int t = t0 + lane;
+                    const unsigned long long b = __ballot(t < nt && sm.tr[min(t, nt - 1)] <= tq && tq < sm.tr[min(t, nt - 1) + 1]);
+                    if (b) { tB = t0 + __builtin_ctzll(b); break; }
                 }
-                if (lane == 0) {
-                    sm.m = m; sm.cutA = cutA; sm.cutB = cutB; sm.tA = tA; sm.tB = tB;
-                    if (med != f) {   // the median swap, made real
-                        const unsigned int vf = V[f], vm = V[med];
-                        K[f] = p; V[f] = vm;
-                        K[med] = k0; V[med] = vf;
-                    }
-                }
+                rows(tB, [&](int x, bool, bool, bool iR, int, int pr) {
+                    const unsigned long long b = __ballot(iR && pr == tq);
+                    if (b) cutB = x - lane + __builtin_ctzll(b);
+                    return b != 0;
+                });
+                if (lane == 0) { sm.cutB = cutB; sm.tB = tB; }
+            }
+            __syncthreads();
+            if (tid == 0 && med != f) {   // the median swap, made real
+                const unsigned int vf = V[f], vm = V[med];
+                K[f] = p; V[f] = vm;
+                K[med] = k0; V[med] = vf;
             }
             __threadfence_block();
             __syncthreads();
-            const int m = sm.m;
             if (m > 0) {
                 // (B) the m last right stoppers (tiles tB ..), by rank from the right
                 for (int t = sm.tB + wv; t < nt; t += PT_NW) {
