@@ -52,6 +52,12 @@ using slo_pcl::u64;
 #ifndef PC_TAIL
 #define PC_TAIL 65536     // the global levels take ranges of more than PC_TAIL items, k_pc_tail the rest
 #endif
+#ifndef PC_FEW
+#define PC_FEW 8          // at most this many streams: PC_TAIL_FEW, and 16 / 8 waves per finish entry
+#endif
+#ifndef PC_TAIL_FEW
+#define PC_TAIL_FEW 16384
+#endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
 // PclWs::pstat, cumulative work counters (slo_get "pcl_work"; the bench
 // prices the kernels' algorithmic bytes with them): [0] items of the ranges
@@ -114,7 +120,7 @@ __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, 
 }
 
 // per stream: tile prefix of the finite counts, and the stream's first range
-__global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
+__global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
                                                   PSeg* seg0, int* cseg0, PcLists wl, int* ctr, int32_t* nfin,
                                                   unsigned long long* pst) {
     __shared__ int wsum[16];
@@ -141,7 +147,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(const int32_t* off, const VgPa
         // overflow keys are the positions: already in order
         if (!p.overflow && n >= 2) {
             const int d = 2 * slo_pcl::lg2(n);
-            if (n > PC_TAIL) {
+            if (n > tail_min) {
                 const int nch = (n - 1 + PC_CH - 1) / PC_CH;
                 const int slot = atomicAdd(&ctr[PCC_NSEG], 1);
                 const int c0 = atomicAdd(&ctr[PCC_NCH], nch);
@@ -428,7 +434,7 @@ __global__ void __launch_bounds__(256) k_pc_lpairs(unsigned int* K, unsigned int
 // chunks and finish entries are counted by block scans and claimed with one
 // atomic per counter (the device-wide counters live in memory shared by all
 // XCDs: an atomic per range serialises there)
-__global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* res, PSeg* nseg, int* ncseg,
+__global__ void __launch_bounds__(256) k_pc_lsplit(int tail_min, const PSeg* seg, const PRes* res, PSeg* nseg, int* ncseg,
                                                     PcLists wl, int* ctr, int cur, int last) {
     __shared__ unsigned int wsum[4];
     __shared__ int base_s[6];
@@ -446,7 +452,7 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(const PSeg* seg, const PRes* 
             for (int h = 0; h < 2; ++h) {
                 const int n = hi[h] - lo[h];
                 if (n <= 1) continue;
-                if (n > PC_TAIL && D > 0 && !last) {
+                if (n > tail_min && D > 0 && !last) {
                     kind[h] = 4;
                     nch[h] = (n - 1 + PC_CH - 1) / PC_CH;
                 } else {
@@ -909,9 +915,9 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
 // ~1.5 log2(n / PC_TAIL) on the configs' clouds); whatever is larger after the
 // G levels is stepped by k_pc_tail like the rest, only with one workgroup.  An
 // empty level still costs its five launches.
-static int pcl_levels(size_t stride) {
+static int pcl_levels(size_t stride, int tail_min) {
     int g = 0;
-    size_t x = PC_TAIL;
+    size_t x = (size_t)tail_min;
     while (x < stride) { x <<= 1; ++g; }
     return g ? g + 3 : 0;
 }
@@ -930,11 +936,16 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     unsigned int* PB = PA + w.items;
     SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
                w.ctr);
-    SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
+    // a few streams leave most of the chip idle: smaller tail ranges (more
+    // global levels, each parallel within a range) and more waves per finish
+    // entry cut the latency of the one range a workgroup works through
+    const bool few = S <= PC_FEW;
+    const int tail_min = few ? PC_TAIL_FEW : PC_TAIL;
+    SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, tail_min, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
                w.ctr, w.nfin, w.pstat);
     SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
-    const int G = pcl_levels(in_stride);
+    const int G = pcl_levels(in_stride, tail_min);
     for (int lv = 0; lv < G; ++lv) {
         const int cur = lv & 1;
         // the grid-stride kernels take whatever the level holds; past the first
@@ -948,7 +959,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
                    w.res, PA, PB, w.ctr, cur);
         SLO_LAUNCH(ctx, "pc_lpairs", k_pc_lpairs, dim3(GG), dim3(256), 0, K, V, w.seg[cur], w.cseg[cur], w.res, PA, PB,
                    w.ctr, cur);
-        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(std::max(1, GS / 4)), dim3(256), 0, w.seg[cur], w.res, w.seg[cur ^ 1],
+        SLO_LAUNCH(ctx, "pc_lsplit", k_pc_lsplit, dim3(std::max(1, GS / 4)), dim3(256), 0, tail_min, w.seg[cur], w.res, w.seg[cur ^ 1],
                    w.cseg[cur ^ 1], L, w.ctr, cur, (int)(lv == G - 1));
     }
     // a workgroup per entry, grid-stride: enough to fill the chip at the LDS
@@ -957,10 +968,17 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
                w.ctr, w.pstat, w.cstat);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, w.pairs);
-    SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2, w.pstat,
-               w.cstat);
-    SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
-               w.pstat, w.cstat);
+    if (few) {
+        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
+                   w.cstat);
+        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
+                   w.cstat);
+    } else {
+        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
+                   w.pstat, w.cstat);
+        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
+                   w.pstat, w.cstat);
+    }
     SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat);
     SLO_CHECK(hipGetLastError());
     return 0;

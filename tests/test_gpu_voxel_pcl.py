@@ -108,9 +108,11 @@ def test_pcl_order_map_and_raw_clouds():
 
 
 def test_pcl_order_many_map_streams():
-    """eight map-like streams at once (the bench's batched regime: global
-    levels, the workgroup tail and the finish lists shared by the streams),
-    each shifted and thinned differently, against the oracle one by one"""
+    """twelve map-like streams at once (the bench's batched regime, more than
+    PC_FEW streams: global levels down to 64 Ki-item ranges, the workgroup
+    tail, four waves per finish entry), each shifted and thinned differently,
+    against the oracle one by one; test_pcl_order_map_and_raw_clouds (six
+    streams) covers the few-streams shape (16 Ki tail ranges, 16 / 8 waves)"""
     rng = np.random.default_rng(13)
     parts = []
     for k in range(5):
@@ -120,8 +122,8 @@ def test_pcl_order_many_map_streams():
         parts.append(p)
     big = np.concatenate(parts)
     clouds = []
-    for s in range(8):
-        c = big[rng.random(len(big)) < 0.6 + 0.05 * s].copy()
+    for s in range(12):
+        c = big[rng.random(len(big)) < 0.4 + 0.05 * s].copy()
         c[:, 1] += np.float32(0.37 * s)
         clouds.append(c)
     got, stats = run_batch(clouds, 0.3)
