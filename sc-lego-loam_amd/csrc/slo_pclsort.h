@@ -526,13 +526,150 @@ __device__ __forceinline__ void wave_sort(u64* items, int n, int depth, unsigned
     wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws, err, prof);
 }
 
-// W waves on one range: the first levels breadth first (level k steps its
-// 2^k ranges on as many waves) until there are 2W ranges, which the waves
-// then take one at a time (an LDS counter) and finish depth first.
+// one introsort step of [f, l) (l - f - 1 <= 4096) by all W waves of the
+// workgroup: stream_step with its rows dealt round-robin to the waves — the
+// per-row stopper counts in LDS, m and the cuts by the first wave from the
+// row prefixes (one row per lane, as stream_step keeps them), barriers
+// between the passes.  Every swapped left stopper lies before the crossing
+// and every partner at or after it, so a wave reads no position another
+// wave writes except partners past the crossing, whose left-stopper flags
+// can only turn on (a right stopper's place takes a left stopper's item):
+// the prefixes of the positions that swap stay exact.
+struct BlockStepSm {
+    int rl[65], rr[65];   // per row stopper counts, then exclusive prefixes
+    int m, cutA, cutB, rA, rB;
+};
+template <int W>
+__device__ __forceinline__ int block_step(u64* items, unsigned short* tbl, int f, int l, BlockStepSm& bs) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    constexpr int INF = 0x7fffffff;
+    const unsigned int* K = reinterpret_cast<const unsigned int*>(items);
+    const int mid = f + (l - f) / 2;
+    const u64 a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+    const int w = median3(vkey(a1), vkey(a2), vkey(a3));
+    const int med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
+    const u64 pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
+    const unsigned int p = vkey(pit), k0 = vkey(a0);
+    const int b0 = f + 1, R = (l - b0 + 63) >> 6;
+    // (1) stopper counts per row (the median swap virtual)
+    for (int r0 = wv; r0 < R; r0 += 4 * W) {
+        unsigned int kk[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u * W) + lane, l - 1) + 1];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int r = r0 + u * W;
+            if (r < R) {
+                const int x = b0 + 64 * r + lane;
+                const unsigned int k = x == med ? k0 : kk[u];
+                const int cl = __popcll(__ballot(x < l && !(k < p))), cr = __popcll(__ballot(x < l && !(p < k)));
+                if (lane == 0) { bs.rl[r] = cl; bs.rr[r] = cr; }
+            }
+        }
+    }
+    __syncthreads();
+    if (wv == 0) {   // (2) the prefixes (lane r = row r), m, the cuts; the median swap made real
+        const int cl = lane < R ? bs.rl[lane] : 0, cr = lane < R ? bs.rr[lane] : 0;
+        int il = cl, ir = cr;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int yl = __shfl_up(il, o, 64), yr = __shfl_up(ir, o, 64);
+            if (lane >= o) { il += yl; ir += yr; }
+        }
+        const int rowL = il - cl, rowR = ir - cr;
+        const int TL = __shfl(il, 63, 64), TR = __shfl(ir, 63, 64);
+        int eL = il, eR = ir;   // stoppers before the row's end
+        const int c = __builtin_ctzll(__ballot(lane < R && eL >= TR - eR));
+        auto row_flags = [&](int r, bool& iL, bool& iR, int& pl, int& pr) {
+            const int x = b0 + 64 * r + lane;
+            unsigned int k = K[2 * min(x, l - 1) + 1];
+            k = x == med ? k0 : k;
+            const bool act = x < l;
+            iL = act && !(k < p);
+            iR = act && !(p < k);
+            pl = __builtin_amdgcn_readlane(rowL, r) + lane_prefix(__ballot(iL));
+            pr = __builtin_amdgcn_readlane(rowR, r) + lane_prefix(__ballot(iR));
+        };
+        int m;
+        {
+            bool iL, iR;
+            int pl, pr;
+            row_flags(c, iL, iR, pl, pr);
+            const int bc = b0 + 64 * c;
+            const unsigned long long fx = __ballot(bc + lane < l && pl >= TR - pr);
+            if (fx) {
+                const int xl = __builtin_ctzll(fx);
+                m = TR - __builtin_amdgcn_readlane(pr, xl);
+                if (xl > 0) m = max(m, __builtin_amdgcn_readlane(pl, xl - 1));
+            } else {
+                const int last = min(63, l - 1 - bc);
+                m = max(TR - __builtin_amdgcn_readlane(eR, c), __builtin_amdgcn_readlane(pl, last));
+            }
+        }
+        int cutA = INF, cutB = INF, rA = R - 1, rB = 0;
+        if (m < TL) {
+            rA = __builtin_ctzll(__ballot(lane < R && rowL <= m && m < eL));
+            bool iL, iR;
+            int pl, pr;
+            row_flags(rA, iL, iR, pl, pr);
+            cutA = b0 + 64 * rA + __builtin_ctzll(__ballot(iL && pl == m));
+        }
+        if (m > 0) {
+            const int t = TR - m;
+            rB = __builtin_ctzll(__ballot(lane < R && rowR <= t && t < eR));
+            bool iL, iR;
+            int pl, pr;
+            row_flags(rB, iL, iR, pl, pr);
+            cutB = b0 + 64 * rB + __builtin_ctzll(__ballot(iR && pr == t));
+        }
+        if (lane < R) { bs.rl[lane] = rowL; bs.rr[lane] = rowR; }
+        if (lane == 0) {
+            bs.m = m; bs.cutA = cutA; bs.cutB = cutB; bs.rA = m < TL ? rA : R - 1; bs.rB = rB;
+            items[f] = pit;
+            items[med] = a0;
+        }
+        bs.rl[64] = TR;   // (every lane writes the same value)
+    }
+    __syncthreads();
+    const int m = bs.m, TR = bs.rl[64];
+    if (m > 0) {
+        // (3) the m last right stoppers, by rank from the right
+        const int rB = bs.rB;
+        for (int r = rB + wv; r < R; r += W) {
+            const int x = b0 + 64 * r + lane;
+            const bool iR = x < l && !(p < K[2 * min(x, l - 1) + 1]);
+            const int kr = TR - 1 - (bs.rr[r] + lane_prefix(__ballot(iR)));
+            if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
+        }
+        __syncthreads();
+        // (4) the m first left stoppers swap with their partners
+        const int rEnd = bs.rA;
+        for (int r = wv; r <= rEnd; r += W) {
+            const int x = b0 + 64 * r + lane;
+            const u64 it = items[min(x, l - 1)];
+            const bool iL = x < l && !(vkey(it) < p);
+            const int pl = bs.rl[r] + lane_prefix(__ballot(iL));
+            if (iL && pl < m) {
+                const int y = tbl[f + pl];
+                const u64 py = items[y];
+                items[x] = py;
+                items[y] = it;
+            }
+        }
+        __syncthreads();
+    }
+    return min(bs.cutA, m > 0 ? bs.cutB : INF);
+}
+
+// W waves on one range: the first levels breadth first — while a level has
+// at most W / 2 ranges the whole workgroup steps each (block_step), then one
+// wave per range — until there are 2W ranges, which the waves then take one
+// at a time (an LDS counter) and finish depth first.
 template <int W>
 struct BlockQ {
     unsigned int cur[2 * W], nxt[2 * W];
     int ncur, take;
+    BlockStepSm bs;
 };
 
 template <int TLANE, int W>
@@ -551,22 +688,27 @@ __device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigne
     __syncthreads();
     for (int k = 1; k < 2 * W; k <<= 1) {
         const int nc = bq.ncur;
-        for (int i = wv; i < nc; i += W) {
+        // the first levels (fewer ranges than waves, the largest steps) are
+        // taken by the whole workgroup one range at a time
+        const bool coop = 2 * nc <= W;
+        for (int i = coop ? 0 : wv; i < nc; i += coop ? 1 : W) {
             const unsigned int e = bq.cur[i];
             const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
             unsigned int a = e, b = 0;
             if (l - f > TLANE && d > 0) {
                 const long long t0 = prof ? clock64() : 0;
-                const int cut = wave_step_any(items, tbl, f, l);
+                const int cut = coop && l - f - 1 > 128 ? block_step<W>(items, tbl, f, l, bq.bs)
+                              : (!coop || wv == 0) ? wave_step_any(items, tbl, f, l) : 0;
                 if (prof) prof[l - f - 1 <= 128] += clock64() - t0;
                 if (cut > f && cut < l) {
                     a = renc(f, cut, d - 1);
                     b = renc(cut, l, d - 1);
-                } else if (err && lane == 0) {
+                } else if (err && lane == 0 && (!coop || wv == 0)) {
                     atomicAdd(err, 1);
                 }
             }
-            if (lane == 0) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
+            if (lane == 0 && (!coop || wv == 0)) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
+            if (coop) __syncthreads();   // the next range's step reads what this one wrote
         }
         __syncthreads();
         if (threadIdx.x == 0) {   // the next level's ranges of two or more items
