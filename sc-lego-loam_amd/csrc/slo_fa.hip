@@ -894,11 +894,11 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #define RING_TLANE 64
 #endif
 #ifndef RING_W
-#define RING_W 4
+#define RING_W 4            // waves per ring; 16 when the context has a few streams (latency)
 #endif
-template <int PMAX>
-__global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
-    constexpr int NT = 64 * RING_W;
+template <int PMAX, int RW>
+__global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
+    constexpr int NT = 64 * RW;
     const int s = blockIdx.y, ring = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const size_t rr = (size_t)s * R + ring;
@@ -907,10 +907,10 @@ __global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
     float4* out = v.r_lf_ds + rr * C;
     __shared__ unsigned long long keys[PMAX];
     __shared__ unsigned short tbl[PMAX];
-    __shared__ slo_pcl::WaveSmem ws[RING_W];
-    __shared__ slo_pcl::BlockQ<RING_W> bq;
-    __shared__ float mm[RING_W][6];
-    __shared__ int wsum[RING_W];
+    __shared__ slo_pcl::WaveSmem ws[RW];
+    __shared__ slo_pcl::BlockQ<RW> bq;
+    __shared__ float mm[RW][6];
+    __shared__ int wsum[RW];
     __shared__ int serr;
     if (n == 0) {
         if (tid == 0) v.ring_cnt[rr * 4 + 3] = 0;
@@ -939,7 +939,7 @@ __global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
     }
     if (tid == 0) serr = 0;
     __syncthreads();
-    for (int w = 0; w < RING_W; ++w) {   // min / max are exact: any order gives the same bounds
+    for (int w = 0; w < RW; ++w) {   // min / max are exact: any order gives the same bounds
         mnx = fminf(mnx, mm[w][0]); mny = fminf(mny, mm[w][1]); mnz = fminf(mnz, mm[w][2]);
         mxx = fmaxf(mxx, mm[w][3]); mxy = fmaxf(mxy, mm[w][4]); mxz = fmaxf(mxz, mm[w][5]);
     }
@@ -969,7 +969,7 @@ __global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
         }
     }
     __syncthreads();
-    slo_pcl::block_sort<RING_TLANE, RING_W>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr);
+    slo_pcl::block_sort<RING_TLANE, RW>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr);
     if (tid == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
     // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan
     const int chunk = (n + NT - 1) / NT;
@@ -985,7 +985,7 @@ __global__ void __launch_bounds__(64 * RING_W) k_fa_ring_ds_pcl(DevView v) {
     if (lane == 63) wsum[wv] = incl;
     __syncthreads();
     int before = 0, total = 0;
-    for (int w = 0; w < RING_W; ++w) {
+    for (int w = 0; w < RW; ++w) {
         if (w < wv) before += wsum[w];
         total += wsum[w];
     }
@@ -1060,10 +1060,14 @@ int fa_features_run(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // RING_W waves per ring; slo_create refuses rings over 4096 points
-        if (v.cfg.horizon_scan <= 2048)
-            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<2048>, dim3(R, S), dim3(64 * RING_W), 0, v);
-        else
-            SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds_pcl<4096>, dim3(R, S), dim3(64 * RING_W), 0, v);
+        const bool few = S <= 8;
+        if (v.cfg.horizon_scan <= 2048) {
+            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<2048, 16>), dim3(R, S), dim3(64 * 16), 0, v);
+            else SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<2048, RING_W>), dim3(R, S), dim3(64 * RING_W), 0, v);
+        } else {
+            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<4096, 16>), dim3(R, S), dim3(64 * 16), 0, v);
+            else SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<4096, RING_W>), dim3(R, S), dim3(64 * RING_W), 0, v);
+        }
     } else {
         int ds_keys = 256;   // LDS keys of k_fa_ring_ds: a ring holds <= horizon_scan points
         while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
