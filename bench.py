@@ -24,17 +24,19 @@ host generator the CPU baseline uses.  A one-stream leg (single_stream)
 reports the same pipeline for a single C3 stream: scans/s and per-scan
 latency.
 
-roofline: the dominant kernel (--roofline-kernel, vg_scatter: the largest
-single kernel by device time, the VoxelGrid radix scatter) timed by in-stream
-device timestamps on its context's stream inside the timed region (the same
-for --roofline-also, mo_knn, reported under roofline_also); achieved = its
+roofline: the dominant kernel (--roofline-kernel auto: the largest single
+kernel by device time in the instrumented pass — with the reference's
+VoxelGrid order, pc_finish_b, the LDS finish of the PCL-order sort) timed by
+in-stream device timestamps on its context's stream inside the timed region
+(the same for --roofline-also, reported under roofline_also); achieved = its
 algorithmic bytes per launch (DESIGN.md "Roofline", from the per-stream counts
 of a separate instrumented pass with the same
 launch mix) / that average launch time, against HBM peak.  `isolated` repeats
 it for the instrumented pass, where the contexts run one after the other.  cpu_baseline: the
 oracle (oracle/, C++ restatement of the reference path), rank 0 at N = 1, on
-the same steady-state window: (B) one stream per host core available to the
-process (sched_getaffinity), --cpu-scans scans each after the pre-roll;
+the same steady-state window: (B) one stream per usable host core (min of
+sched_getaffinity and the cgroup CPU quota), --cpu-scans scans each after the
+pre-roll;
 (A) the reference's topology — one stream as a 3-stage pipeline
 (imageProjection | featureAssociation | mapOptimization, launch/run.launch) on
 3 cores — bounded by its slowest stage's per-scan time, measured.
@@ -79,7 +81,7 @@ def parse():
                     help="extra Scan Context history per stream (scans before scan 0, a KITTI-00 mid-drive history: "
                          "detects search ~1000 keyframes, SCc:264-289); the pre-roll builds the recent part")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="mo_knn,vg_scatter,pc_lpairs,fa_search_corner",
+    ap.add_argument("--roofline-also", default="mo_knn,pc_tail,pc_lpairs,fa_search_corner",
                     help="further kernels timed live the same way, reported under roofline_also (comma list)")
     ap.add_argument("--roofline-kernel", default="auto",
                     help="kernel timed inside the timed region (the roofline's kernel); auto = the largest kernel by "
@@ -185,6 +187,10 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
             return int(40 * pw[1])
         if name in ("pc_finish_w", "pc_finish_s", "pc_finish_b"):   # a finish entry's items in and out
             return int(16 * pw[2 + ("pc_finish_w", "pc_finish_s", "pc_finish_b").index(name)])
+        if name == "pc_tail":     # per stepped item: its key counted (4 B) and read again on its side of the
+            # crossing (4 B) plus the left side's index (4 B); per pair: partner position out and in, both
+            # items read and written
+            return int(12 * pw[7] + 40 * pw[8])
         if name == "pc_count":    # the points
             return int(16 * pw[5])
         if name == "pc_write":    # the points in, (key, index) out

@@ -191,7 +191,10 @@ int slo_batch_sc_distance(slo_ctx* ctx, const double* d_sc1, const double* d_sc2
  * order, to d_out + s * out_stride, at most out_cap (more are clipped and
  * flagged in slo_get(.., "vg_stats")[1]), their count to d_nout[s].  The
  * order inside a voxel follows cfg.voxel_order (SLO_VOXEL_PCL: std::sort's,
- * as PCL).  Asynchronous on slo_stream(ctx). */
+ * as PCL).  vg_stats[0] counts the ranges the PCL-order sort finished on one
+ * lane (a spent introsort depth budget: adversarial inputs), [2] / [3] / [4]
+ * inconsistent wave-sort steps, tail cuts and tail partners (internal checks;
+ * always 0).  Asynchronous on slo_stream(ctx). */
 int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,
                          void* d_out, size_t out_stride, int32_t* d_nout, int out_cap);
 

@@ -1,4 +1,5 @@
-# PCL-order tests, then the microbench at 40 and 170 streams; tag = $1
+# PCL-order VoxelGrid check: its GPU tests, then the microbench (tools/vg_bench.py) at 40 and 170 streams
+# with the sort's error counters; tag = $1
 set -euo pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
