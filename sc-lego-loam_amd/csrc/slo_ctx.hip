@@ -345,6 +345,7 @@ void slo_destroy(slo_ctx* ctx) {
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
     slo::graphs_drop(ctx);
+    slo::vg_side_free(ctx);
     slo::vg_free(ctx);
     slo::pcl_free(ctx);
     slo::grid_free(ctx->grid_c);
@@ -689,18 +690,26 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     else if (name == "vg_stats") {   // PCL-order sort (slo_vgpcl.hip): [0] ranges the one-lane fallback took,
                                      // [2] inconsistent wave-sort steps, [3] / [4] inconsistent tail cuts /
                                      // partners (2-4 must stay 0); [1] clipped outputs
-        int32_t a[5] = {0, 0, 0, 0, 0}, c[4] = {0, 0, 0, 0};
-        if (ctx->pws.cstat) SLO_CHECK(hipMemcpy(c, ctx->pws.cstat, 16, hipMemcpyDeviceToHost));
-        a[0] = c[0];
-        a[2] = c[1];
-        a[3] = c[2];
-        a[4] = c[3];
-        SLO_CHECK(hipMemcpy(&a[1], ctx->mws.errflag, 4, hipMemcpyDeviceToHost));
+        int32_t a[5] = {0, 0, 0, 0, 0};
+        for (const slo::PclWs* pw : {&ctx->pws, &ctx->pws2}) {   // the side stream's sorts count in pws2
+            int32_t c[4] = {0, 0, 0, 0};
+            if (pw->cstat) SLO_CHECK(hipMemcpy(c, pw->cstat, 16, hipMemcpyDeviceToHost));
+            a[0] += c[0]; a[2] += c[1]; a[3] += c[2]; a[4] += c[3];
+        }
+        for (const slo::MapWs* mw : {&ctx->mws, &ctx->mws2}) {
+            int32_t e = 0;
+            if (mw->errflag) SLO_CHECK(hipMemcpy(&e, mw->errflag, 4, hipMemcpyDeviceToHost));
+            a[1] |= e;
+        }
         tmp.resize(20); memcpy(tmp.data(), a, 20); count = 5; esz = 4;
     }
     else if (name == "pcl_work") {   // PCL-order sort work counters, cumulative (slo_vgpcl.hip PW_*)
         unsigned long long a[32] = {0};
-        if (ctx->pws.pstat) SLO_CHECK(hipMemcpy(a, ctx->pws.pstat, sizeof(a), hipMemcpyDeviceToHost));
+        for (const slo::PclWs* pw : {&ctx->pws, &ctx->pws2}) {   // the side stream's sorts count in pws2
+            unsigned long long b[32] = {0};
+            if (pw->pstat) SLO_CHECK(hipMemcpy(b, pw->pstat, sizeof(b), hipMemcpyDeviceToHost));
+            for (int i = 0; i < 32; ++i) a[i] += b[i];
+        }
         tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 32; esz = 8;
     }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }

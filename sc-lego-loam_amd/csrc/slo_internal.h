@@ -529,6 +529,13 @@ struct slo_ctx {
     // mapping workspaces
     slo::MapWs mws;
     slo::PclWs pws;
+    // contexts of a few streams run the mapping step's local-map VoxelGrids on
+    // a side stream beside the current scan's (slo_map.hip map_run): its own
+    // workspaces, swapped in while its launches are issued (VgSide)
+    hipStream_t side = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    slo::MapWs mws2;
+    slo::PclWs pws2;
     slo::HashGrid grid_c, grid_s, grid_oc, grid_os;
     bool map_ready = false;
     // loop-closure verification (cfg.loop_verify)
@@ -573,6 +580,7 @@ void fa_swap_last(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 void pcl_free(slo_ctx* ctx);
+void vg_side_free(slo_ctx* ctx);   // the side stream of map_run and its workspaces (slo_vg.hip)
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);
 int grid_alloc(slo_ctx* ctx, HashGrid& g, int T, size_t ent_stride, float cell);

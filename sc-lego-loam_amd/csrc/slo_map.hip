@@ -21,6 +21,8 @@
 // per-stream lane then merges the slices, rounds once to float and runs the
 // 6x6 QR / degeneracy projection.
 #include "slo_internal.h"
+#include "slo_vgcommon.h"
+#include <memory>
 #include "slo_libm.h"
 #include "slo_pose.h"
 #include "slo_linalg.h"
@@ -956,12 +958,25 @@ int map_run(slo_ctx* ctx) {
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
     SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
-    // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263)
+    // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263).  With a
+    // few streams the chip is mostly idle and a VoxelGrid's latency is what a
+    // scan waits for, so the two local-map filters run on the side stream
+    // (their own workspaces) while the current scan's five run here.
     int r;
-    if ((r = vg_run(ctx, "map_corner", v.map_c, v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner,
-                    v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc))) return r;
-    if ((r = vg_run(ctx, "map_surf", v.map_s, v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf,
-                    v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms))) return r;
+    const bool fork = S <= SLO_VG_FORK_STREAMS;
+    if (fork) {
+        if ((r = vg_side_ready(ctx))) return r;
+        SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+        SLO_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    }
+    {
+        std::unique_ptr<VgSide> side(fork ? new VgSide(ctx) : nullptr);
+        if ((r = vg_run(ctx, "map_corner", v.map_c, v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner,
+                        v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc))) return r;
+        if ((r = vg_run(ctx, "map_surf", v.map_s, v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf,
+                        v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms))) return r;
+    }
+    if (fork) SLO_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
     if ((r = vg_run(ctx, "raw", nullptr, v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
                     fld(&StreamState::n_raw_ds), SS, v.P))) return r;
     if ((r = vg_run(ctx, "corner", v.corner_last, v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS,
@@ -971,6 +986,7 @@ int map_run(slo_ctx* ctx) {
                     v.cur_s_ds, v.H, fld(&StreamState::n_surf_ds), SS, v.H))) return r;
     if ((r = vg_run(ctx, "outlier", v.outl_cam, v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier,
                     v.cur_o_ds, v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko))) return r;
+    if (fork) SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));   // k_mo_concat's map_ok reads the map DS sizes
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
     if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
                     v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;

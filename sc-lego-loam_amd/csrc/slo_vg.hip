@@ -1269,6 +1269,29 @@ int vg_alloc(slo_ctx* ctx) {
     return 0;
 }
 
+int vg_side_ready(slo_ctx* ctx) {
+    if (ctx->side) return 0;
+    SLO_CHECK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming));
+    VgSide sc(ctx);
+    return vg_alloc(ctx);
+}
+
+void vg_side_free(slo_ctx* ctx) {
+    if (!ctx->side) return;
+    hipStreamSynchronize(ctx->side);
+    {
+        VgSide sc(ctx);
+        vg_free(ctx);
+        pcl_free(ctx);
+    }
+    hipEventDestroy(ctx->ev_fork);
+    hipEventDestroy(ctx->ev_join);
+    hipStreamDestroy(ctx->side);
+    ctx->side = nullptr;
+}
+
 void vg_free(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
     void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta,

@@ -3,6 +3,7 @@
 // the per-stream voxel parameters of PCL's applyFilter and the voxel key.
 #pragma once
 #include "slo_internal.h"
+#include <utility>
 
 namespace slo {
 
@@ -89,5 +90,23 @@ __device__ inline T vg_block_scan(T x, T* wsum, T* total) {
 // finite points first, the non-finite ones after them with the "none" key
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
                 unsigned int* K, unsigned int* V);
+
+#ifndef SLO_VG_FORK_STREAMS
+#define SLO_VG_FORK_STREAMS 8   // contexts of at most this many streams run the local-map VoxelGrids on ctx->side
+#endif
+// Issues the enclosed launches on ctx->side with the side workspaces: the
+// context's stream and VoxelGrid / PCL-sort workspaces are swapped for the
+// scope's lifetime (one host thread drives a context).
+struct VgSide {
+    slo_ctx* c;
+    explicit VgSide(slo_ctx* ctx) : c(ctx) { swap_(); }
+    ~VgSide() { swap_(); }
+    void swap_() {
+        std::swap(c->stream, c->side);
+        std::swap(c->mws, c->mws2);
+        std::swap(c->pws, c->pws2);
+    }
+};
+int vg_side_ready(slo_ctx* ctx);   // creates the side stream, its events and workspaces once
 
 }  // namespace slo
