@@ -975,6 +975,10 @@ int map_run(slo_ctx* ctx) {
                         v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc))) return r;
         if ((r = vg_run(ctx, "map_surf", v.map_s, v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf,
                         v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms))) return r;
+        if (fork) {   // the hash grids over the DS maps follow them on the side stream
+            if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
+            if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
+        }
     }
     if (fork) SLO_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
     if ((r = vg_run(ctx, "raw", nullptr, v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
@@ -991,9 +995,9 @@ int map_run(slo_ctx* ctx) {
     if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
                     v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;
     if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(1024), 0, v);
-    // hash grids over the DS maps
-    if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
-    if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
+    // hash grids over the DS maps (on the side stream when forked, above)
+    if (!fork && (r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
+    if (!fork && (r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
     for (int it = 0; it < 10; ++it) {
         SLO_LAUNCH(ctx, "mo_knn", k_mo_knn, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
