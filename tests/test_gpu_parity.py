@@ -64,6 +64,8 @@ def _tools_path():
     (4, 2, 2, 10),    # OS1-64 as shipped (64 x 1024)
     (2, 2, 1, 6),     # VLS-128 (C5 sensor)
     (7, 5, 2, 10),    # C5 dense 128 x 2048 (262 k points per scan), two mapping rounds
+    (6, 3, 10, 10),   # C3 with 10 streams: the batched kernel shapes (more than 8 streams per context:
+                      # one-wave ring VoxelGrids, 64 Ki tail ranges, 4-wave finish entries, no mapping fork)
 ])
 def test_pipeline_bit_exact(preset, config, streams, scans):
     _torch()

@@ -35,6 +35,7 @@ def launch_names():
 TEMPLATED = {"k_pc_finish<4096, 4>": "pc_finish_b", "k_pc_finish<2048, 4>": "pc_finish_s",
              "k_pc_finish<512, 1>": "pc_finish_w", "k_fa_ring_ds_pcl<2048, 4>": "fa_ring_ds",
              "k_fa_ring_ds_pcl<2048, 16>": "fa_ring_ds", "k_fa_ring_ds_pcl<4096, 4>": "fa_ring_ds",
+             "k_fa_ring_ds_pcl<2048, 1>": "fa_ring_ds",
              "k_pc_finish<4096, 16>": "pc_finish_b", "k_pc_finish<2048, 8>": "pc_finish_s",
              "k_fa_ring_ds_pcl<4096>": "fa_ring_ds"}
 
