@@ -894,7 +894,7 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #define RING_TLANE 64
 #endif
 #ifndef RING_W
-#define RING_W 1            // waves per ring (4 measured no faster, 25 % slower in the live trace); 16 when
+#define RING_W 1            // waves per ring (4 measured no faster: DESIGN.md §7); 16 when
 #endif                      // the context has a few streams (latency)
 template <int PMAX, int RW>
 __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
