@@ -579,7 +579,14 @@ def main():
         c.timing(False)
         c.timing_filter(None)
     value = S * a.steps * world / el
+    # every stream's sticky error bits (capacity clips; since round 4 also the
+    # PCL-order sorts' guards, PclWs::serr) and the sorts' guard counters
     errs = sum(int(c.get(s, "err")[0]) != 0 for c in ctxs for s in range(c.n_streams))
+    vgs = sum(c.get(0, "vg_stats").astype(np.int64) for c in ctxs)
+    guards = {"fallback_ranges": int(vgs[0]), "inconsistent_steps": int(vgs[2] + vgs[3] + vgs[4]),
+              "clipped_outputs": int(vgs[1] != 0),
+              "note": "PCL-order VoxelGrid sort over the whole run: ranges heapsorted on one lane (exact; adversarial "
+                      "inputs), guards of impossible steps (must be 0; each also sets its stream's err bit)"}
     kfs = np.array([int(c.get(s, "n_keyframes")[0]) for c in ctxs for s in range(c.n_streams)])
 
     if counts is not None:
@@ -680,6 +687,7 @@ def main():
             "single_stream_speedup_vs_cpu_A": (round(one["value"] / cpu["A_reference_topology"]["value"], 2)
                                                if (one and cpu) else None),
             "stream_errors": errs,
+            "sort_guards": guards,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
             "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
             "setup_seconds": round(t_gen, 1), "preroll_seconds": round(t_pre, 1),

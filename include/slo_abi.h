@@ -194,7 +194,12 @@ int slo_batch_sc_distance(slo_ctx* ctx, const double* d_sc1, const double* d_sc2
  * as PCL).  vg_stats[0] counts the ranges the PCL-order sort finished on one
  * lane (a spent introsort depth budget: adversarial inputs), [2] / [3] / [4]
  * inconsistent wave-sort steps, tail cuts and tail partners (internal checks;
- * always 0).  Asynchronous on slo_stream(ctx). */
+ * always 0).  A stream whose range tripped one of the checks [2]-[4] also
+ * gets bit 16 (SORT) of slo_get(.., s, "err"); a stream of 2^24 or more
+ * finite points is not sorted and gets bit 4 (CAPACITY).  Returns SLO_E_ARG
+ * when out_cap > out_stride (the output rows would overlap) and
+ * SLO_E_CAPACITY when n_streams * in_stride exceeds INT32_MAX items (the
+ * sort's positions are 32-bit).  Asynchronous on slo_stream(ctx). */
 int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,
                          void* d_out, size_t out_stride, int32_t* d_nout, int out_cap);
 

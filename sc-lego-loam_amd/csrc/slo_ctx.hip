@@ -553,6 +553,9 @@ static int step_graph(slo_ctx* ctx, const void* d_points, const int32_t* d_count
         }
         if (ctx->ws_gen != ws0) {   // a workspace moved while capturing (not expected): no graph
             hipGraphDestroy(g);
+            // the stream-ordered initialisations of the new workspaces went into
+            // the discarded graph: run them now, before the eager step
+            if (int r = vg_ws_reinit(ctx)) return r;
             return eager_instead("a workspace was reallocated during graph capture");
         }
         ctx->graph_ws[key] = ws0;
@@ -686,7 +689,15 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     }
     else if (name == "tobe_mapped") { tmp.resize(24); memcpy(tmp.data(), st.transformTobeMapped, 24); count = 6; esz = 4; }
     else if (name == "mo_iters") { tmp.resize(4); memcpy(tmp.data(), &st.mo_iters, 4); count = 1; esz = 4; }
-    else if (name == "err") { tmp.resize(4); memcpy(tmp.data(), &st.err, 4); count = 1; esz = 4; }
+    else if (name == "err") {   // the stream's sticky bits, with the VoxelGrid sorts' own per-stream flags
+        int32_t e = st.err;
+        for (const slo::PclWs* pw : {&ctx->pws, &ctx->pws2}) {
+            int32_t x = 0;
+            if (pw->serr) SLO_CHECK(hipMemcpy(&x, pw->serr + stream, 4, hipMemcpyDeviceToHost));
+            e |= x;
+        }
+        tmp.resize(4); memcpy(tmp.data(), &e, 4); count = 1; esz = 4;
+    }
     else if (name == "vg_stats") {   // PCL-order sort (slo_vgpcl.hip): [0] ranges the one-lane fallback took,
                                      // [2] inconsistent wave-sort steps, [3] / [4] inconsistent tail cuts /
                                      // partners (2-4 must stay 0); [1] clipped outputs
@@ -1001,6 +1012,7 @@ int slo_batch_sc_make(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
     int r = slo::vg_run(ctx, "raw", (const float4*)d_points, v.P, d_counts, 1, v.cfg.leaf_sc, v.cur_raw_ds, v.P,
                         &v.st->n_raw_ds, SS, v.P);
+    if (!r) r = slo::pcl_fold_err(ctx);
     if (r) return r;
     return slo::sc_make_run(ctx, v.cur_raw_ds, v.P, &v.st->n_raw_ds, SS, ctx->S);
 }
@@ -1088,6 +1100,10 @@ int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const
                          void* d_out, size_t out_stride, int32_t* d_nout, int out_cap) {
     if (!ctx || !d_in || !d_n || !d_out || !d_nout || in_stride == 0 || out_cap < 0 || !(leaf > 0.0f))
         return SLO_E_ARG;
+    if ((size_t)out_cap > out_stride) {   // stream s writes out[s * out_stride + r] for r < out_cap
+        ctx->err = "slo_batch_voxel_grid: out_cap exceeds out_stride (output rows would overlap)";
+        return SLO_E_ARG;
+    }
     SLO_CHECK(hipSetDevice(ctx->dev));
     return slo::vg_run(ctx, "user", (const float4*)d_in, in_stride, d_n, 1, leaf, (float4*)d_out, out_stride, d_nout,
                        1, out_cap);

@@ -256,7 +256,8 @@ struct DevView {
 #define SLO_ERR_SC_HISTORY 2    // Scan Context history full: descriptor dropped
 #define SLO_ERR_MAP_CAPACITY 4  // a map / cloud capacity clipped a cloud
 #define SLO_ERR_INPUT 8         // slo_batch_pc2_unpack: a message exceeded max_points
-#define SLO_ERR_SORT 16         // PCL-order ring sort: an inconsistent step (slo_pclsort.h wave_sort; never expected)
+#define SLO_ERR_SORT 16         // PCL-order sort (ring or batched VoxelGrid): an inconsistent step caught by a
+                                // guard (slo_pclsort.h, slo_vgpcl.hip; never expected)
 
 // Locality-preserving bucket of cell (x, y, z): x-adjacent cells get adjacent
 // buckets, so a ring walk reads each row of cells' bucket words from one cache
@@ -469,6 +470,9 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
     int* ctr = nullptr;           // [16] per-call counters (ranges, chunks, finish entries)
     int* cstat = nullptr;         // [16] cumulative: [0] ranges the one-lane fallback took, [1] inconsistent
                                   // wave-sort steps, [2] / [3] inconsistent tail cuts / partners (1-3 must stay 0)
+    int32_t* serr = nullptr;      // [S] sticky per stream: SLO_ERR_SORT (a guard of 1-3 fired on one of its
+                                  // ranges), SLO_ERR_MAP_CAPACITY (2^24 or more items: not sorted); folded
+                                  // into StreamState::err (k_pc_fold_err, slo_get "err")
     unsigned long long* pstat = nullptr;   // [32] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
     unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
@@ -579,7 +583,9 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan);
 void fa_swap_last(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
+int vg_ws_reinit(slo_ctx* ctx);    // the stream-ordered initialisation of the VoxelGrid workspaces, again
 void pcl_free(slo_ctx* ctx);
+int pcl_fold_err(slo_ctx* ctx);    // PclWs::serr of both sort workspaces into StreamState::err (slo_vgpcl.hip)
 void vg_side_free(slo_ctx* ctx);   // the side stream of map_run and its workspaces (slo_vg.hip)
 int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
            float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap);

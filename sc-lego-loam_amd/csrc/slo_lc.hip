@@ -671,7 +671,7 @@ int lc_run(slo_ctx* ctx) {
             return r;
         if (int r = lc_icp_iterate(ctx)) return r;
     }
-    return 0;
+    return pcl_fold_err(ctx);
 }
 
 int lc_icp_run(slo_ctx* ctx, const float4* src, size_t src_stride, const int32_t* nsrc, const float4* tgt,

@@ -963,7 +963,8 @@ int map_run(slo_ctx* ctx) {
     // scan waits for, so the two local-map filters run on the side stream
     // (their own workspaces) while the current scan's five run here.
     int r;
-    const bool fork = S <= SLO_VG_FORK_STREAMS;
+    // (not while kernels are stamped: both streams' stamps would share one ring)
+    const bool fork = S <= SLO_VG_FORK_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
     if (fork) {
         if ((r = vg_side_ready(ctx))) return r;
         SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
@@ -1005,7 +1006,7 @@ int map_run(slo_ctx* ctx) {
     }
     SLO_LAUNCH(ctx, "mo_finish", k_mo_finish, dim3(S), dim3(256), 0, v);
     SLO_CHECK(hipGetLastError());
-    return 0;
+    return pcl_fold_err(ctx);   // the VoxelGrid sorts' per-stream flags into StreamState::err
 }
 
 }  // namespace slo

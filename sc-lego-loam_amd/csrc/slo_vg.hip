@@ -1269,6 +1269,15 @@ int vg_alloc(slo_ctx* ctx) {
     return 0;
 }
 
+// the look-back posts of both VoxelGrid workspaces back to zero (ensure_ws
+// zeroes them on ctx->stream when they are allocated; after a graph capture
+// that allocated them, that memset is in the discarded graph)
+int vg_ws_reinit(slo_ctx* ctx) {
+    for (MapWs* w : {&ctx->mws, &ctx->mws2})
+        if (w->lbk) SLO_CHECK(hipMemsetAsync(w->lbk, 0, sizeof(unsigned long long) * VG_NB * w->tiles, ctx->stream));
+    return 0;
+}
+
 int vg_side_ready(slo_ctx* ctx) {
     if (ctx->side) return 0;
     SLO_CHECK(hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking));

@@ -94,6 +94,21 @@ __device__ inline void pc_median(const unsigned int* K, int f, int l, unsigned i
     vmed = kf;
 }
 
+// the stream whose item range [off[s], off[s + 1]) holds position pos (a
+// guard's range, to flag that stream: PclWs::serr)
+__device__ inline int pc_stream_of(const int32_t* off, int S, int pos) {
+    int lo = 0, hi = S - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (off[mid] <= pos) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+__device__ inline void pc_flag(int32_t* serr, const int32_t* off, int S, int pos, int bit) {
+    atomicOr(&serr[pc_stream_of(off, S, pos)], bit);
+}
+
 // ---- items: finite points first, in input order
 __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, const int32_t* off,
                                                     const VgParams* prm, int* tcnt, int maxT, int S, int* ctr) {
@@ -122,7 +137,7 @@ __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, 
 // per stream: tile prefix of the finite counts, and the stream's first range
 __global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* off, const VgParams* prm, int* tcnt, int maxT,
                                                   PSeg* seg0, int* cseg0, PcLists wl, int* ctr, int32_t* nfin,
-                                                  unsigned long long* pst) {
+                                                  unsigned long long* pst, int32_t* serr) {
     __shared__ int wsum[16];
     __shared__ int slot_c0[2];
     const int s = blockIdx.x, tid = threadIdx.x;
@@ -144,8 +159,11 @@ __global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* o
         nfin[s] = n;
         atomicAdd(&pst[PW_INPUT], (unsigned long long)(off[s + 1] - off[s]));
         slot_c0[0] = -1;
+        // a range's size is kept in 24 bits of its list entry: a larger
+        // stream is left unsorted and flagged (never at the configs' sizes)
+        if (n >= (1 << 24)) atomicOr(&serr[s], SLO_ERR_MAP_CAPACITY);
         // overflow keys are the positions: already in order
-        if (!p.overflow && n >= 2) {
+        else if (!p.overflow && n >= 2) {
             const int d = 2 * slo_pcl::lg2(n);
             if (n > tail_min) {
                 const int nch = (n - 1 + PC_CH - 1) / PC_CH;
@@ -513,17 +531,20 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(int tail_min, const PSeg* seg
 #endif
 template <int NMAX, int W>
 __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
-                                                       unsigned long long* pst, int* cstat) {
+                                                       unsigned long long* pst, int* cstat, const int32_t* off,
+                                                       int S, int32_t* serr) {
     __shared__ u64 items[NMAX];
     __shared__ unsigned short tbl[NMAX];
     __shared__ slo_pcl::WaveSmem ws[W];
     __shared__ slo_pcl::BlockQ<W> bq;
+    __shared__ int ferr;   // the entry's inconsistent steps (slo_pclsort.h guards)
     const int nw = ctr[PCC_NW + list], tid = threadIdx.x;
     unsigned long long wn = 0, we = 0;   // work counters, one atomic per wave
     long long prof[3] = {0, 0, 0};
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
         const int f = w.x, n = min(w.y & 0xffffff, NMAX), d = w.y >> 24;
+        if (tid == 0) ferr = 0;
         for (int i0 = 0; i0 < n; i0 += 8 * 64 * W) {   // eight loads of each array in flight
             unsigned int kk[8], vv[8];
 #pragma unroll
@@ -537,7 +558,12 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
                 if (i0 + u * 64 * W + tid < n) items[i0 + u * 64 * W + tid] = ((u64)kk[u] << 32) | vv[u];
         }
         __syncthreads();
-        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, cstat + 1, prof);
+        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, prof);
+        __syncthreads();
+        if (tid == 0 && ferr) {   // never expected: counted and the stream flagged
+            atomicAdd(&cstat[1], ferr);
+            pc_flag(serr, off, S, f, SLO_ERR_SORT);
+        }
         for (int i = tid; i < n; i += 64 * W) {
             const u64 it = items[i];
             K[f + i] = (unsigned int)(it >> 32);
@@ -581,7 +607,8 @@ struct TailSm {
 };
 
 __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
-                                                    int* ctr, unsigned long long* pst, int* cstat) {
+                                                    int* ctr, unsigned long long* pst, int* cstat, const int32_t* off,
+                                                    int S, int32_t* serr) {
     __shared__ TailSm sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int INF = 0x7fffffff;
@@ -789,6 +816,7 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
                             y[u] = y[u] >= 0 ? (int)PB[f + y[u]] : -1;
                             if (y[u] >= l || (y[u] >= 0 && y[u] <= f)) {   // cannot happen: counted, not followed
                                 atomicAdd(&cstat[3], 1);
+                                pc_flag(serr, off, S, f, SLO_ERR_SORT);
                                 y[u] = -1;
                             }
                         }
@@ -812,8 +840,9 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
             __syncthreads();   // every swap is done before tid 0 reads the next range's pivot
             if (tid == 0) {   // the halves
                 int cut = min(sm.cutA, m > 0 ? sm.cutB : INF);
-                if (cut <= f || cut >= l) {   // cannot happen: counted; the range is left as it is
+                if (cut <= f || cut >= l) {   // cannot happen: counted, the stream flagged; the range is left as it is
                     atomicAdd(&cstat[2], 1);
+                    pc_flag(serr, off, S, f, SLO_ERR_SORT);
                     cut = l;
                 }
                 wact += (unsigned long long)(l - f);
@@ -880,6 +909,8 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         SLO_CHECK(hipMemset(w.cstat, 0, 16 * sizeof(int)));
         SLO_CHECK(hipMalloc(&w.pstat, 32 * sizeof(unsigned long long)));
         SLO_CHECK(hipMemset(w.pstat, 0, 32 * sizeof(unsigned long long)));
+        SLO_CHECK(hipMalloc(&w.serr, S * sizeof(int32_t)));
+        SLO_CHECK(hipMemset(w.serr, 0, S * sizeof(int32_t)));
     }
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
@@ -925,6 +956,10 @@ static int pcl_levels(size_t stride, int tail_min) {
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
                 unsigned int* K, unsigned int* V) {
     const int S = ctx->S;
+    if ((size_t)S * in_stride > (size_t)INT32_MAX) {   // item positions are 32-bit
+        ctx->err = "PCL-order VoxelGrid: n_streams * in_stride exceeds INT32_MAX items";
+        return SLO_E_CAPACITY;
+    }
     const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
     if (int r = pcl_ws(ctx, (size_t)S * in_stride, (size_t)maxT)) return r;
     PclWs& w = ctx->pws;
@@ -942,7 +977,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     const bool few = S <= PC_FEW;
     const int tail_min = few ? PC_TAIL_FEW : PC_TAIL;
     SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, tail_min, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
-               w.ctr, w.nfin, w.pstat);
+               w.ctr, w.nfin, w.pstat, w.serr);
     SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
     const int G = pcl_levels(in_stride, tail_min);
@@ -966,27 +1001,43 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     // each size class takes (43 / 23 / 5.6 KB per entry)
     const int FG = std::max(256, std::min(8192, S * 16));
     SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
-               w.ctr, w.pstat, w.cstat);
+               w.ctr, w.pstat, w.cstat, off, S, w.serr);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, w.pairs);
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
-                   w.cstat);
+                   w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
-                   w.cstat);
+                   w.cstat, off, S, w.serr);
     } else {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
-                   w.pstat, w.cstat);
+                   w.pstat, w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
-                   w.pstat, w.cstat);
+                   w.pstat, w.cstat, off, S, w.serr);
     }
-    SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat);
+    SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat, off, S, w.serr);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+// the sort's per-stream flags into StreamState::err (records, bench and
+// slo_get see them; slo_get also reads PclWs::serr itself)
+__global__ void k_pc_fold_err(StreamState* st, const int32_t* e0, const int32_t* e1, int S) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= S) return;
+    const int32_t e = (e0 ? e0[s] : 0) | (e1 ? e1[s] : 0);
+    if (e) st[s].err |= e;
+}
+int pcl_fold_err(slo_ctx* ctx) {
+    if (!ctx->pws.serr && !ctx->pws2.serr) return 0;
+    SLO_LAUNCH(ctx, "pc_fold_err", k_pc_fold_err, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v.st, ctx->pws.serr,
+               ctx->pws2.serr, ctx->S);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
 
 void pcl_free(slo_ctx* ctx) {
     PclWs& w = ctx->pws;
-    void* ps[] = {w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl,
+    void* ps[] = {w.serr, w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl,
                   w.tcnt};
     for (void* p : ps) if (p) hipFree(p);
     w = PclWs();

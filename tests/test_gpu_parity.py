@@ -105,6 +105,30 @@ def test_c4_os1_64_steady_state():
     assert len(full) >= 3                                         # detects that searched the tree snapshot
 
 
+def _bench_cap(cfg):
+    cfg.keyframe_cloud_cap = 32768   # bench.py --keyframe-cap; a clipped cloud would set the stream's err
+
+
+def test_c3_bench_shape_171_streams():
+    """The bench's per-context shape: 171 C3 streams in one context (bench.py,
+    512 streams in 3 contexts, keyframe_cloud_cap 32768) driven from the
+    device generator for 216 scans — 50-keyframe local maps, the batched
+    PCL-order sorts at their full size (the shape no smaller test reaches),
+    Scan Context detects past the exclusion — with four streams spread over
+    the context compared against the faithful oracle at every mapping step
+    (front end every 24th scan), and no stream of the 171 reporting an error
+    bit (capacity clips or a sort guard)."""
+    _torch()
+    rep, worst, counts = _run(6, 3, 171, 216, every=24, cfg_edit=_bench_cap, compare=[0, 57, 113, 170],
+                              device_gen=True)
+    _assert_clean(rep, worst, counts)
+    assert counts["stream_errors"] == 0, counts
+    kf = [r["n_kf"][1] for r in rep if "n_kf" in r]
+    assert kf[-1] >= 52                                           # the 50-keyframe deque is full
+    assert sum(1 for r in rep if r["flags_cpu"] & 2) >= 4 * 40    # >= 40 mapping steps per compared stream
+    print(f"171-stream C3: {counts}")
+
+
 def _k50(cfg):
     cfg.sc_num_candidates = 50
 

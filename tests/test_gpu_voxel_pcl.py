@@ -133,6 +133,91 @@ def test_pcl_order_many_map_streams():
     assert stats[0] == 0 and stats[2] == 0 and stats[3] == 0 and stats[4] == 0
 
 
+def _map_like_clouds(n_distinct, seed):
+    """map-like clouds (five hdl64 scans side by side, ~570 k points), each
+    thinned, shifted and cut differently"""
+    rng = np.random.default_rng(seed)
+    parts = []
+    for k in range(5):
+        p = O.gen_scan(6, 3, 0, 4 * k)
+        p = p[np.isfinite(p[:, :3]).all(1)].copy()
+        p[:, 0] += np.float32(2.0 * k)
+        parts.append(p)
+    big = np.concatenate(parts)
+    out = []
+    for d in range(n_distinct):
+        c = big[rng.random(len(big)) < 0.25 + 0.7 * d / max(1, n_distinct - 1)].copy()
+        c[:, 1] += np.float32(0.37 * d)
+        c[:, 2] -= np.float32(0.11 * d)
+        out.append(c[: len(c) - int(rng.integers(0, 5000))])
+    return out
+
+
+def test_pcl_order_bench_shape_171_streams():
+    """The bench's per-context shape (bench.py: 512 streams in 3 contexts ->
+    171 streams; the local-map surf VoxelGrid's input stride at C3 with
+    keyframe_cloud_cap 32768, MO:1224-1230) — the shape at which round 3's
+    vg_bench runs faulted before the tail kernel's barrier fix — at leaf 0.3:
+    every stream bit for bit against the oracle's std::sort VoxelGrid, every
+    guard counter 0 and no stream's error word set."""
+    torch = _torch()
+    cfg = slo_amd.preset(6)
+    S = 171
+    stride = 50 * (32768 + cfg.n_scan * ((cfg.horizon_scan + 4) // 5))   # v.cap_ms (slo_ctx.hip)
+    distinct = _map_like_clouds(19, 21)
+    clouds = [distinct[s % len(distinct)] for s in range(S)]
+    cap = max(len(c) for c in clouds)
+    ctx = slo_amd.Context(cfg, 0, S)
+    try:
+        d_in = torch.empty((S, stride, 4), dtype=torch.float32, device="cuda")
+        for s, c in enumerate(clouds):
+            d_in[s, :len(c)] = torch.from_numpy(c).cuda()
+        d_n = torch.tensor([len(c) for c in clouds], dtype=torch.int32, device="cuda")
+        d_out = torch.zeros((S, cap, 4), dtype=torch.float32, device="cuda")
+        d_nout = torch.zeros(S, dtype=torch.int32, device="cuda")
+        for rep in range(2):   # twice: the second call reuses every workspace and list counter
+            ctx.batch_voxel_grid(d_in.data_ptr(), stride, d_n.data_ptr(), 0.3, d_out.data_ptr(), cap,
+                                 d_nout.data_ptr(), cap)
+            ctx.synchronize()
+            nout, out = d_nout.cpu().numpy(), d_out.cpu().numpy()
+            want = [O.voxel_grid(c, 0.3, stable=False) for c in distinct]
+            for s in range(S):
+                w = want[s % len(distinct)]
+                assert nout[s] == len(w) and mismatch(out[s, :nout[s]], w) == 0, (rep, s)
+        stats = ctx.get(0, "vg_stats")
+        assert stats[0] == 0 and stats[2] == 0 and stats[3] == 0 and stats[4] == 0, stats.tolist()
+        assert all(int(ctx.get(s, "err")[0]) == 0 for s in range(S))
+        work = ctx.get(0, "pcl_work")
+        print(f"171 streams x {stride} stride: {int(work[5])} points, {int(work[6])} finish entries, "
+              f"tail items {int(work[7])}, vg_stats {stats.tolist()}")
+    finally:
+        ctx.close()
+
+
+def test_voxel_grid_argument_checks():
+    """out_cap beyond out_stride would let a stream write into the next one's
+    row: refused (SLO_E_ARG) before any launch; so are a zero stride and a
+    non-positive leaf"""
+    torch = _torch()
+    cfg = slo_amd.preset(0)
+    ctx = slo_amd.Context(cfg, 0, 2)
+    try:
+        d_in = torch.zeros((2, 100, 4), dtype=torch.float32, device="cuda")
+        d_n = torch.full((2,), 100, dtype=torch.int32, device="cuda")
+        d_out = torch.zeros((2, 50, 4), dtype=torch.float32, device="cuda")
+        d_nout = torch.zeros(2, dtype=torch.int32, device="cuda")
+        for args in ((100, 0.3, 50, 51), (0, 0.3, 50, 50), (100, 0.0, 50, 50)):
+            st, leaf, ost, cap = args
+            with pytest.raises(slo_amd.SloError):
+                ctx.batch_voxel_grid(d_in.data_ptr(), st, d_n.data_ptr(), leaf, d_out.data_ptr(), ost,
+                                     d_nout.data_ptr(), cap)
+        ctx.batch_voxel_grid(d_in.data_ptr(), 100, d_n.data_ptr(), 0.3, d_out.data_ptr(), 50, d_nout.data_ptr(), 50)
+        ctx.synchronize()
+        assert d_nout.cpu().tolist() == [1, 1]   # 100 points at the origin: one voxel each
+    finally:
+        ctx.close()
+
+
 def test_pcl_order_killer_sequences_and_one_voxel(model, tmp_path):
     rng = np.random.default_rng(12)
     k5 = killer_keys(model, 5000, tmp_path)           # heapsort inside the LDS finish

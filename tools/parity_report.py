@@ -29,13 +29,18 @@ def posediff(a, b):
 
 
 def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=True, every=1, n_points=None,
-        scan_fn=None, cfg_edit=None, imu_fn=None):
+        scan_fn=None, cfg_edit=None, imu_fn=None, compare=None, device_gen=False, map_every=1):
     """n_points(k, s) -> points of stream s's scan k handed over (ragged and
     empty scans; default: all); scan_fn(k, s) -> the scan itself (default: the
     synthetic generator); cfg_edit(cfg) changes both configs (GPU and oracle);
     imu_fn(k, s) -> (n, 11) float64 IMU messages (slo_imu_msg) stream s's
-    imuHandler receives before scan k (both sides)."""
+    imuHandler receives before scan k (both sides).  compare: the streams run
+    on the oracle and compared (default: all); device_gen: the GPU's scans come
+    from the device generator (slo_gen_device_*, bit-identical to the host
+    generator), so a context of hundreds of streams costs no host staging;
+    map_every: mapping results compared at every map_every-th mapping step."""
     import torch
+    from concurrent.futures import ThreadPoolExecutor
     cfg = slo_amd.preset(preset_id)
     ocfg = O.preset(preset_id)
     if cfg_edit:
@@ -43,14 +48,25 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
         cfg_edit(ocfg)
     P = cfg.max_points
     ctx = slo_amd.Context(cfg, 0, n_streams)
-    ors = [O.OracleStream(ocfg, stable_voxel=cfg.voxel_order == 1) for _ in range(n_streams)]
+    cmp = list(range(n_streams)) if compare is None else list(compare)
+    ors = {s: O.OracleStream(ocfg, stable_voxel=cfg.voxel_order == 1) for s in cmp}
+    pool = ThreadPoolExecutor(max_workers=min(8, len(cmp))) if len(cmp) > 1 else None
+    gen = slo_amd.DeviceGenerator(preset_id, config_id, 0, n_streams) if device_gen else None
+    dbuf = torch.empty((1, n_streams, P, 4), dtype=torch.float32, device="cuda") if device_gen else None
     report = []
     worst = {"odom": 0.0, "map": 0.0, "keypose": 0.0}
-    counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0, "flag_mismatch": 0}
+    counts = {"bit_mismatch": 0, "detect_mismatch": 0, "detects": 0, "loops": 0, "flag_mismatch": 0,
+              "stream_errors": 0}
+    n_map = 0
     for k in range(n_scans):
-        scans = [scan_fn(k, s) if scan_fn else O.gen_scan(preset_id, config_id, s, k) for s in range(n_streams)]
+        if device_gen:
+            scans = {s: O.gen_scan(preset_id, config_id, s, k) for s in cmp}
+            gen.scans(k, 1, dbuf.data_ptr())
+            pts = dbuf[0]
+        else:
+            scans = [scan_fn(k, s) if scan_fn else O.gen_scan(preset_id, config_id, s, k) for s in range(n_streams)]
+            pts = torch.from_numpy(np.stack(scans)).cuda()
         ns = [min(P, n_points(k, s)) if n_points else P for s in range(n_streams)]
-        pts = torch.from_numpy(np.stack(scans)).cuda()
         cnt = torch.tensor(ns, dtype=torch.int32, device="cuda")
         if imu_fn:
             msgs = [np.asarray(imu_fn(k, s), np.float64).reshape(-1, 11) for s in range(n_streams)]
@@ -63,9 +79,14 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
             d_n = torch.tensor([len(m) for m in msgs], dtype=torch.int32, device="cuda")
             ctx.batch_imu(d_imu.data_ptr(), per, d_n.data_ptr())
         ctx.batch_process(pts.data_ptr(), cnt.data_ptr(), 0.1 * k)
+        step = lambda s: ors[s].step(scans[s][:ns[s]], 0.1 * k)  # noqa: E731
+        fls = dict(zip(cmp, pool.map(step, cmp))) if pool else {s: step(s) for s in cmp}
         ctx.synchronize()
-        for s in range(n_streams):
-            fl_o = ors[s].step(scans[s][:ns[s]], 0.1 * k)
+        mapped = any(fl & 2 for fl in fls.values())
+        n_map += int(mapped)
+        check_map = mapped and (n_map - 1) % map_every == 0
+        for s in cmp:
+            fl_o = fls[s]
             fl_g = int(ctx.get(s, "flags")[0])
             row = {"scan": k, "stream": s, "flags_cpu": fl_o & 14, "flags_gpu": fl_g}
             counts["flag_mismatch"] += int((fl_o & 14) != fl_g)
@@ -89,7 +110,7 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 row["imu"] = mismatch(ctx.get(s, "imu"), ors[s].get("imu"))
             row["odom"] = posediff(ctx.get(s, "transform_sum"), ors[s].get("transform_sum"))
             worst["odom"] = max(worst["odom"], row["odom"])
-            if fl_o & 2:
+            if fl_o & 2 and check_map:
                 row["mapped"] = posediff(ctx.get(s, "mapped"), ors[s].get("mapped"))
                 worst["map"] = max(worst["map"], row["mapped"])
                 row["mo_iters"] = [int(ctx.get(s, "mo_iters")[0]), int(ors[s].get("mo_iters")[0])]
@@ -107,7 +128,7 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
                 row["n_kf"] = [len(kg) // 6, len(ko) // 6]
                 if len(kg) == len(ko):
                     worst["keypose"] = max(worst["keypose"], posediff(kg, ko))
-            if fl_o & 4:
+            if fl_o & 4 and check_map:
                 for name in SC:
                     row[name] = mismatch(ctx.get(s, name), ors[s].get(name))
             if fl_o & 8:
@@ -126,6 +147,12 @@ def run(preset_id=5, config_id=2, n_streams=2, n_scans=6, verbose=True, front=Tr
             report.append(row)
             if verbose:
                 print(json.dumps(row), flush=True)
+    # sticky error bits of every stream (capacity clips, the VoxelGrid sorts' guards), compared or not
+    counts["stream_errors"] = sum(int(ctx.get(s, "err")[0]) != 0 for s in range(n_streams))
+    if pool:
+        pool.shutdown()
+    if gen:
+        gen.close()
     ctx.close()
     return report, worst, counts
 
