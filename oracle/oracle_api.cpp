@@ -30,6 +30,7 @@ struct OracleStream {
     LoopResult loop[2];      // RS, SC verification of the last detect (cfg.loop_verify)
     int scan_index = 0;
     float integrated[6] = {0};   // /integrated_to_init (transformFusion's transformMapped)
+    int gemm_mode = 0;           // oracle_common.h gemm_AtA / gemm_AtB (0 double-double, 1 OpenCV's order)
     explicit OracleStream(const slo_config& c) : cfg(c), ip(c), fa(c), mo(c) {}
 
     // returns bit flags: 1 = FA odometry ran, 2 = mapping ran, 4 = keyframe, 8 = detect ran
@@ -39,6 +40,7 @@ struct OracleStream {
     }
     // the nodes up to mapOptimization::run (flags 1, 2, 4)
     int step_map(const float* pts, int n, double t) {
+        t_gemm_mode = gemm_mode;   // this thread runs this stream now
         int flags = 0;
         det_valid = false;
         ip.cloudHandler(pts, n);
@@ -88,6 +90,8 @@ void* oracle_create(const slo_config* cfg, int stable_voxel) {
     return s;
 }
 void oracle_destroy(void* h) { delete (OracleStream*)h; }
+// the normal equations' accumulation order (oracle_common.h gemm_AtA): 0 double-double (default), 1 OpenCV 3.x
+void oracle_set_gemm_mode(void* h, int mode) { ((OracleStream*)h)->gemm_mode = mode; }
 
 int oracle_step(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step(pts, n, t); }
 int oracle_step_map(void* h, const float* pts, int n, double t) { return ((OracleStream*)h)->step_map(pts, n, t); }
@@ -425,6 +429,25 @@ void oracle_xsc_query(void* h, const float* recs, int nq, int global0, int32_t* 
             of[0] = (float)((float)(am * (360.0 / (double)x.NS)) * M_PI / 180.0);
         }
     }
+}
+
+// ---- the normal equations' GEMMs (oracle_common.h gemm_AtA / gemm_AtB) in
+// either accumulation mode, on an n x m float matrix A and n-vector B
+void oracle_gemm_at(const float* A, const float* B, int n, int m, int mode, float* AtA, float* AtB) {
+    const int m0 = t_gemm_mode;
+    t_gemm_mode = mode;
+    std::vector<float> a(A, A + (size_t)n * m), b(B, B + n);
+    gemm_AtA(a, n, m, AtA);
+    gemm_AtB(a, b, n, m, AtB);
+    t_gemm_mode = m0;
+}
+
+// tally on / off (both modes evaluated while on); [entries computed, entries
+// where the two modes differ] since the last call (tallies reset)
+void oracle_gemm_tally(int on) { g_gemm_tally = on != 0; }
+void oracle_gemm_stats(long long* out) {
+    out[0] = g_gemm_entries.exchange(0);
+    out[1] = g_gemm_differ.exchange(0);
 }
 
 // ---- slo_ddsum.h under test: sum of the exact float products a[i]*b[i]

@@ -26,6 +26,7 @@
 #include <vector>
 #include <algorithm>
 #include <limits>
+#include <atomic>
 #include "../sc-lego-loam_amd/csrc/slo_ddsum.h"
 
 namespace oracle {
@@ -197,29 +198,73 @@ struct KdTree {
 };
 
 // ------------------------------------------------------------ OpenCV restatements
-// cv::Mat GEMM for CV_32F: products and sums in double, one accumulator per
-// output in k order (GEMMSingleMul<float,double>), result rounded to float.
-// AtB (single-column output) goes through the transposed-B branch, which
-// keeps two accumulators (even / odd k) and adds them at the end.
 // matAtA = matAt * matA, matAtB = matAt * matB (cv::Mat GEMM on float Mats,
-// FA:1324-1326 / 1425-1427, MO:1445-1447).  OpenCV's accumulation order is
-// unpinned (Q11); products of floats are exact in double and the sum is
-// taken in double-double and rounded once (slo_ddsum.h), which is the
-// correctly rounded float of the exact sum — the same value the GPU's tree
-// reduction produces.
+// FA:1324-1326 / 1425-1427, MO:1445-1447).  Two accumulation modes
+// (t_gemm_mode, per calling thread, set per stream by oracle_step):
+//   0 (default; what the GPU computes): products of floats are exact in
+//     double; the sum is taken in double-double and rounded once
+//     (slo_ddsum.h) — the correctly rounded float of the exact sum, which the
+//     GPU's tree reductions reproduce;
+//   1 OpenCV 3.x's own C++ GEMM as recalled (Q11; OpenCV is absent here, so
+//     this too is unpinned): cv::gemm on a 6 x 6 / 3 x 3 result takes
+//     GEMMSingleMul<float, double>.  matAtA (flags 0, d.width * 4 <= 1600):
+//     one double accumulator per output, k in order, rounded to float once.
+//     matAtB (a one-column result, so B is read as a transposed row, GEMM_2_T):
+//     four double accumulators over k mod 4 (CV_ENABLE_UNROLLED), the tail
+//     into the first, then s0 + s1 + s2 + s3 left to right, rounded once.
+// tools/faithful_drift.py --gemm measures what the difference does to the
+// poses.
+inline thread_local int t_gemm_mode = 0;
+// process-wide tallies (only while g_gemm_tally is on: both modes are then
+// evaluated and the stream's mode picks the one used): entries computed,
+// entries where the two modes give different floats
+inline std::atomic<bool> g_gemm_tally{false};
+inline std::atomic<long long> g_gemm_entries{0}, g_gemm_differ{0};
 inline void gemm_AtA(const std::vector<float>& A, int n, int m, float* AtA) {
+    const bool both = g_gemm_tally.load(std::memory_order_relaxed);
+    long long differ = 0;
     for (int i = 0; i < m; ++i)
         for (int j = 0; j < m; ++j) {
+            double q = 0;
             slo_dd::DD s = slo_dd::zero();
-            for (int k = 0; k < n; ++k) slo_dd::add(s, (double)A[k * m + i] * (double)A[k * m + j]);
-            AtA[i * m + j] = slo_dd::to_float(s);
+            const bool dd = both || t_gemm_mode != 1, seq = both || t_gemm_mode == 1;
+            for (int k = 0; k < n; ++k) {
+                const double p = (double)A[k * m + i] * (double)A[k * m + j];
+                if (seq) q += p;
+                if (dd) slo_dd::add(s, p);
+            }
+            const float f0 = slo_dd::to_float(s), f1 = (float)q;
+            differ += memcmp(&f0, &f1, 4) != 0;
+            AtA[i * m + j] = t_gemm_mode == 1 ? f1 : f0;
         }
+    if (both) {
+        g_gemm_entries += (long long)m * m;
+        g_gemm_differ += differ;
+    }
 }
 inline void gemm_AtB(const std::vector<float>& A, const std::vector<float>& B, int n, int m, float* AtB) {
+    const bool both = g_gemm_tally.load(std::memory_order_relaxed);
+    long long differ = 0;
     for (int i = 0; i < m; ++i) {
+        double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+        int k = 0;
+        for (; k <= n - 4; k += 4) {
+            s0 += (double)A[k * m + i] * (double)B[k];
+            s1 += (double)A[(k + 1) * m + i] * (double)B[k + 1];
+            s2 += (double)A[(k + 2) * m + i] * (double)B[k + 2];
+            s3 += (double)A[(k + 3) * m + i] * (double)B[k + 3];
+        }
+        for (; k < n; ++k) s0 += (double)A[k * m + i] * (double)B[k];
         slo_dd::DD s = slo_dd::zero();
-        for (int k = 0; k < n; ++k) slo_dd::add(s, (double)A[k * m + i] * (double)B[k]);
-        AtB[i] = slo_dd::to_float(s);
+        if (both || t_gemm_mode != 1)
+            for (int k2 = 0; k2 < n; ++k2) slo_dd::add(s, (double)A[k2 * m + i] * (double)B[k2]);
+        const float f0 = slo_dd::to_float(s), f1 = (float)(s0 + s1 + s2 + s3);
+        differ += memcmp(&f0, &f1, 4) != 0;
+        AtB[i] = t_gemm_mode == 1 ? f1 : f0;
+    }
+    if (both) {
+        g_gemm_entries += m;
+        g_gemm_differ += differ;
     }
 }
 // small dense C = A(r x k) * B(k x c), double accumulation

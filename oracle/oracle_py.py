@@ -108,6 +108,11 @@ def lib():
         L.oracle_xsc_ingest.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
         L.oracle_xsc_query.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                        ctypes.c_void_p]
+        L.oracle_set_gemm_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_gemm_stats.argtypes = [ctypes.c_void_p]
+        L.oracle_gemm_tally.argtypes = [ctypes.c_int]
+        L.oracle_gemm_at.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_ddsum.restype = ctypes.c_float
         L.oracle_ddsum.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
         _LIB = L
@@ -260,10 +265,41 @@ def sc_knn(cfg, data, q, K):
     return idx, dist
 
 
+def gemm_at(A, B, mode):
+    """(matAt * matA, matAt * matB) of an n x m float matrix in the oracle's
+    accumulation mode (0 double-double, 1 OpenCV 3.x GEMMSingleMul order)"""
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    n, m = A.shape
+    ata, atb = np.zeros((m, m), np.float32), np.zeros(m, np.float32)
+    lib().oracle_gemm_at(A.ctypes.data, B.ctypes.data, n, m, int(mode), ata.ctypes.data, atb.ctypes.data)
+    return ata, atb
+
+
+def gemm_tally(on):
+    """evaluate both accumulation modes of every normal-equation entry from
+    now on (gemm_stats counts them)"""
+    lib().oracle_gemm_tally(int(bool(on)))
+
+
+def gemm_stats():
+    """(normal-equation entries computed, entries where double-double and
+    OpenCV's order round to different floats) since the last call, while
+    gemm_tally is on"""
+    out = np.zeros(2, np.int64)
+    lib().oracle_gemm_stats(out.ctypes.data)
+    return int(out[0]), int(out[1])
+
+
 class OracleStream:
-    def __init__(self, cfg, stable_voxel=False):
+    def __init__(self, cfg, stable_voxel=False, gemm_mode=0):
+        """gemm_mode: the normal equations' accumulation (oracle_common.h
+        gemm_AtA): 0 double-double rounded once (what the GPU computes), 1
+        OpenCV 3.x GEMMSingleMul's double order"""
         self.cfg = cfg
         self.h = lib().oracle_create(ctypes.byref(cfg), int(stable_voxel))
+        if gemm_mode:
+            lib().oracle_set_gemm_mode(self.h, int(gemm_mode))
 
     def __del__(self):
         if getattr(self, "h", None):

@@ -97,3 +97,63 @@ def test_empty_and_single_term():
     for mode in (0, 1, 2):
         assert dd(np.array([3.0], np.float32), np.array([np.float32(1.1)], np.float32), mode) == \
             exact_float32(Fraction(3) * Fraction(float(np.float32(1.1))))
+
+
+# ---- the oracle's second accumulation mode: OpenCV 3.x's own GEMM order (Q11)
+def _opencv_order(A, B):
+    """GEMMSingleMul<float, double> as oracle_common.h restates it, in Python
+    doubles: matAtA one accumulator per entry in k order; matAtB four
+    accumulators over k mod 4, the tail into the first, summed left to right"""
+    A = np.asarray(A, np.float32).astype(np.float64)
+    B = np.asarray(B, np.float32).astype(np.float64)
+    n, m = A.shape
+    ata = np.zeros((m, m), np.float32)
+    atb = np.zeros(m, np.float32)
+    for i in range(m):
+        for j in range(m):
+            s = 0.0
+            for k in range(n):
+                s += float(A[k, i]) * float(A[k, j])
+            ata[i, j] = np.float32(s)
+        s = [0.0, 0.0, 0.0, 0.0]
+        k = 0
+        while k <= n - 4:
+            for u in range(4):
+                s[u] += float(A[k + u, i]) * float(B[k + u])
+            k += 4
+        while k < n:
+            s[0] += float(A[k, i]) * float(B[k])
+            k += 1
+        atb[i] = np.float32(((s[0] + s[1]) + s[2]) + s[3])
+    return ata, atb
+
+
+def test_gemm_modes_restated():
+    """mode 1 equals the Python restatement of OpenCV's order bit for bit on
+    random mixed-magnitude data; mode 0 is the correctly rounded float of the
+    exact sums (Fraction)"""
+    rng = np.random.default_rng(3)
+    for n, m in ((1, 3), (7, 3), (64, 6), (203, 6)):
+        A = (rng.standard_normal((n, m)) * np.exp2(rng.integers(-20, 20, (n, m)))).astype(np.float32)
+        B = (rng.standard_normal(n) * np.exp2(rng.integers(-20, 20, n))).astype(np.float32)
+        ata1, atb1 = O.gemm_at(A, B, 1)
+        want = _opencv_order(A, B)
+        assert np.array_equal(ata1.view(np.uint32), want[0].view(np.uint32)), (n, m)
+        assert np.array_equal(atb1.view(np.uint32), want[1].view(np.uint32)), (n, m)
+        ata0, atb0 = O.gemm_at(A, B, 0)
+        for i in range(m):
+            q = sum(Fraction(float(A[k, i])) * Fraction(float(B[k])) for k in range(n))
+            assert atb0[i] == exact_float32(q)
+
+
+def test_gemm_modes_differ_where_expected():
+    """products 1, 2^-24, 2^-60: a sequential double sum stops at 1 + 2^-24,
+    the float midpoint, which rounds to even (1.0); the exact sum lies above
+    it (1 + 2^-23).  The two modes differ only in such ~2^-29-wide windows
+    around float rounding boundaries, and tools/faithful_drift.py --gemm
+    measures that no C1-C5 stream reaches one."""
+    A = np.array([[1.0], [2.0 ** -12], [2.0 ** -30]], np.float32)
+    ata0, atb0 = O.gemm_at(A, A[:, 0], 0)
+    ata1, atb1 = O.gemm_at(A, A[:, 0], 1)
+    assert ata1[0, 0] == np.float32(1.0) and atb1[0] == np.float32(1.0)
+    assert ata0[0, 0] == np.float32(1.0 + 2.0 ** -23) and atb0[0] == np.float32(1.0 + 2.0 ** -23)

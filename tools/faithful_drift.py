@@ -1,7 +1,13 @@
-"""How far the GPU-ordered oracle (stable in-voxel order, which the GPU
-reproduces bit for bit) drifts from the reference-faithful oracle (PCL's
-std::sort in-voxel order, FA:779-780, MO:1224-1262) on the same stream.
-CPU only.  python tools/faithful_drift.py --preset 6 --config 3 --scans 240"""
+"""How far two oracle variants drift apart on the same stream, CPU only.
+
+Default: the stable in-voxel order (round 2's GPU) against the
+reference-faithful oracle (PCL's std::sort in-voxel order, FA:779-780,
+MO:1224-1262).  --gemm: both in the faithful voxel order, the normal
+equations summed in double-double and rounded once (what the GPU computes)
+against OpenCV 3.x's own GEMM order (sequential double for matAtA, four
+interleaved accumulators for matAtB; FA:1324-1326, 1425-1427, MO:1445-1447;
+oracle_common.h gemm_AtA).
+python tools/faithful_drift.py --preset 6 --config 3 --scans 240 [--gemm]"""
 import argparse
 import json
 import os
@@ -32,17 +38,27 @@ def pose_dev(a, b):
     return float(angdiff(a[:, :3], b[:, :3]).max()), float(np.abs(a[:, 3:] - b[:, 3:]).max())
 
 
-def run(pid, cid, n_scans, cfg_edit=None, verbose=False):
+def run(pid, cid, n_scans, cfg_edit=None, verbose=False, gemm=False):
     cfg = O.preset(pid)
     if cfg_edit:
         cfg_edit(cfg)
-    a = O.OracleStream(cfg, stable_voxel=True)
-    b = O.OracleStream(cfg, stable_voxel=False)
+    if gemm:
+        a = O.OracleStream(cfg, stable_voxel=False, gemm_mode=0)
+        b = O.OracleStream(cfg, stable_voxel=False, gemm_mode=1)
+    else:
+        a = O.OracleStream(cfg, stable_voxel=True)
+        b = O.OracleStream(cfg, stable_voxel=False)
     worst = {"odom_rad": 0.0, "odom_m": 0.0, "map_rad": 0.0, "map_m": 0.0, "key_rad": 0.0, "key_m": 0.0}
     flags_diff = detect_diff = ringbin_diff = 0
+    first_div = None
+    O.gemm_tally(gemm)
+    O.gemm_stats()   # reset the tallies
     for k in range(n_scans):
         pts = O.gen_scan(pid, cid, 0, k)
         fa, fb = a.step(pts, 0.1 * k), b.step(pts, 0.1 * k)
+        if first_div is None and not np.array_equal(a.get("transform_sum").view(np.uint32),
+                                                    b.get("transform_sum").view(np.uint32)):
+            first_div = k
         flags_diff += int((fa & 14) != (fb & 14))
         r, t = pose_dev(a.get("transform_sum"), b.get("transform_sum"))
         worst["odom_rad"], worst["odom_m"] = max(worst["odom_rad"], r), max(worst["odom_m"], t)
@@ -63,7 +79,9 @@ def run(pid, cid, n_scans, cfg_edit=None, verbose=False):
             detect_diff += int(len(da) == 0 or len(db) == 0 or da[0] != db[0])
         if verbose and (k % 20 == 0):
             print(k, json.dumps(worst), flush=True)
-    return {"worst": worst, "flags_diff": flags_diff, "detect_diff": detect_diff, "ring_key_diff": ringbin_diff}
+    ent, dif = O.gemm_stats()
+    return {"worst": worst, "flags_diff": flags_diff, "detect_diff": detect_diff, "ring_key_diff": ringbin_diff,
+            "first_divergence_scan": first_div, "normal_equation_entries": ent, "entries_modes_differ": dif}
 
 
 if __name__ == "__main__":
@@ -73,6 +91,7 @@ if __name__ == "__main__":
     ap.add_argument("--scans", type=int, default=240)
     ap.add_argument("--sc-off", action="store_true")
     ap.add_argument("--k50", action="store_true")
+    ap.add_argument("--gemm", action="store_true", help="double-double vs OpenCV's GEMM order (faithful voxel order)")
     a = ap.parse_args()
 
     def edit(c):
@@ -80,4 +99,4 @@ if __name__ == "__main__":
             c.loop_closure_enable = 0
         if a.k50:
             c.sc_num_candidates = 50
-    print(json.dumps(run(a.preset, a.config, a.scans, edit, verbose=True)))
+    print(json.dumps(run(a.preset, a.config, a.scans, edit, verbose=True, gemm=a.gemm)))
