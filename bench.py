@@ -54,6 +54,13 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sc-lego-loam_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md:36); 6290 measured float4 copy
+# f64 MFMA peak (v_mfma_f64_16x16x4_f64, every SIMD issuing back to back), measured by
+# tools/mfma_f64_check.hip (profiles/r04/mfma_f64.txt); the Scan Context Gram's roof
+MFMA_F64_PEAK_TFLOPS = 75.2   # measured, profiles/r04/mfma_f64.txt (spec 78.6)
+# MFMA flop issued per Scan Context pair (slo_scdist.h sc_gram_mfma): 4 x 4 tiles x 4 accumulators x
+# ceil(NR / 16) MFMAs of 16 x 16 x 4 x 2 flop
+def sc_pair_mfma_flop(nr):
+    return 16 * 4 * ((nr + 15) // 16) * 16 * 16 * 4 * 2
 METRIC = "scans/sec end-to-end (proj+feat+LM+SC), 64-ring 1800-col, 1/2/4/8 GPU"
 
 
@@ -81,7 +88,7 @@ def parse():
                     help="extra Scan Context history per stream (scans before scan 0, a KITTI-00 mid-drive history: "
                          "detects search ~1000 keyframes, SCc:264-289); the pre-roll builds the recent part")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="mo_knn,pc_tail,pc_lpairs,fa_search_corner",
+    ap.add_argument("--roofline-also", default="mo_knn,pc_tail,pc_lpairs,fa_search_corner,sc_detect",
                     help="further kernels timed live the same way, reported under roofline_also (comma list)")
     ap.add_argument("--roofline-kernel", default="auto",
                     help="kernel timed inside the timed region (the roofline's kernel); auto = the largest kernel by "
@@ -104,7 +111,66 @@ def parse():
                          "the run can be cut to exactly the timed window (tools/trace_window.py)")
     ap.add_argument("--traffic-from", default=None,
                     help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
+    ap.add_argument("--sc-k", type=int, default=0, help="Scan Context candidates (NUM_CANDIDATES_FROM_TREE); 0 = preset")
+    ap.add_argument("--sc-off", action="store_true", help="loopClosureEnableFlag = false (C2: radius-search local map)")
+    ap.add_argument("--map-keyframes", type=int, default=0, help="slo_config.map_keyframes (radius branch); 0 = default")
+    ap.add_argument("--keyframe-ring", type=int, default=0, help="slo_config.keyframe_ring; 0 = default")
+    ap.add_argument("--workload", default="C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 "
+                                          "K=10, steady state")
+    ap.add_argument("--extra", default="c2,c5",
+                    help="further BASELINE.json configs measured at 1 GPU after the headline, each by its own bench.py "
+                         "process, reported under config_lines (outside value); 'none' = none")
     return ap.parse_args()
+
+
+# BASELINE.json configs measured beside the headline (C3) at 1 GPU: bench.py arguments
+EXTRA = {
+    "c2": ["--preset", "os64_1800", "--config-id", "2", "--sc-off", "--streams", "512", "--map-keyframes", "32",
+           "--keyframe-ring", "128", "--workload",
+           "C2 Ouster-64 synthetic 64x1800 stream, segmentation + features + LM, Scan Context off (radius-search "
+           "local map, MO:1167-1222), steady state"],
+    "c5": ["--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--workload",
+           "C5 128-ring x 2048-col dense synthetic scan, Scan Context K=50, LM against the ~1M-point raw local "
+           "map (HBM-bound stress), steady state"],
+}
+
+
+def cfg_edit(cfg, a):
+    """the command line's configuration edits, for the GPU and the CPU baseline alike"""
+    if a.sc_k:
+        cfg.sc_num_candidates = a.sc_k
+    if a.sc_off:
+        cfg.loop_closure_enable = 0
+    if a.map_keyframes:
+        cfg.map_keyframes = a.map_keyframes
+    if a.keyframe_ring:
+        cfg.keyframe_ring = a.keyframe_ring
+
+
+def extra_lines(a):
+    """run each --extra config as its own bench.py process at 1 GPU (after this one has released the device) and
+    return its JSON line, trimmed to the fields a config line needs"""
+    import subprocess
+    out = {}
+    for name in [x for x in a.extra.split(",") if x and x != "none"]:
+        cmd = [sys.executable, os.path.abspath(__file__), "--extra", "none", "--single-steps", "0", "--icp-jobs", "0",
+               "--steps", "20", "--warmup", "3", "--cpu-scans", "4", "--cpu-distinct", "4"] + EXTRA[name]
+        t0 = time.time()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            j = json.loads(line[-1]) if (r.returncode == 0 and line) else None
+        except subprocess.TimeoutExpired:
+            r, j = None, None
+        if j is None:
+            out[name] = {"error": f"rc={getattr(r, 'returncode', 'timeout')}",
+                         "stderr_tail": (r.stderr[-600:] if r else "")}
+            continue
+        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_also",
+                "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors", "sort_guards", "dtype")
+        out[name] = {k: j.get(k) for k in keep}
+        out[name]["wall_seconds"] = round(time.time() - t0, 1)
+    return out
 
 
 def stream_counts(ctx, S):
@@ -195,6 +261,8 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
             return int(16 * pw[5])
         if name == "pc_write":    # the points in, (key, index) out
             return int(24 * pw[5])
+    if name == "sc_detect" and c.get("sc_pairs") is not None:   # MFMA flop (bound "mfma")
+        return int(c["sc_pairs"]) * sc_pair_mfma_flop(cfg.sc_num_ring)
     if name == "vg_reduce":       # sorted (key, index) in, the point gathered, per item
         return map_steps * int(c["vg_in"].sum()) * (8 + 16)
     if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
@@ -322,9 +390,11 @@ def cpu_baseline(a, pid, ncpu, start):
     th = a.cpu_threads or eff
     stage = (ctypes.c_double * 4)()
     one = (ctypes.c_double * 4)()
+    ocfg = O.preset(pid)
+    cfg_edit(ocfg, a)
     t0 = time.time()
-    secs = O.lib().oracle_bench(pid, a.config_id, th, a.cpu_scans, start, a.history,
-                                min(a.cpu_distinct, th), stage, one)
+    secs = O.lib().oracle_bench_cfg(ctypes.byref(ocfg), a.config_id, th, a.cpu_scans, start, a.history,
+                                    min(a.cpu_distinct, th), stage, one)
     wall = time.time() - t0
     n = a.cpu_scans
     # (A): one stream as the reference's 3 processes on 3 cores; the pipeline
@@ -409,6 +479,7 @@ def main():
     cfg = slo_amd.preset(a.preset)
     cfg.keyframe_cloud_cap = a.keyframe_cap
     cfg.voxel_order = a.voxel_order
+    cfg_edit(cfg, a)
     pid = slo_amd.PRESETS[a.preset]
     P = cfg.max_points
     S = a.streams
@@ -524,6 +595,7 @@ def main():
             c.timing(True)
             c.timing_reset()
         pw0 = [c.get(0, "pcl_work").astype(np.int64) for c in ctxs]
+        wk0 = [c.get(0, "work").astype(np.int64) for c in ctxs]
         for k in range(P0):
             step(k, serial=True)
             sync_all()
@@ -536,7 +608,9 @@ def main():
         parts = [stream_counts(c, c.n_streams) for c in ctxs]
         counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         counts["pcl_work"] = sum(c.get(0, "pcl_work").astype(np.int64) - w0 for c, w0 in zip(ctxs, pw0))
-        workload = {k: round(float(v.mean()), 1) for k, v in counts.items() if v.ndim == 1 and k != "pcl_work"}
+        counts["sc_pairs"] = int(sum(c.get(0, "work").astype(np.int64)[0] - w0[0] for c, w0 in zip(ctxs, wk0)))
+        workload = {k: round(float(v.mean()), 1) for k, v in counts.items()
+                    if k not in ("pcl_work", "sc_pairs") and v.ndim == 1}
     # the largest single kernel by device time (vg_sort:<filter> entries time groups of launches)
     dominant = max(((kn, v) for kn, v in kt.items() if not kn.startswith("vg_sort:")),
                    key=lambda kv: kv[1][0])[0] if kt else None
@@ -607,6 +681,22 @@ def main():
             live_s = lms / 1e3 / ln if ln else None
             ach = bpl / live_s / 1e9 if (bpl is not None and live_s) else None
             iso = bpl / (rms / 1e3 / rn) / 1e9 if (bpl is not None and rms > 0) else None
+            if rk == "sc_detect":   # the Scan Context Gram on the matrix cores: flop, not bytes
+                tf = lambda f, t: f / t / 1e12 if (f is not None and t) else None  # noqa: E731
+                live_t, iso_t = tf(bpl, live_s), tf(bpl, rms / 1e3 / rn if rn else None)
+                pk = MFMA_F64_PEAK_TFLOPS
+                return {"bound": "mfma", "dtype": "f64", "achieved": round(live_t, 4) if live_t else None,
+                        "peak": pk, "unit": "TFLOP/s",
+                        "frac": round(live_t / pk, 6) if (live_t and pk) else None, "kernel": rk,
+                        "avg_launch_us": round(live_s * 1e6, 2) if live_s else None, "launches_timed": ln,
+                        "flop_per_launch": int(bpl) if bpl is not None else None,
+                        "pairs_in_window": counts.get("sc_pairs"),
+                        "isolated": {"achieved": round(iso_t, 4) if iso_t else None,
+                                     "frac": round(iso_t / pk, 6) if (iso_t and pk) else None,
+                                     "avg_launch_us": round(rms / rn * 1e3, 2) if rn else None},
+                        "share_of_device_time": round(rms / total_ms, 4) if total_ms else None,
+                        "note": "issued MFMA flop (64 x 64 padded Gram, ceil(NR/16) k-steps per Eigen accumulator) "
+                                "per distance pair; the kernel's other work (ring-key K-NN, sector-key alignment) is VALU"}
             traffic, tsrc = pmc_traffic(a.traffic_from, rk)
             return {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
@@ -666,8 +756,8 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": "C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 K=10, "
-                                   "steady state",
+            "config": {"workload": a.workload, "sc_candidates": cfg.sc_num_candidates,
+                       "loop_closure": bool(cfg.loop_closure_enable),
                        "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
                        "scans_per_step": S * world, "preroll_scans": a.preroll,
                        "context_phase_lag": [lag(g) for g in range(n_ctx)],
@@ -694,6 +784,8 @@ def main():
             "context_hbm_gb": round(ctx_bytes / 2**30, 2),
             "loop_verify_icp": icp,
         }
+        if world == 1 and a.extra not in ("", "none"):   # the other BASELINE configs at 1 GPU, each by its own process
+            out["config_lines"] = extra_lines(a)
         print(json.dumps(out), flush=True)
     if pool is not None:
         pool.shutdown()

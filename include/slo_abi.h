@@ -203,6 +203,34 @@ int slo_batch_sc_distance(slo_ctx* ctx, const double* d_sc1, const double* d_sc2
 int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const int32_t* d_n, float leaf,
                          void* d_out, size_t out_stride, int32_t* d_nout, int out_cap);
 
+/* ---------------------------------------------------------------- Mode S: one stream over several contexts
+ * One vehicle's stream split over contexts, on one GPU or several (SURVEY
+ * §8(e) mode S; the reference deploys the same split as processes,
+ * launch/run.launch:14-17).  Front contexts take turns at the scans' front
+ * ends — imageProjection::cloudHandler and featureAssociation's feature
+ * extraction (adjustDistortion .. extractFeatures, FA:1833-1841) — and one
+ * owner context runs every scan's back end: the odometry (FA:1843-1858),
+ * mapOptimization and Scan Context.  Two device buffers travel per scan:
+ * - the carry, from a scan's front end to the next scan's: the state a front
+ *   end inherits (featureAssociation's persistent arrays, read where a scan
+ *   does not rewrite them; the cloud_info arrays past the scan's points; the
+ *   orientations an empty scan keeps — SURVEY Appendix A Q5);
+ * - the features, from a scan's front end to the owner.
+ * Every context needs the same config and n_streams.  Not with IMU input (its
+ * ring would have to travel too).  Asynchronous on slo_stream(ctx); the caller
+ * moves the buffers (hipMemcpyPeer, RCCL send / recv: slo_amd/modes.py). */
+size_t slo_modes_carry_bytes(slo_ctx* ctx);
+size_t slo_modes_features_bytes(slo_ctx* ctx);
+/* the front end of the scan in d_points / d_counts (as slo_batch_process);
+ * d_carry_in: the previous scan's carry (NULL for a stream's first scan);
+ * writes this scan's carry and its features (device buffers of the sizes above) */
+int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan,
+                      const void* d_carry_in, void* d_carry_out, void* d_features_out);
+/* the back end of the scan whose front end wrote d_features; d_points /
+ * d_counts: that scan again (mapping reads the raw cloud, MO:1236) */
+int slo_back_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
+                     double t_scan);
+
 /* ---------------------------------------------------------------- loop-closure verification
  * mapOptmization.cpp:841-1110 (detectLoopClosure + performLoopClosure, minus
  * the GTSAM factors).  Needs cfg.loop_verify = 1 and

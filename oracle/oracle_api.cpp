@@ -41,10 +41,92 @@ struct OracleStream {
     // the nodes up to mapOptimization::run (flags 1, 2, 4)
     int step_map(const float* pts, int n, double t) {
         t_gemm_mode = gemm_mode;   // this thread runs this stream now
-        int flags = 0;
         det_valid = false;
         ip.cloudHandler(pts, n);
         fa.run(ip.segmentedCloud, ip.segMsg, ip.outlierCloud, t);
+        return after_fa(pts, n, t);
+    }
+
+    // ---- Mode S: one stream's scans split between objects.
+    // front(): imageProjection + featureAssociation's feature extraction
+    // (adjustDistortion .. extractFeatures, FA:1833-1841) of one scan on one
+    // object; back(): the odometry (FA:1843-1858), mapping and Scan Context
+    // of that scan on the owner object, from the front's feature clouds.
+    // What a scan's front end inherits from the previous scan's — the
+    // carry — is the stale state of Appendix A Q5: featureAssociation's
+    // persistent arrays (cloudSmoothness, cloudCurvature,
+    // cloudNeighborPicked, cloudLabel: read at positions this scan does not
+    // rewrite), the cloud_info arrays' tails past this scan's points
+    // (segmentedCloudColInd[ind + 5] reads past the end, FA:730-745) and the
+    // orientations an empty scan keeps.  front() runs imageProjection first
+    // (it needs nothing from the previous scan) and merges the carry after it.
+    // IMU input is not part of Mode S (the IMU ring would have to travel too).
+    struct Carry {
+        SegInfo seg;
+        std::vector<Smooth> smooth;
+        std::vector<float> curv;
+        std::vector<int> picked, label;
+    };
+    struct Features { Cloud sharp, less_sharp, flat, less_flat, outlier; };
+    void front(const float* pts, int n, double t, const Carry* in, Carry* out, Features* f) {
+        t_gemm_mode = gemm_mode;
+        ip.cloudHandler(pts, n);
+        if (in) {
+            const size_t S = ip.segmentedCloud.size(), H = ip.segMsg.segmentedCloudColInd.size();
+            for (size_t i = S; i < H; ++i) {
+                ip.segMsg.segmentedCloudColInd[i] = in->seg.segmentedCloudColInd[i];
+                ip.segMsg.segmentedCloudGroundFlag[i] = in->seg.segmentedCloudGroundFlag[i];
+                ip.segMsg.segmentedCloudRange[i] = in->seg.segmentedCloudRange[i];
+            }
+            if (ip.laserCloudIn.empty()) {
+                ip.segMsg.startOrientation = in->seg.startOrientation;
+                ip.segMsg.endOrientation = in->seg.endOrientation;
+                ip.segMsg.orientationDiff = in->seg.orientationDiff;
+            }
+            fa.cloudSmoothness = in->smooth;
+            fa.cloudCurvature = in->curv;
+            fa.cloudNeighborPicked = in->picked;
+            fa.cloudLabel = in->label;
+        }
+        fa.timeScanCur = t;
+        fa.segmentedCloud = ip.segmentedCloud;
+        fa.segInfo = ip.segMsg;
+        fa.outlierCloud = ip.outlierCloud;
+        fa.published_to_mapping = false;
+        fa.adjustDistortion();
+        fa.calculateSmoothness();
+        fa.markOccludedPoints();
+        fa.extractFeatures();
+        *out = Carry{ip.segMsg, fa.cloudSmoothness, fa.cloudCurvature, fa.cloudNeighborPicked, fa.cloudLabel};
+        *f = Features{fa.cornerPointsSharp, fa.cornerPointsLessSharp, fa.surfPointsFlat, fa.surfPointsLessFlat,
+                      fa.outlierCloud};
+    }
+    // flags as step()
+    int back(const Features& f, const float* pts, int n, double t) {
+        t_gemm_mode = gemm_mode;
+        det_valid = false;
+        fa.timeScanCur = t;
+        fa.cornerPointsSharp = f.sharp;
+        fa.cornerPointsLessSharp = f.less_sharp;
+        fa.surfPointsFlat = f.flat;
+        fa.surfPointsLessFlat = f.less_flat;
+        fa.outlierCloud = f.outlier;
+        fa.published_to_mapping = false;
+        if (!fa.systemInitedLM) {
+            fa.checkSystemInitialization();
+        } else {
+            fa.updateInitialGuess();
+            fa.updateTransformation();
+            fa.integrateTransformation();
+            fa.publishCloudsLast();
+        }
+        const int fl = after_fa(pts, n, t);
+        return fl | step_loop(fl, t);
+    }
+
+    // featureAssociation has run on this scan: the hand-offs and mapping
+    int after_fa(const float* pts, int n, double t) {
+        int flags = 0;
         if (fa.systemInitedLM && scan_index > 0) flags |= 1;
         if (flags & 1) {
             // TransformFusion::laserOdometryHandler (TF:186-219) on this scan's
@@ -79,6 +161,28 @@ struct OracleStream {
     }
 };
 
+// ---- Mode S (OracleStream::front / back) over byte blobs, so that ranks can
+// exchange them: a carry is the stale state a scan's front end leaves for the
+// next one, features are what the front end hands the owner
+static size_t blob_put(std::vector<char>& b, const void* p, size_t n) {
+    const size_t o = b.size();
+    b.resize(o + n);
+    if (n) memcpy(b.data() + o, p, n);
+    return o;
+}
+template <class T> static void vec_put(std::vector<char>& b, const std::vector<T>& v) {
+    const int64_t n = (int64_t)v.size();
+    blob_put(b, &n, 8);
+    blob_put(b, v.data(), sizeof(T) * v.size());
+}
+template <class T> static const char* vec_get(const char* p, std::vector<T>& v) {
+    int64_t n;
+    memcpy(&n, p, 8);
+    v.resize((size_t)n);
+    if (n) memcpy(v.data(), p + 8, sizeof(T) * (size_t)n);
+    return p + 8 + sizeof(T) * (size_t)n;
+}
+
 extern "C" {
 
 int oracle_config_preset(int preset, slo_config* out) { return slo_config_preset_impl(preset, out); }
@@ -90,6 +194,54 @@ void* oracle_create(const slo_config* cfg, int stable_voxel) {
     return s;
 }
 void oracle_destroy(void* h) { delete (OracleStream*)h; }
+
+static std::vector<char> g_blob[2];   // the last front call's carry and features (per process; tests only)
+// front end of one scan; carry_in = NULL for the first scan.  Returns the
+// byte sizes of the carry and the features, fetched with oracle_front_blob.
+int oracle_front(void* h, const float* pts, int n, double t, const void* carry_in, int64_t* sizes) {
+    OracleStream* s = (OracleStream*)h;
+    OracleStream::Carry in, out;
+    if (carry_in) {
+        const char* p = (const char*)carry_in;
+        float o[3];
+        memcpy(o, p, 12);
+        p += 12;
+        in.seg.startOrientation = o[0]; in.seg.endOrientation = o[1]; in.seg.orientationDiff = o[2];
+        p = vec_get(p, in.seg.segmentedCloudColInd);
+        p = vec_get(p, in.seg.segmentedCloudGroundFlag);
+        p = vec_get(p, in.seg.segmentedCloudRange);
+        p = vec_get(p, in.smooth);
+        p = vec_get(p, in.curv);
+        p = vec_get(p, in.picked);
+        p = vec_get(p, in.label);
+    }
+    OracleStream::Features f;
+    s->front(pts, n, t, carry_in ? &in : nullptr, &out, &f);
+    std::vector<char>& c = g_blob[0];
+    c.clear();
+    const float o[3] = {out.seg.startOrientation, out.seg.endOrientation, out.seg.orientationDiff};
+    blob_put(c, o, 12);
+    vec_put(c, out.seg.segmentedCloudColInd);
+    vec_put(c, out.seg.segmentedCloudGroundFlag);
+    vec_put(c, out.seg.segmentedCloudRange);
+    vec_put(c, out.smooth);
+    vec_put(c, out.curv);
+    vec_put(c, out.picked);
+    vec_put(c, out.label);
+    std::vector<char>& b = g_blob[1];
+    b.clear();
+    for (const Cloud* cl : {&f.sharp, &f.less_sharp, &f.flat, &f.less_flat, &f.outlier}) vec_put(b, *cl);
+    sizes[0] = (int64_t)c.size();
+    sizes[1] = (int64_t)b.size();
+    return 0;
+}
+void oracle_front_blob(int which, void* out) { memcpy(out, g_blob[which].data(), g_blob[which].size()); }
+int oracle_back(void* h, const void* features, const float* pts, int n, double t) {
+    OracleStream::Features f;
+    const char* p = (const char*)features;
+    for (Cloud* cl : {&f.sharp, &f.less_sharp, &f.flat, &f.less_flat, &f.outlier}) p = vec_get(p, *cl);
+    return ((OracleStream*)h)->back(f, pts, n, t);
+}
 // the normal equations' accumulation order (oracle_common.h gemm_AtA): 0 double-double (default), 1 OpenCV 3.x
 void oracle_set_gemm_mode(void* h, int mode) { ((OracleStream*)h)->gemm_mode = mode; }
 
@@ -499,10 +651,22 @@ int oracle_gen_scan(int preset, int config_id, int stream_id, int k, float* out)
 // mo, sc); stage_one[4] = the same for a copy of stream 0 run over the same
 // scans alone, before the parallel run (the reference's one-stream
 // 3-process topology, SURVEY (A)).
+static double bench_impl(const slo_config& cfg, int config_id, int n_threads, int n_scans, int preroll, int history,
+                         int n_distinct, double* stage_s, double* stage_one);
 double oracle_bench(int preset, int config_id, int n_threads, int n_scans, int preroll, int history, int n_distinct,
                     double* stage_s, double* stage_one) {
     slo_config cfg;
-    if (slo_config_preset_impl(preset, &cfg) || n_threads <= 0 || n_scans <= 0) return -1;
+    if (slo_config_preset_impl(preset, &cfg)) return -1;
+    return bench_impl(cfg, config_id, n_threads, n_scans, preroll, history, n_distinct, stage_s, stage_one);
+}
+// the same with the caller's configuration (a preset with edits: SC off, K = 50, ...)
+double oracle_bench_cfg(const slo_config* cfg, int config_id, int n_threads, int n_scans, int preroll, int history,
+                        int n_distinct, double* stage_s, double* stage_one) {
+    return bench_impl(*cfg, config_id, n_threads, n_scans, preroll, history, n_distinct, stage_s, stage_one);
+}
+static double bench_impl(const slo_config& cfg, int config_id, int n_threads, int n_scans, int preroll, int history,
+                         int n_distinct, double* stage_s, double* stage_one) {
+    if (n_threads <= 0 || n_scans <= 0) return -1;
     if (n_distinct <= 0 || n_distinct > n_threads) n_distinct = n_threads;
     const int P = cfg.n_scan * cfg.horizon_scan;
     std::vector<OracleStream*> base(n_distinct, nullptr);

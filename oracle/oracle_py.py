@@ -73,6 +73,8 @@ def lib():
         L.oracle_gen_scan.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         L.oracle_bench.restype = ctypes.c_double
         L.oracle_bench.argtypes = [ctypes.c_int] * 7 + [ctypes.c_void_p, ctypes.c_void_p]
+        L.oracle_bench_cfg.restype = ctypes.c_double
+        L.oracle_bench_cfg.argtypes = [ctypes.POINTER(SloConfig)] + [ctypes.c_int] * 6 + [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_sc_distance.restype = ctypes.c_double
         L.oracle_sc_distance.argtypes = [ctypes.POINTER(SloConfig), ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.POINTER(ctypes.c_int)]
@@ -109,6 +111,10 @@ def lib():
         L.oracle_xsc_query.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                        ctypes.c_void_p]
         L.oracle_set_gemm_mode.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.oracle_front.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double, ctypes.c_void_p,
+                                   ctypes.c_void_p]
+        L.oracle_front_blob.argtypes = [ctypes.c_int, ctypes.c_void_p]
+        L.oracle_back.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         L.oracle_gemm_stats.argtypes = [ctypes.c_void_p]
         L.oracle_gemm_tally.argtypes = [ctypes.c_int]
         L.oracle_gemm_at.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -315,6 +321,27 @@ class OracleStream:
         (stamp, qx, qy, qz, qw, ax, ay, az, wx, wy, wz)"""
         m = np.ascontiguousarray(msgs, np.float64).reshape(-1, 11)
         lib().oracle_imu(self.h, m.ctypes.data, len(m))
+
+    def front(self, pts, t, carry=None):
+        """Mode S front end of one scan (imageProjection + feature extraction)
+        with the previous scan's carry (None for the first scan) -> (carry,
+        features), both uint8 arrays (OracleStream::front)"""
+        pts = np.ascontiguousarray(pts, np.float32)
+        sizes = np.zeros(2, np.int64)
+        c = None if carry is None else np.ascontiguousarray(carry, np.uint8)
+        lib().oracle_front(self.h, pts.ctypes.data, len(pts), float(t), None if c is None else c.ctypes.data,
+                           sizes.ctypes.data)
+        out = [np.empty(int(n), np.uint8) for n in sizes]
+        for k in range(2):
+            lib().oracle_front_blob(k, out[k].ctypes.data)
+        return out[0], out[1]
+
+    def back(self, features, pts, t):
+        """Mode S back end (odometry, mapping, Scan Context) of one scan from
+        its front end's features -> flags as step()"""
+        pts = np.ascontiguousarray(pts, np.float32)
+        f = np.ascontiguousarray(features, np.uint8)
+        return lib().oracle_back(self.h, f.ctypes.data, pts.ctypes.data, len(pts), float(t))
 
     def step_map(self, pts, t):
         """the nodes up to mapOptimization::run: flags 1, 2, 4"""

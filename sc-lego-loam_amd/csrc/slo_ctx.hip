@@ -234,6 +234,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.st, S);
     c.add(&ctx->d_io, 1);
     c.add(&v.imu, S);
+    c.add(&v.wctr, 8);
     // ---- mapping + Scan Context history
     // Capacities are worst-case bounds, so no cloud is ever clipped: a
     // VoxelGrid output is no larger than its input, the surf DS of a scan is
@@ -601,6 +602,131 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     return slo::pg_after_loops(ctx);   // the loop factors (MO:1038-1046, 1083-1091)
 }
 
+// ---------------------------------------------------------------- Mode S
+// The slabs that travel between the contexts of one stream split over
+// several (include/slo_abi.h "Mode S"): each a [S][...] array of the arena,
+// copied whole.  carry: featureAssociation's persistent arrays (Q5), the
+// cloud_info arrays (their tails past a scan's points are read, FA:730-745)
+// and the orientations an empty scan keeps; features: what odometry and
+// mapping read of a scan's front end.
+}  // extern "C"
+namespace slo {
+struct ModesSlab { void* p; size_t bytes; };
+static std::vector<ModesSlab> modes_carry(slo_ctx* ctx) {
+    const DevView& v = ctx->v;
+    const size_t S = ctx->S, H = v.H;
+    return {{v.smooth, S * H * sizeof(Smooth)}, {v.curv, S * H * 4}, {v.picked, S * H * 4}, {v.clabel, S * H * 4},
+            {v.seg_col, S * H * 4}, {v.seg_ground, S * H}, {v.seg_range, S * H * 4}, {v.orient, S * 3 * 4}};
+}
+#define MODES_NCOUNT 8   // per stream: n_sharp, n_less_sharp, n_flat, n_less_flat, seg_count, outlier_count, err, first_half
+static std::vector<ModesSlab> modes_features(slo_ctx* ctx, int32_t** counts) {
+    const DevView& v = ctx->v;
+    const size_t S = ctx->S, H = v.H, R = v.cfg.n_scan;
+    *counts = nullptr;   // (a slab of its own, packed by k_modes_counts)
+    return {{v.sharp, S * v.cap_sharp * 16}, {v.less_sharp, S * v.cap_less_sharp * 16}, {v.flat, S * v.cap_flat * 16},
+            {v.less_flat, S * v.cap_less_flat * 16}, {v.outlier, S * H * 16}, {v.roff_cur, S * 2 * (R + 1) * 4},
+            {nullptr, S * MODES_NCOUNT * 4}};
+}
+static size_t modes_bytes(const std::vector<ModesSlab>& sl) {
+    size_t o = 0;
+    for (const auto& x : sl) o += (x.bytes + 255) & ~(size_t)255;
+    return o;
+}
+// copy every slab with a pointer between the arena and the buffer (out: arena -> buffer)
+static int modes_copy(slo_ctx* ctx, const std::vector<ModesSlab>& sl, char* buf, bool out, int first, int last) {
+    size_t o = 0;
+    for (int k = 0; k < (int)sl.size(); ++k) {
+        if (k >= first && k < last && sl[k].p)
+            SLO_CHECK(hipMemcpyAsync(out ? (void*)(buf + o) : sl[k].p, out ? sl[k].p : (const void*)(buf + o),
+                                     sl[k].bytes, hipMemcpyDeviceToDevice, ctx->stream));
+        o += (sl[k].bytes + 255) & ~(size_t)255;
+    }
+    return 0;
+}
+// after imageProjection: the cloud_info tails past this scan's points and, for
+// a scan without a finite point, the orientations come from the carry
+__global__ void k_modes_merge(DevView v, const uint32_t* col, const uint8_t* gnd, const float* rng, const float* orient) {
+    const int s = blockIdx.y;
+    const size_t b = (size_t)s * v.H;
+    const int n = v.st[s].seg_count;
+    for (int i = n + blockIdx.x * blockDim.x + threadIdx.x; i < v.H; i += gridDim.x * blockDim.x) {
+        v.seg_col[b + i] = col[b + i];
+        v.seg_ground[b + i] = gnd[b + i];
+        v.seg_range[b + i] = rng[b + i];
+    }
+    if (blockIdx.x == 0 && threadIdx.x < 3 && v.fl[2 * s + 1] < 0) v.orient[3 * s + threadIdx.x] = orient[3 * s + threadIdx.x];
+}
+__global__ void k_modes_counts(DevView v, int32_t* c, int out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    StreamState& st = v.st[s];
+    int32_t* q = c + (size_t)s * MODES_NCOUNT;
+    if (out) {
+        q[0] = st.n_sharp; q[1] = st.n_less_sharp; q[2] = st.n_flat; q[3] = st.n_less_flat;
+        q[4] = st.seg_count; q[5] = st.outlier_count; q[6] = st.err; q[7] = st.first_half;
+    } else {
+        st.n_sharp = q[0]; st.n_less_sharp = q[1]; st.n_flat = q[2]; st.n_less_flat = q[3];
+        st.seg_count = q[4]; st.outlier_count = q[5]; st.err |= q[6]; st.first_half = q[7];
+    }
+}
+}  // namespace slo
+extern "C" {
+
+size_t slo_modes_carry_bytes(slo_ctx* ctx) { return ctx ? slo::modes_bytes(slo::modes_carry(ctx)) : 0; }
+size_t slo_modes_features_bytes(slo_ctx* ctx) {
+    int32_t* c;
+    return ctx ? slo::modes_bytes(slo::modes_features(ctx, &c)) : 0;
+}
+
+int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan,
+                      const void* d_carry_in, void* d_carry_out, void* d_features_out) {
+    if (!ctx || !d_points || !d_counts || !d_carry_out || !d_features_out) return SLO_E_ARG;
+    if (ctx->cfg.use_cloud_ring && !ctx->v.rings) { ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings"; return SLO_E_STATE; }
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
+    if (int r = slo::ip_run(ctx)) return r;
+    const auto carry = slo::modes_carry(ctx);
+    if (d_carry_in) {   // the previous scan's stale state (that scan's front end ran elsewhere)
+        char* ci = (char*)d_carry_in;
+        if (int r = slo::modes_copy(ctx, carry, ci, false, 0, 4)) return r;   // FA's persistent arrays, whole
+        size_t o[8], x = 0;
+        for (int k = 0; k < 8; ++k) { o[k] = x; x += (carry[k].bytes + 255) & ~(size_t)255; }
+        const DevView& v = ctx->v;
+        SLO_LAUNCH(ctx, "modes_merge", slo::k_modes_merge, dim3(std::max(1, std::min(64, (v.H + 255) / 256)), ctx->S),
+                   dim3(256), 0, v, (const uint32_t*)(ci + o[4]), (const uint8_t*)(ci + o[5]), (const float*)(ci + o[6]),
+                   (const float*)(ci + o[7]));
+    }
+    if (int r = slo::fa_features_run(ctx)) return r;
+    if (int r = slo::modes_copy(ctx, carry, (char*)d_carry_out, true, 0, 8)) return r;
+    int32_t* cnt;
+    const auto feat = slo::modes_features(ctx, &cnt);
+    if (int r = slo::modes_copy(ctx, feat, (char*)d_features_out, true, 0, 6)) return r;
+    const size_t oc = slo::modes_bytes(feat) - ((feat[6].bytes + 255) & ~(size_t)255);
+    SLO_LAUNCH(ctx, "modes_counts", slo::k_modes_counts, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
+               (int32_t*)((char*)d_features_out + oc), 1);
+    SLO_CHECK(hipGetLastError());
+    return SLO_OK;
+}
+
+int slo_back_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
+                     double t_scan) {
+    if (!ctx || !d_features || !d_points || !d_counts) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
+    int32_t* cnt;
+    const auto feat = slo::modes_features(ctx, &cnt);
+    if (int r = slo::modes_copy(ctx, feat, (char*)d_features, false, 0, 6)) return r;
+    const size_t oc = slo::modes_bytes(feat) - ((feat[6].bytes + 255) & ~(size_t)255);
+    SLO_LAUNCH(ctx, "modes_counts", slo::k_modes_counts, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
+               (int32_t*)((char*)d_features + oc), 0);
+    const bool first = !ctx->fa_inited;
+    if (int r = slo::fa_odometry_run(ctx, first)) return r;
+    slo::fa_advance(ctx, first);
+    int r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
+    if (r || !ctx->cfg.loop_closure_enable) return r;
+    return slo_batch_sc_detect(ctx);
+}
+
 int slo_batch_loop_closure(slo_ctx* ctx) {
     if (!ctx) return SLO_E_ARG;
     if (!ctx->cfg.loop_verify) { ctx->err = "loop verification needs cfg.loop_verify"; return SLO_E_STATE; }
@@ -693,8 +819,10 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         int32_t e = st.err;
         for (const slo::PclWs* pw : {&ctx->pws, &ctx->pws2}) {
             int32_t x = 0;
-            if (pw->serr) SLO_CHECK(hipMemcpy(&x, pw->serr + stream, 4, hipMemcpyDeviceToHost));
-            e |= x;
+            for (int g = 0; pw->serr && g < VG_MAXG; ++g) {   // every filter's virtual stream (vg_run_groups)
+                SLO_CHECK(hipMemcpy(&x, pw->serr + (size_t)g * ctx->S + stream, 4, hipMemcpyDeviceToHost));
+                e |= x;
+            }
         }
         tmp.resize(4); memcpy(tmp.data(), &e, 4); count = 1; esz = 4;
     }
@@ -724,6 +852,7 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 32; esz = 8;
     }
     else if (name == "dbg") { tmp.resize(64); memcpy(tmp.data(), st.dbg, 64); count = 8; esz = 8; }
+    else if (name == "work") dev(v.wctr, 8, 8);   // context-wide work counters (DevView::wctr)
     else if (name == "imu") {   // FA's IMU scalars (slo::ImuState), as float64
         slo::ImuState m;
         SLO_CHECK(hipMemcpy(&m, v.imu + stream, sizeof(m), hipMemcpyDeviceToHost));

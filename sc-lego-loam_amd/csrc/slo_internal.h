@@ -192,6 +192,8 @@ struct DevView {
     int32_t* ind_corner; // [S][cap_sharp][2]  pointSearchCornerInd1..2
     StreamState* st;     // [S]
     ImuState* imu;       // [S] (slo_batch_imu / slo_imu_handler)
+    unsigned long long* wctr;   // [8] cumulative work counters (slo_get "work"): [0] Scan Context pairs whose
+                                // distance was evaluated (k_sc_detect; the bench prices sc_detect's MFMA work)
     // ---- mapping (mapOptmization.cpp)
     int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
     int KFMAX;           // keyframe pose / Scan Context history capacity
@@ -463,6 +465,7 @@ struct MapWs {  // VoxelGrid workspace (slo_vg.hip), sized on the host from the 
     int32_t* osw = nullptr;       // [32] tickets (pass, XCD), [8] tiles per XCD, [S] XCD tile offsets
     unsigned long long* lbk = nullptr;   // [tiles][256] (tag, inclusive flag, count)
 };
+#define VG_MAXG 8   // VoxelGrid filters one call can batch (vg_run_groups): per-virtual-stream arrays hold VG_MAXG * S
 struct PSeg;
 struct PRes;
 struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the input strides only

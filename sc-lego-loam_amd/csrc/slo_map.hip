@@ -958,13 +958,32 @@ int map_run(slo_ctx* ctx) {
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
     SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
-    // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263).  With a
-    // few streams the chip is mostly idle and a VoxelGrid's latency is what a
-    // scan waits for, so the two local-map filters run on the side stream
-    // (their own workspaces) while the current scan's five run here.
+    // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263): the six
+    // filters as one batched VoxelGrid call (vg_run_groups: (filter, stream)
+    // pairs as the sort's units), so a scan waits for one sort chain, not six
     int r;
-    // (not while kernels are stamped: both streams' stamps would share one ring)
-    const bool fork = S <= SLO_VG_FORK_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
+#ifndef SLO_MAP_BATCHED_VG
+#define SLO_MAP_BATCHED_VG 1
+#endif
+    const bool fork = !SLO_MAP_BATCHED_VG && S <= SLO_VG_FORK_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
+    if (SLO_MAP_BATCHED_VG) {
+        const VgGroup gs[6] = {
+            {v.map_c, (size_t)v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner, v.map_c_ds,
+             (size_t)v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc},
+            {v.map_s, (size_t)v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf, v.map_s_ds,
+             (size_t)v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms},
+            {nullptr, (size_t)v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, (size_t)v.P,
+             fld(&StreamState::n_raw_ds), SS, v.P},
+            {v.corner_last, (size_t)v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS, v.cfg.leaf_corner,
+             v.cur_c_ds, (size_t)v.cap_less_sharp, fld(&StreamState::n_corner_ds), SS, v.cap_less_sharp},
+            {v.surf_last, (size_t)v.cap_less_flat, fld(&StreamState::surfLastNum), SS, v.cfg.leaf_surf, v.cur_s_ds,
+             (size_t)v.H, fld(&StreamState::n_surf_ds), SS, v.H},
+            {v.outl_cam, (size_t)v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier, v.cur_o_ds,
+             (size_t)v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko}};
+        if ((r = vg_run_groups(ctx, "map_step", gs, 6))) return r;
+    } else {
+    // (round 3's form: one call per filter; with a few streams the two
+    // local-map filters run on a side stream while the current scan's run here)
     if (fork) {
         if ((r = vg_side_ready(ctx))) return r;
         SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
@@ -992,6 +1011,7 @@ int map_run(slo_ctx* ctx) {
     if ((r = vg_run(ctx, "outlier", v.outl_cam, v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier,
                     v.cur_o_ds, v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko))) return r;
     if (fork) SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));   // k_mo_concat's map_ok reads the map DS sizes
+    }
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
     if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
                     v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;

@@ -40,6 +40,7 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
             st.det_loop_id = -1; st.det_yaw = 0; st.det_min_dist = 10000000; st.det_nn_idx = 0;
             s_skip = 1;
         } else {
+            atomicAdd(&v.wctr[0], (unsigned long long)K);   // K candidate distances follow
             if (st.sc_counter % v.cfg.sc_tree_making_period == 0) st.sc_tree_n = N - v.cfg.sc_num_exclude_recent;
             st.sc_counter = st.sc_counter + 1;
             s_treen = st.sc_tree_n;

@@ -7,7 +7,8 @@
 //   sc_pair_distance  SCManager::distanceBtnScanContext (SCc:116-148): the
 //               sector-key alignment over all shifts (fastAlignUsingVkey,
 //               SCc:93-113), the 7-shift window sorted ascending, the
-//               column-cosine distance per shift (distDirectSC, SCc:69-90),
+//               column-cosine distance per shift (distDirectSC, SCc:69-90)
+//               from the column Gram on the matrix cores (sc_gram_mfma),
 //               first minimum — run by a whole workgroup.
 #pragma once
 #include "slo_internal.h"
@@ -68,21 +69,75 @@ __device__ inline unsigned long long wave_min_u64(unsigned long long x) {
 }
 
 // workgroup scratch of sc_pair_distance
+#define SC_GS (SC_NS + 1)   // Gram row stride (doubles): odd, so a column walk spreads over the banks
 struct ScPairLds {
     double sim[7 * SC_NS];
     int simok[7 * SC_NS];
     double dist7[7];
     double shnorm[SC_NS];
     int shifts[7];
+    double n1[SC_NS], n2[SC_NS];   // column norms of sc1 / sc2 (the MFMA form)
+    double G[SC_NS * SC_GS];       // column Gram sc1^T sc2 (the MFMA form)
 };
 
+// ---- the column cosines of distDirectSC (SCc:69-90) on the matrix cores.
+// Every shift's cosines are entries of ONE column Gram G = sc1^T sc2 (NS x NS,
+// G[i][j] = sum over rings r of sc1[r][i] * sc2[r][j]): shift sh reads
+// G[j][(j - sh) mod NS].  Eigen's SSE2 order for such a 20-term dot (ESum:
+// four lane accumulators over r mod 4, each a sequential double sum of exact
+// float x float products, combined (0 + 2) + (1 + 3)) maps onto
+// v_mfma_f64_16x16x4_f64, which computes a k-ordered chain of fused
+// multiply-adds bit for bit (tools/mfma_f64_check.hip: 0 of 5.1 M random
+// outputs differ from the chain): accumulator u takes rings u, u + 4, u + 8,
+// u + 12 as k = 0..3 of one MFMA and u + 16, ... in the next, from a zero C.
+// A product of two floats is exact in double, so fma(a, b, acc) = acc + a*b,
+// as Eigen adds it (a zero start turns a leading -0 product into +0, which
+// no cosine, norm or mean can tell apart).  The workgroup's four waves take
+// the four 16-row tile rows of the 64 x 64 padded Gram: per wave 4 tiles x
+// 4 accumulators x ceil(NR / 16) MFMAs (32 at NR = 20).  Needs NR % 4 == 0
+// (ESum's combine, as the VALU form) and 256 threads.
+typedef double sc_d4 __attribute__((ext_vector_type(4)));
+__device__ inline void sc_gram_mfma(const double* sc1, const double* sc2, int NR, int NS, double* G) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, kq = lane >> 4, c = lane & 15;
+    const int nm = (NR + 15) >> 4;
+    const int ia = 16 * w + c;
+    for (int J = 0; J < 4; ++J) {
+        const int jb = 16 * J + c;
+        sc_d4 acc[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc[u] = sc_d4{0.0, 0.0, 0.0, 0.0};
+        for (int m = 0; m < nm; ++m) {
+            double a[4], b[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {   // unconditional (clamped) loads, all in flight before the MFMAs
+                const int r = u + 4 * kq + 16 * m, rr = min(r, NR - 1);
+                a[u] = sc1[rr * NS + min(ia, NS - 1)];
+                b[u] = sc2[rr * NS + min(jb, NS - 1)];
+                a[u] = (r < NR && ia < NS) ? a[u] : 0.0;
+                b[u] = (r < NR && jb < NS) ? b[u] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b[u], acc[u], 0, 0, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {   // D row (lane >> 4) + 4 q, column lane & 15
+            const int i = 16 * w + kq + 4 * q;
+            if (i < NS && jb < NS) G[i * SC_GS + jb] = (acc[0][q] + acc[2][q]) + (acc[1][q] + acc[3][q]);
+        }
+    }
+}
+
 // distanceBtnScanContext(sc1, sc2) -> (*dist, *align), valid in thread 0;
-// every thread of the workgroup must call it (it synchronises)
+// every thread of the workgroup must call it (it synchronises).  With 256
+// threads and NR % 4 == 0 (every preset: 20 rings) the column cosines come
+// from the MFMA Gram (sc_gram_mfma), else from per-thread ESum dots; the two
+// give the same doubles.
 __device__ inline void sc_pair_distance(const double* sc1, const double* vk1, const double* sc2, const double* vk2,
                                         int NR, int NS, double search_ratio, ScPairLds& L, double* dist,
                                         int* align) {
     const int tid = threadIdx.x;
-    // fastAlignUsingVkey: 60 shifts on 60 lanes
+    const bool mfma = blockDim.x == 256 && NR >= 4 && (NR & 3) == 0;
+    // fastAlignUsingVkey: 60 shifts on 60 lanes; the column norms beside it
     if (tid < NS) {
         ESum e;
         for (int j = 0; j < NS; ++j) {
@@ -90,7 +145,17 @@ __device__ inline void sc_pair_distance(const double* sc1, const double* vk1, co
             e.add(d * d);
         }
         L.shnorm[tid] = sqrt(e.get());
+    } else if (mfma && tid >= 64 && tid < 64 + 2 * NS && tid < 256) {
+        const int j = (tid - 64) % NS;
+        const double* d = tid < 64 + NS ? sc1 : sc2;
+        ESum e;
+        for (int r = 0; r < NR; ++r) {
+            const double a = d[r * NS + j];
+            e.add(a * a);
+        }
+        (tid < 64 + NS ? L.n1 : L.n2)[j] = sqrt(e.get());
     }
+    if (mfma) sc_gram_mfma(sc1, sc2, NR, NS, L.G);
     __syncthreads();
     if (tid == 0) {
         int argmin = 0;
@@ -119,14 +184,19 @@ __device__ inline void sc_pair_distance(const double* sc1, const double* vk1, co
         L.simok[t] = 0;
         if (sh < 0) continue;
         const int j2 = ((j - sh) % NS + NS) % NS;
-        ESum n1, n2, dt;
-        for (int r = 0; r < NR; ++r) {
-            double a = sc1[r * NS + j], b = sc2[r * NS + j2];
-            n1.add(a * a); n2.add(b * b); dt.add(a * b);
+        double nn1, nn2, dt;
+        if (mfma) {
+            nn1 = L.n1[j]; nn2 = L.n2[j2]; dt = L.G[j * SC_GS + j2];
+        } else {
+            ESum n1, n2, d;
+            for (int r = 0; r < NR; ++r) {
+                double a = sc1[r * NS + j], b = sc2[r * NS + j2];
+                n1.add(a * a); n2.add(b * b); d.add(a * b);
+            }
+            nn1 = sqrt(n1.get()); nn2 = sqrt(n2.get()); dt = d.get();
         }
-        double nn1 = sqrt(n1.get()), nn2 = sqrt(n2.get());
         if ((nn1 == 0) | (nn2 == 0)) continue;
-        L.sim[t] = dt.get() / (nn1 * nn2);
+        L.sim[t] = dt / (nn1 * nn2);
         L.simok[t] = 1;
     }
     __syncthreads();

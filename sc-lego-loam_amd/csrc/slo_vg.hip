@@ -27,11 +27,10 @@ namespace slo {
 // meta words [total, max cell count, long-voxel count]
 // A count above the stream's input stride (a caller's io->npts: nothing else
 // bounds it) is clamped to the stride — the workspace is sized from the
-// strides — and flagged (errflag bit 4, slo_get "vg_stats").
-__global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int S, int32_t* off,
-                                                    unsigned int* bounds, int32_t* meta, int32_t* osw, int tile,
-                                                    int in_stride, int32_t* errflag) {
-    const int32_t* n = src.cnt();
+// strides — and flagged (errflag bit 4, slo_get "vg_stats").  S here and in
+// every VoxelGrid kernel counts virtual streams (VgSrc).
+__global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int S, int32_t* off, unsigned int* bounds,
+                                                    int32_t* meta, int32_t* osw, int tile, int32_t* errflag) {
     __shared__ int wsum[16];
     __shared__ int carry;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -39,8 +38,8 @@ __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int
     __syncthreads();
     for (int b0 = 0; b0 < S; b0 += 1024) {
         const int s = b0 + tid;
-        const int x0 = s < S ? n[(size_t)s * n_stride] : 0;
-        const int x = max(0, min(x0, in_stride));
+        const int x0 = s < S ? src.count(s) : 0;
+        const int x = s < S ? max(0, min(x0, (int)min(src.grp(s).stride, (size_t)0x7fffffff))) : 0;
         if (x != x0) atomicOr(errflag, 4);
         int incl = x;   // inclusive wave scan
         for (int o = 1; o < 64; o <<= 1) {
@@ -73,13 +72,11 @@ __global__ void __launch_bounds__(1024) k_vg_prefix(VgSrc src, int n_stride, int
     }
 }
 
-__global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, size_t in_stride, const int32_t* off,
-                                                   unsigned int* bounds) {
-    const float4* in = src.pts();
+__global__ void __launch_bounds__(256) k_vg_bounds(VgSrc src, const int32_t* off, unsigned int* bounds) {
     const int s = blockIdx.y;
     const int n = off[s + 1] - off[s];
     unsigned int mn[3] = {0xffffffffu, 0xffffffffu, 0xffffffffu}, mx[3] = {0, 0, 0};
-    const float4* pts = in + (size_t)s * in_stride;
+    const float4* pts = src.row(s);
     const int step = gridDim.x * blockDim.x;
     for (int i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < n; i0 += 8 * step) {   // eight loads in flight
         float4 pp[8];
@@ -129,11 +126,11 @@ __device__ inline bool vg_block(int S, int& s, int& chunk) {
 }
 static inline dim3 vg_tile_grid(int GX, int S) { return dim3(GX, (S + 7) / 8 * 8); }
 
-__global__ void k_vg_params(const unsigned int* bounds, const int32_t* off, int S, float leaf, VgParams* prm) {
+__global__ void k_vg_params(VgSrc src, const unsigned int* bounds, const int32_t* off, int S, VgParams* prm) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
     VgParams p;
-    p.inv = 1.0f / leaf;
+    p.inv = 1.0f / src.grp(s).leaf;   // Array4f::Ones() / leaf_size_
     p.overflow = 0;
     const int n = off[s + 1] - off[s];
     p.ntiles = (n + VG_TILE - 1) / VG_TILE;
@@ -197,11 +194,11 @@ __device__ inline unsigned long long vg_peers(unsigned int d, int dbits, unsigne
 // later passes load all keys at once (their values: vg_tile_vals).
 #define VG_LB 8
 template <bool FIRST>
-__device__ inline void vg_tile_load(const float4* in, size_t in_stride, const VgParams& p, int s, int base, int a,
-                                    int m, int j0, const unsigned int* kin, const unsigned int* vin,
-                                    unsigned int (&key)[VG_IPT], unsigned int (&val)[VG_IPT]) {
+__device__ inline void vg_tile_load(const float4* row, const VgParams& p, int base, int a, int m, int j0,
+                                    const unsigned int* kin, const unsigned int* vin, unsigned int (&key)[VG_IPT],
+                                    unsigned int (&val)[VG_IPT]) {
     if (FIRST) {
-        const float4* src = in + (size_t)s * in_stride + a;
+        const float4* src = row + a;
 #pragma unroll
         for (int h = 0; h < VG_IPT; h += VG_LB) {
             float4 q[VG_LB];
@@ -246,13 +243,13 @@ __device__ inline void vg_tile_vals(int base, int a, int m, int j0, const unsign
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, const int32_t* off,
-                                                  const VgParams* prm, int pass, const unsigned int* ka,
-                                                  const unsigned int* kb, int* cnt, int maxT, int S) {
-    const float4* in = FIRST ? src.pts() : nullptr;
+__global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, const int32_t* off, const VgParams* prm, int pass,
+                                                  const unsigned int* ka, const unsigned int* kb, int* cnt, int maxT,
+                                                  int S) {
     __shared__ int h[VG_NB];
     int s, chunk;
     if (!vg_block(S, s, chunk)) return;
+    const float4* in = FIRST ? src.row(s) : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     if (pass >= p.npass) return;
@@ -265,7 +262,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_hist(VgSrc src, size_t in_stride, c
         __syncthreads();
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         unsigned int key[VG_IPT], val[VG_IPT];
-        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, nullptr, key, val);
+        vg_tile_load<FIRST>(in, p, base, a, m, w * (VG_TILE / VG_W) + lane, kin, nullptr, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
@@ -313,7 +310,7 @@ __global__ void __launch_bounds__(1024) k_vg_scan(const int32_t* off, const VgPa
 }
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_scatter(VgSrc src, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_scatter(VgSrc src, const int32_t* off,
                                                      const VgParams* prm, int pass, unsigned int* ka,
                                                      unsigned int* va, unsigned int* kb, unsigned int* vb,
                                                      const int* cnt, int maxT, int S) {
@@ -321,9 +318,9 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
     __shared__ int wc[VG_W][VG_NB];   // per wave slice: running digit counts, then the slice's digit offsets
     __shared__ int lb[VG_NB];         // global base of each digit minus its first position in the tile
     __shared__ int wsum[VG_W];
-    const float4* in = FIRST ? src.pts() : nullptr;
     int s, chunk;
     if (!vg_block(S, s, chunk)) return;
+    const float4* in = FIRST ? src.row(s) : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     if (pass >= p.npass) return;
@@ -341,7 +338,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
-        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
+        vg_tile_load<FIRST>(in, p, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
@@ -419,12 +416,12 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
 static_assert(VG_NB <= VG_T, "one look-back thread per digit");
 
 template <bool FIRST>
-__global__ void __launch_bounds__(VG_T) k_vg_ghist(VgSrc src, size_t in_stride, const int32_t* off,
-                                                   const VgParams* prm, int32_t* gh, int S) {
-    const float4* in = src.pts();
+__global__ void __launch_bounds__(VG_T) k_vg_ghist(VgSrc src, const int32_t* off, const VgParams* prm, int32_t* gh,
+                                                   int S) {
     __shared__ int h[VG_PASSES][VG_NB];
     int s, chunk;
     if (!vg_block(S, s, chunk)) return;
+    const float4* in = src.row(s);
     const int tid = threadIdx.x;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base, nb = 1 << p.dbits;
@@ -437,7 +434,7 @@ __global__ void __launch_bounds__(VG_T) k_vg_ghist(VgSrc src, size_t in_stride, 
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = k * VG_T + tid;
-            key[k] = j < m ? vg_key(in[(size_t)s * in_stride + a + j], p, a + j) : 0u;
+            key[k] = j < m ? vg_key(in[a + j], p, a + j) : 0u;
         }
         const unsigned long long lt = (1ull << (tid & 63)) - 1ull;
 #pragma unroll
@@ -477,7 +474,7 @@ __device__ inline unsigned long long vg_post(unsigned int tag, bool incl, int c)
 
 template <bool FIRST>
 __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SCATTER_OCC))) k_vg_onesweep(
-        VgSrc src, size_t in_stride, const int32_t* off, const VgParams* prm, int pass, unsigned int* ka,
+        VgSrc src, const int32_t* off, const VgParams* prm, int pass, unsigned int* ka,
         unsigned int* va, unsigned int* kb, unsigned int* vb, const int32_t* gbase, int32_t* osw,
         unsigned long long* lbk, const int32_t* meta, int maxT, int S, int32_t* errflag) {
     __shared__ unsigned int lk[VG_TILE], lv[VG_TILE];
@@ -485,7 +482,6 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
     __shared__ int lb[VG_NB];
     __shared__ int wsum[VG_W];
     __shared__ int tk_s;
-    const float4* in = FIRST ? src.pts() : nullptr;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int x = blockIdx.x & 7;                 // the XCD this workgroup runs on (round-robin dispatch)
     const int ntx = osw[32 + x], J = (S - x + 7) >> 3;
@@ -502,6 +498,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
             if (osw[40 + x + 8 * mid] <= tk) lo = mid; else hi = mid - 1;
         }
         const int s = x + 8 * lo, t = tk - osw[40 + s];
+        const float4* in = FIRST ? src.row(s) : nullptr;
         const VgParams p = prm[s];
         if (pass >= p.npass) { __syncthreads(); continue; }
         const bool ob = vg_out_b(p, pass);
@@ -516,7 +513,7 @@ __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(VG_SC
         __syncthreads();
         unsigned int key[VG_IPT], val[VG_IPT];
         int rk[VG_IPT];
-        vg_tile_load<FIRST>(in, in_stride, p, s, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
+        vg_tile_load<FIRST>(in, p, base, a, m, w * (VG_TILE / VG_W) + lane, kin, vin, key, val);
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
             const int j = w * (VG_TILE / VG_W) + k * 64 + lane;
@@ -632,8 +629,8 @@ __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, con
     }
 }
 
-__global__ void __launch_bounds__(1024) k_vg_hscan(const VgParams* prm, int* hcnt, int maxT, int32_t* nvox,
-                                                   int32_t* nout, int nout_stride, int out_cap, int32_t* errflag) {
+__global__ void __launch_bounds__(1024) k_vg_hscan(VgSrc src, const VgParams* prm, int* hcnt, int maxT, int32_t* nvox,
+                                                   int32_t* errflag) {
     __shared__ int wsum[16];
     const int s = blockIdx.x, tid = threadIdx.x;
     const int nt = prm[s].ntiles;
@@ -649,10 +646,11 @@ __global__ void __launch_bounds__(1024) k_vg_hscan(const VgParams* prm, int* hcn
         run += x;
     }
     if (tid == 0) {
+        const VgGroup& q = src.grp(s);
         nvox[s] = total;
         int c = total;
-        if (c > out_cap) { c = out_cap; atomicOr(errflag, 1); }
-        nout[(size_t)s * nout_stride] = c;
+        if (c > q.out_cap) { c = q.out_cap; atomicOr(errflag, 1); }
+        q.nout[(size_t)(s % src.S) * q.nout_stride] = c;
     }
 }
 
@@ -702,21 +700,20 @@ __global__ void __launch_bounds__(VG_T) k_vg_ranges(const unsigned int* keys, co
 // up to VG_SHORT points: one thread each, loads issued 4 at a time ahead of
 // the chain.  Longer ones are listed for k_vg_long.
 #define VG_SHORT 32
-struct VgOut { float4* out; size_t stride; int cap; };
 
-__device__ inline void vg_store(const VgOut& o, int s, int r, float sx, float sy, float sz, float si, int cnt) {
+__device__ inline void vg_store(const VgOut& o, int r, float sx, float sy, float sz, float si, int cnt) {
     const float c = (float)cnt;
-    if (r < o.cap) o.out[(size_t)s * o.stride + r] = make_float4(sx / c, sy / c, sz / c, si / c);
+    if (r < o.cap) o.out[r] = make_float4(sx / c, sy / c, sz / c, si / c);
 }
 
-__global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, size_t in_stride, const unsigned int* vals,
-                                                      const int32_t* off, const int32_t* nvox, const int* starts,
-                                                      const int* ends, int32_t* meta, int4* longv, int nlong_cap,
-                                                      VgOut o) {
+__global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, const unsigned int* vals, const int32_t* off,
+                                                      const int32_t* nvox, const int* starts, const int* ends,
+                                                      int32_t* meta, int4* longv, int nlong_cap) {
     const int s = blockIdx.y;
+    const VgOut o = srcv.out_row(s);
     const int base = off[s], nv = min(nvox[s], o.cap);
     const unsigned int* v = vals + base;
-    const float4* src = srcv.pts() + (size_t)s * in_stride;
+    const float4* src = srcv.row(s);
     for (int r = blockIdx.x * VG_T + threadIdx.x; r < nv; r += gridDim.x * VG_T) {
         const int j = starts[base + r], e = ends[base + r];
         if (e - j > VG_SHORT) {
@@ -733,16 +730,15 @@ __global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, size_t in_stri
             for (int u = 0; u < 4; ++u)
                 if (i + u < e) { sx += q4[u].x; sy += q4[u].y; sz += q4[u].z; si += q4[u].w; }
         }
-        vg_store(o, s, r, sx, sy, sz, si, e - j);
+        vg_store(o, r, sx, sy, sz, si, e - j);
     }
 }
 
 // Long voxels, one wave each (persistent grid over the list): the wave
 // stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
 // intensity chains over them in order.
-__global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, const unsigned int* vals,
-                                                 const int32_t* off, const int32_t* meta, const int4* longv,
-                                                 int nlong_cap, VgOut o) {
+__global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int* vals, const int32_t* off,
+                                                 const int32_t* meta, const int4* longv, int nlong_cap) {
     __shared__ float4 buf[4][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nlong = min(meta[2], nlong_cap);
@@ -751,7 +747,7 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
         const int4 L = longv[t];
         const int s = L.x, a = L.y, r = L.z, e = L.w;
         const unsigned int* v = vals + off[s];
-        const float4* src = srcv.pts() + (size_t)s * in_stride;
+        const float4* src = srcv.row(s);
         float acc = 0.0f;
         for (int c0 = a; c0 < e; c0 += 256) {
             const int m = min(256, e - c0);
@@ -775,7 +771,7 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
         }
         const float sx = __shfl(acc, 0, 64), sy = __shfl(acc, 1, 64), sz = __shfl(acc, 2, 64),
                     si = __shfl(acc, 3, 64);
-        if (lane == 0) vg_store(o, s, r, sx, sy, sz, si, e - a);
+        if (lane == 0) vg_store(srcv.out_row(s), r, sx, sy, sz, si, e - a);
     }
 }
 
@@ -790,10 +786,9 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, size_t in_stride, c
 #ifndef SLO_VG_FUSED
 #define SLO_VG_FUSED 1
 #endif
-__global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride, const unsigned int* keys,
-                                                    const unsigned int* vals, const int32_t* off, const VgParams* prm,
-                                                    const int* hcnt, int maxT, int32_t* meta, int4* longv,
-                                                    int nlong_cap, VgOut o, int S) {
+__global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, const unsigned int* keys, const unsigned int* vals,
+                                                    const int32_t* off, const VgParams* prm, const int* hcnt, int maxT,
+                                                    int32_t* meta, int4* longv, int nlong_cap, int S) {
     constexpr int SL = VG_TILE / VG_W;   // items per wave slice
     __shared__ int lst[VG_W][SL + 1];
     __shared__ unsigned int lvv[VG_W][SL];   // the slice's point indices (the gathers read them from LDS)
@@ -806,7 +801,8 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
     const unsigned int none = vg_none(p);
     const unsigned int* k = keys + base;
     const unsigned int* v = vals + base;
-    const float4* src = srcv.pts() + (size_t)s * in_stride;
+    const float4* src = srcv.row(s);
+    const VgOut o = srcv.out_row(s);
     const unsigned long long lt = (1ull << lane) - 1ull;
     int* L = lst[w];
     for (int t = chunk; t < p.ntiles; t += gridDim.x) {
@@ -888,18 +884,17 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, size_t in_stride
                 for (int u = 0; u < 4; ++u)
                     if (i + u < e) { sx += q4[u].x; sy += q4[u].y; sz += q4[u].z; si += q4[u].w; }
             }
-            vg_store(o, s, r, sx, sy, sz, si, e - j);
+            vg_store(o, r, sx, sy, sz, si, e - j);
         }
         __syncthreads();   // wsum and the lists are reused by the next tile
     }
 }
 
-// workspace for S streams of up to `stride` items: allocated on the host from
-// the strides alone (never from a device count), grown geometrically
-static int ensure_ws(slo_ctx* ctx, size_t stride) {
+// workspace for `items` items (the sum over the call's filters of S * stride)
+// in tiles of at most maxT per virtual stream: allocated on the host from the
+// strides alone (never from a device count), grown geometrically
+static int ensure_ws(slo_ctx* ctx, size_t items, size_t tiles) {
     MapWs& w = ctx->mws;
-    const size_t S = (size_t)ctx->S;
-    const size_t items = S * stride, maxT = (stride + VG_TILE - 1) / VG_TILE, tiles = S * std::max<size_t>(1, maxT);
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
         void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.longv};
@@ -929,32 +924,48 @@ static int ensure_ws(slo_ctx* ctx, size_t stride) {
     return 0;
 }
 
-// The segmented sort of S streams' (key, point index) items: stream s's n =
-// d_n[s * n_stride] points at in + s * in_stride, keyed by their PCL voxel
-// index at `leaf`.
-// On return *keys / *vals hold the sorted items of stream s at [off[s],
-// off[s + 1]) of the workspace, *spare_k / *spare_v the free ping-pong halves.
-static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
-                   float leaf, unsigned int** keys, unsigned int** vals, unsigned int** spare_k,
-                   unsigned int** spare_v) {
+// the host-side shape of a call: virtual streams, the largest stride, the
+// workspace bound and the tiles per virtual stream
+struct VgShape {
+    int SV;
+    size_t max_stride, items;
+    int maxT;
+};
+static VgShape vg_shape(const VgSrc& src) {
+    VgShape h{src.nv(), 1, 0, 1};
+    for (int g = 0; g < src.G; ++g) {
+        h.max_stride = std::max(h.max_stride, src.g[g].stride);
+        h.items += (size_t)src.S * src.g[g].stride;
+    }
+    h.maxT = std::max(1, (int)((h.max_stride + VG_TILE - 1) / VG_TILE));
+    return h;
+}
+
+// The segmented sort of the call's virtual streams' (key, point index)
+// items: virtual stream v = g * S + s holds filter g's stream s, keyed by its
+// PCL voxel index at the filter's leaf.  On return *keys / *vals hold the
+// sorted items of virtual stream v at [off[v], off[v + 1]) of the workspace,
+// *spare_k / *spare_v the free ping-pong halves.
+static int vg_sort(slo_ctx* ctx, const char* tag, const VgSrc& src, const VgShape& h, unsigned int** keys,
+                   unsigned int** vals, unsigned int** spare_k, unsigned int** spare_v) {
     MapWs& w = ctx->mws;
-    const int S = ctx->S;
-    if (int r = ensure_ws(ctx, in_stride)) return r;
-    const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
+    const int S = h.SV;
+    if (S > VG_MAXG * ctx->S) { ctx->err = "VoxelGrid: too many filters in one call"; return SLO_E_ARG; }
+    if (int r = ensure_ws(ctx, h.items, (size_t)S * h.maxT)) return r;
+    const int maxT = h.maxT;
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
-    const int bx = std::max(1, std::min(64, (int)((in_stride + 255) / 256)));
+    const int bx = std::max(1, std::min(64, (int)((h.max_stride + 255) / 256)));
     const dim3 grid = vg_tile_grid(GX, S);
-    const VgSrc src{in, d_n, ctx->v.io};
-    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, n_stride, S, w.off, w.bounds, w.meta,
-               ctx->vg_onesweep ? w.osw : nullptr, VG_TILE, (int)std::min<size_t>(in_stride, 0x7fffffff), w.errflag);
-    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, in_stride, w.off, w.bounds);
-    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, w.bounds, w.off, S, leaf, w.prm);
+    SLO_LAUNCH(ctx, "vg_prefix", k_vg_prefix, dim3(1), dim3(1024), 0, src, S, w.off, w.bounds, w.meta,
+               ctx->vg_onesweep ? w.osw : nullptr, VG_TILE, w.errflag);
+    SLO_LAUNCH(ctx, "vg_bounds", k_vg_bounds, dim3(bx, S), dim3(256), 0, src, w.off, w.bounds);
+    SLO_LAUNCH(ctx, "vg_params", k_vg_params, dim3((S + 63) / 64), dim3(64), 0, src, w.bounds, w.off, S, w.prm);
     hipEvent_t ev = nullptr;
     const std::string sort_name = std::string("vg_sort:") + tag;   // per filter in the timing table
     const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
     if (ctx->cfg.voxel_order == SLO_VOXEL_PCL) {   // the reference's order (slo_vgpcl.hip)
-        if (int r = vg_pcl_sort(ctx, src, in_stride, w.prm, w.off, w.keys, w.vals)) return r;
+        if (int r = vg_pcl_sort(ctx, src, h.max_stride, h.items, w.prm, w.off, w.keys, w.vals)) return r;
         if (tm) timing_end(ctx, sort_name.c_str(), ev);
         *keys = w.keys; *vals = w.vals; *spare_k = w.keys2; *spare_v = w.vals2;
         return 0;
@@ -962,15 +973,15 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     // pair A = keys2/vals2, pair B = keys/vals (every stream's last pass writes B)
     unsigned int *ka = w.keys2, *va = w.vals2, *kb = w.keys, *vb = w.vals;
     if (ctx->vg_onesweep) {
-        SLO_LAUNCH(ctx, "vg_ghist", k_vg_ghist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, w.gh, S);
+        SLO_LAUNCH(ctx, "vg_ghist", k_vg_ghist<true>, grid, dim3(VG_T), 0, src, w.off, w.prm, w.gh, S);
         SLO_LAUNCH(ctx, "vg_gscan", k_vg_gscan, dim3(S), dim3(VG_T), 0, w.off, w.prm, w.gh, w.gbase);
         for (int pass = 0; pass < VG_PASSES; ++pass) {
             if (pass == 0) {
-                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<true>, dim3(VG_OSW_G), dim3(VG_T), 0, src, in_stride,
-                           w.off, w.prm, pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
+                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<true>, dim3(VG_OSW_G), dim3(VG_T), 0, src, w.off, w.prm,
+                           pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
             } else {
-                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<false>, dim3(VG_OSW_G), dim3(VG_T), 0, src, in_stride,
-                           w.off, w.prm, pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
+                SLO_LAUNCH(ctx, "vg_onesweep", k_vg_onesweep<false>, dim3(VG_OSW_G), dim3(VG_T), 0, src, w.off, w.prm,
+                           pass, ka, va, kb, vb, w.gbase, w.osw, w.lbk, w.meta, maxT, S, w.errflag);
             }
         }
         if (tm) timing_end(ctx, sort_name.c_str(), ev);
@@ -979,19 +990,19 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     }
     for (int pass = 0; pass < VG_PASSES; ++pass) {
         if (pass == 0) {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
-                       kb, w.cnt, maxT, S);
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<true>, grid, dim3(VG_T), 0, src, w.off, w.prm, pass, ka, kb, w.cnt,
+                       maxT, S);
         } else {
-            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass, ka,
-                       kb, w.cnt, maxT, S);
+            SLO_LAUNCH(ctx, "vg_hist", k_vg_hist<false>, grid, dim3(VG_T), 0, src, w.off, w.prm, pass, ka, kb, w.cnt,
+                       maxT, S);
         }
         SLO_LAUNCH(ctx, "vg_scan", k_vg_scan, dim3(S), dim3(1024), 0, w.off, w.prm, pass, w.cnt, maxT);
         if (pass == 0) {
-            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       ka, va, kb, vb, w.cnt, maxT, S);
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<true>, grid, dim3(VG_T), 0, src, w.off, w.prm, pass, ka, va, kb,
+                       vb, w.cnt, maxT, S);
         } else {
-            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, src, in_stride, w.off, w.prm, pass,
-                       ka, va, kb, vb, w.cnt, maxT, S);
+            SLO_LAUNCH(ctx, "vg_scatter", k_vg_scatter<false>, grid, dim3(VG_T), 0, src, w.off, w.prm, pass, ka, va,
+                       kb, vb, w.cnt, maxT, S);
         }
     }
     if (tm) timing_end(ctx, sort_name.c_str(), ev);
@@ -999,42 +1010,53 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const float4* in, size_t in_st
     return 0;
 }
 
-// One batched VoxelGrid over S streams: stream s's n = d_n[s * n_stride]
-// points at in + s * in_stride (in == nullptr: the context's input scan,
-// DevView::io); its centroids go to out + s * out_stride (at
-// most out_cap; more sets errflag and is clipped) and their count to
-// d_nout[s * nout_stride].  Everything is sized from the strides, so the host
-// only issues launches (no round trip).
-int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
-           float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
+// G batched VoxelGrid filters (VgGroup, at most VG_MAXG) over the context's S
+// streams in one launch sequence.  Everything is sized from the strides, so
+// the host only issues launches (no round trip).
+int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G) {
+    if (G < 1 || G > VG_MAXG) { ctx->err = "vg_run_groups: 1..VG_MAXG filters"; return SLO_E_ARG; }
     MapWs& w = ctx->mws;
-    const int S = ctx->S;
+    VgSrc src;
+    src.io = ctx->v.io;
+    src.S = ctx->S;
+    src.G = G;
+    for (int g = 0; g < VG_MAXG; ++g) src.g[g] = groups[std::min(g, G - 1)];
+    const VgShape h = vg_shape(src);
+    const int S = h.SV;
     unsigned int *k0, *v0, *k1, *v1;
-    if (int r = vg_sort(ctx, tag, in, in_stride, d_n, n_stride, leaf, &k0, &v0, &k1, &v1)) return r;
-    const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
+    if (int r = vg_sort(ctx, tag, src, h, &k0, &v0, &k1, &v1)) return r;
+    const int maxT = h.maxT;
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     const dim3 grid = vg_tile_grid(GX, S);
-    const VgOut o{out, out_stride, out_cap};
-    const VgSrc src{in, d_n, ctx->v.io};
+    int out_cap = 0;
+    for (int g = 0; g < G; ++g) out_cap = std::max(out_cap, groups[g].out_cap);
     // the ping-pong buffers the sort is done with hold the voxel ranges
     int* starts = (int*)k1;
     int* ends = (int*)v1;
     SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, S);
-    SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, w.prm, w.hcnt, maxT, w.nvox, d_nout, nout_stride,
-               out_cap, w.errflag);
+    SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, src, w.prm, w.hcnt, maxT, w.nvox, w.errflag);
     if (SLO_VG_FUSED) {
-        SLO_LAUNCH(ctx, "vg_reduce", k_vg_reduce, grid, dim3(VG_T), 0, src, in_stride, k0, v0, w.off, w.prm, w.hcnt,
-                   maxT, w.meta, w.longv, (int)w.nlong_cap, o, S);
+        SLO_LAUNCH(ctx, "vg_reduce", k_vg_reduce, grid, dim3(VG_T), 0, src, k0, v0, w.off, w.prm, w.hcnt, maxT, w.meta,
+                   w.longv, (int)w.nlong_cap, S);
     } else {
         SLO_LAUNCH(ctx, "vg_ranges", k_vg_ranges, dim3(GX, S), dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, starts, ends);
         SLO_LAUNCH(ctx, "vg_centroid", k_vg_centroid,
-                   dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src,
-                   in_stride, v0, w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap, o);
+                   dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src, v0,
+                   w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap);
     }
-    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, in_stride, v0, w.off, w.meta, w.longv,
-               (int)w.nlong_cap, o);
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, v0, w.off, w.meta, w.longv, (int)w.nlong_cap);
     SLO_CHECK(hipGetLastError());
     return 0;
+}
+
+// One batched VoxelGrid over S streams: stream s's n = d_n[s * n_stride]
+// points at in + s * in_stride (in == nullptr: the context's input scan,
+// DevView::io); its centroids go to out + s * out_stride (at most out_cap;
+// more sets errflag and is clipped) and their count to d_nout[s * nout_stride].
+int vg_run(slo_ctx* ctx, const char* tag, const float4* in, size_t in_stride, const int32_t* d_n, int n_stride,
+           float leaf, float4* out, size_t out_stride, int32_t* d_nout, int nout_stride, int out_cap) {
+    const VgGroup g{in, in_stride, d_n, n_stride, leaf, out, out_stride, d_nout, nout_stride, out_cap};
+    return vg_run_groups(ctx, tag, &g, 1);
 }
 
 // ---------------------------------------------------------------- spatial hash grid
@@ -1253,7 +1275,7 @@ void grid_free(HashGrid& g) {
 
 int vg_alloc(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
-    const int S = ctx->S;
+    const int S = VG_MAXG * ctx->S;   // per virtual stream (vg_run_groups: up to VG_MAXG filters per call)
     SLO_CHECK(hipMalloc(&w.off, sizeof(int32_t) * (S + 1)));
     SLO_CHECK(hipMalloc(&w.bounds, sizeof(unsigned int) * 6 * S));
     SLO_CHECK(hipMalloc(&w.prm, sizeof(VgParams) * S));

@@ -7,14 +7,46 @@
 
 namespace slo {
 
-// a VoxelGrid input: a cloud [S][stride] with counts n[s * n_stride], or
-// (in == nullptr) the context's input scan through its io slot
-struct VgSrc {
+// One VoxelGrid filter over the context's S streams: stream s's
+// n[s * n_stride] points at in + s * stride (in == nullptr: the context's
+// input scan through its io slot, counts io->npts), VoxelGrid(leaf), its
+// centroids to out + s * out_stride (at most out_cap, more are clipped and
+// flagged) and their count to nout[s * nout_stride].
+struct VgGroup {
     const float4* in;
+    size_t stride;
     const int32_t* n;
+    int n_stride;
+    float leaf;
+    float4* out;
+    size_t out_stride;
+    int32_t* nout;
+    int nout_stride;
+    int out_cap;
+};
+// A VoxelGrid call (a kernel argument): G filters of S streams each, run as
+// G * S virtual streams v = g * S + s.  Every workspace array, tile list and
+// sort range is per virtual stream, so the filters of a mapping step
+// (MO:1224-1263) sort together in one launch sequence.
+struct VgOut { float4* out; int cap; };
+struct VgSrc {
     const SloIo* io;
-    __device__ const float4* pts() const { return in ? in : io->pts; }
-    __device__ const int32_t* cnt() const { return in ? n : io->npts; }
+    int S, G;
+    VgGroup g[VG_MAXG];
+    __host__ __device__ int nv() const { return S * G; }
+    __device__ const VgGroup& grp(int v) const { return g[v / S]; }
+    __device__ const float4* row(int v) const {   // the virtual stream's input cloud
+        const VgGroup& q = g[v / S];
+        return (q.in ? q.in : io->pts) + (size_t)(v % S) * q.stride;
+    }
+    __device__ int count(int v) const {
+        const VgGroup& q = g[v / S];
+        return q.in ? q.n[(size_t)(v % S) * q.n_stride] : io->npts[v % S];
+    }
+    __device__ VgOut out_row(int v) const {      // its output row and capacity
+        const VgGroup& q = g[v / S];
+        return VgOut{q.out + (size_t)(v % S) * q.out_stride, q.out_cap};
+    }
 };
 
 __device__ inline unsigned int f2ord(float f) {
@@ -85,11 +117,16 @@ __device__ inline T vg_block_scan(T x, T* wsum, T* total) {
     return before + incl - x;
 }
 
-// PCL's std::sort order of S streams' items (slo_vgpcl.hip): K / V receive
-// stream s's sorted (voxel key, point index) items at [off[s], off[s + 1]),
-// finite points first, the non-finite ones after them with the "none" key
-int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
-                unsigned int* K, unsigned int* V);
+// PCL's std::sort order of the call's virtual streams' items
+// (slo_vgpcl.hip): K / V receive virtual stream v's sorted (voxel key, point
+// index) items at [off[v], off[v + 1]), finite points first, the non-finite
+// ones after them with the "none" key.  max_stride: the largest input stride;
+// items: the workspace bound, sum over the filters of S * stride.
+int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t max_stride, size_t items, const VgParams* prm,
+                const int32_t* off, unsigned int* K, unsigned int* V);
+
+// G batched VoxelGrid filters over the context's S streams (slo_vg.hip)
+int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G);
 
 #ifndef SLO_VG_FORK_STREAMS
 #define SLO_VG_FORK_STREAMS 8   // contexts of at most this many streams run the local-map VoxelGrids on ctx->side

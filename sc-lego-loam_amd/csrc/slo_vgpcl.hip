@@ -110,7 +110,7 @@ __device__ inline void pc_flag(int32_t* serr, const int32_t* off, int S, int pos
 }
 
 // ---- items: finite points first, in input order
-__global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, const int32_t* off,
                                                     const VgParams* prm, int* tcnt, int maxT, int S, int* ctr) {
     __shared__ unsigned int wsum[VG_W];
     if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x < 16) ctr[threadIdx.x] = 0;
@@ -118,7 +118,7 @@ __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, size_t in_stride, 
     if (s >= S) return;
     const VgParams p = prm[s];
     const int n = off[s + 1] - off[s];
-    const float4* in = src.pts() + (size_t)s * in_stride;
+    const float4* in = src.row(s);
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         float4 q[VG_IPT];
@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* o
     }
 }
 
-__global__ void __launch_bounds__(VG_T) k_pc_write(VgSrc src, size_t in_stride, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) k_pc_write(VgSrc src, const int32_t* off,
                                                     const VgParams* prm, const int* tcnt, const int32_t* nfin,
                                                     int maxT, unsigned int* K, unsigned int* V, int S) {
     __shared__ unsigned int wsum[VG_W];
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(VG_T) k_pc_write(VgSrc src, size_t in_stride, 
     if (s >= S) return;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base, nf = nfin[s];
-    const float4* in = src.pts() + (size_t)s * in_stride;
+    const float4* in = src.row(s);
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
         // blocked: thread tid holds items a + tid*VG_IPT + k, so the block scan keeps input order
@@ -898,9 +898,9 @@ __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned i
 }
 
 // ---- workspace and driver
-static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
+static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
     PclWs& w = ctx->pws;
-    const size_t S = (size_t)ctx->S;
+    const size_t S = (size_t)VG_MAXG * ctx->S;   // per virtual stream (vg_run_groups)
     if (!w.ctr) {
         SLO_CHECK(hipMalloc(&w.ctr, 16 * sizeof(int)));
         SLO_CHECK(hipMemset(w.ctr, 0, 16 * sizeof(int)));
@@ -917,7 +917,7 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         void* old[] = {w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl};
         for (void* q : old) if (q) hipFree(q);
         w.items = it;
-        const size_t segcap = S + it / PC_T + 2;
+        const size_t segcap = S + it / PC_T + 2;   // S >= the call's virtual streams
         const size_t chcap = it / PC_CH + segcap;
         const size_t wcap0 = it / 2 + S + 2, wcapk = it / PC_WT + S + 2;   // disjoint entries of >= 2 / > PC_WT items
         ++ctx->ws_gen;
@@ -932,9 +932,9 @@ static int pcl_ws(slo_ctx* ctx, size_t items, size_t maxT) {
         w.wcap0 = wcap0;
         w.wcapk = wcapk;
     }
-    if (S * maxT > w.tiles) {
+    if ((size_t)SV * maxT > w.tiles) {
         if (w.tcnt) hipFree(w.tcnt);
-        w.tiles = std::max(S * maxT, w.tiles + w.tiles / 2);
+        w.tiles = std::max((size_t)SV * maxT, w.tiles + w.tiles / 2);
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.tcnt, sizeof(int) * w.tiles));
     }
@@ -953,15 +953,15 @@ static int pcl_levels(size_t stride, int tail_min) {
     return g ? g + 3 : 0;
 }
 
-int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams* prm, const int32_t* off,
-                unsigned int* K, unsigned int* V) {
-    const int S = ctx->S;
-    if ((size_t)S * in_stride > (size_t)INT32_MAX) {   // item positions are 32-bit
+int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, const VgParams* prm,
+                const int32_t* off, unsigned int* K, unsigned int* V) {
+    const int S = src.nv();   // virtual streams: (filter, stream) pairs
+    if (items > (size_t)INT32_MAX) {   // item positions are 32-bit
         ctx->err = "PCL-order VoxelGrid: n_streams * in_stride exceeds INT32_MAX items";
         return SLO_E_CAPACITY;
     }
     const int maxT = std::max(1, (int)((in_stride + VG_TILE - 1) / VG_TILE));
-    if (int r = pcl_ws(ctx, (size_t)S * in_stride, (size_t)maxT)) return r;
+    if (int r = pcl_ws(ctx, S, items, (size_t)maxT)) return r;
     PclWs& w = ctx->pws;
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     PcLists L;
@@ -969,7 +969,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     for (int k = 1; k < 5; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
     unsigned int* PA = (unsigned int*)w.pairs;
     unsigned int* PB = PA + w.items;
-    SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, maxT, S,
+    SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, off, prm, w.tcnt, maxT, S,
                w.ctr);
     // a few streams leave most of the chip idle: smaller tail ranges (more
     // global levels, each parallel within a range) and more waves per finish
@@ -978,7 +978,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
     const int tail_min = few ? PC_TAIL_FEW : PC_TAIL;
     SLO_LAUNCH(ctx, "pc_scan", k_pc_scan, dim3(S), dim3(1024), 0, tail_min, off, prm, w.tcnt, maxT, w.seg[0], w.cseg[0], L,
                w.ctr, w.nfin, w.pstat, w.serr);
-    SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, in_stride, off, prm, w.tcnt, w.nfin,
+    SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
     const int G = pcl_levels(in_stride, tail_min);
     for (int lv = 0; lv < G; ++lv) {
@@ -1024,7 +1024,9 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, const VgParams
 __global__ void k_pc_fold_err(StreamState* st, const int32_t* e0, const int32_t* e1, int S) {
     const int s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= S) return;
-    const int32_t e = (e0 ? e0[s] : 0) | (e1 ? e1[s] : 0);
+    int32_t e = 0;
+    for (int g = 0; g < VG_MAXG; ++g)   // every filter's virtual stream of stream s
+        e |= (e0 ? e0[g * S + s] : 0) | (e1 ? e1[g * S + s] : 0);
     if (e) st[s].err |= e;
 }
 int pcl_fold_err(slo_ctx* ctx) {

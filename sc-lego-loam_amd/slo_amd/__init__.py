@@ -45,6 +45,7 @@ _DT["imu"] = np.float64
 _DT["vg_in"] = np.int32
 _DT["vg_stats"] = np.int32
 _DT["pcl_work"] = np.uint64
+_DT["work"] = np.uint64      # DevView::wctr: [0] Scan Context pairs whose distance was evaluated
 
 
 class SloError(RuntimeError):

@@ -124,6 +124,8 @@ EXPORTS = [
     "slo_xsc_create", "slo_xsc_destroy", "slo_xsc_ingest", "slo_xsc_query",
     # synthetic stream generator on the device (csrc/slo_gendev.hip)
     "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
+    # Mode S: one stream's front ends and back end on different contexts
+    "slo_modes_carry_bytes", "slo_modes_features_bytes", "slo_front_process", "slo_back_process",
     # pose-graph back end (csrc/slo_pg.hip, host side)
     "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform", "slo_set_key_poses",
 ]
@@ -211,5 +213,11 @@ def lib():
     L.slo_image_projection_pc2.argtypes = [P, ctypes.POINTER(Pc2), ctypes.POINTER(SegView)]
     L.slo_batch_pc2_unpack.argtypes = [P, P, ctypes.c_size_t, P, ctypes.POINTER(Pc2Layout), P, P, P]
     L.slo_record_floats.argtypes = []
+    L.slo_modes_carry_bytes.argtypes = [P]
+    L.slo_modes_carry_bytes.restype = ctypes.c_size_t
+    L.slo_modes_features_bytes.argtypes = [P]
+    L.slo_modes_features_bytes.restype = ctypes.c_size_t
+    L.slo_front_process.argtypes = [P, P, P, ctypes.c_double, P, P, P]
+    L.slo_back_process.argtypes = [P, P, P, P, ctypes.c_double]
     _LIB = L
     return L

@@ -1,0 +1,170 @@
+"""Mode S: one vehicle's stream over several ranks.
+
+The reference deploys one stream as a pipeline of processes
+(imageProjection | featureAssociation | mapOptimization,
+launch/run.launch:14-17).  Mode S deals the scans' front ends round-robin
+over `world` ranks — scan k's imageProjection and featureAssociation feature
+extraction (FA:1833-1841) on rank k % world — and runs every scan's back end
+(odometry FA:1843-1858, mapOptimization, Scan Context) on the owner, rank 0.
+Per scan two buffers travel (include/slo_abi.h "Mode S"):
+- the carry, from scan k's front rank to scan k+1's: the stale state a front
+  end inherits from the previous scan;
+- the features, from scan k's front rank to the owner.
+The owner's poses, keyframes and loop ids are bit-identical to a one-context
+run (tests/test_modes_gloo.py on the oracle, tests/test_gpu_modes.py on the
+GPU).
+
+What it can buy is bounded by the owner (Amdahl): the front ends leave the
+owner, the back ends do not, and the carry chain serialises the feature
+extraction of consecutive scans (each waits for the previous scan's carry);
+only imageProjection runs fully in parallel.  DESIGN.md §8 gives the bound
+from the measured stage split.
+
+Engines: `SloEngine` (libslo contexts on one GPU: the front contexts and the
+owner) and `OracleEngine` (the CPU restatement, for the gloo rehearsal).  The
+protocol is the same for both: `run_rank_oracle` over torch.distributed
+point-to-point (gloo), `run_local_slo` with the buffers handed over inside one
+process.
+"""
+import numpy as np
+
+
+class OracleEngine:
+    """the oracle's OracleStream.front / back (oracle/oracle_api.cpp), CPU"""
+
+    def __init__(self, cfg, fronts=1):
+        import oracle_py as O
+        self.O = O
+        self.fronts = [O.OracleStream(cfg) for _ in range(fronts)]
+        self.owner = O.OracleStream(cfg)
+
+    def front(self, slot, pts, t, carry):
+        c, f = self.fronts[slot].front(pts, t, carry)
+        return c, f
+
+    def back(self, features, pts, t):
+        return self.owner.back(features, pts, t)
+
+
+class SloEngine:
+    """libslo on one GPU: `fronts` front contexts and one owner context, each
+    one stream (or n_streams vehicles split the same way), buffers as torch
+    uint8 device tensors"""
+
+    def __init__(self, cfg, fronts=1, device=0, n_streams=1, graphs=False):
+        import torch
+        import slo_amd
+        self.torch = torch
+        self.L = slo_amd._abi.lib()
+        self.fronts = [slo_amd.Context(cfg, device, n_streams) for _ in range(fronts)]
+        self.owner = slo_amd.Context(cfg, device, n_streams)
+        self.cbytes = int(self.L.slo_modes_carry_bytes(self.owner.h))
+        self.fbytes = int(self.L.slo_modes_features_bytes(self.owner.h))
+        self.dev = torch.device("cuda", device)
+
+    def buffers(self):
+        t = self.torch
+        return (t.empty(self.cbytes, dtype=t.uint8, device=self.dev),
+                t.empty(self.fbytes, dtype=t.uint8, device=self.dev))
+
+    def front(self, slot, d_points, d_counts, t, carry_in, carry_out, features_out):
+        ctx = self.fronts[slot]
+        ctx._ok(self.L.slo_front_process(ctx.h, d_points, d_counts, float(t),
+                                         None if carry_in is None else carry_in.data_ptr(), carry_out.data_ptr(),
+                                         features_out.data_ptr()), "slo_front_process")
+        ctx.synchronize()   # the buffers are complete before they travel
+
+    def back(self, features, d_points, d_counts, t):
+        self.owner._ok(self.L.slo_back_process(self.owner.h, features.data_ptr(), d_points, d_counts, float(t)),
+                       "slo_back_process")
+
+    def close(self):
+        for c in self.fronts + [self.owner]:
+            c.close()
+
+
+def front_rank(k, world):
+    """the rank that runs scan k's front end"""
+    return k % world
+
+
+TAG_CARRY, TAG_FEATURES = 1, 2   # a front rank sends both to the owner in one scan: tags keep them apart
+
+
+class DistTransport:
+    """torch.distributed point-to-point (gloo on CPU tensors, RCCL on device
+    tensors); variable-size blobs go as (length, bytes)"""
+
+    def __init__(self):
+        import torch
+        import torch.distributed as dist
+        self.t, self.d = torch, dist
+        self.pending, self.keep = [], []
+
+    def send(self, x, dst, tag):
+        t = self.t
+        x = t.as_tensor(np.ascontiguousarray(x)) if isinstance(x, np.ndarray) else x
+        n = t.tensor([x.numel()], dtype=t.int64, device=x.device)
+        self.pending += [self.d.isend(n, dst, tag=tag), self.d.isend(x, dst, tag=tag)]
+        self.keep += [n, x]   # alive until drain()
+
+    def recv(self, src, tag, like=None):
+        t = self.t
+        dev = like.device if like is not None else "cpu"
+        n = t.zeros(1, dtype=t.int64, device=dev)
+        self.d.recv(n, src, tag=tag)
+        x = t.empty(int(n.item()), dtype=t.uint8, device=dev) if like is None else like[:int(n.item())]
+        self.d.recv(x, src, tag=tag)
+        return x.numpy() if like is None else x
+
+    def drain(self):
+        for r in self.pending:
+            r.wait()
+        self.pending, self.keep = [], []
+
+
+def run_rank_oracle(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
+    """Mode S on the oracle engine: this rank's part of scans 0 .. n_scans-1.
+    scan_fn(k) -> (points, t).  The owner (rank 0) calls on_back(k, flags)
+    after each back end; returns the owner's flags."""
+    carry = None
+    flags = []
+    for k in range(n_scans):
+        f = front_rank(k, world)
+        pts, t = scan_fn(k)
+        feat = None
+        if rank == f:
+            prev = front_rank(k - 1, world) if k > 0 else None
+            if prev is not None and prev != rank:
+                carry = transport.recv(prev, TAG_CARRY)
+            carry, feat = engine.front(0, pts, t, carry)
+            nxt = front_rank(k + 1, world)
+            if k + 1 < n_scans and nxt != rank:
+                transport.send(carry, nxt, TAG_CARRY)
+            if rank != 0:
+                transport.send(feat, 0, TAG_FEATURES)
+        if rank == 0:
+            if f != 0:
+                feat = transport.recv(f, TAG_FEATURES)
+            fl = engine.back(feat, pts, t)
+            flags.append(fl)
+            if on_back:
+                on_back(k, fl)
+        transport.drain()
+    return flags
+
+
+def run_local_slo(engine, world, d_scans, d_counts, times, on_back=None):
+    """Mode S inside one process on one GPU: `world` front contexts take the
+    scans' front ends in turn (engine.fronts[k % world]), the owner runs every
+    back end; the carry and features move as device buffers (the ranks of a
+    multi-GPU run move the same buffers with RCCL send / recv).  d_scans[k]:
+    the device pointer of scan k's points."""
+    carry = [engine.buffers()[0] for _ in range(2)]
+    feat = engine.buffers()[1]
+    for k in range(len(times)):
+        cin = carry[(k + 1) & 1] if k > 0 else None
+        engine.front(k % world, d_scans[k], d_counts, times[k], cin, carry[k & 1], feat)
+        engine.back(feat, d_scans[k], d_counts, times[k])
+        if on_back:
+            on_back(k)

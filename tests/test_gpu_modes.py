@@ -1,0 +1,70 @@
+"""Mode S on the GPU (include/slo_abi.h "Mode S", slo_amd/modes.py): one
+stream's front ends (slo_front_process) dealt round-robin over 2 and 3 front
+contexts, every back end (slo_back_process) on an owner context, the carry
+and the features handed over as device buffers — what the ranks of a
+multi-GPU run send each other.  The owner's odometry and mapped poses, key
+poses, Scan Context descriptors and detect records equal a one-context run of
+the same stream (slo_batch_process, itself bit-exact against the oracle in
+test_gpu_parity.py) bit for bit at every scan."""
+import numpy as np
+import pytest
+
+import slo_amd
+from slo_amd import modes
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    assert torch.cuda.is_available(), "no HIP device"
+    return torch
+
+
+@pytest.mark.parametrize("preset,config,scans,world", [
+    (0, 1, 220, 2),    # C1 VLP-16 past 51 keyframes: Scan Context detects run on the owner
+    (6, 3, 40, 3),     # C3 hdl64_1800, three front contexts
+])
+def test_mode_s_owner_matches_one_context(preset, config, scans, world):
+    torch = _torch()
+    cfg = slo_amd.preset(preset)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(preset, config, 0, 1)
+    buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    one = slo_amd.Context(cfg, 0, 1)
+    eng = modes.SloEngine(cfg, fronts=world)
+    bad, detects = [], 0
+    try:
+        def check(k):
+            nonlocal detects
+            one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            fl = int(one.get(0, "flags")[0])
+            if fl != int(eng.owner.get(0, "flags")[0]):
+                bad.append((k, "flags"))
+            names = ["transform_sum", "integrated", "err"]
+            if fl & 2:
+                names += ["mapped", "keyposes", "map_surf_ds", "surf_total_ds"]
+            if fl & 4:
+                names += ["sc_desc", "ring_key"]
+            if fl & 8:
+                names += ["detect", "detect_f"]
+                detects += 1
+            for name in names:
+                a, b = one.get(0, name), eng.owner.get(0, name)
+                if a.shape != b.shape or not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+                    bad.append((k, name))
+
+        modes.run_local_slo(eng, world, [buf[k].data_ptr() for k in range(scans)], cnt.data_ptr(),
+                            [0.1 * k for k in range(scans)], on_back=check)
+        assert bad == [], bad[:5]
+        assert int(one.get(0, "err")[0]) == 0
+        kf = len(one.get(0, "keyposes")) // 6
+        print(f"Mode S {world} fronts: {scans} scans, {kf} keyframes, {detects} detects, owner bit-identical")
+        if preset == 0:
+            assert detects >= 1
+    finally:
+        eng.close()
+        one.close()

@@ -75,3 +75,47 @@ def test_sc_helpers_match_oracle(scans):
             assert bits(dist[i].item()) == bits(od) and int(shift[i]) == osh
     finally:
         ctx.close()
+
+
+def test_sc_distance_mfma_adversarial():
+    """distanceBtnScanContext over 3000 random pairs of descriptors built to
+    expose any slip in the matrix-core Gram (slo_scdist.h sc_gram_mfma): float
+    cells of mixed magnitudes (2^-12 .. 2^8) and both signs (points below the
+    sensor height), empty cells and empty columns, so that a wrong tile
+    layout, a wrong ring order in any of Eigen's four accumulators or a
+    different combine would change the doubles; batched on the device against
+    the oracle's Eigen-order restatement, bit for bit, distance and shift."""
+    import torch
+    assert torch.cuda.is_available(), "no HIP device"
+    pid = 6
+    ocfg = O.preset(pid)
+    NR, NS = ocfg.sc_num_ring, ocfg.sc_num_sector
+    rng = np.random.default_rng(17)
+    n = 3000
+
+    def desc():
+        mag = np.exp2(rng.integers(-12, 9, (NR, NS))).astype(np.float32)
+        d = (rng.uniform(-0.3, 1.0, (NR, NS)).astype(np.float32) * mag).astype(np.float32)
+        d[rng.random((NR, NS)) < 0.3] = 0.0                      # empty cells
+        d[:, rng.random(NS) < 0.1] = 0.0                         # empty sectors
+        return d.astype(np.float64)
+
+    A = [desc() for _ in range(n)]
+    B = [desc() if k % 3 else np.roll(A[k], int(rng.integers(0, NS)), axis=1) for k in range(n)]
+    ctx = slo_amd.Context(slo_amd.preset(pid), 0, 1)
+    try:
+        d1 = torch.from_numpy(np.stack(A)).cuda()
+        d2 = torch.from_numpy(np.stack(B)).cuda()
+        dist = torch.zeros(n, dtype=torch.float64, device="cuda")
+        shift = torch.zeros(n, dtype=torch.int32, device="cuda")
+        ctx._ok(ctx.L.slo_batch_sc_distance(ctx.h, d1.data_ptr(), d2.data_ptr(), n, dist.data_ptr(),
+                                            shift.data_ptr()), "slo_batch_sc_distance")
+        ctx.synchronize()
+        got_d, got_s = dist.cpu().numpy(), shift.cpu().numpy()
+        bad = 0
+        for k in range(n):
+            od, osh = O.sc_distance(ocfg, A[k], B[k])
+            bad += int(bits(got_d[k]) != bits(od) or int(got_s[k]) != osh)
+        assert bad == 0, f"{bad} of {n} pairs differ"
+    finally:
+        ctx.close()

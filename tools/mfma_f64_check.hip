@@ -37,6 +37,22 @@ __global__ void k_mfma(const double* A, const double* B, const double* C, double
     for (int r = 0; r < 4; ++r) D[(size_t)t * 256 + ((l >> 4) + 4 * r) * 16 + (l & 15)] = acc[r];
 }
 
+// throughput: every wave issues ITER x 4 independent 16x16x4 f64 MFMAs back to back
+#define ITER 4096
+__global__ void __launch_bounds__(256) k_rate(double* out, double seed) {
+    const int l = threadIdx.x & 63;
+    const double a = seed + l, b = seed - l;
+    d4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+    for (int i = 0; i < ITER; ++i) {
+        c0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c0, 0, 0, 0);
+        c1 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, a, c1, 0, 0, 0);
+        c2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a, a, c2, 0, 0, 0);
+        c3 = __builtin_amdgcn_mfma_f64_16x16x4f64(b, b, c3, 0, 0, 0);
+    }
+    const double s = (c0[0] + c1[1]) + (c2[2] + c3[3]);
+    if (s == 12345.678) out[0] = s;   // keep the chains alive
+}
+
 int main(int argc, char** argv) {
     const int tiles = argc > 1 ? atoi(argv[1]) : 20000;
     std::mt19937_64 g(7);
@@ -75,5 +91,19 @@ int main(int argc, char** argv) {
     printf("elements %lld  mismatches: H0 k-ordered fma chain %lld, H1 reversed %lld, H2 rounded products %lld, "
            "H3 tree %lld\n", n, bad[0], bad[1], bad[2], bad[3]);
     printf(bad[0] == 0 ? "MFMA_F64_IS_K_ORDERED_FMA_CHAIN\n" : "MFMA_F64_NOT_H0\n");
+    // f64 MFMA peak, measured: 8192 workgroups of four waves (every SIMD busy)
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    const int wg = 8192;
+    hipLaunchKernelGGL(k_rate, dim3(wg), dim3(256), 0, 0, dD, 0.5);   // warm-up
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(k_rate, dim3(wg), dim3(256), 0, 0, dD, 0.25);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    const double flop = (double)wg * 4 * ITER * 4 * 2048.0;
+    printf("f64 MFMA 16x16x4: %.1f TFLOP/s over %.3f ms (%d waves x %d MFMAs)\n", flop / (ms * 1e-3) / 1e12, ms,
+           wg * 4, ITER * 4);
     return 0;
 }
