@@ -129,7 +129,8 @@ EXTRA = {
            "--keyframe-ring", "128", "--workload",
            "C2 Ouster-64 synthetic 64x1800 stream, segmentation + features + LM, Scan Context off (radius-search "
            "local map, MO:1167-1222), steady state"],
-    "c5": ["--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--workload",
+    "c5": ["--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--keyframe-cap", "65536",
+           "--workload",
            "C5 128-ring x 2048-col dense synthetic scan, Scan Context K=50, LM against the ~1M-point raw local "
            "map (HBM-bound stress), steady state"],
 }
@@ -154,7 +155,8 @@ def extra_lines(a):
     out = {}
     for name in [x for x in a.extra.split(",") if x and x != "none"]:
         cmd = [sys.executable, os.path.abspath(__file__), "--extra", "none", "--single-steps", "0", "--icp-jobs", "0",
-               "--steps", "20", "--warmup", "3", "--cpu-scans", "4", "--cpu-distinct", "4"] + EXTRA[name]
+               "--steps", "12", "--warmup", "3", "--profile-steps", "4", "--cpu-scans", "4", "--cpu-distinct", "4"] \
+            + EXTRA[name]
         t0 = time.time()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -167,7 +169,8 @@ def extra_lines(a):
                          "stderr_tail": (r.stderr[-600:] if r else "")}
             continue
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_also",
-                "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors", "sort_guards", "dtype")
+                "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors", "sort_guards", "dtype",
+                "setup_seconds", "preroll_seconds", "context_hbm_gb")
         out[name] = {k: j.get(k) for k in keep}
         out[name]["wall_seconds"] = round(time.time() - t0, 1)
     return out
@@ -457,6 +460,41 @@ def single_stream(torch, slo_amd, a, cfg, pid, local):
         ctx.close()
 
 
+def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local):
+    """one C3 stream as Mode S on one GPU (slo_amd.modes.run_pipelined_slo): a
+    front context (imageProjection + feature extraction) and the owner
+    (odometry, mapping, Scan Context) on their own HIP streams and host
+    threads, scan k + 1's front end beside scan k's back end — the
+    reference's own process split (launch/run.launch:14-17).  Same results as
+    the one-context leg (tests/test_gpu_modes.py)."""
+    from slo_amd import modes
+    P = cfg.max_points
+    eng = modes.SloEngine(cfg, fronts=1, device=local)
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
+    n = a.preroll + a.warmup + a.single_steps
+    try:
+        buf = torch.empty((n, 1, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+        gen.scans(0, n, buf.data_ptr())
+        cnt = torch.full((1,), P, dtype=torch.int32, device=f"cuda:{local}")
+        ptr = [buf[k].data_ptr() for k in range(n)]
+        tim = [0.1 * k for k in range(n)]
+        k0 = a.preroll + a.warmup
+        modes.run_pipelined_slo(eng, 1, ptr[:k0], cnt.data_ptr(), tim[:k0])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        tf, tb = modes.run_pipelined_slo(eng, 1, ptr[k0:], cnt.data_ptr(), tim[k0:])
+        el = time.perf_counter() - t0
+        m = n - k0
+        return {"value": round(m / el, 2), "unit": "scans/s", "streams": 1, "scans_timed": m,
+                "stage_ms_per_scan": {"front": round(tf / m * 1e3, 3), "back": round(tb / m * 1e3, 3)},
+                "keyframes_at_end": int(eng.owner.get(0, "n_keyframes")[0]),
+                "err": int(eng.owner.get(0, "err")[0]) | int(eng.fronts[0].get(0, "err")[0]),
+                "note": "Mode S on one GPU: front context and owner pipelined (two host threads)"}
+    finally:
+        gen.close()
+        eng.close()
+
+
 def main():
     a = parse()
     import torch
@@ -733,9 +771,10 @@ def main():
     torch.cuda.empty_cache()
 
     # ---- one stream alone (C3 is defined on one KITTI replay)
-    one = None
+    one = one_p = None
     if rank == 0 and a.single_steps > 0:
         one = single_stream(torch, slo_amd, a, cfg, pid, local)
+        one_p = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local)
 
     # ---- loop verification (MO:964-1110), measured apart
     # from the headline (not part of the metric): a batch of --icp-jobs ICP
@@ -776,6 +815,9 @@ def main():
             "single_stream": one,
             "single_stream_speedup_vs_cpu_A": (round(one["value"] / cpu["A_reference_topology"]["value"], 2)
                                                if (one and cpu) else None),
+            "single_stream_pipelined": one_p,
+            "single_stream_pipelined_speedup_vs_cpu_A": (round(one_p["value"] / cpu["A_reference_topology"]["value"],
+                                                               2) if (one_p and cpu) else None),
             "stream_errors": errs,
             "sort_guards": guards,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},

@@ -222,8 +222,10 @@ int slo_batch_voxel_grid(slo_ctx* ctx, const void* d_in, size_t in_stride, const
 size_t slo_modes_carry_bytes(slo_ctx* ctx);
 size_t slo_modes_features_bytes(slo_ctx* ctx);
 /* the front end of the scan in d_points / d_counts (as slo_batch_process);
- * d_carry_in: the previous scan's carry (NULL for a stream's first scan);
- * writes this scan's carry and its features (device buffers of the sizes above) */
+ * d_carry_in: the previous scan's carry (NULL for a stream's first scan, or
+ * when the previous scan's front end ran on this same context); writes this
+ * scan's carry (NULL: not needed, the next front end runs here too) and its
+ * features (device buffers of the sizes above) */
 int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan,
                       const void* d_carry_in, void* d_carry_out, void* d_features_out);
 /* the back end of the scan whose front end wrote d_features; d_points /

@@ -680,7 +680,7 @@ size_t slo_modes_features_bytes(slo_ctx* ctx) {
 
 int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan,
                       const void* d_carry_in, void* d_carry_out, void* d_features_out) {
-    if (!ctx || !d_points || !d_counts || !d_carry_out || !d_features_out) return SLO_E_ARG;
+    if (!ctx || !d_points || !d_counts || !d_features_out) return SLO_E_ARG;
     if (ctx->cfg.use_cloud_ring && !ctx->v.rings) { ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings"; return SLO_E_STATE; }
     SLO_CHECK(hipSetDevice(ctx->dev));
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
@@ -697,7 +697,8 @@ int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
                    (const float*)(ci + o[7]));
     }
     if (int r = slo::fa_features_run(ctx)) return r;
-    if (int r = slo::modes_copy(ctx, carry, (char*)d_carry_out, true, 0, 8)) return r;
+    if (d_carry_out)   // (NULL: the next scan's front end runs on this context, whose arrays hold it already)
+        if (int r = slo::modes_copy(ctx, carry, (char*)d_carry_out, true, 0, 8)) return r;
     int32_t* cnt;
     const auto feat = slo::modes_features(ctx, &cnt);
     if (int r = slo::modes_copy(ctx, feat, (char*)d_features_out, true, 0, 6)) return r;

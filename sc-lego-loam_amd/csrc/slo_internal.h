@@ -478,7 +478,6 @@ struct PclWs {  // PCL-order VoxelGrid sort (slo_vgpcl.hip), sized from the inpu
                                   // into StreamState::err (k_pc_fold_err, slo_get "err")
     unsigned long long* pstat = nullptr;   // [32] cumulative work counters (slo_vgpcl.hip PW_*)
     int32_t* nfin = nullptr;      // [S] finite points per stream
-    unsigned long long* pairs = nullptr;   // [items] pair positions (left | right halves), finish scratch
     PSeg* seg[2] = {nullptr, nullptr};     // ranges of the current / next level
     PRes* res = nullptr;          // per range of the current level: pivot, m, cuts
     int* cseg[2] = {nullptr, nullptr};     // chunk -> range

@@ -897,15 +897,17 @@ static int ensure_ws(slo_ctx* ctx, size_t items, size_t tiles) {
     MapWs& w = ctx->mws;
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
-        void* old[] = {w.keys, w.keys2, w.vals, w.vals2, w.longv};
+        void* old[] = {w.keys, w.keys2, w.vals, w.longv};   // (vals2 lives in keys2's allocation)
         for (void* q : old) if (q) hipFree(q);
         w.items = it;
         w.nlong_cap = it / VG_SHORT + 1;
         ++ctx->ws_gen;
         SLO_CHECK(hipMalloc(&w.keys, 4 * it));
-        SLO_CHECK(hipMalloc(&w.keys2, 4 * it));
+        // keys2 | vals2 as one allocation: the PCL-order sort uses it as its
+        // pair positions and, whole, as the heapsort fallback's 8-byte scratch
+        SLO_CHECK(hipMalloc(&w.keys2, 8 * it));
+        w.vals2 = w.keys2 + it;
         SLO_CHECK(hipMalloc(&w.vals, 4 * it));
-        SLO_CHECK(hipMalloc(&w.vals2, 4 * it));
         SLO_CHECK(hipMalloc(&w.longv, sizeof(int4) * w.nlong_cap));
     }
     if (tiles > w.tiles) {
@@ -965,7 +967,7 @@ static int vg_sort(slo_ctx* ctx, const char* tag, const VgSrc& src, const VgShap
     const bool tm = ctx->timing && timing_on(ctx, sort_name.c_str());
     if (tm) timing_begin(ctx, sort_name.c_str(), &ev);
     if (ctx->cfg.voxel_order == SLO_VOXEL_PCL) {   // the reference's order (slo_vgpcl.hip)
-        if (int r = vg_pcl_sort(ctx, src, h.max_stride, h.items, w.prm, w.off, w.keys, w.vals)) return r;
+        if (int r = vg_pcl_sort(ctx, src, h.max_stride, h.items, w.prm, w.off, w.keys, w.vals, w.keys2)) return r;
         if (tm) timing_end(ctx, sort_name.c_str(), ev);
         *keys = w.keys; *vals = w.vals; *spare_k = w.keys2; *spare_v = w.vals2;
         return 0;
@@ -1325,7 +1327,7 @@ void vg_side_free(slo_ctx* ctx) {
 
 void vg_free(slo_ctx* ctx) {
     MapWs& w = ctx->mws;
-    void* ps[] = {w.keys, w.keys2, w.vals, w.vals2, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta,
+    void* ps[] = {w.keys, w.keys2, w.vals, w.cnt, w.hcnt, w.longv, w.off, w.bounds, w.prm, w.errflag, w.meta,
                   w.nvox, w.gh, w.gbase, w.osw, w.lbk};
     for (void* p : ps) if (p) hipFree(p);
     w = MapWs();

@@ -122,8 +122,9 @@ __device__ inline T vg_block_scan(T x, T* wsum, T* total) {
 // index) items at [off[v], off[v + 1]), finite points first, the non-finite
 // ones after them with the "none" key.  max_stride: the largest input stride;
 // items: the workspace bound, sum over the filters of S * stride.
+// spare: 2 * items 32-bit words of scratch (MapWs keys2 | vals2)
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t max_stride, size_t items, const VgParams* prm,
-                const int32_t* off, unsigned int* K, unsigned int* V);
+                const int32_t* off, unsigned int* K, unsigned int* V, unsigned int* spare);
 
 // G batched VoxelGrid filters over the context's S streams (slo_vg.hip)
 int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G);

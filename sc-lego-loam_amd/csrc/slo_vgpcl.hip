@@ -914,14 +914,13 @@ static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
     }
     if (items > w.items) {
         const size_t it = std::max(items, w.items + w.items / 2);
-        void* old[] = {w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl};
+        void* old[] = {w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl};
         for (void* q : old) if (q) hipFree(q);
         w.items = it;
         const size_t segcap = S + it / PC_T + 2;   // S >= the call's virtual streams
         const size_t chcap = it / PC_CH + segcap;
         const size_t wcap0 = it / 2 + S + 2, wcapk = it / PC_WT + S + 2;   // disjoint entries of >= 2 / > PC_WT items
         ++ctx->ws_gen;
-        SLO_CHECK(hipMalloc(&w.pairs, sizeof(u64) * it));
         SLO_CHECK(hipMalloc(&w.seg[0], sizeof(PSeg) * segcap));
         SLO_CHECK(hipMalloc(&w.seg[1], sizeof(PSeg) * segcap));
         SLO_CHECK(hipMalloc(&w.res, sizeof(PRes) * segcap));
@@ -954,7 +953,7 @@ static int pcl_levels(size_t stride, int tail_min) {
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, const VgParams* prm,
-                const int32_t* off, unsigned int* K, unsigned int* V) {
+                const int32_t* off, unsigned int* K, unsigned int* V, unsigned int* spare) {
     const int S = src.nv();   // virtual streams: (filter, stream) pairs
     if (items > (size_t)INT32_MAX) {   // item positions are 32-bit
         ctx->err = "PCL-order VoxelGrid: n_streams * in_stride exceeds INT32_MAX items";
@@ -967,8 +966,10 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     PcLists L;
     L.l[0] = w.wl;
     for (int k = 1; k < 5; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
-    unsigned int* PA = (unsigned int*)w.pairs;
-    unsigned int* PB = PA + w.items;
+    // the pair positions of a step: the left stoppers' (PA) and their partners
+    // (PB), in the VoxelGrid workspace's spare halves (2 * items words)
+    unsigned int* PA = spare;
+    unsigned int* PB = spare + items;
     SLO_LAUNCH(ctx, "pc_count", k_pc_count, dim3(GX, S), dim3(VG_T), 0, src, off, prm, w.tcnt, maxT, S,
                w.ctr);
     // a few streams leave most of the chip idle: smaller tail ranges (more
@@ -1002,7 +1003,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     const int FG = std::max(256, std::min(8192, S * 16));
     SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
                w.ctr, w.pstat, w.cstat, off, S, w.serr);
-    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, w.pairs);
+    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare);
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
                    w.cstat, off, S, w.serr);
@@ -1039,7 +1040,7 @@ int pcl_fold_err(slo_ctx* ctx) {
 
 void pcl_free(slo_ctx* ctx) {
     PclWs& w = ctx->pws;
-    void* ps[] = {w.serr, w.ctr, w.nfin, w.cstat, w.pstat, w.pairs, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl,
+    void* ps[] = {w.serr, w.ctr, w.nfin, w.cstat, w.pstat, w.seg[0], w.seg[1], w.res, w.cseg[0], w.cseg[1], w.ccnt, w.wl,
                   w.tcnt};
     for (void* p : ps) if (p) hipFree(p);
     w = PclWs();

@@ -70,7 +70,8 @@ class SloEngine:
     def front(self, slot, d_points, d_counts, t, carry_in, carry_out, features_out):
         ctx = self.fronts[slot]
         ctx._ok(self.L.slo_front_process(ctx.h, d_points, d_counts, float(t),
-                                         None if carry_in is None else carry_in.data_ptr(), carry_out.data_ptr(),
+                                         None if carry_in is None else carry_in.data_ptr(),
+                                         None if carry_out is None else carry_out.data_ptr(),
                                          features_out.data_ptr()), "slo_front_process")
         ctx.synchronize()   # the buffers are complete before they travel
 
@@ -168,3 +169,59 @@ def run_local_slo(engine, world, d_scans, d_counts, times, on_back=None):
         engine.back(feat, d_scans[k], d_counts, times[k])
         if on_back:
             on_back(k)
+
+
+def run_pipelined_slo(engine, world, d_scans, d_counts, times, depth=3, on_back=None):
+    """Mode S as a two-stage pipeline on one GPU — the reference's own
+    process split (imageProjection + feature extraction | odometry +
+    mapOptimization) — with a host thread per stage: the front thread runs
+    scan k + 1's front end while the owner runs scan k's back end, through a
+    ring of `depth` feature buffers.  Only when the work runs changes, not
+    what: the owner's results equal run_local_slo's (tests/test_gpu_modes.py).
+    Returns (front seconds, back seconds) summed over the scans, each stage
+    timed on its own thread."""
+    import queue
+    import threading
+    import time
+    n = len(times)
+    feats = [engine.buffers()[1] for _ in range(depth)]
+    carry = [engine.buffers()[0] for _ in range(2)] if world > 1 else [None, None]
+    free, ready = queue.Queue(), queue.Queue()
+    for i in range(depth):
+        free.put(i)
+    err, tf = [], [0.0]
+
+    def fronts():
+        try:
+            for k in range(n):
+                slot = free.get()
+                t0 = time.perf_counter()
+                cin = carry[(k + 1) & 1] if (k > 0 and world > 1) else None
+                engine.front(k % world, d_scans[k], d_counts, times[k], cin, carry[k & 1], feats[slot])
+                tf[0] += time.perf_counter() - t0
+                ready.put((k, slot))
+        except Exception as e:   # handed to the owner thread, which raises it
+            err.append(e)
+            ready.put(None)
+
+    th = threading.Thread(target=fronts)
+    th.start()
+    tb = 0.0
+    try:
+        for _ in range(n):
+            item = ready.get()
+            if item is None:
+                break
+            k, slot = item
+            t0 = time.perf_counter()
+            engine.back(feats[slot], d_scans[k], d_counts, times[k])
+            engine.owner.synchronize()   # the owner has read the slot
+            tb += time.perf_counter() - t0
+            free.put(slot)
+            if on_back:
+                on_back(k)
+    finally:
+        th.join()
+    if err:
+        raise err[0]
+    return tf[0], tb

@@ -36,6 +36,7 @@ int main(void) {
         CHECK(slo_batch_sc_distance(NULL, d, d, 1, &dist, &sh) == SLO_E_ARG);
         CHECK(slo_batch_voxel_grid(NULL, d, 1, NULL, 0.5f, d, 1, NULL, 1) == SLO_E_ARG);
         CHECK(slo_front_process(NULL, d, NULL, 0.0, NULL, d, d) == SLO_E_ARG);
+        CHECK(slo_front_process(NULL, d, NULL, 0.0, NULL, NULL, NULL) == SLO_E_ARG);
         CHECK(slo_back_process(NULL, d, d, NULL, 0.0) == SLO_E_ARG);
         CHECK(slo_modes_carry_bytes(NULL) == 0 && slo_modes_features_bytes(NULL) == 0);
         CHECK(cfg.voxel_order == SLO_VOXEL_PCL);

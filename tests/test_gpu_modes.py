@@ -68,3 +68,42 @@ def test_mode_s_owner_matches_one_context(preset, config, scans, world):
     finally:
         eng.close()
         one.close()
+
+
+@pytest.mark.parametrize("world", [1, 2])
+def test_mode_s_pipelined_matches_one_context(world):
+    """the two-stage pipeline on one GPU (modes.run_pipelined_slo: a host
+    thread per stage, scan k + 1's front end beside scan k's back end)
+    changes when the work runs, not what: C3 hdl64_1800 for 60 scans, the
+    owner's records equal a one-context run's bit for bit"""
+    torch = _torch()
+    preset, config, scans = 6, 3, 60
+    cfg = slo_amd.preset(preset)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(preset, config, 0, 1)
+    buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    one = slo_amd.Context(cfg, 0, 1)
+    eng = modes.SloEngine(cfg, fronts=world)
+    try:
+        ref = {}
+        for k in range(scans):
+            one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            ref[k] = {n: one.get(0, n).copy() for n in ("transform_sum", "mapped", "keyposes", "flags")}
+        got = {}
+
+        def grab(k):
+            got[k] = {n: eng.owner.get(0, n).copy() for n in ref[k]}
+
+        tf, tb = modes.run_pipelined_slo(eng, world, [buf[k].data_ptr() for k in range(scans)], cnt.data_ptr(),
+                                         [0.1 * k for k in range(scans)], on_back=grab)
+        for k in range(scans):
+            for n in ref[k]:
+                assert np.array_equal(ref[k][n].view(np.uint8), got[k][n].view(np.uint8)), (k, n)
+        print(f"pipelined Mode S, {world} front context(s): front {tf / scans * 1e3:.3f} ms, "
+              f"back {tb / scans * 1e3:.3f} ms per scan")
+    finally:
+        eng.close()
+        one.close()
