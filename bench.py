@@ -460,16 +460,19 @@ def single_stream(torch, slo_amd, a, cfg, pid, local):
         ctx.close()
 
 
-def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local):
-    """one C3 stream as Mode S on one GPU (slo_amd.modes.run_pipelined_slo): a
+def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=2):
+    """one C3 stream as Mode S on one GPU, each stage on its own context, HIP
+    stream and host thread — the reference's own process split
+    (launch/run.launch:14-17).  stages=2 (slo_amd.modes.run_pipelined_slo): a
     front context (imageProjection + feature extraction) and the owner
-    (odometry, mapping, Scan Context) on their own HIP streams and host
-    threads, scan k + 1's front end beside scan k's back end — the
-    reference's own process split (launch/run.launch:14-17).  Same results as
-    the one-context leg (tests/test_gpu_modes.py)."""
+    (odometry, mapping, Scan Context), scan k + 1's front end beside scan k's
+    back end.  stages=3 (run_pipelined3_slo): the back end split into
+    odometry | mapping + transformFusion + Scan Context.  Same results as the
+    one-context leg (tests/test_gpu_modes.py)."""
     from slo_amd import modes
     P = cfg.max_points
-    eng = modes.SloEngine(cfg, fronts=1, device=local)
+    eng = modes.SloEngine(cfg, fronts=1, device=local, split_back=stages == 3)
+    run = modes.run_pipelined3_slo if stages == 3 else modes.run_pipelined_slo
     gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
     n = a.preroll + a.warmup + a.single_steps
     try:
@@ -479,17 +482,19 @@ def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local):
         ptr = [buf[k].data_ptr() for k in range(n)]
         tim = [0.1 * k for k in range(n)]
         k0 = a.preroll + a.warmup
-        modes.run_pipelined_slo(eng, 1, ptr[:k0], cnt.data_ptr(), tim[:k0])
+        run(eng, 1, ptr[:k0], cnt.data_ptr(), tim[:k0])
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        tf, tb = modes.run_pipelined_slo(eng, 1, ptr[k0:], cnt.data_ptr(), tim[k0:])
+        ts = run(eng, 1, ptr[k0:], cnt.data_ptr(), tim[k0:])
         el = time.perf_counter() - t0
         m = n - k0
+        names = ("front", "odometry", "mapping") if stages == 3 else ("front", "back")
         return {"value": round(m / el, 2), "unit": "scans/s", "streams": 1, "scans_timed": m,
-                "stage_ms_per_scan": {"front": round(tf / m * 1e3, 3), "back": round(tb / m * 1e3, 3)},
+                "stage_ms_per_scan": {k: round(t / m * 1e3, 3) for k, t in zip(names, ts)},
                 "keyframes_at_end": int(eng.owner.get(0, "n_keyframes")[0]),
                 "err": int(eng.owner.get(0, "err")[0]) | int(eng.fronts[0].get(0, "err")[0]),
-                "note": "Mode S on one GPU: front context and owner pipelined (two host threads)"}
+                "note": ("Mode S on one GPU: front | odometry | mapping contexts pipelined (three host threads)"
+                         if stages == 3 else "Mode S on one GPU: front context and owner pipelined (two host threads)")}
     finally:
         gen.close()
         eng.close()
@@ -771,10 +776,11 @@ def main():
     torch.cuda.empty_cache()
 
     # ---- one stream alone (C3 is defined on one KITTI replay)
-    one = one_p = None
+    one = one_p = one_p3 = None
     if rank == 0 and a.single_steps > 0:
         one = single_stream(torch, slo_amd, a, cfg, pid, local)
         one_p = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local)
+        one_p3 = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=3)
 
     # ---- loop verification (MO:964-1110), measured apart
     # from the headline (not part of the metric): a batch of --icp-jobs ICP
@@ -818,6 +824,9 @@ def main():
             "single_stream_pipelined": one_p,
             "single_stream_pipelined_speedup_vs_cpu_A": (round(one_p["value"] / cpu["A_reference_topology"]["value"],
                                                                2) if (one_p and cpu) else None),
+            "single_stream_pipelined3": one_p3,
+            "single_stream_pipelined3_speedup_vs_cpu_A": (
+                round(one_p3["value"] / cpu["A_reference_topology"]["value"], 2) if (one_p3 and cpu) else None),
             "stream_errors": errs,
             "sort_guards": guards,
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},

@@ -232,6 +232,21 @@ int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
  * d_counts: that scan again (mapping reads the raw cloud, MO:1236) */
 int slo_back_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
                      double t_scan);
+/* The back end in two stages (the reference's featureAssociation |
+ * mapOptimization process boundary, launch/run.launch:15-16): an odometry
+ * context runs slo_odom_process — featureAssociation's odometry and publish
+ * gate (FA:1843-1858, 1790-1814) — and hands a third buffer to a mapping
+ * context, which runs slo_map_process — transformFusion's
+ * laserOdometryHandler (TF:186-219), mapOptimization (MO:1685-1699) and Scan
+ * Context, in scan order.  The mapping context then holds what the owner of
+ * slo_back_process would: slo_get on it reads the same poses, keyframes,
+ * descriptors and detect records.  The odometry buffer: the published corner /
+ * surf clouds (after TransformToEnd), the outliers, their counts, the
+ * stream's err bits and transformSum. */
+size_t slo_modes_odom_bytes(slo_ctx* ctx);
+int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
+                     double t_scan, void* d_odom_out);
+int slo_map_process(slo_ctx* ctx, const void* d_odom, const void* d_points, const int32_t* d_counts, double t_scan);
 
 /* ---------------------------------------------------------------- loop-closure verification
  * mapOptmization.cpp:841-1110 (detectLoopClosure + performLoopClosure, minus

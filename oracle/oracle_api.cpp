@@ -123,6 +123,61 @@ struct OracleStream {
         const int fl = after_fa(pts, n, t);
         return fl | step_loop(fl, t);
     }
+    // back() in two stages on two objects, the reference's featureAssociation
+    // | mapOptimization process boundary (launch/run.launch:15-16): odom()
+    // runs the odometry and hands on what featureAssociation publishes to
+    // mapping (FA:1790-1814) — the *Last clouds, the outliers, transformSum,
+    // whether this scan was published — and whether the odometry ran (for
+    // transformFusion); mapstage() runs transformFusion's
+    // laserOdometryHandler, mapOptimization and Scan Context.
+    struct Odom {
+        Cloud corner_last, surf_last, outlier;
+        float sum[6];
+        int ran, published;
+    };
+    void odom(const Features& f, double t, Odom* o) {
+        t_gemm_mode = gemm_mode;
+        fa.timeScanCur = t;
+        fa.cornerPointsSharp = f.sharp;
+        fa.cornerPointsLessSharp = f.less_sharp;
+        fa.surfPointsFlat = f.flat;
+        fa.surfPointsLessFlat = f.less_flat;
+        fa.outlierCloud = f.outlier;
+        fa.published_to_mapping = false;
+        if (!fa.systemInitedLM) {
+            fa.checkSystemInitialization();
+        } else {
+            fa.updateInitialGuess();
+            fa.updateTransformation();
+            fa.integrateTransformation();
+            fa.publishCloudsLast();
+        }
+        o->ran = fa.systemInitedLM && scan_index > 0;
+        o->published = fa.published_to_mapping;
+        o->corner_last = fa.laserCloudCornerLast;
+        o->surf_last = fa.laserCloudSurfLast;
+        o->outlier = fa.outlierCloud;
+        memcpy(o->sum, fa.transformSum, sizeof o->sum);
+        scan_index++;
+    }
+    int mapstage(const Odom& o, const float* pts, int n, double t) {
+        t_gemm_mode = gemm_mode;
+        det_valid = false;
+        memcpy(fa.transformSum, o.sum, sizeof o.sum);   // what get("transform_sum") reads on this object
+        int flags = o.ran ? 1 : 0;
+        if (flags & 1) {   // as after_fa
+            float sum[6], incre[6];
+            odom_handoff(o.sum, sum);
+            MapOptimization::associate_to_map(sum, mo.tfBef, mo.tfAft, incre, integrated);
+        }
+        if (o.published) {
+            const bool ran = mo.run(o.corner_last, o.surf_last, o.outlier, o.sum, pts, n, t);
+            if (ran) flags |= 2;
+            if (ran && mo.saved_keyframe) flags |= 4;
+        }
+        scan_index++;
+        return flags | step_loop(flags, t);
+    }
 
     // featureAssociation has run on this scan: the hand-offs and mapping
     int after_fa(const float* pts, int n, double t) {
@@ -241,6 +296,32 @@ int oracle_back(void* h, const void* features, const float* pts, int n, double t
     const char* p = (const char*)features;
     for (Cloud* cl : {&f.sharp, &f.less_sharp, &f.flat, &f.less_flat, &f.outlier}) p = vec_get(p, *cl);
     return ((OracleStream*)h)->back(f, pts, n, t);
+}
+// the back end's two stages over a blob (OracleStream::odom / mapstage):
+// odom returns the blob's size, fetched with oracle_front_blob(2, ...)
+static std::vector<char> g_odom;
+int64_t oracle_odom(void* h, const void* features, double t) {
+    OracleStream::Features f;
+    const char* p = (const char*)features;
+    for (Cloud* cl : {&f.sharp, &f.less_sharp, &f.flat, &f.less_flat, &f.outlier}) p = vec_get(p, *cl);
+    OracleStream::Odom o;
+    ((OracleStream*)h)->odom(f, t, &o);
+    g_odom.clear();
+    for (const Cloud* cl : {&o.corner_last, &o.surf_last, &o.outlier}) vec_put(g_odom, *cl);
+    blob_put(g_odom, o.sum, sizeof o.sum);
+    blob_put(g_odom, &o.ran, 4);
+    blob_put(g_odom, &o.published, 4);
+    return (int64_t)g_odom.size();
+}
+void oracle_odom_blob(void* out) { memcpy(out, g_odom.data(), g_odom.size()); }
+int oracle_mapstage(void* h, const void* odom, const float* pts, int n, double t) {
+    OracleStream::Odom o;
+    const char* p = (const char*)odom;
+    for (Cloud* cl : {&o.corner_last, &o.surf_last, &o.outlier}) p = vec_get(p, *cl);
+    memcpy(o.sum, p, sizeof o.sum);
+    memcpy(&o.ran, p + 24, 4);
+    memcpy(&o.published, p + 28, 4);
+    return ((OracleStream*)h)->mapstage(o, pts, n, t);
 }
 // the normal equations' accumulation order (oracle_common.h gemm_AtA): 0 double-double (default), 1 OpenCV 3.x
 void oracle_set_gemm_mode(void* h, int mode) { ((OracleStream*)h)->gemm_mode = mode; }

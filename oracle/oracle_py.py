@@ -115,6 +115,10 @@ def lib():
                                    ctypes.c_void_p]
         L.oracle_front_blob.argtypes = [ctypes.c_int, ctypes.c_void_p]
         L.oracle_back.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        L.oracle_odom.restype = ctypes.c_int64
+        L.oracle_odom.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_double]
+        L.oracle_odom_blob.argtypes = [ctypes.c_void_p]
+        L.oracle_mapstage.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
         L.oracle_gemm_stats.argtypes = [ctypes.c_void_p]
         L.oracle_gemm_tally.argtypes = [ctypes.c_int]
         L.oracle_gemm_at.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -342,6 +346,23 @@ class OracleStream:
         pts = np.ascontiguousarray(pts, np.float32)
         f = np.ascontiguousarray(features, np.uint8)
         return lib().oracle_back(self.h, f.ctypes.data, pts.ctypes.data, len(pts), float(t))
+
+    def odom(self, features, t):
+        """the back end's first stage (OracleStream::odom): featureAssociation's
+        odometry of one scan from its features -> the odometry blob (uint8)"""
+        f = np.ascontiguousarray(features, np.uint8)
+        n = lib().oracle_odom(self.h, f.ctypes.data, float(t))
+        out = np.empty(int(n), np.uint8)
+        lib().oracle_odom_blob(out.ctypes.data)
+        return out
+
+    def mapstage(self, odom, pts, t):
+        """the back end's second stage (OracleStream::mapstage):
+        transformFusion, mapping and Scan Context of one scan from its odometry
+        blob -> flags as step()"""
+        pts = np.ascontiguousarray(pts, np.float32)
+        o = np.ascontiguousarray(odom, np.uint8)
+        return lib().oracle_mapstage(self.h, o.ctypes.data, pts.ctypes.data, len(pts), float(t))
 
     def step_map(self, pts, t):
         """the nodes up to mapOptimization::run: flags 1, 2, 4"""

@@ -3,6 +3,8 @@
 #include "slo_internal.h"
 #include "../../include/slo_abi.h"
 #include "slo_gen.h"
+#include "slo_libm.h"
+#include "slo_pose.h"
 #include <string.h>
 #include <algorithm>
 #include <atomic>
@@ -723,6 +725,83 @@ int slo_back_process(slo_ctx* ctx, const void* d_features, const void* d_points,
     const bool first = !ctx->fa_inited;
     if (int r = slo::fa_odometry_run(ctx, first)) return r;
     slo::fa_advance(ctx, first);
+    int r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
+    if (r || !ctx->cfg.loop_closure_enable) return r;
+    return slo_batch_sc_detect(ctx);
+}
+
+}  // extern "C"
+namespace slo {
+// the back end split once more (three stages): the odometry context hands
+// the mapping context what mapOptimization reads of featureAssociation — the
+// clouds it publishes (laserCloudCornerLast / SurfLast after TransformToEnd,
+// the outliers, FA:1790-1814) and the odometry pose transformSum (FA:1808)
+#define MODES_NODOM 12   // per stream: cornerLastNum, surfLastNum, outlier_count, err, valid, -, transformSum[6]
+static std::vector<ModesSlab> modes_odom(slo_ctx* ctx) {
+    const DevView& v = ctx->v;
+    const size_t S = ctx->S;
+    return {{v.corner_last, S * v.cap_less_sharp * 16}, {v.surf_last, S * v.cap_less_flat * 16},
+            {v.outlier, S * (size_t)v.H * 16}, {nullptr, S * MODES_NODOM * 4}};
+}
+__global__ void k_modes_odom(DevView v, int32_t* c, int out) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    StreamState& st = v.st[s];
+    int32_t* q = c + (size_t)s * MODES_NODOM;
+    if (out) {
+        q[0] = st.cornerLastNum; q[1] = st.surfLastNum; q[2] = st.outlier_count; q[3] = st.err;
+        q[4] = st.odo_phase != 3; q[5] = 0;
+        for (int k = 0; k < 6; ++k) q[6 + k] = __float_as_int(st.transformSum[k]);
+        return;
+    }
+    st.cornerLastNum = q[0]; st.surfLastNum = q[1]; st.outlier_count = q[2]; st.err |= q[3];
+    for (int k = 0; k < 6; ++k) st.transformSum[k] = __int_as_float(q[6 + k]);
+    if (!q[4]) return;   // the initialisation scan: no odometry, nothing for transformFusion
+    // TransformFusion::laserOdometryHandler (TF:186-219) as k_fa_odo_finish
+    // does it, here in scan order after the previous scan's mapping step, so
+    // with the mapping result that was current when this scan's odometry came
+    float sum[6], incre[6];
+    slo_pose::odom_handoff(st.transformSum, sum);
+    slo_pose::associate_to_map(sum, st.tf_bef, st.tf_aft, incre, st.integrated);
+}
+}  // namespace slo
+extern "C" {
+
+size_t slo_modes_odom_bytes(slo_ctx* ctx) { return ctx ? slo::modes_bytes(slo::modes_odom(ctx)) : 0; }
+
+int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
+                     double t_scan, void* d_odom_out) {
+    if (!ctx || !d_features || !d_points || !d_counts || !d_odom_out) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
+    int32_t* cnt;
+    const auto feat = slo::modes_features(ctx, &cnt);
+    if (int r = slo::modes_copy(ctx, feat, (char*)d_features, false, 0, 6)) return r;
+    const size_t oc = slo::modes_bytes(feat) - ((feat[6].bytes + 255) & ~(size_t)255);
+    SLO_LAUNCH(ctx, "modes_counts", slo::k_modes_counts, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
+               (int32_t*)((char*)d_features + oc), 0);
+    const bool first = !ctx->fa_inited;
+    if (int r = slo::fa_odometry_run(ctx, first)) return r;
+    slo::fa_advance(ctx, first);
+    const auto od = slo::modes_odom(ctx);   // after the swap: the clouds just published
+    if (int r = slo::modes_copy(ctx, od, (char*)d_odom_out, true, 0, 3)) return r;
+    const size_t oq = slo::modes_bytes(od) - ((od[3].bytes + 255) & ~(size_t)255);
+    SLO_LAUNCH(ctx, "modes_odom", slo::k_modes_odom, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
+               (int32_t*)((char*)d_odom_out + oq), 1);
+    SLO_CHECK(hipGetLastError());
+    return SLO_OK;
+}
+
+int slo_map_process(slo_ctx* ctx, const void* d_odom, const void* d_points, const int32_t* d_counts, double t_scan) {
+    if (!ctx || !d_odom || !d_points || !d_counts) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
+    const auto od = slo::modes_odom(ctx);
+    if (int r = slo::modes_copy(ctx, od, (char*)d_odom, false, 0, 3)) return r;
+    const size_t oq = slo::modes_bytes(od) - ((od[3].bytes + 255) & ~(size_t)255);
+    SLO_LAUNCH(ctx, "modes_odom", slo::k_modes_odom, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
+               (int32_t*)((char*)d_odom + oq), 0);
+    slo::fa_advance(ctx, !ctx->fa_inited);   // the publish gate, kept in step with the odometry context's
     int r = slo_batch_map_optimization(ctx, d_points, d_counts, t_scan);
     if (r || !ctx->cfg.loop_closure_enable) return r;
     return slo_batch_sc_detect(ctx);

@@ -126,6 +126,7 @@ EXPORTS = [
     "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
     # Mode S: one stream's front ends and back end on different contexts
     "slo_modes_carry_bytes", "slo_modes_features_bytes", "slo_front_process", "slo_back_process",
+    "slo_modes_odom_bytes", "slo_odom_process", "slo_map_process",
     # pose-graph back end (csrc/slo_pg.hip, host side)
     "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform", "slo_set_key_poses",
 ]
@@ -219,5 +220,9 @@ def lib():
     L.slo_modes_features_bytes.restype = ctypes.c_size_t
     L.slo_front_process.argtypes = [P, P, P, ctypes.c_double, P, P, P]
     L.slo_back_process.argtypes = [P, P, P, P, ctypes.c_double]
+    L.slo_modes_odom_bytes.argtypes = [P]
+    L.slo_modes_odom_bytes.restype = ctypes.c_size_t
+    L.slo_odom_process.argtypes = [P, P, P, P, ctypes.c_double, P]
+    L.slo_map_process.argtypes = [P, P, P, P, ctypes.c_double]
     _LIB = L
     return L

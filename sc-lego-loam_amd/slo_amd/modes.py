@@ -32,18 +32,28 @@ import numpy as np
 class OracleEngine:
     """the oracle's OracleStream.front / back (oracle/oracle_api.cpp), CPU"""
 
-    def __init__(self, cfg, fronts=1):
+    def __init__(self, cfg, fronts=1, split_back=False):
         import oracle_py as O
         self.O = O
         self.fronts = [O.OracleStream(cfg) for _ in range(fronts)]
         self.owner = O.OracleStream(cfg)
+        # split_back: odometry on self.odo, mapping on self.owner (OracleStream.odom / mapstage)
+        self.odo = O.OracleStream(cfg) if split_back else None
 
     def front(self, slot, pts, t, carry):
         c, f = self.fronts[slot].front(pts, t, carry)
         return c, f
 
     def back(self, features, pts, t):
+        if self.odo is not None:
+            return self.mapping(self.odometry(features, t), pts, t)
         return self.owner.back(features, pts, t)
+
+    def odometry(self, features, t):
+        return self.odo.odom(features, t)
+
+    def mapping(self, odom, pts, t):
+        return self.owner.mapstage(odom, pts, t)
 
 
 class SloEngine:
@@ -51,15 +61,19 @@ class SloEngine:
     one stream (or n_streams vehicles split the same way), buffers as torch
     uint8 device tensors"""
 
-    def __init__(self, cfg, fronts=1, device=0, n_streams=1, graphs=False):
+    def __init__(self, cfg, fronts=1, device=0, n_streams=1, split_back=False):
         import torch
         import slo_amd
         self.torch = torch
         self.L = slo_amd._abi.lib()
         self.fronts = [slo_amd.Context(cfg, device, n_streams) for _ in range(fronts)]
         self.owner = slo_amd.Context(cfg, device, n_streams)
+        # split_back: the back end on two contexts, odometry (self.odo) and
+        # mapping (self.owner, which then holds the results)
+        self.odo = slo_amd.Context(cfg, device, n_streams) if split_back else None
         self.cbytes = int(self.L.slo_modes_carry_bytes(self.owner.h))
         self.fbytes = int(self.L.slo_modes_features_bytes(self.owner.h))
+        self.obytes = int(self.L.slo_modes_odom_bytes(self.owner.h))
         self.dev = torch.device("cuda", device)
 
     def buffers(self):
@@ -75,12 +89,29 @@ class SloEngine:
                                          features_out.data_ptr()), "slo_front_process")
         ctx.synchronize()   # the buffers are complete before they travel
 
+    def odom_buffer(self):
+        return self.torch.empty(self.obytes, dtype=self.torch.uint8, device=self.dev)
+
     def back(self, features, d_points, d_counts, t):
+        if self.odo is not None:   # the two back-end stages one after the other
+            o = self.odom_buffer()
+            self.odometry(features, d_points, d_counts, t, o)
+            self.mapping(o, d_points, d_counts, t)
+            return
         self.owner._ok(self.L.slo_back_process(self.owner.h, features.data_ptr(), d_points, d_counts, float(t)),
                        "slo_back_process")
 
+    def odometry(self, features, d_points, d_counts, t, odom_out):
+        self.odo._ok(self.L.slo_odom_process(self.odo.h, features.data_ptr(), d_points, d_counts, float(t),
+                                             odom_out.data_ptr()), "slo_odom_process")
+        self.odo.synchronize()   # the odometry buffer is complete, the features slot read
+
+    def mapping(self, odom, d_points, d_counts, t):
+        self.owner._ok(self.L.slo_map_process(self.owner.h, odom.data_ptr(), d_points, d_counts, float(t)),
+                       "slo_map_process")
+
     def close(self):
-        for c in self.fronts + [self.owner]:
+        for c in self.fronts + [self.owner] + ([self.odo] if self.odo is not None else []):
             c.close()
 
 
@@ -89,7 +120,7 @@ def front_rank(k, world):
     return k % world
 
 
-TAG_CARRY, TAG_FEATURES = 1, 2   # a front rank sends both to the owner in one scan: tags keep them apart
+TAG_CARRY, TAG_FEATURES, TAG_ODOM = 1, 2, 3   # a front rank sends two of them to one rank in one scan
 
 
 class DistTransport:
@@ -148,6 +179,41 @@ def run_rank_oracle(engine, rank, world, scan_fn, n_scans, transport, on_back=No
             if f != 0:
                 feat = transport.recv(f, TAG_FEATURES)
             fl = engine.back(feat, pts, t)
+            flags.append(fl)
+            if on_back:
+                on_back(k, fl)
+        transport.drain()
+    return flags
+
+
+def run_rank_oracle3(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
+    """Mode S with the back end split over two ranks, the reference's three
+    processes (launch/run.launch:14-17) as ranks: rank 0 the mapping stage
+    (transformFusion, mapOptimization, Scan Context: the owner), rank 1 the
+    odometry, ranks 2 .. world-1 the front ends in turn (world >= 3).  Scan
+    k's features go from its front rank to rank 1, its odometry blob from
+    rank 1 to rank 0.  The engine needs split_back=True on ranks 0 and 1.
+    Returns the owner's flags (rank 0), as run_rank_oracle."""
+    assert world >= 3, "a front rank, the odometry rank and the owner"
+    nf = world - 2
+    carry = None
+    flags = []
+    for k in range(n_scans):
+        f = 2 + k % nf
+        pts, t = scan_fn(k)
+        if rank == f:
+            prev = 2 + (k - 1) % nf if k > 0 else None
+            if prev is not None and prev != rank:
+                carry = transport.recv(prev, TAG_CARRY)
+            carry, feat = engine.front(0, pts, t, carry)
+            nxt = 2 + (k + 1) % nf
+            if k + 1 < n_scans and nxt != rank:
+                transport.send(carry, nxt, TAG_CARRY)
+            transport.send(feat, 1, TAG_FEATURES)
+        elif rank == 1:
+            transport.send(engine.odometry(transport.recv(f, TAG_FEATURES), t), 0, TAG_ODOM)
+        elif rank == 0:
+            fl = engine.mapping(transport.recv(1, TAG_ODOM), pts, t)
             flags.append(fl)
             if on_back:
                 on_back(k, fl)
@@ -225,3 +291,99 @@ def run_pipelined_slo(engine, world, d_scans, d_counts, times, depth=3, on_back=
     if err:
         raise err[0]
     return tf[0], tb
+
+
+def run_pipelined3_slo(engine, world, d_scans, d_counts, times, depth=6, on_back=None):
+    """Mode S as three stages on one GPU, the reference's three processes
+    (imageProjection + feature extraction | odometry | mapOptimization with
+    transformFusion and Scan Context, launch/run.launch:14-17): a host thread
+    per stage, each on its own contexts (engine built with split_back=True),
+    rings of `depth` feature and odometry buffers between them.  The mapping
+    stage is bursty (a ~3 ms mapping step every mapping_process_interval,
+    little in between): the rings absorb the bursts — on C3, depth 3 gave 933
+    scans/s, depth 6 1184 (tools/pipe_depth.py).  Scan k + 2's
+    front end, scan k + 1's odometry and scan k's mapping step run at once.
+    The mapping context's results equal a one-context run's
+    (tests/test_gpu_modes.py).  Returns (front, odometry, mapping) seconds
+    summed over the scans, each stage timed on its own thread."""
+    import queue
+    import threading
+    import time
+    assert engine.odo is not None, "run_pipelined3_slo needs SloEngine(split_back=True)"
+    n = len(times)
+    feats = [engine.buffers()[1] for _ in range(depth)]
+    odoms = [engine.odom_buffer() for _ in range(depth)]
+    carry = [engine.buffers()[0] for _ in range(2)] if world > 1 else [None, None]
+    ffree, fready, ofree, oready = queue.Queue(), queue.Queue(), queue.Queue(), queue.Queue()
+    for i in range(depth):
+        ffree.put(i)
+        ofree.put(i)
+    err, tf, to = [], [0.0], [0.0]
+
+    def fronts():
+        try:
+            for k in range(n):
+                slot = ffree.get()
+                if slot is None:   # a later stage stopped
+                    fready.put(None)
+                    return
+                t0 = time.perf_counter()
+                cin = carry[(k + 1) & 1] if (k > 0 and world > 1) else None
+                engine.front(k % world, d_scans[k], d_counts, times[k], cin, carry[k & 1], feats[slot])
+                tf[0] += time.perf_counter() - t0
+                fready.put((k, slot))
+        except Exception as e:   # handed on down the pipeline, raised by the caller
+            err.append(e)
+            fready.put(None)
+
+    def odometry():
+        try:
+            for _ in range(n):
+                item = fready.get()
+                if item is None:
+                    break
+                k, fs = item
+                os_ = ofree.get()
+                if os_ is None:
+                    break
+                t0 = time.perf_counter()
+                engine.odometry(feats[fs], d_scans[k], d_counts, times[k], odoms[os_])
+                to[0] += time.perf_counter() - t0
+                ffree.put(fs)
+                oready.put((k, os_))
+            else:
+                return
+            ffree.put(None)   # stopped early: stop the other stages too
+            oready.put(None)
+        except Exception as e:
+            err.append(e)
+            ffree.put(None)
+            oready.put(None)
+
+    ths = [threading.Thread(target=fronts), threading.Thread(target=odometry)]
+    for th in ths:
+        th.start()
+    tm = 0.0
+    try:
+        for _ in range(n):
+            item = oready.get()
+            if item is None:
+                break
+            k, os_ = item
+            t0 = time.perf_counter()
+            engine.mapping(odoms[os_], d_scans[k], d_counts, times[k])
+            engine.owner.synchronize()   # the mapping context has read the slot
+            tm += time.perf_counter() - t0
+            ofree.put(os_)
+            if on_back:
+                on_back(k)
+    except BaseException:
+        ofree.put(None)
+        ffree.put(None)
+        raise
+    finally:
+        for th in ths:
+            th.join()
+    if err:
+        raise err[0]
+    return tf[0], to[0], tm

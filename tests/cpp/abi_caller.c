@@ -39,6 +39,9 @@ int main(void) {
         CHECK(slo_front_process(NULL, d, NULL, 0.0, NULL, NULL, NULL) == SLO_E_ARG);
         CHECK(slo_back_process(NULL, d, d, NULL, 0.0) == SLO_E_ARG);
         CHECK(slo_modes_carry_bytes(NULL) == 0 && slo_modes_features_bytes(NULL) == 0);
+        CHECK(slo_odom_process(NULL, d, d, NULL, 0.0, d) == SLO_E_ARG);
+        CHECK(slo_map_process(NULL, d, d, NULL, 0.0) == SLO_E_ARG);
+        CHECK(slo_modes_odom_bytes(NULL) == 0);
         CHECK(cfg.voxel_order == SLO_VOXEL_PCL);
     }
     CHECK(SLO_REC_DESC + 20 * 60 <= SLO_RECORD_FLOATS);

@@ -30,12 +30,12 @@ def _scan(k):
     return O.gen_scan(PID, CID, 0, k), 0.1 * k
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, split=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cfg = O.preset(PID)
-        eng = modes.OracleEngine(cfg)
+        eng = modes.OracleEngine(cfg, split_back=split)
         ref = O.OracleStream(cfg) if rank == 0 else None
         bad, detects, kf = [], 0, 0
 
@@ -54,18 +54,21 @@ def _worker(rank, world, port, q):
             detects += int(bool(fr & 8))
             kf = len(ref.get("keyposes")) // 6
 
-        modes.run_rank_oracle(eng, rank, world, _scan, N, modes.DistTransport(), on_back=check if rank == 0 else None)
+        run = modes.run_rank_oracle3 if split else modes.run_rank_oracle
+        run(eng, rank, world, _scan, N, modes.DistTransport(), on_back=check if rank == 0 else None)
         q.put((rank, bad, detects, kf))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_mode_s_owner_matches_one_process(world):
+@pytest.mark.parametrize("world,split", [(2, False), (3, False), (3, True), (4, True)])
+def test_mode_s_owner_matches_one_process(world, split):
+    """split: the reference's three processes as ranks (modes.run_rank_oracle3:
+    mapping on rank 0, odometry on rank 1, front ends on the rest)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)])
@@ -75,6 +78,20 @@ def test_mode_s_owner_matches_one_process(world):
     rank, bad, detects, kf = res[0]
     assert bad == [], bad[:5]
     assert kf >= 52 and detects >= 1, (kf, detects)
+
+
+def test_split_back_end_matches_one_object():
+    """OracleStream.odom / mapstage on two objects equal back() on one: flags,
+    odometry, fused and mapped poses, keyframes at every scan (C1, 120 scans)"""
+    cfg = O.preset(PID)
+    one, two = modes.OracleEngine(cfg), modes.OracleEngine(cfg, split_back=True)
+    for k in range(120):
+        pts, t = _scan(k)
+        _, f = one.front(0, pts, t, None)
+        _, f2 = two.front(0, pts, t, None)
+        assert one.back(f, pts, t) == two.back(f2, pts, t), k
+        for name in ("transform_sum", "integrated", "mapped", "keyposes"):
+            assert np.array_equal(one.owner.get(name).view(np.uint8), two.owner.get(name).view(np.uint8)), (k, name)
 
 
 def test_carry_is_the_one_object_state():
