@@ -893,6 +893,9 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #ifndef RING_TLANE
 #define RING_TLANE 64
 #endif
+#ifndef SLO_DIAG_RING
+#define SLO_DIAG_RING 0     // 1: k_fa_ring_ds_pcl's sort counters in StreamState::dbg (tools/ring_diag.py; not with SLO_DIAG)
+#endif
 #ifndef RING_W
 #define RING_W 1            // waves per ring (4 measured no faster: DESIGN.md §7); 16 when
 #endif                      // the context has a few streams (latency)
@@ -916,6 +919,16 @@ __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
         if (tid == 0) v.ring_cnt[rr * 4 + 3] = 0;
         return;
     }
+#if SLO_DIAG_RING
+    // dbg[0] sort cycles, [1] the slowest sort, [2..5] block_sort's phases (thread 0): group levels, wave level,
+    // bookkeeping, queue; [6] / [7] the slowest sort's cycles with its ring's size / ring
+    unsigned long long t_r = clock64();
+#define RING_STAMP(k) if (tid == 0) { const unsigned long long t_n = clock64(); atomicAdd(&v.st[s].dbg[k], t_n - t_r); t_r = t_n; }
+    long long rprof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, *rp = rprof;
+#else
+#define RING_STAMP(k)
+    long long* rp = nullptr;
+#endif
     const float inv = 1.0f / v.cfg.leaf_less_flat;
     float mnx = FLT_MAX, mny = FLT_MAX, mnz = FLT_MAX, mxx = -FLT_MAX, mxy = -FLT_MAX, mxz = -FLT_MAX;
     for (int b = 0; b < n; b += 8 * NT) {   // eight loads in flight per thread
@@ -969,7 +982,21 @@ __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
         }
     }
     __syncthreads();
-    slo_pcl::block_sort<RING_TLANE, RW>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr);
+#if SLO_DIAG_RING
+    t_r = clock64();
+#endif
+    slo_pcl::block_sort<RING_TLANE, RW>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr, rp);
+#if SLO_DIAG_RING
+    if (tid == 0) atomicMax(&v.st[s].dbg[1], clock64() - t_r);
+#endif
+    RING_STAMP(0)
+#if SLO_DIAG_RING
+    if (tid == 0) {   // thread 0's phases of block_sort
+        for (int k = 4; k < 8; ++k) atomicAdd(&v.st[s].dbg[k - 2], (unsigned long long)rprof[k]);
+        atomicMax(&v.st[s].dbg[6], ((unsigned long long)(clock64() - t_r) << 16) | ((unsigned)n << 4) | 0);
+        atomicMax(&v.st[s].dbg[7], ((unsigned long long)(clock64() - t_r) << 8) | (unsigned)ring);
+    }
+#endif
     if (tid == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
     // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan
     const int chunk = (n + NT - 1) / NT;
@@ -1004,6 +1031,7 @@ __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
         out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
     }
     if (tid == 0) v.ring_cnt[rr * 4 + 3] = total;
+#undef RING_STAMP
 }
 
 // concatenate per-ring outputs in ring order: one block per (ring, stream),

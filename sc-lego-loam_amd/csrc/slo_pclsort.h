@@ -452,7 +452,8 @@ __device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, in
 // one wave; tbl holds an entry per position (a step writes tbl[f .. f + m),
 // so waves on disjoint ranges share it).  *err (if given) counts ranges
 // handed to a lane for a reason other than their size (must stay 0).
-// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges
+// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges; [3] items
+// of the ranges over TLANE handed to a lane task
 template <int TLANE>
 __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int depth, unsigned short* tbl,
                                                 WaveSmem& ws, int* err = nullptr, long long* prof = nullptr) {
@@ -487,7 +488,10 @@ __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int 
             const bool small = len >= 2 && len <= 64 && d > 0 && !stepped;
             if (small) hs = wave_small_sort(items, f, len, d, ws.tw, &hend);
             else if (len >= 2) hs = 1ull;   // the whole range
-            if (prof) prof[2] += clock64() - t0;
+            if (prof) {
+                prof[2] += clock64() - t0;
+                if (!small && len >= 2) prof[3] += len;   // items heapsorted by one lane
+            }
             while (hs) {
                 const int b = __builtin_ctzll(hs);
                 hs &= hs - 1;
@@ -526,39 +530,53 @@ __device__ __forceinline__ void wave_sort(u64* items, int n, int depth, unsigned
     wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws, err, prof);
 }
 
-// one introsort step of [f, l) (l - f - 1 <= 4096) by all W waves of the
-// workgroup: stream_step with its rows dealt round-robin to the waves — the
-// per-row stopper counts in LDS, m and the cuts by the first wave from the
-// row prefixes (one row per lane, as stream_step keeps them), barriers
-// between the passes.  Every swapped left stopper lies before the crossing
-// and every partner at or after it, so a wave reads no position another
-// wave writes except partners past the crossing, whose left-stopper flags
-// can only turn on (a right stopper's place takes a left stopper's item):
-// the prefixes of the positions that swap stay exact.
+// one introsort step of [f, l) (l - f - 1 <= 4096) by a group of gw waves of
+// the workgroup (waves gw * g .. gw * g + gw - 1; every wave of the workgroup
+// calls this, each group with its own range and BlockStepSm, so the groups of
+// one level step their ranges side by side): stream_step with its rows dealt
+// round-robin to the group's waves — the per-row stopper counts in LDS, m and
+// the cuts by the group's first wave from the row prefixes (one row per lane,
+// as stream_step keeps them), workgroup barriers between the passes (four,
+// whatever the group does, so every wave meets every barrier).  Every swapped
+// left stopper lies before the crossing and every partner at or after it, so
+// a wave reads no position another wave writes except partners past the
+// crossing, whose left-stopper flags can only turn on (a right stopper's
+// place takes a left stopper's item): the prefixes of the positions that swap
+// stay exact.  mode 0: the group has nothing to step; 1: its first wave takes
+// the (<= 129-item) range's step alone (wave_step_any); 2: the group's step.
+// Returns the cut (modes 1, 2).
 struct BlockStepSm {
     int rl[65], rr[65];   // per row stopper counts, then exclusive prefixes
     int m, cutA, cutB, rA, rB;
 };
-template <int W>
-__device__ __forceinline__ int block_step(u64* items, unsigned short* tbl, int f, int l, BlockStepSm& bs) {
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+__device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f, int l, int mode, BlockStepSm& bs,
+                                          int gw) {
+    const int lane = threadIdx.x & 63, lw = (threadIdx.x >> 6) & (gw - 1);
     constexpr int INF = 0x7fffffff;
     const unsigned int* K = reinterpret_cast<const unsigned int*>(items);
+    const bool big = mode == 2;
     const int mid = f + (l - f) / 2;
-    const u64 a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
-    const int w = median3(vkey(a1), vkey(a2), vkey(a3));
-    const int med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
-    const u64 pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
-    const unsigned int p = vkey(pit), k0 = vkey(a0);
-    const int b0 = f + 1, R = (l - b0 + 63) >> 6;
+    u64 a0 = 0, pit = 0;
+    unsigned int p = 0, k0 = 0;
+    int med = 0;
+    if (big) {
+        a0 = items[f];
+        const u64 a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+        const int w = median3(vkey(a1), vkey(a2), vkey(a3));
+        med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
+        pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
+        p = vkey(pit);
+        k0 = vkey(a0);
+    }
+    const int b0 = f + 1, R = big ? (l - b0 + 63) >> 6 : 0;
     // (1) stopper counts per row (the median swap virtual)
-    for (int r0 = wv; r0 < R; r0 += 4 * W) {
+    for (int r0 = lw; r0 < R; r0 += 4 * gw) {
         unsigned int kk[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u * W) + lane, l - 1) + 1];
+        for (int u = 0; u < 4; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u * gw) + lane, l - 1) + 1];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-            const int r = r0 + u * W;
+            const int r = r0 + u * gw;
             if (r < R) {
                 const int x = b0 + 64 * r + lane;
                 const unsigned int k = x == med ? k0 : kk[u];
@@ -568,7 +586,10 @@ __device__ __forceinline__ int block_step(u64* items, unsigned short* tbl, int f
         }
     }
     __syncthreads();
-    if (wv == 0) {   // (2) the prefixes (lane r = row r), m, the cuts; the median swap made real
+    if (lw == 0 && mode == 1) {
+        bs.cutA = wave_step_any(items, tbl, f, l);
+        bs.m = 0;
+    } else if (lw == 0 && big) {   // (2) the prefixes (lane r = row r), m, the cuts; the median swap made real
         const int cl = lane < R ? bs.rl[lane] : 0, cr = lane < R ? bs.rr[lane] : 0;
         int il = cl, ir = cr;
 #pragma unroll
@@ -631,20 +652,19 @@ __device__ __forceinline__ int block_step(u64* items, unsigned short* tbl, int f
         bs.rl[64] = TR;   // (every lane writes the same value)
     }
     __syncthreads();
-    const int m = bs.m, TR = bs.rl[64];
-    if (m > 0) {
-        // (3) the m last right stoppers, by rank from the right
-        const int rB = bs.rB;
-        for (int r = rB + wv; r < R; r += W) {
+    const int m = big ? bs.m : 0, TR = big ? bs.rl[64] : 0;
+    if (m > 0) {   // (3) the m last right stoppers, by rank from the right
+        for (int r = bs.rB + lw; r < R; r += gw) {
             const int x = b0 + 64 * r + lane;
             const bool iR = x < l && !(p < K[2 * min(x, l - 1) + 1]);
             const int kr = TR - 1 - (bs.rr[r] + lane_prefix(__ballot(iR)));
             if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
         }
-        __syncthreads();
-        // (4) the m first left stoppers swap with their partners
+    }
+    __syncthreads();
+    if (m > 0) {   // (4) the m first left stoppers swap with their partners
         const int rEnd = bs.rA;
-        for (int r = wv; r <= rEnd; r += W) {
+        for (int r = lw; r <= rEnd; r += gw) {
             const int x = b0 + 64 * r + lane;
             const u64 it = items[min(x, l - 1)];
             const bool iL = x < l && !(vkey(it) < p);
@@ -656,20 +676,21 @@ __device__ __forceinline__ int block_step(u64* items, unsigned short* tbl, int f
                 items[y] = it;
             }
         }
-        __syncthreads();
     }
-    return min(bs.cutA, m > 0 ? bs.cutB : INF);
+    __syncthreads();
+    return mode == 0 ? 0 : min(bs.cutA, m > 0 ? bs.cutB : INF);
 }
 
 // W waves on one range: the first levels breadth first — while a level has
-// at most W / 2 ranges the whole workgroup steps each (block_step), then one
-// wave per range — until there are 2W ranges, which the waves then take one
-// at a time (an LDS counter) and finish depth first.
+// at most W / 2 ranges, each range is stepped by a group of W / G waves (G
+// the level's ranges rounded up to a power of two; group_step), the groups
+// side by side — then one wave per range, until there are 2W ranges, which
+// the waves then take one at a time (an LDS counter) and finish depth first.
 template <int W>
 struct BlockQ {
     unsigned int cur[2 * W], nxt[2 * W];
     int ncur, take;
-    BlockStepSm bs;
+    BlockStepSm bs[W > 1 ? W / 2 : 1];
 };
 
 template <int TLANE, int W>
@@ -686,29 +707,66 @@ __device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigne
         bq.take = 0;
     }
     __syncthreads();
+    long long tph = prof ? clock64() : 0;   // prof[4..7] (thread 0's): group levels, wave level, bookkeeping, queue
+    auto phase = [&](int k) {
+        if (prof) {
+            const long long t = clock64();
+            prof[k] += t - tph;
+            tph = t;
+        }
+    };
     for (int k = 1; k < 2 * W; k <<= 1) {
         const int nc = bq.ncur;
-        // the first levels (fewer ranges than waves, the largest steps) are
-        // taken by the whole workgroup one range at a time
-        const bool coop = 2 * nc <= W;
-        for (int i = coop ? 0 : wv; i < nc; i += coop ? 1 : W) {
-            const unsigned int e = bq.cur[i];
-            const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
-            unsigned int a = e, b = 0;
-            if (l - f > TLANE && d > 0) {
-                const long long t0 = prof ? clock64() : 0;
-                const int cut = coop && l - f - 1 > 128 ? block_step<W>(items, tbl, f, l, bq.bs)
-                              : (!coop || wv == 0) ? wave_step_any(items, tbl, f, l) : 0;
-                if (prof) prof[l - f - 1 <= 128] += clock64() - t0;
-                if (cut > f && cut < l) {
-                    a = renc(f, cut, d - 1);
-                    b = renc(cut, l, d - 1);
-                } else if (err && lane == 0 && (!coop || wv == 0)) {
-                    atomicAdd(err, 1);
-                }
+        phase(6);
+        if (2 * nc <= W) {   // the first levels (fewer ranges than waves, the largest steps): wave groups
+            int G = 1;
+            while (G < nc) G <<= 1;
+            const int gw = W / G, g = wv / gw;
+            unsigned int e = 0;
+            int f = 0, l = 0, d = 0, mode = 0;
+            if (g < nc) {
+                e = bq.cur[g];
+                f = (int)(e & 0x1fffu);
+                l = (int)((e >> 13) & 0x1fffu);
+                d = (int)(e >> 26);
+                if (l - f > TLANE && d > 0) mode = l - f - 1 > 128 ? 2 : 1;
             }
-            if (lane == 0 && (!coop || wv == 0)) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
-            if (coop) __syncthreads();   // the next range's step reads what this one wrote
+            const long long t0 = prof ? clock64() : 0;
+            const int cut = group_step(items, tbl, f, l, mode, bq.bs[g < nc ? g : 0], gw);
+            if (prof && mode) prof[mode == 1] += clock64() - t0;
+            if (g < nc && wv % gw == 0 && lane == 0) {
+                unsigned int a = e, b = 0;
+                if (mode) {
+                    if (cut > f && cut < l) {
+                        a = renc(f, cut, d - 1);
+                        b = renc(cut, l, d - 1);
+                    } else if (err) {
+                        atomicAdd(err, 1);
+                    }
+                }
+                bq.nxt[2 * g] = a;
+                bq.nxt[2 * g + 1] = b;
+            }
+            phase(4);
+        } else {
+            for (int i = wv; i < nc; i += W) {
+                const unsigned int e = bq.cur[i];
+                const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
+                unsigned int a = e, b = 0;
+                if (l - f > TLANE && d > 0) {
+                    const long long t0 = prof ? clock64() : 0;
+                    const int cut = wave_step_any(items, tbl, f, l);
+                    if (prof) prof[l - f - 1 <= 128] += clock64() - t0;
+                    if (cut > f && cut < l) {
+                        a = renc(f, cut, d - 1);
+                        b = renc(cut, l, d - 1);
+                    } else if (err && lane == 0) {
+                        atomicAdd(err, 1);
+                    }
+                }
+                if (lane == 0) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
+            }
+            phase(5);
         }
         __syncthreads();
         if (threadIdx.x == 0) {   // the next level's ranges of two or more items
@@ -730,7 +788,9 @@ __device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigne
         wave_sort_range<TLANE>(items, (int)(e & 0x1fffu), (int)((e >> 13) & 0x1fffu), (int)(e >> 26), tbl, ws[wv],
                                err, prof);
     }
+    phase(6);
     __syncthreads();
+    phase(7);
 }
 
 }  // namespace slo_pcl

@@ -540,7 +540,7 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
     __shared__ int ferr;   // the entry's inconsistent steps (slo_pclsort.h guards)
     const int nw = ctr[PCC_NW + list], tid = threadIdx.x;
     unsigned long long wn = 0, we = 0;   // work counters, one atomic per wave
-    long long prof[3] = {0, 0, 0};
+    long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
         const int f = w.x, n = min(w.y & 0xffffff, NMAX), d = w.y >> 24;
