@@ -427,6 +427,99 @@ __device__ __forceinline__ unsigned long long wave_small_sort(u64* items, int f,
     return __ballot(heap && i == lo);
 }
 
+// ---- std::sort's heapsort of a whole range (a spent depth budget; libstdc++
+// __partial_sort(first, last, last): make_heap, then sort_heap — the
+// restatement is slo_sort::heap_sort_), by one wave, exactly:
+//   * make_heap adjusts the parents from the last to the first; parents of
+//     one tree level own disjoint subtrees and every deeper parent comes
+//     first, so the wave takes a level at a time, one parent per lane;
+//   * each pop (__pop_heap, __adjust_heap, __push_heap) moves the hole from
+//     the root to a leaf along the larger children (ties: the right one) —
+//     a path that does not depend on the value being placed — and the value
+//     then rises while its parent is less.  Along a root-to-leaf path of a
+//     heap the keys do not increase, so it settles below the m path nodes
+//     not less than it: path node i < m takes node i + 1's item, node m the
+//     value.  The wave holds the top six levels (63 nodes) in registers, one
+//     per lane, and loads the deeper part of the path five levels (62 nodes)
+//     at a time: one LDS round trip per pop for ranges under 2048 items,
+//     against two dependent loads per level for one lane.
+// The final insertion sort std::sort runs over a heapsorted range moves
+// nothing (slo_sort::introsort_range), so it is not run.
+__device__ __forceinline__ u64 rl64(u64 x, int i) {
+    i = __builtin_amdgcn_readfirstlane(i);
+    const unsigned int lo = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)x, i);
+    const unsigned int hi = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(x >> 32), i);
+    return ((u64)hi << 32) | lo;
+}
+__device__ inline void wave_heap_sort(u64* a, int n) {
+    const int lane = threadIdx.x & 63;
+    if (n < 2) return;
+    const int P = (n - 2) / 2;   // the last parent
+    for (int L = lg2(P + 1); L >= 0; --L) {
+        const int lo = (1 << L) - 1, hi = min((1 << (L + 1)) - 2, P);
+        for (int x = lo + lane; x <= hi; x += 64) slo_sort::adjust_heap_(a, x, n, a[x], Less());
+        wave_fence();
+    }
+    constexpr int TOPN = 63;
+    u64 top = lane < min(n, TOPN) ? a[lane] : 0ull;
+    const int tlev = 31 - __builtin_clz(lane + 1);        // tree level of node `lane`
+    const int cj = 31 - __builtin_clz(lane + 2), cq = lane + 2 - (1 << cj);   // chunk slot: level cj, position cq
+    for (int len = n - 1; len >= 1; --len) {
+        // __pop_heap(first, first + len, first + len)
+        const u64 mx = rl64(top, 0);
+        u64 v;
+        if (len < TOPN) {
+            v = rl64(top, len);
+            if (lane == len) top = mx;
+        } else {
+            v = a[len];
+            if (lane == 0) a[len] = mx;
+        }
+        const int lim = (len - 1) / 2;   // nodes below lim have two children
+        int h = 0, k = 0, ph = 0;
+        u64 pv = 0;
+        while (h < lim && 2 * h + 2 < TOPN) {   // the path through the register levels
+            const int r = 2 * h + 2;
+            const u64 R = rl64(top, r), Lf = rl64(top, r - 1);
+            const bool left = vkey(R) < vkey(Lf);
+            h = left ? r - 1 : r;
+            ++k;
+            if (lane == k) { ph = h; pv = left ? Lf : R; }
+        }
+        while (h < lim) {   // deeper: the five levels below h in one load
+            const int node = (h + 1) * (1 << cj) - 1 + cq;
+            const u64 sub = (lane < 62 && node < len) ? a[node] : 0ull;
+            int rel = 0;
+            for (int j = 1; j <= 5 && h < lim; ++j) {
+                const int tr = (1 << j) - 1 + 2 * rel;   // the right child's slot
+                const u64 R = rl64(sub, tr), Lf = rl64(sub, tr - 1);
+                const bool left = vkey(R) < vkey(Lf);
+                rel = 2 * rel + (left ? 0 : 1);
+                h = 2 * h + (left ? 1 : 2);
+                ++k;
+                if (lane == k) { ph = h; pv = left ? Lf : R; }
+            }
+        }
+        if ((len & 1) == 0 && h == (len - 2) / 2) {   // the last parent's only child
+            const int c = 2 * h + 1;
+            const u64 cv = c < TOPN ? rl64(top, c) : a[c];
+            ++k;
+            if (lane == k) { ph = c; pv = cv; }
+        }
+        const unsigned int kv = vkey(v);
+        const int m = __popcll(__ballot(lane >= 1 && lane <= k && !(vkey(pv) < kv)));
+        const u64 up = shfl64(pv, min(lane + 1, 63));   // (every lane takes part: a permute reads no inactive lane)
+        const u64 w = lane < m ? up : v;
+        const int phl = __shfl(ph, min(tlev, 63), 64);
+        const u64 wl = shfl64(w, min(tlev, 63));
+        if (lane <= m && ph >= TOPN) a[ph] = w;
+        if (lane < TOPN && tlev <= m && phl == lane) top = wl;
+        wave_fence();
+    }
+    if (lane < min(n, TOPN)) a[lane] = top;
+    wave_fence();
+}
+
 // the queued lane tasks, one per lane, through the sequential restatement
 __device__ __forceinline__ void lane_flush(u64* items, const unsigned int* q, int nq) {
     const int lane = threadIdx.x & 63;
@@ -437,6 +530,33 @@ __device__ __forceinline__ void lane_flush(u64* items, const unsigned int* q, in
         slo_sort::introsort_range(items + f, l - f, d, Less());
     }
     wave_fence();
+}
+
+// The workgroup's pool of ranges (block_sort, W > 1): waves that finish
+// their range take the next one, and a wave stepping a range of more than
+// kPushT items hands its right half to the pool instead of its own stack, so
+// one deep range no longer keeps one wave busy while the others wait.  Slots
+// are claimed with an LDS counter and filled after; a taker waits for the
+// slot's nonzero entry (an entry always has l >= 2).  Which wave sorts which
+// disjoint range does not change the result.
+constexpr int kPoolCap = 256;
+constexpr int kPushT = 128;
+struct Pool {
+    unsigned int e[kPoolCap];
+    int head, tail, active;
+};
+__device__ __forceinline__ int ld_vol(const int* p) { return *(volatile const int*)p; }
+// lane 0 of the calling wave pushes e if there is room for it and for a
+// concurrent push by each other wave; returns whether it did (wave-uniform)
+__device__ __forceinline__ bool pool_push(Pool* pool, unsigned int e, int W) {
+    int ok = 0;
+    if ((threadIdx.x & 63) == 0 && ld_vol(&pool->tail) < kPoolCap - W) {
+        const int t = atomicAdd(&pool->tail, 1);
+        // release: the range's items, as this wave left them, before its entry
+        __hip_atomic_store(&pool->e[t], e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        ok = 1;
+    }
+    return __builtin_amdgcn_readfirstlane(ok) != 0;
 }
 
 // one step of [f, l) by the calling wave, the variant its size picks
@@ -452,11 +572,12 @@ __device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, in
 // one wave; tbl holds an entry per position (a step writes tbl[f .. f + m),
 // so waves on disjoint ranges share it).  *err (if given) counts ranges
 // handed to a lane for a reason other than their size (must stay 0).
-// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges; [3] items
-// of the ranges over TLANE handed to a lane task
+// prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges and heapsorts;
+// [3] items heapsorted (wave_heap_sort)
 template <int TLANE>
 __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int depth, unsigned short* tbl,
-                                                WaveSmem& ws, int* err = nullptr, long long* prof = nullptr) {
+                                                WaveSmem& ws, int* err = nullptr, long long* prof = nullptr,
+                                                Pool* pool = nullptr, int W = 1) {
     static_assert(TLANE >= 16 && TLANE <= 64, "ranges of <= TLANE items go to wave_small_sort");
     const int lane = threadIdx.x & 63;
     if (l0 - f0 <= 1) return;
@@ -486,11 +607,13 @@ __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int 
             int hend = 0;
             const long long t0 = prof ? clock64() : 0;
             const bool small = len >= 2 && len <= 64 && d > 0 && !stepped;
+            const bool heap = !small && !stepped && d == 0 && len > 16;   // introsort_range's heapsort, by the wave
             if (small) hs = wave_small_sort(items, f, len, d, ws.tw, &hend);
+            else if (heap) wave_heap_sort(items + f, len);
             else if (len >= 2) hs = 1ull;   // the whole range
             if (prof) {
                 prof[2] += clock64() - t0;
-                if (!small && len >= 2) prof[3] += len;   // items heapsorted by one lane
+                if (heap) prof[3] += len;   // items heapsorted by the wave
             }
             while (hs) {
                 const int b = __builtin_ctzll(hs);
@@ -512,8 +635,10 @@ __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int 
             d = (int)(e >> 26);
             continue;
         }
-        if (lane == 0) ws.stk[sp] = renc(cut, l, d - 1);
-        ++sp;
+        if (!(pool && l - cut > kPushT && pool_push(pool, renc(cut, l, d - 1), W))) {
+            if (lane == 0) ws.stk[sp] = renc(cut, l, d - 1);
+            ++sp;
+        }
         l = cut;
         --d;
     }
@@ -684,13 +809,15 @@ __device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f
 // W waves on one range: the first levels breadth first — while a level has
 // at most W / 2 ranges, each range is stepped by a group of W / G waves (G
 // the level's ranges rounded up to a power of two; group_step), the groups
-// side by side — then one wave per range, until there are 2W ranges, which
-// the waves then take one at a time (an LDS counter) and finish depth first.
+// side by side — then the ranges go to the workgroup's pool (Pool), from
+// which the waves take them and sort them depth first, handing the right
+// halves of large steps back to the pool.
 template <int W>
 struct BlockQ {
-    unsigned int cur[2 * W], nxt[2 * W];
-    int ncur, take;
+    unsigned int cur[W], nxt[W];
+    int ncur;
     BlockStepSm bs[W > 1 ? W / 2 : 1];
+    Pool pool;
 };
 
 template <int TLANE, int W>
@@ -701,13 +828,7 @@ __device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigne
         wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws[0], err, prof);
         return;
     }
-    if (threadIdx.x == 0) {
-        bq.cur[0] = renc(0, n, depth);
-        bq.ncur = n >= 2 ? 1 : 0;
-        bq.take = 0;
-    }
-    __syncthreads();
-    long long tph = prof ? clock64() : 0;   // prof[4..7] (thread 0's): group levels, wave level, bookkeeping, queue
+    long long tph = prof ? clock64() : 0;   // prof[4..7] (thread 0's): group levels, -, pool entry, pool
     auto phase = [&](int k) {
         if (prof) {
             const long long t = clock64();
@@ -715,78 +836,109 @@ __device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigne
             tph = t;
         }
     };
-    for (int k = 1; k < 2 * W; k <<= 1) {
+    Pool& pool = bq.pool;
+    for (int i = threadIdx.x; i < kPoolCap; i += 64 * W) pool.e[i] = 0u;
+    if (threadIdx.x == 0) {
+        bq.cur[0] = renc(0, n, depth);
+        bq.ncur = n >= 2 ? 1 : 0;
+        pool.head = pool.tail = 0;
+        pool.active = W;
+    }
+    __syncthreads();
+    // the first levels (at most W / 2 ranges, the largest steps): wave groups
+    for (;;) {
         const int nc = bq.ncur;
-        phase(6);
-        if (2 * nc <= W) {   // the first levels (fewer ranges than waves, the largest steps): wave groups
-            int G = 1;
-            while (G < nc) G <<= 1;
-            const int gw = W / G, g = wv / gw;
-            unsigned int e = 0;
-            int f = 0, l = 0, d = 0, mode = 0;
-            if (g < nc) {
-                e = bq.cur[g];
-                f = (int)(e & 0x1fffu);
-                l = (int)((e >> 13) & 0x1fffu);
-                d = (int)(e >> 26);
-                if (l - f > TLANE && d > 0) mode = l - f - 1 > 128 ? 2 : 1;
-            }
-            const long long t0 = prof ? clock64() : 0;
-            const int cut = group_step(items, tbl, f, l, mode, bq.bs[g < nc ? g : 0], gw);
-            if (prof && mode) prof[mode == 1] += clock64() - t0;
-            if (g < nc && wv % gw == 0 && lane == 0) {
-                unsigned int a = e, b = 0;
-                if (mode) {
-                    if (cut > f && cut < l) {
-                        a = renc(f, cut, d - 1);
-                        b = renc(cut, l, d - 1);
-                    } else if (err) {
-                        atomicAdd(err, 1);
-                    }
+        if (2 * nc > W || nc == 0) break;
+        bool more = false;   // a range of this level still needs a step
+        for (int i = 0; i < nc; ++i) {
+            const unsigned int e = bq.cur[i];
+            more |= (int)((e >> 13) & 0x1fffu) - (int)(e & 0x1fffu) > TLANE && (int)(e >> 26) > 0;
+        }
+        if (!more) break;
+        int G = 1;
+        while (G < nc) G <<= 1;
+        const int gw = W / G, g = wv / gw;
+        unsigned int e = 0;
+        int f = 0, l = 0, d = 0, mode = 0;
+        if (g < nc) {
+            e = bq.cur[g];
+            f = (int)(e & 0x1fffu);
+            l = (int)((e >> 13) & 0x1fffu);
+            d = (int)(e >> 26);
+            if (l - f > TLANE && d > 0) mode = l - f - 1 > 128 ? 2 : 1;
+        }
+        const long long t0 = prof ? clock64() : 0;
+        const int cut = group_step(items, tbl, f, l, mode, bq.bs[g < nc ? g : 0], gw);
+        if (prof && mode) prof[mode == 1] += clock64() - t0;
+        if (g < nc && wv % gw == 0 && lane == 0) {
+            unsigned int a = e, b = 0;
+            if (mode) {
+                if (cut > f && cut < l) {
+                    a = renc(f, cut, d - 1);
+                    b = renc(cut, l, d - 1);
+                } else if (err) {
+                    atomicAdd(err, 1);
                 }
-                bq.nxt[2 * g] = a;
-                bq.nxt[2 * g + 1] = b;
             }
-            phase(4);
-        } else {
-            for (int i = wv; i < nc; i += W) {
-                const unsigned int e = bq.cur[i];
-                const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
-                unsigned int a = e, b = 0;
-                if (l - f > TLANE && d > 0) {
-                    const long long t0 = prof ? clock64() : 0;
-                    const int cut = wave_step_any(items, tbl, f, l);
-                    if (prof) prof[l - f - 1 <= 128] += clock64() - t0;
-                    if (cut > f && cut < l) {
-                        a = renc(f, cut, d - 1);
-                        b = renc(cut, l, d - 1);
-                    } else if (err && lane == 0) {
-                        atomicAdd(err, 1);
-                    }
-                }
-                if (lane == 0) { bq.nxt[2 * i] = a; bq.nxt[2 * i + 1] = b; }
-            }
-            phase(5);
+            bq.nxt[2 * g] = a;
+            bq.nxt[2 * g + 1] = b;
         }
         __syncthreads();
         if (threadIdx.x == 0) {   // the next level's ranges of two or more items
             int c = 0;
             for (int i = 0; i < 2 * nc; ++i) {
-                const unsigned int e = bq.nxt[i];
-                if ((int)((e >> 13) & 0x1fffu) - (int)(e & 0x1fffu) >= 2) bq.cur[c++] = e;
+                const unsigned int x = bq.nxt[i];
+                if ((int)((x >> 13) & 0x1fffu) - (int)(x & 0x1fffu) >= 2) bq.cur[c++] = x;
             }
             bq.ncur = c;
         }
         __syncthreads();
     }
+    phase(4);
+    // the pool: the level's ranges first, then whatever the waves hand in
+    if (threadIdx.x == 0) {
+        for (int i = 0; i < bq.ncur; ++i) pool.e[i] = bq.cur[i];
+        pool.tail = bq.ncur;
+    }
+    __syncthreads();
+    phase(6);
     for (;;) {
-        int q = 0;
-        if (lane == 0) q = atomicAdd(&bq.take, 1);
-        q = __builtin_amdgcn_readfirstlane(q);
-        if (q >= bq.ncur) break;
-        const unsigned int e = bq.cur[q];
-        wave_sort_range<TLANE>(items, (int)(e & 0x1fffu), (int)((e >> 13) & 0x1fffu), (int)(e >> 26), tbl, ws[wv],
-                               err, prof);
+        unsigned int e = 0;
+        if (lane == 0) {
+            for (;;) {   // claim the next slot, if any
+                const int h = ld_vol(&pool.head);
+                if (h >= ld_vol(&pool.tail)) break;
+                if (atomicCAS(&pool.head, h, h + 1) == h) {
+                    while ((e = __hip_atomic_load(&pool.e[h], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0u)
+                        __builtin_amdgcn_s_sleep(1);
+                    break;
+                }
+            }
+        }
+        e = __builtin_amdgcn_readfirstlane(e);
+        if (e) {
+            wave_sort_range<TLANE>(items, (int)(e & 0x1fffu), (int)((e >> 13) & 0x1fffu), (int)(e >> 26), tbl, ws[wv],
+                                   err, prof, &pool, W);
+            continue;
+        }
+        // idle: done once no wave holds a range and the pool is empty (only
+        // a wave holding a range hands one in)
+        int done = 0;
+        if (lane == 0) {
+            atomicSub(&pool.active, 1);
+            for (;;) {
+                if (ld_vol(&pool.head) < ld_vol(&pool.tail)) {
+                    atomicAdd(&pool.active, 1);
+                    break;
+                }
+                if (ld_vol(&pool.active) == 0) {
+                    done = 1;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+        if (__builtin_amdgcn_readfirstlane(done)) break;
     }
     phase(6);
     __syncthreads();

@@ -218,14 +218,21 @@ def test_voxel_grid_argument_checks():
         ctx.close()
 
 
-def test_pcl_order_killer_sequences_and_one_voxel(model, tmp_path):
+@pytest.mark.parametrize("copies", [1, 2])
+def test_pcl_order_killer_sequences_and_one_voxel(model, tmp_path, copies):
+    """median-of-three killers (std::sort's heapsort fallback, taken by the
+    wave: slo_pclsort.h wave_heap_sort), one voxel, few voxels, organ pipes;
+    copies=2 runs ten streams (the batched finish shape: four waves per entry)
+    instead of five (the few-stream shape: sixteen)"""
     rng = np.random.default_rng(12)
     k5 = killer_keys(model, 5000, tmp_path)           # heapsort inside the LDS finish
     k100 = killer_keys(model, 100000, tmp_path)       # depth limit past the global levels
     one = np.zeros(20000, np.uint32)                  # every point in one voxel
     few = rng.integers(0, 50, 3000).astype(np.uint32)
     runs = np.concatenate([np.arange(4000, dtype=np.uint32) // 7, (np.arange(4000, dtype=np.uint32) // 5)[::-1]])
-    clouds = [cloud_from_keys(k, rng) for k in (k5, k100, one, few, runs)]
+    small = [killer_keys(model, n, tmp_path) for n in (70, 129, 300, 1000, 2047, 4096)]   # one heapsort each
+    clouds = [cloud_from_keys(k, rng) for k in (k5, k100, one, few, runs)] * copies
+    clouds += [cloud_from_keys(k, rng) for k in small]
     got, stats = run_batch(clouds, 1.0)
     for s, c in enumerate(clouds):
         want = O.voxel_grid(c, 1.0, stable=False)
