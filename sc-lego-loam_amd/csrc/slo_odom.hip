@@ -539,6 +539,96 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
     ind[3 * i] = closest; ind[3 * i + 1] = i2; ind[3 * i + 2] = i3;
 }
 
+// The same for a context of a few streams, where one stream's queries leave
+// most of the chip idle and the search is the odometry's latency: eight lanes
+// per query.  The 1-NN's grid rows are dealt over the eight (each lane also
+// probes the query's own cell and prunes by its own best; a point a lane
+// skips is farther than that lane's best, so the minima merged by (distance,
+// index) are the exact 1-NN), then the five ring walks run one per lane —
+// lane 0 the closest point's ring (the 2nd point), lanes 1-4 rings cscan - 2,
+// - 1, + 1, + 2 (the 3rd) — and the 3rd point's four bests merge in
+// WalkBest's order, a strict total order on (distance, class, index): the
+// minimum over all offers, whatever the order of the rings.  Same results as
+// k_fa_search_surf.
+#define SURF_QL 8
+#ifndef SLO_ODO_FEW
+#define SLO_ODO_FEW 8   // at most this many streams: k_fa_search_surf_few
+#endif
+__device__ inline bool walk_better(float d, int c, int t, const WalkBest& w) {
+    return d < w.d || (d == w.d && (c < w.cls || (c == w.cls && t < w.t)));
+}
+__global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    const StreamState& st = v.st[s];
+    if (st.odo_phase != 0) return;
+    constexpr int QPB = 256 / SURF_QL;   // queries per workgroup
+    const int sub = threadIdx.x & (SURF_QL - 1);
+    const int i = chunk * QPB + (int)(threadIdx.x / SURF_QL);
+    const int nq = st.n_flat;
+    if (chunk * QPB >= nq) return;   // uniform
+    const bool active = i < nq;
+    const float gate = v.cfg.nearest_feature_search_sq_dist;
+    const int R = v.cfg.n_scan;
+    float tc[6];
+    for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
+    const P4 sel = slo_pose::transform_to_start(ld4(v.flat + (size_t)s * v.cap_flat, active ? i : 0), tc);
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + 1) * (R + 1);
+    auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
+    // 1-NN (nn1_grid over a share of the rows)
+    int ci = INT_MAX;
+    float cd = gate;
+    if (active && isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z))
+        grid_ball_rows<SLO_ODO_SURF_R>(v.g_os, s, sel.x, sel.y, sel.z, sub, GridRows<SLO_ODO_SURF_R>::N, SURF_QL, true,
+                                       [&]() { return cd; }, [&](const float4& p) {
+            const float d = sqdist_flann(sel, p);
+            const int idx = __float_as_int(p.w);
+            if (d < cd || (d == cd && idx < ci)) { cd = d; ci = idx; }
+        });
+#pragma unroll
+    for (int o = 1; o < SURF_QL; o <<= 1) {
+        const float d2 = __shfl_xor(cd, o, 64);
+        const int i2 = __shfl_xor(ci, o, 64);
+        if (d2 < cd || (d2 == cd && i2 < ci)) { cd = d2; ci = i2; }
+    }
+    if (ci == INT_MAX) { ci = -1; cd = FLT_MAX; }
+    const float4* sx = v.sx_surf_last + (size_t)s * v.cap_less_flat;
+    const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
+    const int surfLastNum = st.surfLastNum;
+    const bool found = active && cd < gate && ci >= 0 && ci < surfLastNum;   // the same in the query's eight lanes
+    WalkBest w;
+    w.init(gate);
+    if (found && sub <= 4) {
+        const int closest = ci;
+        const int cscan = (int)slast[closest].w;
+        const int lim = min(nq, surfLastNum);                        // Q7: bounded by the flat count
+        const int e0 = ring_first(cscan + 1), e2 = ring_first(cscan + 3);
+        const int b0 = ring_first(cscan), b2 = ring_first(cscan - 2);
+        if (sub == 0) {
+            ring_walk(sx, rf, R, cscan, sel, closest + 1, min(e0, lim), b0, closest, w);   // ring == cscan
+        } else {
+            const int f0 = max(closest + 1, e0), f1 = min(e2, lim), bb1 = min(b0, closest);
+            ring_walk(sx, rf, R, cscan + (sub <= 2 ? sub - 3 : sub - 2), sel, f0, f1, b2, bb1, w);   // other rings
+        }
+    }
+    // the 3rd point: the best of lanes 1-4 (lane 0's walk is the 2nd point's)
+    WalkBest w3;
+    w3.init(gate);
+    if (sub >= 1 && sub <= 4) w3 = w;
+#pragma unroll
+    for (int o = 1; o < SURF_QL; o <<= 1) {
+        const float d2 = __shfl_xor(w3.d, o, 64);
+        const int c2 = __shfl_xor(w3.cls, o, 64), t2 = __shfl_xor(w3.t, o, 64);
+        if (walk_better(d2, c2, t2, w3)) { w3.d = d2; w3.cls = c2; w3.t = t2; }
+    }
+    if (!active || sub != 0) return;
+    int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
+    ind[3 * i] = found ? ci : -1;
+    ind[3 * i + 1] = found ? w.index() : -1;
+    ind[3 * i + 2] = found ? w3.index() : -1;
+}
+
 // findCorrespondingCornerFeatures (FA:1044-1153): one workgroup = 64 queries
 // (consecutive in x order, sharp_perm) x 4 waves.  1-NN by brute force over
 // the x-window of the x-sorted tree cloud that can hold a point within the
@@ -875,9 +965,12 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
     if (!first_scan) {
-        const int nbs = (v.cap_flat + 255) / 256, nbc = (v.cap_sharp + 63) / 64;
+        const bool few = S <= SLO_ODO_FEW && !SLO_SURF_LINEAR;
+        const int nbs = few ? (v.cap_flat + 255 / SURF_QL) / (256 / SURF_QL) : (v.cap_flat + 255) / 256;
+        const int nbc = (v.cap_sharp + 63) / 64;
         for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
+            if (few) SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf_few, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
+            else SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
             SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
         }
         for (int b = 0; b < 5; ++b) {

@@ -21,7 +21,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 SHORT="--cpu-scans 0 --single-steps 0 --steps 12 --profile-steps 0 --icp-jobs 0 --extra none --trace-marker $*"
-PMC_KERNELS=${PMC_KERNELS:-"spin|sleep|k_pc_|k_mo_knn|k_mo_corr|k_vg_|k_fa_ring_ds|k_fa_search|k_fa_sort|k_ip_tile|k_grid"}
+PMC_KERNELS=${PMC_KERNELS:-"spin|sleep|k_pc_|k_mo_knn|k_mo_corr|k_vg_|k_fa_ring_ds|k_fa_search|k_fa_sort|k_fa_sx|k_ip_tile|k_grid"}
 
 # run "$@" under its own limit ($LIM s), printing a line every 30 s; returns its status
 hb() {
@@ -73,4 +73,12 @@ LIM=600 hb rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY 
 python3 tools/pmc_generic.py "$OUT/pmc_sq" > "$OUT/sq.txt"
 rm -rf "$OUT/pmc_sq"
 cat "$OUT/sq.txt"
+echo "[profile] LDS"
+# LDS-array busy cycles (SQ_LDS_IDX_ACTIVE) and bank-conflict cycles, for an LDS roofline of the LDS-resident sorts
+LIM=600 hb rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES \
+    --kernel-include-regex "spin|sleep|k_pc_finish|k_fa_ring_ds|k_pc_tail" --output-format csv \
+    -d "$OUT/pmc_lds" -o pmc -- python3 bench.py $SHORT > "$OUT/pmc_lds.log" 2>&1
+python3 tools/pmc_generic.py "$OUT/pmc_lds" > "$OUT/lds.txt"
+rm -rf "$OUT/pmc_lds"
+cat "$OUT/lds.txt"
 echo "[profile] done"

@@ -14,7 +14,7 @@ import slo_amd  # noqa: E402
 
 def main():
     scans = 40
-    for S in (1, 64):
+    for S in [int(x) for x in sys.argv[1:]] or (1, 64):
         cfg = slo_amd.preset(6)
         P = cfg.max_points
         gen = slo_amd.DeviceGenerator(6, 3, 0, S)
