@@ -897,8 +897,8 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #define SLO_DIAG_RING 0     // 1: k_fa_ring_ds_pcl's sort counters in StreamState::dbg (tools/ring_diag.py; not with SLO_DIAG)
 #endif
 #ifndef RING_W
-#define RING_W 1            // waves per ring (4 measured no faster: DESIGN.md §7); 16 when
-#endif                      // the context has a few streams (latency)
+#define RING_W 4            // waves per ring (170 streams: 1.13 ms per launch against 1.53 with one wave,
+#endif                      // since block_sort's pool); 16 when the context has a few streams
 template <int PMAX, int RW>
 __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
     constexpr int NT = 64 * RW;

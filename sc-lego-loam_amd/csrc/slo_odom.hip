@@ -541,13 +541,12 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
 
 // The same for a context of a few streams, where one stream's queries leave
 // most of the chip idle and the search is the odometry's latency: eight lanes
-// per query.  The 1-NN's grid rows are dealt over the eight (each lane also
-// probes the query's own cell and prunes by its own best; a point a lane
-// skips is farther than that lane's best, so the minima merged by (distance,
-// index) are the exact 1-NN), then the five ring walks run one per lane —
-// lane 0 the closest point's ring (the 2nd point), lanes 1-4 rings cscan - 2,
-// - 1, + 1, + 2 (the 3rd) — and the 3rd point's four bests merge in
-// WalkBest's order, a strict total order on (distance, class, index): the
+// per query.  Each lane finds the 1-NN (the same walk as k_fa_search_surf's
+// thread; dealing the grid rows over the lanes measured twice as slow, every
+// lane pruning by its own, looser bound), then the five ring walks run one
+// per lane — lane 0 the closest point's ring (the 2nd point), lanes 1-4 rings
+// cscan - 2, - 1, + 1, + 2 (the 3rd) — and the 3rd point's four bests merge
+// in WalkBest's order, a strict total order on (distance, class, index): the
 // minimum over all offers, whatever the order of the rings.  Same results as
 // k_fa_search_surf.
 #define SURF_QL 8
@@ -576,23 +575,9 @@ __global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
     const P4 sel = slo_pose::transform_to_start(ld4(v.flat + (size_t)s * v.cap_flat, active ? i : 0), tc);
     const int32_t* rf = v.roff_last + ((size_t)s * 2 + 1) * (R + 1);
     auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
-    // 1-NN (nn1_grid over a share of the rows)
-    int ci = INT_MAX;
-    float cd = gate;
-    if (active && isfinite(sel.x) && isfinite(sel.y) && isfinite(sel.z))
-        grid_ball_rows<SLO_ODO_SURF_R>(v.g_os, s, sel.x, sel.y, sel.z, sub, GridRows<SLO_ODO_SURF_R>::N, SURF_QL, true,
-                                       [&]() { return cd; }, [&](const float4& p) {
-            const float d = sqdist_flann(sel, p);
-            const int idx = __float_as_int(p.w);
-            if (d < cd || (d == cd && idx < ci)) { cd = d; ci = idx; }
-        });
-#pragma unroll
-    for (int o = 1; o < SURF_QL; o <<= 1) {
-        const float d2 = __shfl_xor(cd, o, 64);
-        const int i2 = __shfl_xor(ci, o, 64);
-        if (d2 < cd || (d2 == cd && i2 < ci)) { cd = d2; ci = i2; }
-    }
-    if (ci == INT_MAX) { ci = -1; cd = FLT_MAX; }
+    int ci = -1;
+    float cd = FLT_MAX;
+    if (active) nn1_grid(v.g_os, s, gate, sel, ci, cd);
     const float4* sx = v.sx_surf_last + (size_t)s * v.cap_less_flat;
     const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
     const int surfLastNum = st.surfLastNum;
