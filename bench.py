@@ -256,6 +256,8 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
             return int(40 * pw[1])
         if name in ("pc_finish_w", "pc_finish_s", "pc_finish_b"):   # a finish entry's items in and out
             return int(16 * pw[2 + ("pc_finish_w", "pc_finish_s", "pc_finish_b").index(name)])
+        if name == "pc_finish_bx":   # the 4 Ki entries too wide for 32-bit items (PW_FINX)
+            return int(16 * pw[20])
         if name == "pc_tail":     # per stepped item: its key counted (4 B) and read again on its side of the
             # crossing (4 B) plus the left side's index (4 B); per pair: partner position out and in, both
             # items read and written

@@ -54,10 +54,24 @@ namespace slo_pcl {
 
 typedef unsigned long long u64;
 
+// Items: 64-bit (voxel index << 32 | point index), or 32-bit within one LDS
+// range whose keys span less than 2^20 ((key - min) << 12 | position in the
+// range, k_pc_finish32).  Only keys are ever compared.
+constexpr int kPosBits = 12;
 __host__ __device__ inline unsigned int vkey(u64 it) { return (unsigned int)(it >> 32); }
+__host__ __device__ inline unsigned int vkey(unsigned int it) { return it >> kPosBits; }
 struct Less {
     __host__ __device__ bool operator()(const u64& a, const u64& b) const { return (a >> 32) < (b >> 32); }
 };
+template <class It>
+struct LessT {
+    __host__ __device__ bool operator()(const It& a, const It& b) const { return vkey(a) < vkey(b); }
+};
+// the key at position x, read as a 32-bit word
+__device__ __forceinline__ unsigned int key_at(const u64* a, int x) {
+    return reinterpret_cast<const unsigned int*>(a)[2 * x + 1];
+}
+__device__ __forceinline__ unsigned int key_at(const unsigned int* a, int x) { return a[x] >> kPosBits; }
 
 __host__ __device__ inline int lg2(int n) {
     int r = 0;
@@ -109,18 +123,18 @@ __device__ __forceinline__ unsigned int renc(int f, int l, int d) {
 // ballot of the crossing and two lane reads, and the LDS sees the median
 // swap, the right-stopper table (tbl[f + rank]), its reads, the partner reads and
 // the swaps.  Returns the cut.
-template <int R>
-__device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f, int l) {
+template <int R, class It>
+__device__ __forceinline__ int wave_step(It* items, unsigned short* tbl, int f, int l) {
     const int lane = threadIdx.x & 63;
     constexpr int INF = 0x7fffffff;
     const int mid = f + (l - f) / 2;
-    const u64 a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
-    u64 it[R];
+    const It a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+    It it[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) it[r] = items[min(f + 1 + 64 * r + lane, l - 1)];
     const int w = median3(vkey(a1), vkey(a2), vkey(a3));
     const int med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
-    const u64 pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
+    const It pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
     const unsigned int p = vkey(pit);
     bool iL[R], iR[R];
     int pl[R], pr[R];
@@ -177,7 +191,7 @@ __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f,
     }
     wave_fence();
     int y[R];
-    u64 py[R];
+    It py[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) y[r] = (iL[r] && pl[r] < m) ? (int)tbl[f + pl[r]] : -1;
 #pragma unroll
@@ -197,16 +211,16 @@ __device__ __forceinline__ int wave_step(u64* items, unsigned short* tbl, int f,
 // rowL / rowR hold, in lane r, the left / right stoppers before row r, so a
 // row's exclusive prefixes are one lane read and a lane count away in every
 // later pass; keys are the high words of the items.
-__device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int f, int l) {
+template <class It>
+__device__ __forceinline__ int stream_step(It* items, unsigned short* tbl, int f, int l) {
     const int lane = threadIdx.x & 63;
     constexpr int INF = 0x7fffffff;
     constexpr int U = 4;   // rows in flight
-    const unsigned int* K = reinterpret_cast<const unsigned int*>(items);
     const int mid = f + (l - f) / 2;
-    const u64 a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+    const It a0 = items[f], a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
     const int w = median3(vkey(a1), vkey(a2), vkey(a3));
     const int med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
-    const u64 pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
+    const It pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
     const unsigned int p = vkey(pit), k0 = vkey(a0);
     const int b0 = f + 1, R = (l - b0 + 63) >> 6;   // rows of [f + 1, l)
     // (1) stopper counts per row (the median swap taken virtually)
@@ -214,7 +228,7 @@ __device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int 
     for (int r0 = 0; r0 < R; r0 += U) {
         unsigned int kk[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u) + lane, l - 1) + 1];
+        for (int u = 0; u < U; ++u) kk[u] = key_at(items, min(b0 + 64 * (r0 + u) + lane, l - 1));
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int r = r0 + u;
@@ -241,7 +255,7 @@ __device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int 
     // a row's stoppers with their exclusive prefixes (the median swap virtual)
     auto row_flags = [&](int r, bool& iL, bool& iR, int& pl, int& pr) {
         const int x = b0 + 64 * r + lane;
-        unsigned int k = K[2 * min(x, l - 1) + 1];
+        unsigned int k = key_at(items, min(x, l - 1));
         k = x == med ? k0 : k;
         const bool act = x < l;
         iL = act && !(k < p);
@@ -290,11 +304,10 @@ __device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int 
     wave_fence();
     if (m > 0) {
         // (4) the m last right stoppers (rows rB ..), by rank from the right
-        const unsigned int* Kr = K;
         for (int r0 = rB; r0 < R; r0 += U) {
             unsigned int kk[U];
 #pragma unroll
-            for (int u = 0; u < U; ++u) kk[u] = Kr[2 * min(b0 + 64 * (r0 + u) + lane, l - 1) + 1];
+            for (int u = 0; u < U; ++u) kk[u] = key_at(items, min(b0 + 64 * (r0 + u) + lane, l - 1));
 #pragma unroll
             for (int u = 0; u < U; ++u) {
                 const int r = r0 + u;
@@ -312,7 +325,7 @@ __device__ __forceinline__ int stream_step(u64* items, unsigned short* tbl, int 
         // partner at or after it, so a batch's loads see no earlier write
         const int rEnd = m < TL ? rA : R - 1;
         for (int r0 = 0; r0 <= rEnd; r0 += U) {
-            u64 it[U], py[U];
+            It it[U], py[U];
             int y[U];
 #pragma unroll
             for (int u = 0; u < U; ++u) it[u] = items[min(b0 + 64 * (r0 + u) + lane, l - 1)];
@@ -359,15 +372,20 @@ __device__ __forceinline__ u64 shfl64(u64 v, int src) {
     const unsigned int hi = (unsigned int)__shfl((int)(unsigned int)(v >> 32), src, 64);
     return ((u64)hi << 32) | lo;
 }
+__device__ __forceinline__ u64 ishfl(u64 v, int src) { return shfl64(v, src); }
+__device__ __forceinline__ unsigned int ishfl(unsigned int v, int src) {
+    return (unsigned int)__shfl((int)v, src, 64);
+}
 
 // items[f, f + n), n <= 64; tw: 128 bytes of this wave's LDS.  Returns the
 // lanes that start a spent-depth segment (bit lo), the segment's end in *hend
 // (per lane) for the caller's lane tasks.
-__device__ __forceinline__ unsigned long long wave_small_sort(u64* items, int f, int n, int depth, unsigned char* tw,
+template <class It>
+__device__ __forceinline__ unsigned long long wave_small_sort(It* items, int f, int n, int depth, unsigned char* tw,
                                                               int* hend) {
     const int i = threadIdx.x & 63;
     const bool live = i < n;
-    u64 it = items[f + min(i, n - 1)];
+    It it = items[f + min(i, n - 1)];
     int lo = 0, hi = n, dd = depth;
     for (;;) {
         const bool act = live && hi - lo > 16 && dd > 0;
@@ -380,7 +398,7 @@ __device__ __forceinline__ unsigned long long wave_small_sort(u64* items, int f,
         const int w = median3(ka, kb, kc);
         const int med = w == 0 ? lo + 1 : (w == 1 ? mid : hi - 1);
         const unsigned int p = w == 0 ? ka : (w == 1 ? kb : kc);
-        it = shfl64(it, act ? (i == lo ? med : (i == med ? lo : i)) : i);   // the median swap
+        it = ishfl(it, act ? (i == lo ? med : (i == med ? lo : i)) : i);   // the median swap
         const unsigned int k = vkey(it);
         const bool inr = act && i > lo;
         const bool iL = inr && !(k < p), iR = inr && !(p < k);
@@ -403,7 +421,7 @@ __device__ __forceinline__ unsigned long long wave_small_sort(u64* items, int f,
         if (sL) src = tw[64 + lo + pl];
         if (sR) src = tw[lo + (TR - 1 - pr)];
         wave_fence();
-        it = shfl64(it, src);
+        it = ishfl(it, src);
         if (act) {
             if (i < cut) hi = cut;
             else lo = cut;
@@ -451,25 +469,30 @@ __device__ __forceinline__ u64 rl64(u64 x, int i) {
     const unsigned int hi = (unsigned int)__builtin_amdgcn_readlane((int)(unsigned int)(x >> 32), i);
     return ((u64)hi << 32) | lo;
 }
-__device__ inline void wave_heap_sort(u64* a, int n) {
+__device__ __forceinline__ u64 irl(u64 x, int i) { return rl64(x, i); }
+__device__ __forceinline__ unsigned int irl(unsigned int x, int i) {
+    return (unsigned int)__builtin_amdgcn_readlane((int)x, __builtin_amdgcn_readfirstlane(i));
+}
+template <class It>
+__device__ inline void wave_heap_sort(It* a, int n) {
     const int lane = threadIdx.x & 63;
     if (n < 2) return;
     const int P = (n - 2) / 2;   // the last parent
     for (int L = lg2(P + 1); L >= 0; --L) {
         const int lo = (1 << L) - 1, hi = min((1 << (L + 1)) - 2, P);
-        for (int x = lo + lane; x <= hi; x += 64) slo_sort::adjust_heap_(a, x, n, a[x], Less());
+        for (int x = lo + lane; x <= hi; x += 64) slo_sort::adjust_heap_(a, x, n, a[x], LessT<It>());
         wave_fence();
     }
     constexpr int TOPN = 63;
-    u64 top = lane < min(n, TOPN) ? a[lane] : 0ull;
+    It top = lane < min(n, TOPN) ? a[lane] : (It)0;
     const int tlev = 31 - __builtin_clz(lane + 1);        // tree level of node `lane`
     const int cj = 31 - __builtin_clz(lane + 2), cq = lane + 2 - (1 << cj);   // chunk slot: level cj, position cq
     for (int len = n - 1; len >= 1; --len) {
         // __pop_heap(first, first + len, first + len)
-        const u64 mx = rl64(top, 0);
-        u64 v;
+        const It mx = irl(top, 0);
+        It v;
         if (len < TOPN) {
-            v = rl64(top, len);
+            v = irl(top, len);
             if (lane == len) top = mx;
         } else {
             v = a[len];
@@ -477,10 +500,10 @@ __device__ inline void wave_heap_sort(u64* a, int n) {
         }
         const int lim = (len - 1) / 2;   // nodes below lim have two children
         int h = 0, k = 0, ph = 0;
-        u64 pv = 0;
+        It pv = 0;
         while (h < lim && 2 * h + 2 < TOPN) {   // the path through the register levels
             const int r = 2 * h + 2;
-            const u64 R = rl64(top, r), Lf = rl64(top, r - 1);
+            const It R = irl(top, r), Lf = irl(top, r - 1);
             const bool left = vkey(R) < vkey(Lf);
             h = left ? r - 1 : r;
             ++k;
@@ -488,11 +511,11 @@ __device__ inline void wave_heap_sort(u64* a, int n) {
         }
         while (h < lim) {   // deeper: the five levels below h in one load
             const int node = (h + 1) * (1 << cj) - 1 + cq;
-            const u64 sub = (lane < 62 && node < len) ? a[node] : 0ull;
+            const It sub = (lane < 62 && node < len) ? a[node] : (It)0;
             int rel = 0;
             for (int j = 1; j <= 5 && h < lim; ++j) {
                 const int tr = (1 << j) - 1 + 2 * rel;   // the right child's slot
-                const u64 R = rl64(sub, tr), Lf = rl64(sub, tr - 1);
+                const It R = irl(sub, tr), Lf = irl(sub, tr - 1);
                 const bool left = vkey(R) < vkey(Lf);
                 rel = 2 * rel + (left ? 0 : 1);
                 h = 2 * h + (left ? 1 : 2);
@@ -502,16 +525,16 @@ __device__ inline void wave_heap_sort(u64* a, int n) {
         }
         if ((len & 1) == 0 && h == (len - 2) / 2) {   // the last parent's only child
             const int c = 2 * h + 1;
-            const u64 cv = c < TOPN ? rl64(top, c) : a[c];
+            const It cv = c < TOPN ? irl(top, c) : a[c];
             ++k;
             if (lane == k) { ph = c; pv = cv; }
         }
         const unsigned int kv = vkey(v);
         const int m = __popcll(__ballot(lane >= 1 && lane <= k && !(vkey(pv) < kv)));
-        const u64 up = shfl64(pv, min(lane + 1, 63));   // (every lane takes part: a permute reads no inactive lane)
-        const u64 w = lane < m ? up : v;
+        const It up = ishfl(pv, min(lane + 1, 63));   // (every lane takes part: a permute reads no inactive lane)
+        const It w = lane < m ? up : v;
         const int phl = __shfl(ph, min(tlev, 63), 64);
-        const u64 wl = shfl64(w, min(tlev, 63));
+        const It wl = ishfl(w, min(tlev, 63));
         if (lane <= m && ph >= TOPN) a[ph] = w;
         if (lane < TOPN && tlev <= m && phl == lane) top = wl;
         wave_fence();
@@ -521,13 +544,14 @@ __device__ inline void wave_heap_sort(u64* a, int n) {
 }
 
 // the queued lane tasks, one per lane, through the sequential restatement
-__device__ __forceinline__ void lane_flush(u64* items, const unsigned int* q, int nq) {
+template <class It>
+__device__ __forceinline__ void lane_flush(It* items, const unsigned int* q, int nq) {
     const int lane = threadIdx.x & 63;
     wave_fence();
     if (lane < nq) {
         const unsigned int e = q[lane];
         const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
-        slo_sort::introsort_range(items + f, l - f, d, Less());
+        slo_sort::introsort_range(items + f, l - f, d, LessT<It>());
     }
     wave_fence();
 }
@@ -560,7 +584,8 @@ __device__ __forceinline__ bool pool_push(Pool* pool, unsigned int e, int W) {
 }
 
 // one step of [f, l) by the calling wave, the variant its size picks
-__device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, int f, int l) {
+template <class It>
+__device__ __forceinline__ int wave_step_any(It* items, unsigned short* tbl, int f, int l) {
     const int len = l - f;
     return len - 1 <= 64 ? wave_step<1>(items, tbl, f, l)
          : len - 1 <= 128 ? wave_step<2>(items, tbl, f, l) : stream_step(items, tbl, f, l);
@@ -574,8 +599,8 @@ __device__ __forceinline__ int wave_step_any(u64* items, unsigned short* tbl, in
 // handed to a lane for a reason other than their size (must stay 0).
 // prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges and heapsorts;
 // [3] items heapsorted (wave_heap_sort)
-template <int TLANE>
-__device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int depth, unsigned short* tbl,
+template <int TLANE, class It>
+__device__ __forceinline__ void wave_sort_range(It* items, int f0, int l0, int depth, unsigned short* tbl,
                                                 WaveSmem& ws, int* err = nullptr, long long* prof = nullptr,
                                                 Pool* pool = nullptr, int W = 1) {
     static_assert(TLANE >= 16 && TLANE <= 64, "ranges of <= TLANE items go to wave_small_sort");
@@ -649,8 +674,8 @@ __device__ __forceinline__ void wave_sort_range(u64* items, int f0, int l0, int 
     }
 }
 
-template <int TLANE>
-__device__ __forceinline__ void wave_sort(u64* items, int n, int depth, unsigned short* tbl, WaveSmem& ws,
+template <int TLANE, class It>
+__device__ __forceinline__ void wave_sort(It* items, int n, int depth, unsigned short* tbl, WaveSmem& ws,
                                           int* err = nullptr, long long* prof = nullptr) {
     wave_sort_range<TLANE>(items, 0, n, depth, tbl, ws, err, prof);
 }
@@ -674,19 +699,19 @@ struct BlockStepSm {
     int rl[65], rr[65];   // per row stopper counts, then exclusive prefixes
     int m, cutA, cutB, rA, rB;
 };
-__device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f, int l, int mode, BlockStepSm& bs,
+template <class It>
+__device__ __forceinline__ int group_step(It* items, unsigned short* tbl, int f, int l, int mode, BlockStepSm& bs,
                                           int gw) {
     const int lane = threadIdx.x & 63, lw = (threadIdx.x >> 6) & (gw - 1);
     constexpr int INF = 0x7fffffff;
-    const unsigned int* K = reinterpret_cast<const unsigned int*>(items);
     const bool big = mode == 2;
     const int mid = f + (l - f) / 2;
-    u64 a0 = 0, pit = 0;
+    It a0 = 0, pit = 0;
     unsigned int p = 0, k0 = 0;
     int med = 0;
     if (big) {
         a0 = items[f];
-        const u64 a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
+        const It a1 = items[f + 1], a2 = items[mid], a3 = items[l - 1];
         const int w = median3(vkey(a1), vkey(a2), vkey(a3));
         med = w == 0 ? f + 1 : (w == 1 ? mid : l - 1);
         pit = w == 0 ? a1 : (w == 1 ? a2 : a3);
@@ -698,7 +723,7 @@ __device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f
     for (int r0 = lw; r0 < R; r0 += 4 * gw) {
         unsigned int kk[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) kk[u] = K[2 * min(b0 + 64 * (r0 + u * gw) + lane, l - 1) + 1];
+        for (int u = 0; u < 4; ++u) kk[u] = key_at(items, min(b0 + 64 * (r0 + u * gw) + lane, l - 1));
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int r = r0 + u * gw;
@@ -728,7 +753,7 @@ __device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f
         const int c = __builtin_ctzll(__ballot(lane < R && eL >= TR - eR));
         auto row_flags = [&](int r, bool& iL, bool& iR, int& pl, int& pr) {
             const int x = b0 + 64 * r + lane;
-            unsigned int k = K[2 * min(x, l - 1) + 1];
+            unsigned int k = key_at(items, min(x, l - 1));
             k = x == med ? k0 : k;
             const bool act = x < l;
             iL = act && !(k < p);
@@ -781,7 +806,7 @@ __device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f
     if (m > 0) {   // (3) the m last right stoppers, by rank from the right
         for (int r = bs.rB + lw; r < R; r += gw) {
             const int x = b0 + 64 * r + lane;
-            const bool iR = x < l && !(p < K[2 * min(x, l - 1) + 1]);
+            const bool iR = x < l && !(p < key_at(items, min(x, l - 1)));
             const int kr = TR - 1 - (bs.rr[r] + lane_prefix(__ballot(iR)));
             if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
         }
@@ -791,12 +816,12 @@ __device__ __forceinline__ int group_step(u64* items, unsigned short* tbl, int f
         const int rEnd = bs.rA;
         for (int r = lw; r <= rEnd; r += gw) {
             const int x = b0 + 64 * r + lane;
-            const u64 it = items[min(x, l - 1)];
+            const It it = items[min(x, l - 1)];
             const bool iL = x < l && !(vkey(it) < p);
             const int pl = bs.rl[r] + lane_prefix(__ballot(iL));
             if (iL && pl < m) {
                 const int y = tbl[f + pl];
-                const u64 py = items[y];
+                const It py = items[y];
                 items[x] = py;
                 items[y] = it;
             }
@@ -820,8 +845,8 @@ struct BlockQ {
     Pool pool;
 };
 
-template <int TLANE, int W>
-__device__ __forceinline__ void block_sort(u64* items, int n, int depth, unsigned short* tbl, WaveSmem* ws,
+template <int TLANE, int W, class It>
+__device__ __forceinline__ void block_sort(It* items, int n, int depth, unsigned short* tbl, WaveSmem* ws,
                                            BlockQ<W>& bq, int* err = nullptr, long long* prof = nullptr) {
     const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
     if (W == 1) {

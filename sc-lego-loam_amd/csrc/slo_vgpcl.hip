@@ -65,7 +65,8 @@ using slo_pcl::u64;
 // finish lists 0..2, [5] VoxelGrid input points, [6] finish entries, [7]
 // items of the ranges k_pc_tail stepped, [8] pairs it swapped, [9 + 3 list + q]
 // finish cycles of list `list` in streamed steps, register steps, lane tasks
-enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_TAIL = 7, PW_TAIL_PAIRS = 8, PW_PROF = 9 };
+enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_TAIL = 7, PW_TAIL_PAIRS = 8, PW_PROF = 9,
+       PW_FINX = 20 };   // [20]: items of list 5 (the 4 Ki entries too wide for 32-bit items, k_pc_finish on 64-bit)
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
@@ -74,9 +75,10 @@ struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
 enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC_NW + k: range list k
 
 // Range lists: finish entries by size class, list 0 <= PC_WT items, 1 <= PC_ST,
-// 2 <= PC_T (k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
-// over PC_T items (k_pc_fallback: heapsort).  An entry is (first position, size | depth << 24).
-struct PcLists { int2* l[5]; };
+// 2 <= PC_T (k_pc_finish32, then k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
+// over PC_T items (k_pc_fallback: heapsort); 5 the list-2 entries whose keys span 2^20 or more (filled by
+// k_pc_finish32, sorted by k_pc_finish on 64-bit items).  An entry is (first position, size | depth << 24).
+struct PcLists { int2* l[6]; };
 __device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) {
     const int k = n <= PC_WT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
     const int i = atomicAdd(&ctr[PCC_NW + k], 1);
@@ -574,6 +576,92 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
         we += 1ull;
     }
     if ((tid & 63) == 0 && we) {
+        const int sl = list == 5 ? 2 : list;   // list 5: list-2 entries
+        if (tid == 0) {
+            atomicAdd(&pst[list == 5 ? PW_FINX : PW_FIN + list], wn);
+            atomicAdd(&pst[PW_ENTRIES], we);
+        }
+        for (int q = 0; q < 3; ++q) atomicAdd(&pst[PW_PROF + 3 * sl + q], (unsigned long long)prof[q]);
+    }
+}
+
+// ---- the same with 32-bit items, for an entry whose keys span less than
+// 2^20: (key - min) << 12 | position in the entry (slo_pclsort.h kPosBits).
+// Half the LDS of the 64-bit items — 29 KB per 4 Ki entry at four waves, five
+// workgroups per CU instead of three — and the same comparisons, so the same
+// order.  The point indices stay in global memory and follow their items at
+// the write-back (gathered into the items' LDS slots, written back after a
+// barrier).  A wider entry goes to list 5 (k_pc_finish).
+#ifndef PC_F32_OCC
+#define PC_F32_OCC 5      // waves per SIMD k_pc_finish32 is built for (its LDS allows five 4-wave workgroups per CU)
+#endif
+template <int NMAX, int W>
+__global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >= 4 ? PC_F32_OCC : 1))) k_pc_finish32(unsigned int* K, unsigned int* V, PcLists wl, int* ctr,
+                                                         int list, unsigned long long* pst, int* cstat,
+                                                         const int32_t* off, int S, int32_t* serr) {
+    constexpr int NT = 64 * W;
+    static_assert(NMAX <= (1 << slo_pcl::kPosBits), "positions fit kPosBits");
+    __shared__ unsigned int items[NMAX];
+    __shared__ unsigned short tbl[NMAX];
+    __shared__ slo_pcl::WaveSmem ws[W];
+    __shared__ slo_pcl::BlockQ<W> bq;
+    __shared__ int ferr;
+    __shared__ unsigned int kmn[W], kmx[W];
+    const int nw = ctr[PCC_NW + list], tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    unsigned long long wn = 0, we = 0;
+    long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
+        const int2 w = wl.l[list][e];
+        const int f = w.x, n = min(w.y & 0xffffff, NMAX), d = w.y >> 24;
+        if (tid == 0) ferr = 0;
+        unsigned int mn = 0xffffffffu, mx = 0u;
+        for (int i0 = 0; i0 < n; i0 += 4 * NT) {   // the raw keys into LDS, four loads in flight
+            unsigned int kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) kk[u] = K[f + min(i0 + u * NT + tid, n - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int i = i0 + u * NT + tid;
+                mn = min(mn, kk[u]);
+                mx = max(mx, kk[u]);
+                if (i < n) items[i] = kk[u];
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            mn = min(mn, (unsigned int)__shfl_xor((int)mn, o, 64));
+            mx = max(mx, (unsigned int)__shfl_xor((int)mx, o, 64));
+        }
+        if (lane == 0) { kmn[wv] = mn; kmx[wv] = mx; }
+        __syncthreads();
+        for (int q = 0; q < W; ++q) { mn = min(mn, kmn[q]); mx = max(mx, kmx[q]); }
+        if (mx - mn >= (1u << (32 - slo_pcl::kPosBits))) {   // too wide for 32-bit items (uniform)
+            if (tid == 0) wl.l[5][atomicAdd(&ctr[PCC_NW + 5], 1)] = w;
+            __syncthreads();   // kmn / kmx and items are rewritten by the next entry
+            continue;
+        }
+        for (int i = tid; i < n; i += NT) items[i] = ((items[i] - mn) << slo_pcl::kPosBits) | (unsigned int)i;
+        __syncthreads();
+        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, prof);
+        __syncthreads();
+        if (tid == 0 && ferr) {   // never expected: counted and the stream flagged
+            atomicAdd(&cstat[1], ferr);
+            pc_flag(serr, off, S, f, SLO_ERR_SORT);
+        }
+        // the keys out at once; each position's point index gathered into its
+        // LDS slot, written out only after every gather of the entry is done
+        for (int i = tid; i < n; i += NT) {
+            const unsigned int it = items[i];
+            K[f + i] = (it >> slo_pcl::kPosBits) + mn;
+            items[i] = V[f + (it & ((1u << slo_pcl::kPosBits) - 1u))];
+        }
+        __syncthreads();
+        for (int i = tid; i < n; i += NT) V[f + i] = items[i];
+        __syncthreads();
+        wn += (unsigned long long)n;
+        we += 1ull;
+    }
+    if ((tid & 63) == 0 && we) {
         if (tid == 0) {
             atomicAdd(&pst[PW_FIN + list], wn);
             atomicAdd(&pst[PW_ENTRIES], we);
@@ -927,7 +1015,7 @@ static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.cseg[0], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
-        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 4 * wcapk)));
+        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 5 * wcapk)));
         w.wcap0 = wcap0;
         w.wcapk = wcapk;
     }
@@ -965,7 +1053,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     PcLists L;
     L.l[0] = w.wl;
-    for (int k = 1; k < 5; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
+    for (int k = 1; k < 6; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
     // the pair positions of a step: the left stoppers' (PA) and their partners
     // (PB), in the VoxelGrid workspace's spare halves (2 * items words)
     unsigned int* PA = spare;
@@ -1005,12 +1093,16 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
                w.ctr, w.pstat, w.cstat, off, S, w.serr);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare);
     if (few) {
-        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
+        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
+                   w.cstat, off, S, w.serr);
+        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 5, w.pstat,
                    w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
                    w.cstat, off, S, w.serr);
     } else {
-        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
+        SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
+                   w.pstat, w.cstat, off, S, w.serr);
+        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 5,
                    w.pstat, w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
                    w.pstat, w.cstat, off, S, w.serr);
