@@ -1092,19 +1092,20 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
                w.ctr, w.pstat, w.cstat, off, S, w.serr);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare);
+    // 32-bit items first (lists 2 and 1); the entries too wide for them (list 5) after, on 64-bit items
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
                    w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 5, w.pstat,
+        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
                    w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
+        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 5, w.pstat,
                    w.cstat, off, S, w.serr);
     } else {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
                    w.pstat, w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 5,
+        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
                    w.pstat, w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
+        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 5,
                    w.pstat, w.cstat, off, S, w.serr);
     }
     SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat, off, S, w.serr);
