@@ -32,11 +32,13 @@ def launch_names():
 
 # launches whose kernel is a template instance named through macros
 # (SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish<PC_T, PC_FW>), ...)): instance -> timing name
-TEMPLATED = {"k_pc_finish<4096, 4>": "pc_finish_b", "k_pc_finish<2048, 4>": "pc_finish_s",
+TEMPLATED = {"k_pc_finish32<4096, 4>": "pc_finish_b", "k_pc_finish32<2048, 4>": "pc_finish_s",
+             "k_pc_finish32<4096, 16>": "pc_finish_b", "k_pc_finish32<2048, 8>": "pc_finish_s",
+             "k_pc_finish<4096, 4>": "pc_finish_bx", "k_pc_finish<2048, 4>": "pc_finish_s",
              "k_pc_finish<512, 1>": "pc_finish_w", "k_fa_ring_ds_pcl<2048, 4>": "fa_ring_ds",
              "k_fa_ring_ds_pcl<2048, 16>": "fa_ring_ds", "k_fa_ring_ds_pcl<4096, 4>": "fa_ring_ds",
              "k_fa_ring_ds_pcl<2048, 1>": "fa_ring_ds",
-             "k_pc_finish<4096, 16>": "pc_finish_b", "k_pc_finish<2048, 8>": "pc_finish_s",
+             "k_pc_finish<4096, 16>": "pc_finish_bx", "k_pc_finish<2048, 8>": "pc_finish_s",
              "k_fa_ring_ds_pcl<4096>": "fa_ring_ds"}
 
 
