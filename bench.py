@@ -704,8 +704,9 @@ def main():
     vgs = sum(c.get(0, "vg_stats").astype(np.int64) for c in ctxs)
     guards = {"fallback_ranges": int(vgs[0]), "inconsistent_steps": int(vgs[2] + vgs[3] + vgs[4]),
               "clipped_outputs": int(vgs[1] != 0),
-              "note": "PCL-order VoxelGrid sort over the whole run: ranges heapsorted on one lane (exact; adversarial "
-                      "inputs), guards of impossible steps (must be 0; each also sets its stream's err bit)"}
+              "note": "PCL-order VoxelGrid sort over the whole run: fallback_ranges = ranges over 4 Ki items whose "
+                      "introsort depth budget ran out (std::sort's heapsort, done exactly by one wave), guards of "
+                      "impossible steps (must be 0; each also sets its stream's err bit)"}
     kfs = np.array([int(c.get(s, "n_keyframes")[0]) for c in ctxs for s in range(c.n_streams)])
 
     if counts is not None:

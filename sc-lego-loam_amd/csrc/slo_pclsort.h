@@ -473,7 +473,19 @@ __device__ __forceinline__ u64 irl(u64 x, int i) { return rl64(x, i); }
 __device__ __forceinline__ unsigned int irl(unsigned int x, int i) {
     return (unsigned int)__builtin_amdgcn_readlane((int)x, __builtin_amdgcn_readfirstlane(i));
 }
-template <class It>
+// Global: `a` in global memory (k_pc_fallback's scratch): the lanes' stores
+// are ordered before the next reads by a workgroup-scope fence instead of the
+// LDS wave fence.
+template <bool Global>
+__device__ __forceinline__ void heap_fence() {
+    if (Global) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        wave_fence();
+    }
+}
+template <class It, bool Global = false>
 __device__ inline void wave_heap_sort(It* a, int n) {
     const int lane = threadIdx.x & 63;
     if (n < 2) return;
@@ -481,7 +493,7 @@ __device__ inline void wave_heap_sort(It* a, int n) {
     for (int L = lg2(P + 1); L >= 0; --L) {
         const int lo = (1 << L) - 1, hi = min((1 << (L + 1)) - 2, P);
         for (int x = lo + lane; x <= hi; x += 64) slo_sort::adjust_heap_(a, x, n, a[x], LessT<It>());
-        wave_fence();
+        heap_fence<Global>();
     }
     constexpr int TOPN = 63;
     It top = lane < min(n, TOPN) ? a[lane] : (It)0;
@@ -537,10 +549,10 @@ __device__ inline void wave_heap_sort(It* a, int n) {
         const It wl = ishfl(w, min(tlev, 63));
         if (lane <= m && ph >= TOPN) a[ph] = w;
         if (lane < TOPN && tlev <= m && phl == lane) top = wl;
-        wave_fence();
+        heap_fence<Global>();
     }
     if (lane < min(n, TOPN)) a[lane] = top;
-    wave_fence();
+    heap_fence<Global>();
 }
 
 // the queued lane tasks, one per lane, through the sequential restatement

@@ -960,18 +960,43 @@ __global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int
     }
 }
 
-// list 4 — a range over PC_T items whose depth budget is spent (adversarial
-// inputs only): one lane finishes it in global memory with the sequential
-// restatement (heapsort)
+// list 4 — a range over PC_T items whose depth budget is spent (std::sort's
+// heapsort; the dense C5 maps send a few hundred per run here): the first
+// wave heapsorts it (slo_pclsort.h wave_heap_sort: one round trip per pop
+// instead of two dependent loads per tree level on one lane), staged in LDS
+// up to PC_FB_LDS items, in global memory beyond.  A range that came here for another reason (over PT_MAXT tiles,
+// a full stack; never seen) is finished by one lane with the sequential
+// restatement.
+#ifndef PC_FB_LDS
+#define PC_FB_LDS 12288   // a heapsorted range of up to this many items is staged in LDS (96 KB)
+#endif
 __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
                                                       int* cstat, u64* scratch) {
+    __shared__ u64 lds[PC_FB_LDS];
     const int nw = ctr[PCC_NW + 4];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl[e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
+        if (d == 0 && n > 16 && n <= PC_FB_LDS) {   // in LDS
+            for (int i = threadIdx.x; i < n; i += 256) lds[i] = ((u64)K[f + i] << 32) | V[f + i];
+            __syncthreads();
+            if (threadIdx.x < 64) slo_pcl::wave_heap_sort(lds, n);
+            if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
+            __syncthreads();
+            for (int i = threadIdx.x; i < n; i += 256) {
+                const u64 it = lds[i];
+                K[f + i] = (unsigned int)(it >> 32);
+                V[f + i] = (unsigned int)it;
+            }
+            __syncthreads();
+            continue;
+        }
         for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (d == 0 && n > 16) {
+            if (threadIdx.x < 64) slo_pcl::wave_heap_sort<u64, true>(scratch + f, n);
+            if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
+        } else if (threadIdx.x == 0) {
             atomicAdd(&cstat[0], 1);
             slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());
         }
