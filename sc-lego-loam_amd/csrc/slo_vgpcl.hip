@@ -685,6 +685,9 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
 #define PT_ROWS 16
 #define PT_TILE (64 * PT_ROWS)
 #define PT_MAXT 4096
+#ifndef PT_OCC
+#define PT_OCC 8          // waves per SIMD k_pc_tail is built for: four 8-wave workgroups per CU (the LDS allows four)
+#endif
 struct TailSm {
     int tl[PT_MAXT + 1], tr[PT_MAXT + 1];   // per tile stopper counts, then exclusive prefixes (+ totals)
     int sf[64], sl[64], sd[64];             // the stack of ranges still over PC_T
@@ -694,7 +697,7 @@ struct TailSm {
     int wsum[PT_NW];
 };
 
-__global__ void __launch_bounds__(PT_NT) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
+__global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_OCC))) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
                                                     int* ctr, unsigned long long* pst, int* cstat, const int32_t* off,
                                                     int S, int32_t* serr) {
     __shared__ TailSm sm;
