@@ -59,6 +59,12 @@ using slo_pcl::u64;
 #define PC_TAIL_FEW 16384
 #endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
+#ifndef PC_LOCC
+#define PC_LOCC 8         // waves per SIMD k_pc_lrank is built for (latency-bound streaming)
+#endif
+#ifndef PC_WOCC
+#define PC_WOCC 6         // k_pc_write (8 would spill 12 VGPRs)
+#endif
 // PclWs::pstat, cumulative work counters (slo_get "pcl_work"; the bench
 // prices the kernels' algorithmic bytes with them): [0] items of the ranges
 // stepped by the global levels, [1] pairs they swapped, [2..4] items of
@@ -185,7 +191,7 @@ __global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* o
     }
 }
 
-__global__ void __launch_bounds__(VG_T) k_pc_write(VgSrc src, const int32_t* off,
+__global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(PC_WOCC))) k_pc_write(VgSrc src, const int32_t* off,
                                                     const VgParams* prm, const int* tcnt, const int32_t* nfin,
                                                     int maxT, unsigned int* K, unsigned int* V, int S) {
     __shared__ unsigned int wsum[VG_W];
@@ -351,7 +357,7 @@ __global__ void __launch_bounds__(PC_CT) k_pc_lscan(const unsigned int* K, const
 // ranks by ballots on striped rows: position a + q * PC_CT + tid is row q,
 // wave w, lane t; the stoppers before it are the chunk's prefix + the
 // (row, wave) pairs before (q, w) + the lanes below t
-__global__ void __launch_bounds__(PC_CT) k_pc_lrank(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
+__global__ void __launch_bounds__(PC_CT) __attribute__((amdgpu_waves_per_eu(PC_LOCC))) k_pc_lrank(unsigned int* K, unsigned int* V, const PSeg* seg, const int* cseg,
                                                      const int2* ccnt, PRes* res, unsigned int* PA, unsigned int* PB,
                                                      const int* ctr, int cur) {
     constexpr int Q = PC_CH / PC_CT, NWV = PC_CT / 64;
