@@ -786,12 +786,18 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int*
 #ifndef SLO_VG_FUSED
 #define SLO_VG_FUSED 1
 #endif
+#ifndef SLO_VG_LV
+#define SLO_VG_LV 1   // the slice's point indices staged in LDS for the gathers (32.8 KB, four waves per SIMD; without
+                      // them eight, measured slower: 13.8 against 12.6 ms per 6 mapping steps)
+#endif
 __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, const unsigned int* keys, const unsigned int* vals,
                                                     const int32_t* off, const VgParams* prm, const int* hcnt, int maxT,
                                                     int32_t* meta, int4* longv, int nlong_cap, int S) {
     constexpr int SL = VG_TILE / VG_W;   // items per wave slice
     __shared__ int lst[VG_W][SL + 1];
+#if SLO_VG_LV
     __shared__ unsigned int lvv[VG_W][SL];   // the slice's point indices (the gathers read them from LDS)
+#endif
     __shared__ int wsum[VG_W];
     int s, chunk;
     if (!vg_block(S, s, chunk)) return;
@@ -814,18 +820,24 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, const unsigned i
         // comes from the lane below (lane 0: the previous row's lane 63, or the
         // item before the slice)
         unsigned int kk[SL / 64];
+#if SLO_VG_LV
         unsigned int* LV = lvv[w];
+#endif
         if (ms == SL) {
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q) kk[q] = k[i0 + q * 64 + lane];
+#if SLO_VG_LV
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q) LV[q * 64 + lane] = v[i0 + q * 64 + lane];
+#endif
         } else {
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q) kk[q] = q * 64 + lane < ms ? k[i0 + q * 64 + lane] : 0u;
+#if SLO_VG_LV
 #pragma unroll
             for (int q = 0; q < SL / 64; ++q)
                 if (q * 64 + lane < ms) LV[q * 64 + lane] = v[i0 + q * 64 + lane];
+#endif
         }
         unsigned int before = (ms > 0 && i0 > 0) ? k[i0 - 1] : 0u;
 #pragma unroll
@@ -878,7 +890,11 @@ __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, const unsigned i
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {   // indices inside the slice from LDS, past its end from HBM
                     const int ii = i + u;
+#if SLO_VG_LV
                     q4[u] = ii < e ? src[ii - i0 < ms ? LV[ii - i0] : v[ii]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#else
+                    q4[u] = ii < e ? src[v[ii]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#endif
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
