@@ -59,6 +59,10 @@ using slo_pcl::u64;
 #define PC_TAIL_FEW 16384
 #endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
+#ifndef PC_XLEV
+#define PC_XLEV 6         // global levels past log2(stride / tail size), for the uneven splits median-of-three leaves:
+                          // 6 against 3 took the tail 39.9 -> 27.1 ms for 2.2 ms more of levels (18.8k -> 19.0k)
+#endif
 #ifndef PC_LOCC
 #define PC_LOCC 8         // waves per SIMD k_pc_lrank is built for (latency-bound streaming)
 #endif
@@ -83,8 +87,9 @@ enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC
 // Range lists: finish entries by size class, list 0 <= PC_WT items, 1 <= PC_ST,
 // 2 <= PC_T (k_pc_finish32, then k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
 // over PC_T items (k_pc_fallback: heapsort); 5 the list-2 entries whose keys span 2^20 or more (filled by
-// k_pc_finish32, sorted by k_pc_finish on 64-bit items).  An entry is (first position, size | depth << 24).
-struct PcLists { int2* l[6]; };
+// k_pc_finish32, sorted by k_pc_finish on 64-bit items); 6 the list-3 ranges over PT_SMAXT tiles (filled by the
+// small-table k_pc_tail, stepped by the large-table one).  An entry is (first position, size | depth << 24).
+struct PcLists { int2* l[7]; };
 __device__ inline void pc_push(const PcLists& L, int* ctr, int f, int n, int d) {
     const int k = n <= PC_WT ? 0 : n <= PC_ST ? 1 : n <= PC_T ? 2 : 3;
     const int i = atomicAdd(&ctr[PCC_NW + k], 1);
@@ -686,16 +691,17 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
 // a range whose depth budget is spent goes to list 4 (k_pc_fallback,
 // heapsort).  Ranges over PT_MAXT tiles go to list 4 as well (one lane
 // finishes them exactly; never seen: the map clouds' strides are ~1.6 M).
-#define PT_NT 512
-#define PT_NW (PT_NT / 64)
+
 #define PT_ROWS 16
 #define PT_TILE (64 * PT_ROWS)
 #define PT_MAXT 4096
+#define PT_SMAXT 256      // tiles of the small-table tail (4-wave workgroups, 256 Ki items)
 #ifndef PT_OCC
-#define PT_OCC 8          // waves per SIMD k_pc_tail is built for: four 8-wave workgroups per CU (the LDS allows four)
+#define PT_OCC 8          // waves per SIMD k_pc_tail is built for
 #endif
+template <int PT_NW, int MAXT>
 struct TailSm {
-    int tl[PT_MAXT + 1], tr[PT_MAXT + 1];   // per tile stopper counts, then exclusive prefixes (+ totals)
+    int tl[MAXT + 1], tr[MAXT + 1];   // per tile stopper counts, then exclusive prefixes (+ totals)
     int sf[64], sl[64], sd[64];             // the stack of ranges still over PC_T
     int f, l, d, sp, have;                  // the range in hand (have: one is)
     unsigned int piv, k0;
@@ -703,13 +709,20 @@ struct TailSm {
     int wsum[PT_NW];
 };
 
+// (A small-table shape — four waves, tile tables for 64 or 256 tiles, eight
+// ranges in flight per CU, the longer ranges handed to list 6 for this one —
+// measured slower: 19.6 + 25.2 and 37.1 + 19.8 ms against 40.3 ms per 6
+// mapping steps.  The launch is bounded by the few ranges the global levels
+// leave far over PC_TAIL, each stepped depth first by one workgroup.)
+template <int PT_NT, int MAXT, int LIST>
 __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_OCC))) k_pc_tail(unsigned int* K, unsigned int* V, unsigned int* PB, PcLists wl,
                                                     int* ctr, unsigned long long* pst, int* cstat, const int32_t* off,
                                                     int S, int32_t* serr) {
-    __shared__ TailSm sm;
+    constexpr int PT_NW = PT_NT / 64;
+    __shared__ TailSm<PT_NW, MAXT> sm;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     constexpr int INF = 0x7fffffff;
-    const int nw = ctr[PCC_NW + 3];
+    const int nw = ctr[PCC_NW + LIST];
     unsigned long long wact = 0, wpairs = 0;
     // tid 0 pops the next range into sm.f / sm.l / sm.d with its pivot (the
     // median swap taken virtually until the swaps); sm.have is read by every
@@ -729,7 +742,7 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
     };
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         if (tid == 0) {
-            const int2 w = wl.l[3][e];
+            const int2 w = wl.l[LIST][e];
             sm.sf[0] = w.x; sm.sl[0] = w.x + (w.y & 0xffffff); sm.sd[0] = w.y >> 24;
             sm.sp = 1;
             pop();
@@ -739,10 +752,11 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
             const int f = sm.f, l = sm.l, d = sm.d, med = sm.med;
             const unsigned int p = sm.piv, k0 = sm.k0;
             const int b0 = f + 1, nt = (l - b0 + PT_TILE - 1) / PT_TILE;
-            if (d == 0 || nt > PT_MAXT) {   // heapsort (or too long for the tile table): list 4
+            if (d == 0 || nt > MAXT) {   // heapsort: list 4; too long for the tile table: list 6 (or 4)
                 if (tid == 0) {
-                    const int i = atomicAdd(&ctr[PCC_NW + 4], 1);
-                    wl.l[4][i] = make_int2(f, (l - f) | (d << 24));
+                    const int to = d == 0 ? 4 : (MAXT < PT_MAXT ? 6 : 4);
+                    const int i = atomicAdd(&ctr[PCC_NW + to], 1);
+                    wl.l[to][i] = make_int2(f, (l - f) | (d << 24));
                     pop();
                 }
                 __syncthreads();
@@ -1049,7 +1063,7 @@ static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
         SLO_CHECK(hipMalloc(&w.cseg[0], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.cseg[1], sizeof(int) * chcap));
         SLO_CHECK(hipMalloc(&w.ccnt, sizeof(int2) * chcap));
-        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 5 * wcapk)));
+        SLO_CHECK(hipMalloc(&w.wl, sizeof(int2) * (wcap0 + 6 * wcapk)));
         w.wcap0 = wcap0;
         w.wcapk = wcapk;
     }
@@ -1071,7 +1085,7 @@ static int pcl_levels(size_t stride, int tail_min) {
     int g = 0;
     size_t x = (size_t)tail_min;
     while (x < stride) { x <<= 1; ++g; }
-    return g ? g + 3 : 0;
+    return g ? g + PC_XLEV : 0;
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, const VgParams* prm,
@@ -1087,7 +1101,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     const int GX = std::max(1, std::min(maxT, std::max(4, 2048 / S)));
     PcLists L;
     L.l[0] = w.wl;
-    for (int k = 1; k < 6; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
+    for (int k = 1; k < 7; ++k) L.l[k] = w.wl + w.wcap0 + (size_t)(k - 1) * w.wcapk;
     // the pair positions of a step: the left stoppers' (PA) and their partners
     // (PB), in the VoxelGrid workspace's spare halves (2 * items words)
     unsigned int* PA = spare;
@@ -1123,8 +1137,8 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     // a workgroup per entry, grid-stride: enough to fill the chip at the LDS
     // each size class takes (43 / 23 / 5.6 KB per entry)
     const int FG = std::max(256, std::min(8192, S * 16));
-    SLO_LAUNCH(ctx, "pc_tail", k_pc_tail, dim3(std::max(64, std::min(4096, S * 8))), dim3(PT_NT), 0, K, V, PB, L,
-               w.ctr, w.pstat, w.cstat, off, S, w.serr);
+    SLO_LAUNCH(ctx, "pc_tail", (k_pc_tail<512, PT_MAXT, 3>), dim3(std::max(64, std::min(4096, S * 8))), dim3(512), 0,
+               K, V, PB, L, w.ctr, w.pstat, w.cstat, off, S, w.serr);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare);
     // 32-bit items first (lists 2 and 1); the entries too wide for them (list 5) after, on 64-bit items
     if (few) {
