@@ -1081,11 +1081,11 @@ static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
 // ~1.5 log2(n / PC_TAIL) on the configs' clouds); whatever is larger after the
 // G levels is stepped by k_pc_tail like the rest, only with one workgroup.  An
 // empty level still costs its five launches.
-static int pcl_levels(size_t stride, int tail_min) {
+static int pcl_levels(size_t stride, int tail_min, bool few) {
     int g = 0;
     size_t x = (size_t)tail_min;
     while (x < stride) { x <<= 1; ++g; }
-    return g ? g + PC_XLEV : 0;
+    return g ? g + (few ? 3 : PC_XLEV) : 0;   // (a few streams: each level is five launches of latency)
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, const VgParams* prm,
@@ -1117,7 +1117,7 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
                w.ctr, w.nfin, w.pstat, w.serr);
     SLO_LAUNCH(ctx, "pc_write", k_pc_write, dim3(GX, S), dim3(VG_T), 0, src, off, prm, w.tcnt, w.nfin,
                maxT, K, V, S);
-    const int G = pcl_levels(in_stride, tail_min);
+    const int G = pcl_levels(in_stride, tail_min, few);
     for (int lv = 0; lv < G; ++lv) {
         const int cur = lv & 1;
         // the grid-stride kernels take whatever the level holds; past the first
