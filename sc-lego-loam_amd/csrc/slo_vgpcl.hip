@@ -60,8 +60,9 @@ using slo_pcl::u64;
 #endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
 #ifndef PC_XLEV
-#define PC_XLEV 6         // global levels past log2(stride / tail size), for the uneven splits median-of-three leaves:
-                          // 6 against 3 took the tail 39.9 -> 27.1 ms for 2.2 ms more of levels (18.8k -> 19.0k)
+#define PC_XLEV 9         // global levels past log2(stride / tail size), for the uneven splits median-of-three leaves:
+                          // 3 / 6 / 9 / 12: the tail 39.9 / 27.1 / 21.3 / 21.1 ms, the levels 21.0 / 23.3 / 24.9 /
+                          // 26.4 ms per 6 mapping steps; 18.8k / 19.0k / 19.1k / 19.0k scans/s
 #endif
 #ifndef PC_LOCC
 #define PC_LOCC 8         // waves per SIMD k_pc_lrank is built for (latency-bound streaming)
