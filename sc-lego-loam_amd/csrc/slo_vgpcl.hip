@@ -986,35 +986,20 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
 
 // list 4 — a range over PC_T items whose depth budget is spent (std::sort's
 // heapsort; the dense C5 maps send a few hundred per run here): the first
-// wave heapsorts it (slo_pclsort.h wave_heap_sort: one round trip per pop
-// instead of two dependent loads per tree level on one lane), staged in LDS
-// up to PC_FB_LDS items, in global memory beyond.  A range that came here for another reason (over PT_MAXT tiles,
+// wave heapsorts it in global memory (slo_pclsort.h wave_heap_sort: one round
+// trip per pop instead of two dependent loads per tree level on one lane).
+// (Staging ranges of up to 12 Ki items in LDS measured 1 % faster on C5, but
+// its 96 KB of LDS held every launch of the kernel — nearly always empty —
+// until a CU had that much free beside the other contexts' finish kernels:
+// 3 ms per launch in the live trace.)  A range that came here for another reason (over PT_MAXT tiles,
 // a full stack; never seen) is finished by one lane with the sequential
 // restatement.
-#ifndef PC_FB_LDS
-#define PC_FB_LDS 12288   // a heapsorted range of up to this many items is staged in LDS (96 KB)
-#endif
 __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
                                                       int* cstat, u64* scratch) {
-    __shared__ u64 lds[PC_FB_LDS];
     const int nw = ctr[PCC_NW + 4];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl[e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
-        if (d == 0 && n > 16 && n <= PC_FB_LDS) {   // in LDS
-            for (int i = threadIdx.x; i < n; i += 256) lds[i] = ((u64)K[f + i] << 32) | V[f + i];
-            __syncthreads();
-            if (threadIdx.x < 64) slo_pcl::wave_heap_sort(lds, n);
-            if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
-            __syncthreads();
-            for (int i = threadIdx.x; i < n; i += 256) {
-                const u64 it = lds[i];
-                K[f + i] = (unsigned int)(it >> 32);
-                V[f + i] = (unsigned int)it;
-            }
-            __syncthreads();
-            continue;
-        }
         for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
         if (d == 0 && n > 16) {
