@@ -40,7 +40,7 @@ TEMPLATED = {"k_pc_finish32<4096, 4>": "pc_finish_b", "k_pc_finish32<2048, 4>": 
              "k_fa_ring_ds_pcl<2048, 1>": "fa_ring_ds",
              "k_pc_finish<4096, 16>": "pc_finish_bx", "k_pc_finish<2048, 8>": "pc_finish_s",
              "k_fa_ring_ds_pcl<4096>": "fa_ring_ds",
-             "k_pc_tail<256, 256, 3>": "pc_tail", "k_pc_tail<512, 4096, 6>": "pc_tail_l"}
+             "k_pc_tail<512, 4096, 3>": "pc_tail"}
 
 
 def short(kname, names):
