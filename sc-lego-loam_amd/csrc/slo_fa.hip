@@ -909,7 +909,7 @@ __global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
     const float4* in = v.r_lf_scan + rr * C;
     float4* out = v.r_lf_ds + rr * C;
     __shared__ unsigned long long keys[PMAX];
-    __shared__ unsigned short tbl[PMAX];
+    __shared__ unsigned short tbl[PMAX / 2 + 1];
     __shared__ slo_pcl::WaveSmem ws[RW];
     __shared__ slo_pcl::BlockQ<RW> bq;
     __shared__ float mm[RW][6];

@@ -121,7 +121,7 @@ __device__ __forceinline__ unsigned int renc(int f, int l, int d) {
 // f + 1 + 64 r + lane held in R rows of registers.  The median swap is taken
 // virtually while the rows are read (one LDS round trip), m comes from the
 // ballot of the crossing and two lane reads, and the LDS sees the median
-// swap, the right-stopper table (tbl[f + rank]), its reads, the partner reads and
+// swap, the right-stopper table (tbl[f / 2 + rank]), its reads, the partner reads and
 // the swaps.  Returns the cut.
 template <int R, class It>
 __device__ __forceinline__ int wave_step(It* items, unsigned short* tbl, int f, int l) {
@@ -187,13 +187,13 @@ __device__ __forceinline__ int wave_step(It* items, unsigned short* tbl, int f, 
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const int kr = TR - 1 - pr[r];
-        if (iR[r] && kr < m) tbl[f + kr] = (unsigned short)(f + 1 + 64 * r + lane);
+        if (iR[r] && kr < m) tbl[(f >> 1) + kr] = (unsigned short)(f + 1 + 64 * r + lane);
     }
     wave_fence();
     int y[R];
     It py[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) y[r] = (iL[r] && pl[r] < m) ? (int)tbl[f + pl[r]] : -1;
+    for (int r = 0; r < R; ++r) y[r] = (iL[r] && pl[r] < m) ? (int)tbl[(f >> 1) + pl[r]] : -1;
 #pragma unroll
     for (int r = 0; r < R; ++r) py[r] = items[y[r] >= 0 ? y[r] : f];
     wave_fence();
@@ -315,7 +315,7 @@ __device__ __forceinline__ int stream_step(It* items, unsigned short* tbl, int f
                     const int x = b0 + 64 * r + lane;
                     const bool iR = x < l && !(p < kk[u]);
                     const int kr = TR - 1 - (__builtin_amdgcn_readlane(rowR, r) + lane_prefix(__ballot(iR)));
-                    if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
+                    if (iR && kr < m) tbl[(f >> 1) + kr] = (unsigned short)x;
                 }
             }
         }
@@ -341,7 +341,7 @@ __device__ __forceinline__ int stream_step(It* items, unsigned short* tbl, int f
                 }
             }
 #pragma unroll
-            for (int u = 0; u < U; ++u) y[u] = y[u] >= 0 ? (int)tbl[f + y[u]] : -1;
+            for (int u = 0; u < U; ++u) y[u] = y[u] >= 0 ? (int)tbl[(f >> 1) + y[u]] : -1;
 #pragma unroll
             for (int u = 0; u < U; ++u) py[u] = items[y[u] >= 0 ? y[u] : f];
 #pragma unroll
@@ -606,8 +606,10 @@ __device__ __forceinline__ int wave_step_any(It* items, unsigned short* tbl, int
 // Sorts items[f0, l0) (LDS, positions < 8192, l0 - f0 <= 4097) into exactly
 // std::sort's order for a range that the introsort loop reaches with `depth`
 // levels of budget (2 * lg(n) for a whole array).  Called by all 64 lanes of
-// one wave; tbl holds an entry per position (a step writes tbl[f .. f + m),
-// so waves on disjoint ranges share it).  *err (if given) counts ranges
+// one wave; tbl holds an entry per two positions: a step of [f, l) swaps m
+// <= (l - f - 1) / 2 pairs and writes tbl[f / 2 .. f / 2 + m), which ends
+// before (l - 1) / 2 <= the next range's f / 2, so waves on disjoint ranges
+// share it.  *err (if given) counts ranges
 // handed to a lane for a reason other than their size (must stay 0).
 // prof (if given): cycles in [0] streamed steps, [1] register steps, [2] small ranges and heapsorts;
 // [3] items heapsorted (wave_heap_sort)
@@ -820,7 +822,7 @@ __device__ __forceinline__ int group_step(It* items, unsigned short* tbl, int f,
             const int x = b0 + 64 * r + lane;
             const bool iR = x < l && !(p < key_at(items, min(x, l - 1)));
             const int kr = TR - 1 - (bs.rr[r] + lane_prefix(__ballot(iR)));
-            if (iR && kr < m) tbl[f + kr] = (unsigned short)x;
+            if (iR && kr < m) tbl[(f >> 1) + kr] = (unsigned short)x;
         }
     }
     __syncthreads();
@@ -832,7 +834,7 @@ __device__ __forceinline__ int group_step(It* items, unsigned short* tbl, int f,
             const bool iL = x < l && !(vkey(it) < p);
             const int pl = bs.rl[r] + lane_prefix(__ballot(iL));
             if (iL && pl < m) {
-                const int y = tbl[f + pl];
+                const int y = tbl[(f >> 1) + pl];
                 const It py = items[y];
                 items[x] = py;
                 items[y] = it;

@@ -548,7 +548,7 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
                                                        unsigned long long* pst, int* cstat, const int32_t* off,
                                                        int S, int32_t* serr) {
     __shared__ u64 items[NMAX];
-    __shared__ unsigned short tbl[NMAX];
+    __shared__ unsigned short tbl[NMAX / 2 + 1];
     __shared__ slo_pcl::WaveSmem ws[W];
     __shared__ slo_pcl::BlockQ<W> bq;
     __shared__ int ferr;   // the entry's inconsistent steps (slo_pclsort.h guards)
@@ -605,7 +605,8 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
 // the write-back (gathered into the items' LDS slots, written back after a
 // barrier).  A wider entry goes to list 5 (k_pc_finish).
 #ifndef PC_F32_OCC
-#define PC_F32_OCC 5      // waves per SIMD k_pc_finish32 is built for (its LDS allows five 4-wave workgroups per CU)
+#define PC_F32_OCC 6      // waves per SIMD k_pc_finish32 is built for (25 KB of LDS: six 4-wave workgroups per CU;
+                          // pc_finish_b 32.0 -> 31.0 ms per 6 mapping steps against five)
 #endif
 template <int NMAX, int W>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >= 4 ? PC_F32_OCC : 1))) k_pc_finish32(unsigned int* K, unsigned int* V, PcLists wl, int* ctr,
@@ -614,7 +615,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
     constexpr int NT = 64 * W;
     static_assert(NMAX <= (1 << slo_pcl::kPosBits), "positions fit kPosBits");
     __shared__ unsigned int items[NMAX];
-    __shared__ unsigned short tbl[NMAX];
+    __shared__ unsigned short tbl[NMAX / 2 + 1];
     __shared__ slo_pcl::WaveSmem ws[W];
     __shared__ slo_pcl::BlockQ<W> bq;
     __shared__ int ferr;
