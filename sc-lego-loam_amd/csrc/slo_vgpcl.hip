@@ -599,7 +599,7 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
 
 // ---- the same with 32-bit items, for an entry whose keys span less than
 // 2^20: (key - min) << 12 | position in the entry (slo_pclsort.h kPosBits).
-// Half the LDS of the 64-bit items — 29 KB per 4 Ki entry at four waves, five
+// Half the LDS of the 64-bit items — 25 KB per 4 Ki entry at four waves, six
 // workgroups per CU instead of three — and the same comparisons, so the same
 // order.  The point indices stay in global memory and follow their items at
 // the write-back (gathered into the items' LDS slots, written back after a
