@@ -893,6 +893,9 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #ifndef RING_TLANE
 #define RING_TLANE 64
 #endif
+#ifndef RING_OCC
+#define RING_OCC 7          // waves per SIMD of the 4-wave ring VoxelGrid (23 KB of LDS: seven workgroups per CU)
+#endif
 #ifndef SLO_DIAG_RING
 #define SLO_DIAG_RING 0     // 1: k_fa_ring_ds_pcl's sort counters in StreamState::dbg (tools/ring_diag.py; not with SLO_DIAG)
 #endif
@@ -900,7 +903,7 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #define RING_W 4            // waves per ring (170 streams: 1.13 ms per launch against 1.53 with one wave,
 #endif                      // since block_sort's pool); 16 when the context has a few streams
 template <int PMAX, int RW>
-__global__ void __launch_bounds__(64 * RW) k_fa_ring_ds_pcl(DevView v) {
+__global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW == 4 ? RING_OCC : 1))) k_fa_ring_ds_pcl(DevView v) {
     constexpr int NT = 64 * RW;
     const int s = blockIdx.y, ring = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;

@@ -575,7 +575,7 @@ __device__ __forceinline__ void lane_flush(It* items, const unsigned int* q, int
 // are claimed with an LDS counter and filled after; a taker waits for the
 // slot's nonzero entry (an entry always has l >= 2).  Which wave sorts which
 // disjoint range does not change the result.
-constexpr int kPoolCap = 256;
+constexpr int kPoolCap = 128;
 constexpr int kPushT = 128;
 struct Pool {
     unsigned int e[kPoolCap];
