@@ -773,6 +773,7 @@ int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points,
                      double t_scan, void* d_odom_out) {
     if (!ctx || !d_features || !d_points || !d_counts || !d_odom_out) return SLO_E_ARG;
     SLO_CHECK(hipSetDevice(ctx->dev));
+    ctx->odo_stage = true;   // the mapping context computes /integrated_to_init (k_modes_odom)
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     int32_t* cnt;
     const auto feat = slo::modes_features(ctx, &cnt);

@@ -555,6 +555,8 @@ struct slo_ctx {
     float* d_pg_poses = nullptr;
     size_t pg_cap = 0;
     bool mapped_now = false;            // this batch step ran the mapping stage
+    bool odo_stage = false;             // Mode S odometry context (slo_odom_process): its transformFusion
+                                        // output is recomputed by the mapping context, so k_fa_odo_finish skips it
     // the input slot (DevView::io) and the captured steps of slo_batch_process
     // (slo_ctx.hip): step kind (0: no mapping, 1: mapping) x the layout of
     // the odometry ping-pong halves (fa_swap_last)

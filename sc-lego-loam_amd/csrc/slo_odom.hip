@@ -911,7 +911,7 @@ __global__ void __launch_bounds__(256) k_fa_to_end(DevView v) {
 }
 
 // integrate (FA:1697-1725) and the *Last / tree bookkeeping, per stream
-__global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
+__global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v, int fuse) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
     if (st.odo_phase == 3) return;
@@ -926,9 +926,11 @@ __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v) {
         // TransformFusion::laserOdometryHandler (TF:186-219): this scan's
         // odometry through the tf round trip, associated to the map with the
         // last published mapping result (this scan's mapping comes after)
-        float sum[6], incre[6];
-        slo_pose::odom_handoff(st.transformSum, sum);
-        slo_pose::associate_to_map(sum, st.tf_bef, st.tf_aft, incre, st.integrated);
+        if (fuse) {
+            float sum[6], incre[6];
+            slo_pose::odom_handoff(st.transformSum, sum);
+            slo_pose::associate_to_map(sum, st.tf_bef, st.tf_aft, incre, st.integrated);
+        }
         const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;
@@ -964,7 +966,7 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
         }
     }
     SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v);
+    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v, ctx->odo_stage ? 0 : 1);
     const int R = v.cfg.n_scan;
     if (!SLO_SURF_LINEAR)
     {
