@@ -309,7 +309,55 @@ __global__ void __launch_bounds__(256) k_fa_sx_rings(DevView v, int nb) {
     // longer rings: k_fa_sx_long
 }
 
-// rings of more than 512 points (one workgroup each, bitonic sort in LDS)
+// The bitonic network over 64 * NE keys in one wave's registers, for the
+// slice of positions base .. base + 64 NE - 1 of a longer array: each
+// element's direction comes from its position in the whole array (up when
+// (position & size) == 0), so the slices come out sorted in alternating
+// directions, as the network's later stages need.  sx_chunk_sort runs the
+// stages of size 2 .. 64 NE; sx_chunk_merge the strides 32 NE .. 1 of one
+// later stage of size `size`.
+template <int NE>
+__device__ inline void sx_cx(unsigned long long* k, int lane, int base, int size, int stride) {
+    if (stride >= 64) {   // partner in the same lane
+        const int es = stride >> 6;
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            if (e & es) continue;
+            const bool up = ((base + e * 64 + lane) & size) == 0;
+            const unsigned long long x = k[e], y = k[e | es];
+            const bool sw = up ? (x > y) : (x < y);
+            k[e] = sw ? y : x;
+            k[e | es] = sw ? x : y;
+        }
+    } else {              // partner in lane ^ stride
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const unsigned long long y = __shfl_xor(k[e], stride, 64);
+            const bool up = ((base + e * 64 + lane) & size) == 0;
+            const bool take_min = up == ((lane & stride) == 0);
+            k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+        }
+    }
+}
+template <int NE>
+__device__ inline void sx_chunk_sort(unsigned long long* k, int lane, int base) {
+#pragma unroll
+    for (int size = 2; size <= 64 * NE; size <<= 1)
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) sx_cx<NE>(k, lane, base, size, stride);
+}
+template <int NE>
+__device__ inline void sx_chunk_merge(unsigned long long* k, int lane, int base, int size) {
+#pragma unroll
+    for (int stride = 32 * NE; stride > 0; stride >>= 1) sx_cx<NE>(k, lane, base, size, stride);
+}
+
+// rings of more than 512 points, one workgroup of four waves each: every
+// 512-key slice sorted in a wave's registers, then the network's merge stages
+// (size 1024, 2048, 4096) with the strides of 512 and more through LDS and
+// the smaller ones again in registers — five to nine barriers instead of the
+// 66-78 of a bitonic sort in LDS (the (x, index) keys are a total order: any
+// correct sort gives the same result)
 __global__ void __launch_bounds__(256) k_fa_sx_long(DevView v, int nb) {
     int s, r;
     xcd_stream_chunk(blockIdx.x, nb, s, r);
@@ -321,10 +369,43 @@ __global__ void __launch_bounds__(256) k_fa_sx_long(DevView v, int nb) {
     const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
     float4* out = v.sx_surf_next + (size_t)s * v.cap_less_flat;
     __shared__ uint64_t key[SLO_SX_RING_MAX];
-    for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sx_key(in[a + i].x, a + i);
-    int np = 1;
+    constexpr int NE = 8, CH = 64 * NE;   // a wave's slice
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    int np = CH;
     while (np < n) np <<= 1;
-    lds_bitonic(key, n, np);
+    for (int c = wv; c * CH < np; c += 4) {   // the slices, sorted in registers
+        unsigned long long k[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int i = c * CH + e * 64 + lane;
+            k[e] = i < n ? sx_key(in[a + i].x, a + i) : ~0ull;
+        }
+        sx_chunk_sort<NE>(k, lane, c * CH);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) key[c * CH + e * 64 + lane] = k[e];
+    }
+    __syncthreads();
+    for (int size = 2 * CH; size <= np; size <<= 1) {
+        for (int stride = size >> 1; stride >= CH; stride >>= 1) {   // across slices: through LDS
+            for (int i = threadIdx.x; i < np; i += blockDim.x) {
+                const int l = i ^ stride;
+                if (l > i) {
+                    const uint64_t x = key[i], y = key[l];
+                    if ((x > y) == ((i & size) == 0)) { key[i] = y; key[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+        for (int c = wv; c * CH < np; c += 4) {   // within a slice: in registers
+            unsigned long long k[NE];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) k[e] = key[c * CH + e * 64 + lane];
+            sx_chunk_merge<NE>(k, lane, c * CH, size);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) key[c * CH + e * 64 + lane] = k[e];
+        }
+        __syncthreads();
+    }
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int idx = (int)(uint32_t)key[i];
         const float4 p = in[idx];
