@@ -352,6 +352,50 @@ __device__ inline void sx_chunk_merge(unsigned long long* k, int lane, int base,
     for (int stride = 32 * NE; stride > 0; stride >>= 1) sx_cx<NE>(k, lane, base, size, stride);
 }
 
+// key[0, n) in LDS (capacity >= max(512, n rounded up to a power of two))
+// sorted ascending by the workgroup: 512-key slices in the waves' registers,
+// then the merge stages as in k_fa_sx_long
+__device__ inline void lds_slice_sort(uint64_t* key, int n) {
+    constexpr int NE = 8, CH = 64 * NE;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    int np = CH;
+    while (np < n) np <<= 1;
+    __syncthreads();   // the caller's key writes
+    for (int c = wv; c * CH < np; c += nwv) {
+        unsigned long long k[NE];
+#pragma unroll
+        for (int e = 0; e < NE; ++e) {
+            const int i = c * CH + e * 64 + lane;
+            k[e] = i < n ? key[i] : ~0ull;
+        }
+        sx_chunk_sort<NE>(k, lane, c * CH);
+#pragma unroll
+        for (int e = 0; e < NE; ++e) key[c * CH + e * 64 + lane] = k[e];
+    }
+    __syncthreads();
+    for (int size = 2 * CH; size <= np; size <<= 1) {
+        for (int stride = size >> 1; stride >= CH; stride >>= 1) {
+            for (int i = threadIdx.x; i < np; i += blockDim.x) {
+                const int l = i ^ stride;
+                if (l > i) {
+                    const uint64_t x = key[i], y = key[l];
+                    if ((x > y) == ((i & size) == 0)) { key[i] = y; key[l] = x; }
+                }
+            }
+            __syncthreads();
+        }
+        for (int c = wv; c * CH < np; c += nwv) {
+            unsigned long long k[NE];
+#pragma unroll
+            for (int e = 0; e < NE; ++e) k[e] = key[c * CH + e * 64 + lane];
+            sx_chunk_merge<NE>(k, lane, c * CH, size);
+#pragma unroll
+            for (int e = 0; e < NE; ++e) key[c * CH + e * 64 + lane] = k[e];
+        }
+        __syncthreads();
+    }
+}
+
 // rings of more than 512 points, one workgroup of four waves each: every
 // 512-key slice sorted in a wave's registers, then the network's merge stages
 // (size 1024, 2048, 4096) with the strides of 512 and more through LDS and
@@ -425,10 +469,9 @@ __global__ void __launch_bounds__(1024) k_fa_sx_kd(DevView v) {
     const float4* in = v.kd_corner + (size_t)s * v.cap_less_sharp;
     float4* out = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
     __shared__ uint64_t key[NP];
+    static_assert(NP >= 512, "lds_slice_sort pads to 512-key slices");
     for (int i = threadIdx.x; i < n; i += blockDim.x) key[i] = sx_key(in[i].x, i);
-    int np = 1;
-    while (np < n) np <<= 1;
-    lds_bitonic(key, n, np);
+    lds_slice_sort(key, n);
     for (int i = threadIdx.x; i < n; i += blockDim.x) {
         const int idx = (int)(uint32_t)key[i];
         const float4 p = in[idx];
