@@ -167,148 +167,6 @@ __device__ inline void lds_bitonic(uint64_t* key, int n, int np) {
         }
 }
 
-__global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan) {
-    const int s = blockIdx.x;
-    StreamState& st = v.st[s];
-    const int tid = threadIdx.x, T = blockDim.x;
-    const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
-    if (first_scan) {  // checkSystemInitialization (FA:1605-1637): swap, build trees, no odometry
-        const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
-        const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
-        float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
-        float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
-        float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
-        float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
-        for (int i = tid; i < nLS; i += T) { cnext[i] = lsharp[i]; kdc[i] = lsharp[i]; }
-        for (int i = tid; i < nLF; i += T) { snext[i] = lflat[i]; kds[i] = lflat[i]; }
-        copy_ring_offsets(v, s);
-        if (tid == 0) {
-            st.cornerLastNum = nLS; st.surfLastNum = nLF;
-            st.kdCornerNum = nLS; st.kdSurfNum = nLF;
-            st.iters_surf = st.iters_corner = 0;
-            st.odo_phase = 3;
-            st.transformSum[0] += v.imu[s].pitchStart;   // FA:1633-1634
-            st.transformSum[2] += v.imu[s].rollStart;
-        }
-        return;
-    }
-    if (tid == 0) {
-        // updateInitialGuess (FA:1639-1664)
-        ImuState& m = v.imu[s];
-        m.pitchLast = m.pitchCur;
-        m.yawLast = m.yawCur;
-        m.rollLast = m.rollCur;
-        for (int k = 0; k < 3; ++k) {
-            m.shiftFromStart[k] = 0.0f;   // imuShiftFromStart*Cur: never set (no ShiftToStartIMU call)
-            m.veloFromStart[k] = m.veloFromStartCur[k];
-        }
-        float* tcur = st.transformCur;
-        if (m.angFromStart[0] != 0 || m.angFromStart[1] != 0 || m.angFromStart[2] != 0) {
-            tcur[0] = -m.angFromStart[1];
-            tcur[1] = -m.angFromStart[2];
-            tcur[2] = -m.angFromStart[0];
-        }
-        if (m.veloFromStart[0] != 0 || m.veloFromStart[1] != 0 || m.veloFromStart[2] != 0) {
-            tcur[3] -= m.veloFromStart[0] * v.cfg.scan_period;
-            tcur[4] -= m.veloFromStart[1] * v.cfg.scan_period;
-            tcur[5] -= m.veloFromStart[2] * v.cfg.scan_period;
-        }
-        // updateTransformation (FA:1666-1672)
-        st.iters_surf = st.iters_corner = 0;
-        st.odo_phase = (st.cornerLastNum < 10 || st.surfLastNum < 100) ? 2 : 0;
-    }
-    // the sharp points in x order: k_fa_search_corner groups its queries by
-    // it (a grouping only; results do not depend on it)
-    __shared__ uint64_t key[SLO_PERM_MAX];
-    const int ns = st.n_sharp;
-    const float4* sp = v.sharp + (size_t)s * v.cap_sharp;
-    for (int i = tid; i < ns; i += T) key[i] = sx_key(sp[i].x, i);
-    int np = 1;
-    while (np < ns) np <<= 1;
-    lds_bitonic(key, ns, np);
-    for (int i = tid; i < ns; i += T) v.sharp_perm[(size_t)s * v.cap_sharp + i] = (int)(uint32_t)key[i];
-}
-
-// ---------------------------------------------------------------- x-sorted clouds
-// The correspondence searches are nearest-point queries over (a) the whole
-// corner "tree" cloud and (b) single rings of the *Last clouds restricted to
-// index ranges (the reference's ring-ordered walks).  Both run as sweeps over
-// an x-sorted copy: start at the query's x (binary search) and walk outward in
-// both directions until fl((p.x - q.x)^2) exceeds the current bound.  The
-// distance expressions add non-negative squares to that first term, and float
-// subtraction / squaring are monotone, so every point the sweep stops before
-// is strictly farther than the bound: the result (with its tie rule) equals
-// the exhaustive walk's.
-// one wave per (stream, ring), four rings per workgroup: the ring's segment
-// of the cloud becoming surf_last sorted by x — a bitonic network over the
-// segment's 64 * NE (x, index) keys held in registers (lane-local stages in
-// registers, cross-lane stages by shuffles), NE chosen per ring
-template <int NE>
-__device__ inline void sx_sort_wave(const float4* in, float4* out, int a, int n, int lane) {
-    unsigned long long k[NE];
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int i = e * 64 + lane;
-        k[e] = i < n ? sx_key(in[a + i].x, a + i) : ~0ull;
-    }
-    constexpr int N = 64 * NE;
-#pragma unroll
-    for (int size = 2; size <= N; size <<= 1) {
-#pragma unroll
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride >= 64) {   // partner in the same lane
-                const int es = stride >> 6;
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    if (e & es) continue;
-                    const bool up = ((e * 64 + lane) & size) == 0;
-                    const unsigned long long x = k[e], y = k[e | es];
-                    const bool sw = up ? (x > y) : (x < y);
-                    k[e] = sw ? y : x;
-                    k[e | es] = sw ? x : y;
-                }
-            } else {              // partner in lane ^ stride
-#pragma unroll
-                for (int e = 0; e < NE; ++e) {
-                    const unsigned long long y = __shfl_xor(k[e], stride, 64);
-                    const bool up = ((e * 64 + lane) & size) == 0;
-                    const bool take_min = up == ((lane & stride) == 0);
-                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
-                }
-            }
-        }
-    }
-#pragma unroll
-    for (int e = 0; e < NE; ++e) {
-        const int i = e * 64 + lane;
-        if (i < n) {
-            const int idx = (int)(uint32_t)k[e];
-            const float4 p = in[idx];
-            out[a + i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
-        }
-    }
-}
-
-#define SLO_SX_RING_MAX 4096   // >= horizon_scan limit (slo_create): a ring holds <= C points
-__global__ void __launch_bounds__(256) k_fa_sx_rings(DevView v, int nb) {
-    int s, chunk;
-    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
-    if (s >= v.S) return;
-    const int R = v.cfg.n_scan;
-    const int lane = threadIdx.x & 63, r = chunk * 4 + (threadIdx.x >> 6);
-    if (r >= R) return;
-    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
-    const int a = rf[r], n = rf[r + 1] - a;
-    if (n <= 0) return;
-    const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
-    float4* out = v.sx_surf_next + (size_t)s * v.cap_less_flat;
-    if (n <= 64) sx_sort_wave<1>(in, out, a, n, lane);
-    else if (n <= 128) sx_sort_wave<2>(in, out, a, n, lane);
-    else if (n <= 256) sx_sort_wave<4>(in, out, a, n, lane);
-    else if (n <= 512) sx_sort_wave<8>(in, out, a, n, lane);
-    // longer rings: k_fa_sx_long
-}
-
 // The bitonic network over 64 * NE keys in one wave's registers, for the
 // slice of positions base .. base + 64 NE - 1 of a longer array: each
 // element's direction comes from its position in the whole array (up when
@@ -394,6 +252,146 @@ __device__ inline void lds_slice_sort(uint64_t* key, int n) {
         }
         __syncthreads();
     }
+}
+
+__global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan) {
+    const int s = blockIdx.x;
+    StreamState& st = v.st[s];
+    const int tid = threadIdx.x, T = blockDim.x;
+    const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
+    if (first_scan) {  // checkSystemInitialization (FA:1605-1637): swap, build trees, no odometry
+        const float4* lsharp = v.less_sharp + (size_t)s * v.cap_less_sharp;
+        const float4* lflat = v.less_flat + (size_t)s * v.cap_less_flat;
+        float4* cnext = v.corner_next + (size_t)s * v.cap_less_sharp;
+        float4* snext = v.surf_next + (size_t)s * v.cap_less_flat;
+        float4* kdc = v.kd_corner + (size_t)s * v.cap_less_sharp;
+        float4* kds = v.kd_surf + (size_t)s * v.cap_less_flat;
+        for (int i = tid; i < nLS; i += T) { cnext[i] = lsharp[i]; kdc[i] = lsharp[i]; }
+        for (int i = tid; i < nLF; i += T) { snext[i] = lflat[i]; kds[i] = lflat[i]; }
+        copy_ring_offsets(v, s);
+        if (tid == 0) {
+            st.cornerLastNum = nLS; st.surfLastNum = nLF;
+            st.kdCornerNum = nLS; st.kdSurfNum = nLF;
+            st.iters_surf = st.iters_corner = 0;
+            st.odo_phase = 3;
+            st.transformSum[0] += v.imu[s].pitchStart;   // FA:1633-1634
+            st.transformSum[2] += v.imu[s].rollStart;
+        }
+        return;
+    }
+    if (tid == 0) {
+        // updateInitialGuess (FA:1639-1664)
+        ImuState& m = v.imu[s];
+        m.pitchLast = m.pitchCur;
+        m.yawLast = m.yawCur;
+        m.rollLast = m.rollCur;
+        for (int k = 0; k < 3; ++k) {
+            m.shiftFromStart[k] = 0.0f;   // imuShiftFromStart*Cur: never set (no ShiftToStartIMU call)
+            m.veloFromStart[k] = m.veloFromStartCur[k];
+        }
+        float* tcur = st.transformCur;
+        if (m.angFromStart[0] != 0 || m.angFromStart[1] != 0 || m.angFromStart[2] != 0) {
+            tcur[0] = -m.angFromStart[1];
+            tcur[1] = -m.angFromStart[2];
+            tcur[2] = -m.angFromStart[0];
+        }
+        if (m.veloFromStart[0] != 0 || m.veloFromStart[1] != 0 || m.veloFromStart[2] != 0) {
+            tcur[3] -= m.veloFromStart[0] * v.cfg.scan_period;
+            tcur[4] -= m.veloFromStart[1] * v.cfg.scan_period;
+            tcur[5] -= m.veloFromStart[2] * v.cfg.scan_period;
+        }
+        // updateTransformation (FA:1666-1672)
+        st.iters_surf = st.iters_corner = 0;
+        st.odo_phase = (st.cornerLastNum < 10 || st.surfLastNum < 100) ? 2 : 0;
+    }
+    // the sharp points in x order: k_fa_search_corner groups its queries by
+    // it (a grouping only; results do not depend on it)
+    __shared__ uint64_t key[SLO_PERM_MAX];   // (>= 512: lds_slice_sort's slices)
+    const int ns = st.n_sharp;
+    const float4* sp = v.sharp + (size_t)s * v.cap_sharp;
+    for (int i = tid; i < ns; i += T) key[i] = sx_key(sp[i].x, i);
+    lds_slice_sort(key, ns);
+    for (int i = tid; i < ns; i += T) v.sharp_perm[(size_t)s * v.cap_sharp + i] = (int)(uint32_t)key[i];
+}
+
+// ---------------------------------------------------------------- x-sorted clouds
+// The correspondence searches are nearest-point queries over (a) the whole
+// corner "tree" cloud and (b) single rings of the *Last clouds restricted to
+// index ranges (the reference's ring-ordered walks).  Both run as sweeps over
+// an x-sorted copy: start at the query's x (binary search) and walk outward in
+// both directions until fl((p.x - q.x)^2) exceeds the current bound.  The
+// distance expressions add non-negative squares to that first term, and float
+// subtraction / squaring are monotone, so every point the sweep stops before
+// is strictly farther than the bound: the result (with its tie rule) equals
+// the exhaustive walk's.
+// one wave per (stream, ring), four rings per workgroup: the ring's segment
+// of the cloud becoming surf_last sorted by x — a bitonic network over the
+// segment's 64 * NE (x, index) keys held in registers (lane-local stages in
+// registers, cross-lane stages by shuffles), NE chosen per ring
+template <int NE>
+__device__ inline void sx_sort_wave(const float4* in, float4* out, int a, int n, int lane) {
+    unsigned long long k[NE];
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int i = e * 64 + lane;
+        k[e] = i < n ? sx_key(in[a + i].x, a + i) : ~0ull;
+    }
+    constexpr int N = 64 * NE;
+#pragma unroll
+    for (int size = 2; size <= N; size <<= 1) {
+#pragma unroll
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= 64) {   // partner in the same lane
+                const int es = stride >> 6;
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    if (e & es) continue;
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const unsigned long long x = k[e], y = k[e | es];
+                    const bool sw = up ? (x > y) : (x < y);
+                    k[e] = sw ? y : x;
+                    k[e | es] = sw ? x : y;
+                }
+            } else {              // partner in lane ^ stride
+#pragma unroll
+                for (int e = 0; e < NE; ++e) {
+                    const unsigned long long y = __shfl_xor(k[e], stride, 64);
+                    const bool up = ((e * 64 + lane) & size) == 0;
+                    const bool take_min = up == ((lane & stride) == 0);
+                    k[e] = take_min ? (k[e] < y ? k[e] : y) : (k[e] > y ? k[e] : y);
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+        const int i = e * 64 + lane;
+        if (i < n) {
+            const int idx = (int)(uint32_t)k[e];
+            const float4 p = in[idx];
+            out[a + i] = make_float4(p.x, p.y, p.z, __int_as_float(idx));
+        }
+    }
+}
+
+#define SLO_SX_RING_MAX 4096   // >= horizon_scan limit (slo_create): a ring holds <= C points
+__global__ void __launch_bounds__(256) k_fa_sx_rings(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    const int R = v.cfg.n_scan;
+    const int lane = threadIdx.x & 63, r = chunk * 4 + (threadIdx.x >> 6);
+    if (r >= R) return;
+    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
+    const int a = rf[r], n = rf[r + 1] - a;
+    if (n <= 0) return;
+    const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
+    float4* out = v.sx_surf_next + (size_t)s * v.cap_less_flat;
+    if (n <= 64) sx_sort_wave<1>(in, out, a, n, lane);
+    else if (n <= 128) sx_sort_wave<2>(in, out, a, n, lane);
+    else if (n <= 256) sx_sort_wave<4>(in, out, a, n, lane);
+    else if (n <= 512) sx_sort_wave<8>(in, out, a, n, lane);
+    // longer rings: k_fa_sx_long
 }
 
 // rings of more than 512 points, one workgroup of four waves each: every
