@@ -64,9 +64,20 @@ def sc_pair_mfma_flop(nr):
 METRIC = "scans/sec end-to-end (proj+feat+LM+SC), 64-ring 1800-col, 1/2/4/8 GPU"
 
 
-def parse():
+def parse(argv=None):
+    """the command line; `--config c2|c5` stands for that BASELINE config's arguments (EXTRA), so the profiling
+    runs (tools/profile_round.sh) and the config lines measure the same workload"""
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if "--config" in argv:
+        i = argv.index("--config")
+        name = argv[i + 1]
+        argv = argv[:i] + argv[i + 2:] + (EXTRA[name] if name != "c3" else [])
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs of this node: N > 1 starts N ranks (one process per GPU) unless a launcher did")
+    ap.add_argument("--dry-dist", action="store_true",
+                    help="only the rank plumbing on gloo (no GPU): launch, barrier, max-over-ranks, rank 0's JSON line")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help="--dry-dist: this rank exits with 3 (launcher test)")
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--preroll", type=int, default=210,
@@ -110,7 +121,10 @@ def parse():
                     help="launch a torch spin kernel before and after the timed steps, so a rocprofv3 kernel trace of "
                          "the run can be cut to exactly the timed window (tools/trace_window.py)")
     ap.add_argument("--traffic-from", default=None,
-                    help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: newest profiles/r*/summary.json")
+                    help="PMC summary (tools/pmc_summary.py) for roofline.traffic; default: the newest "
+                         "profiles/r*/<--profile-tag>/summary.json")
+    ap.add_argument("--profile-tag", default="c3",
+                    help="the config's profile directory under profiles/rNN/ (c3, c2, c5): roofline.traffic's source")
     ap.add_argument("--sc-k", type=int, default=0, help="Scan Context candidates (NUM_CANDIDATES_FROM_TREE); 0 = preset")
     ap.add_argument("--sc-off", action="store_true", help="loopClosureEnableFlag = false (C2: radius-search local map)")
     ap.add_argument("--map-keyframes", type=int, default=0, help="slo_config.map_keyframes (radius branch); 0 = default")
@@ -120,16 +134,16 @@ def parse():
     ap.add_argument("--extra", default="c2,c5",
                     help="further BASELINE.json configs measured at 1 GPU after the headline, each by its own bench.py "
                          "process, reported under config_lines (outside value); 'none' = none")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 # BASELINE.json configs measured beside the headline (C3) at 1 GPU: bench.py arguments
 EXTRA = {
-    "c2": ["--preset", "os64_1800", "--config-id", "2", "--sc-off", "--streams", "512", "--map-keyframes", "32",
+    "c2": ["--profile-tag", "c2", "--preset", "os64_1800", "--config-id", "2", "--sc-off", "--streams", "512", "--map-keyframes", "32",
            "--keyframe-ring", "128", "--workload",
            "C2 Ouster-64 synthetic 64x1800 stream, segmentation + features + LM, Scan Context off (radius-search "
            "local map, MO:1167-1222), steady state"],
-    "c5": ["--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--keyframe-cap", "65536",
+    "c5": ["--profile-tag", "c5", "--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--keyframe-cap", "65536",
            "--workload",
            "C5 128-ring x 2048-col dense synthetic scan, Scan Context K=50, LM against the ~1M-point raw local "
            "map (HBM-bound stress), steady state"],
@@ -155,8 +169,8 @@ def extra_lines(a):
     out = {}
     for name in [x for x in a.extra.split(",") if x and x != "none"]:
         cmd = [sys.executable, os.path.abspath(__file__), "--extra", "none", "--single-steps", "0", "--icp-jobs", "0",
-               "--steps", "12", "--warmup", "3", "--profile-steps", "4", "--cpu-scans", "4", "--cpu-distinct", "4"] \
-            + EXTRA[name]
+               "--steps", "12", "--warmup", "3", "--profile-steps", "4", "--cpu-scans", "4", "--cpu-distinct", "4",
+               "--config", name]
         t0 = time.time()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -170,22 +184,27 @@ def extra_lines(a):
             continue
         keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_also",
                 "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors", "sort_guards", "dtype",
-                "setup_seconds", "preroll_seconds", "context_hbm_gb")
+                "setup_seconds", "preroll_seconds", "context_hbm_gb", "kernels_ms", "kernels_algo_gbs")
         out[name] = {k: j.get(k) for k in keep}
         out[name]["wall_seconds"] = round(time.time() - t0, 1)
     return out
 
 
+# slo_get "counts" (csrc/slo_ctx.hip): the stream's cloud sizes in one read
+CNT = ("seg_pts", "outlier", "sharp", "less_sharp", "flat", "less_flat", "lf_scan", "corner_last", "surf_last",
+       "kd_corner", "kd_surf", "corner_ds", "surf_total_ds", "map_corner_ds", "map_surf_ds", "raw_ds")
+
+
 def stream_counts(ctx, S):
     """Per-stream sizes of the last step (for algorithmic bytes)."""
-    import numpy as np
-    names = ["flat", "sharp", "surf_last", "corner_last", "seg_pts", "corner_ds", "surf_total_ds",
-             "map_corner_ds", "map_surf_ds"]
-    c = {n: np.array([ctx.get(s, n).shape[0] for s in range(S)], np.int64) for n in names}
+    rows = [ctx.get(s, "counts").astype(np.int64) for s in range(S)]
+    c = {n: np.array([r[i] for r in rows], np.int64) for i, n in enumerate(CNT)}
+    seg = np.diff(np.array([r[len(CNT):] for r in rows], np.int64), axis=1)   # [S][R] less-flat ring segments
+    c["lf_short"] = np.where(seg <= 512, seg, 0).sum(axis=1)   # x-sorted by k_fa_sx_rings (one wave per ring)
+    c["lf_long"] = np.where(seg > 512, seg, 0).sum(axis=1)     # by k_fa_sx_long
     c["fa_iters"] = np.array([ctx.get(s, "fa_iters") for s in range(S)], np.int64)
     c["vg_in"] = np.array([ctx.get(s, "vg_in") for s in range(S)], np.int64)   # [S][7] VoxelGrid items
     c["mo_iters"] = np.array([int(ctx.get(s, "mo_iters")[0]) for s in range(S)], np.int64)
-    c["raw_ds"] = np.array([ctx.get(s, "raw_ds").shape[0] for s in range(S)], np.int64)
     c["map_raw_n"] = np.array([ctx.get(s, "map_raw_n") for s in range(S)], np.int64)   # [S][2] before the VoxelGrids
     c["n_keyframes"] = np.array([int(ctx.get(s, "n_keyframes")[0]) for s in range(S)], np.int64)
     return c
@@ -214,13 +233,48 @@ def path_bytes(c, cfg, history):
 
 def algo_bytes(name, c, cfg, S, steps, map_steps):
     """Algorithmic HBM bytes of ALL launches of `name` in the profiled window
-    (SURVEY §8(d) per-unit figures; points are 16 B).  None = not priced."""
+    (SURVEY §8(d) per-unit figures; points are 16 B; DESIGN.md §4 lists each
+    model).  The per-stream sizes are the last instrumented step's (`c`, from
+    stream_counts); per-scan kernels count `steps` scans of every stream, the
+    mapping step's `map_steps`.  Cumulative device counters (pcl_work, the
+    long-voxel and Scan Context work) are exact deltas over the window.
+    None = not priced (kernels under 1 % of device time in every config)."""
     H = cfg.n_scan * cfg.horizon_scan
     P = cfg.max_points
+    tot = lambda x: int(np.asarray(x).sum())  # noqa: E731
+    per_scan = lambda x: steps * tot(x)        # noqa: E731
+    per_map = lambda x: map_steps * tot(x)     # noqa: E731
+    seg, outl = c["seg_pts"], c["outlier"]
+    # ---- imageProjection (IP:199-460), per scan
+    if name == "ip_init":         # the owner image reset
+        return steps * S * H * 4
     if name == "ip_project":      # read the point, scatter a 4 B owner
         return steps * S * P * (16 + 4)
-    if name == "ip_image":        # owner + point in; range, full cloud, ground, label, CC init out
-        return steps * S * H * (4 + 16 + 4 + 16 + 1 + 4 + 8)
+    if name == "ip_tile":         # per pixel: owner in, its point in (every pixel counted: an upper bound on the
+        # owned ones), range / full cloud / ground / label / parent / csize out
+        return steps * S * H * (4 + 16 + 4 + 16 + 1 + 4 + 4 + 4)
+    if name == "ip_cc_stats":     # per pixel: parent and csize in
+        return steps * S * H * 8
+    if name == "ip_rowcount":     # per pixel: label and ground in, the final label out
+        return steps * S * H * 9
+    if name == "ip_compact":      # per pixel: label, ground, range in; per kept point 25 B out (point, ground
+        # flag, column, range), per outlier 16 B
+        return steps * (S * H * 9) + per_scan(25 * seg + 16 * outl)
+    # ---- featureAssociation (FA:491-784, 1044-1815), per scan
+    if name == "fa_halfpass":     # the segmented point
+        return per_scan(16 * seg)
+    if name == "fa_points":       # point, range, column in; deskewed point, curvature, label, smoothness, picked out
+        return per_scan(seg * (16 + 4 + 4 + 16 + 4 + 4 + 8 + 4))
+    if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
+        return per_scan(seg * (8 + 8 + 4 + 1 + 2))
+    if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
+        return per_scan(seg * (4 + 4 + 4 + 4 + 4 + 2 + 16))
+    if name == "fa_ring_ds":      # FA:779-780: each ring's less-flat points in, their VoxelGrid centroids out
+        return per_scan(16 * c["lf_scan"] + 16 * c["less_flat"])
+    if name == "fa_gather":       # the four feature clouds, per-ring slabs in, concatenated out
+        return per_scan(32 * (c["sharp"] + c["less_sharp"] + c["flat"] + c["less_flat"]))
+    if name == "fa_odo_begin":    # the sharp points in, their x order out
+        return per_scan(20 * c["sharp"])
     srch = lambda it: (it + 4) // 5  # noqa: E731  search iterations actually run
     if name == "fa_search_surf":  # per search: queries + 3 indices, the target cloud once
         return steps * int((srch(c["fa_iters"][:, 0]) * (c["flat"] * 28 + c["surf_last"] * 16)).sum())
@@ -230,22 +284,52 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
         return steps * int((c["fa_iters"][:, 0] * c["flat"] * (16 + 12 + 48)).sum())
     if name == "fa_iter_corner":
         return steps * int((c["fa_iters"][:, 1] * c["sharp"] * (16 + 8 + 32)).sum())
+    if name == "fa_to_end":       # TransformToEnd: less sharp / less flat in, *_next and the tree copies out
+        return per_scan(48 * (c["less_sharp"] + c["less_flat"]))
+    if name == "fa_sx_rings":     # x-sort of the rings of <= 512 less-flat points: point in, (point, index) out
+        return per_scan(32 * c["lf_short"])
+    if name == "fa_sx_long":      # the longer rings
+        return per_scan(32 * c["lf_long"])
+    if name == "fa_sx_kd":        # the corner tree cloud, x-sorted
+        return per_scan(32 * c["kd_corner"])
+    if name == "grid_build_lds":  # the odometry surf grid (T = 2^15 buckets): point in, entry out, offsets out
+        return per_scan(32 * c["kd_surf"]) + steps * S * 4 * ((1 << 15) + 1)
+    # ---- mapOptimization (MO:1122-1522), per mapping step
+    if name == "mo_prepare":      # adjustOutlierCloud (outliers in and out); the radius branch reads the key poses
+        return per_map(32 * outl + (0 if cfg.loop_closure_enable else 24 * c["n_keyframes"]))
+    if name == "mo_assemble":     # the local map's keyframe clouds in (body frame), transformed out
+        return per_map(32 * c["map_raw_n"])
+    if name == "mo_concat":       # surf DS + outlier DS into the surf-total cloud
+        return per_map(32 * c["surf_total_ds"])
+    if name == "grid_count":      # the two map grids: point in, bucket count read-modify-write
+        return per_map(24 * (c["map_corner_ds"] + c["map_surf_ds"]))
+    if name == "grid_scan":       # every bucket's count in, offset out (2^19 + 1 buckets, two grids)
+        return map_steps * S * 2 * ((1 << 19) + 1) * 8
+    if name == "grid_scatter":    # point in, bucket offset in, count read-modify-write, entry out
+        return per_map(44 * (c["map_corner_ds"] + c["map_surf_ds"]))
     if name == "mo_corr":         # per iteration: query + 5 neighbour indices + 5 neighbours
         per = (c["corner_ds"] + c["surf_total_ds"]) * (16 + 20 + 80)
         return map_steps * int((c["mo_iters"] * per).sum())
     if name == "mo_knn":          # per iteration: query + 5 neighbour indices out, the map clouds once
         per = (c["corner_ds"] + c["surf_total_ds"]) * (16 + 20) + (c["map_corner_ds"] + c["map_surf_ds"]) * 16
         return map_steps * int((c["mo_iters"] * per).sum())
-    if name == "vg_scatter":      # the mapping step's 7 VoxelGrid sorts, 4 radix passes each: pass 0 reads the
-        # point (16 B) and writes (key, index) 8 B, passes 1-3 read and write 8 B
-        return map_steps * int(c["vg_in"].sum()) * (16 + 8 + 3 * 16)
-    if name == "vg_onesweep":     # the same four passes as single-pass scatters (the look-back posts are
-        # 256 x 8 B per 4096-item tile, not priced)
-        return map_steps * int(c["vg_in"].sum()) * (16 + 8 + 3 * 16)
+    # ---- the mapping step's batched VoxelGrids (MO:1224-1263)
+    vin = per_map(c["vg_in"]) if "vg_in" in c else 0
+    if name == "vg_bounds":       # every input point once
+        return 16 * vin
+    if name == "vg_heads":        # the sorted keys
+        return 4 * vin
+    if name == "vg_reduce":       # sorted (key, index) in, the point gathered, per item
+        return vin * (8 + 16)
+    if name == "vg_long" and c.get("long_items") is not None:   # long voxels: index + point per item, centroid out
+        return int(20 * c["long_items"] + 16 * c["long_voxels"])
+    if name in ("vg_scatter", "vg_onesweep"):   # the stable radix sort: 4 passes, pass 0 reads the point (16 B)
+        # and writes (key, index) 8 B, passes 1-3 read and write 8 B
+        return vin * (16 + 8 + 3 * 16)
     if name == "vg_ghist":        # every pass's digit counts from one read of the points
-        return map_steps * int(c["vg_in"].sum()) * 16
+        return vin * 16
     if name == "vg_hist":         # pass 0 reads the point, passes 1-3 the 4 B key
-        return map_steps * int(c["vg_in"].sum()) * (16 + 3 * 4)
+        return vin * (16 + 3 * 4)
     pw = c.get("pcl_work")        # PCL-order sort work counters over the instrumented pass (slo_vgpcl.hip PW_*)
     if pw is not None:
         if name == "pc_lcount":   # the keys of every stepped range
@@ -262,37 +346,40 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
             # crossing (4 B) plus the left side's index (4 B); per pair: partner position out and in, both
             # items read and written
             return int(12 * pw[7] + 40 * pw[8])
+        if name == "pc_fallback":   # the spent-depth ranges' items in and out (PW_FALL; std::sort's heapsort)
+            return int(16 * pw[21])
         if name == "pc_count":    # the points
             return int(16 * pw[5])
         if name == "pc_write":    # the points in, (key, index) out
             return int(24 * pw[5])
     if name == "sc_detect" and c.get("sc_pairs") is not None:   # MFMA flop (bound "mfma")
         return int(c["sc_pairs"]) * sc_pair_mfma_flop(cfg.sc_num_ring)
-    if name == "vg_reduce":       # sorted (key, index) in, the point gathered, per item
-        return map_steps * int(c["vg_in"].sum()) * (8 + 16)
-    if name == "fa_sort":         # smoothness in/out, curvature, ground flag, candidate list out
-        return steps * int(c["seg_pts"].sum()) * (8 + 8 + 4 + 1 + 2)
-    if name == "fa_pick":         # picked, label in/out, column, candidates, points of the outputs
-        return steps * int(c["seg_pts"].sum()) * (4 + 4 + 4 + 4 + 4 + 2 + 16)
     return None
 
 
-def pmc_traffic(path, kernel):
+def pmc_traffic(path, kernel, tag=None):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
-    (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, MI355X_MICROARCH.md), or None."""
+    (FETCH_SIZE x2 x1024 + WRITE_SIZE x1024, MI355X_MICROARCH.md), or None.
+    Default source: the newest round's profile of this config
+    (profiles/rNN[a-z]/<tag>/summary.json, tag = c3 / c2 / c5), else the newest
+    round-level profile (profiles/rNN[a-z]/summary.json, C3 only)."""
     import glob
-    import json
-    if path is None:   # the latest round's profile: profiles/rNN[a-z]/
-        import re
-        cands = [((int(m.group(1)), m.group(2)), p)
-                 for p in glob.glob(os.path.join(ROOT, "profiles", "r*", "summary.json"))
-                 for m in [re.search(r"profiles/r(\d+)([a-z]?)/summary\.json$", p)] if m]
-        path = max(cands)[1] if cands else None
+    import re
+    if path is None:
+        pats = ([(os.path.join(ROOT, "profiles", "r*", tag, "summary.json"),
+                  r"profiles/r(\d+)([a-z]?)/" + tag + r"/summary\.json$")] if tag else [])
+        if tag in (None, "c3"):
+            pats.append((os.path.join(ROOT, "profiles", "r*", "summary.json"), r"profiles/r(\d+)([a-z]?)/summary\.json$"))
+        for pat, rx in pats:
+            cands = [((int(m.group(1)), m.group(2)), p) for p in glob.glob(pat) for m in [re.search(rx, p)] if m]
+            if cands:
+                path = max(cands)[1]
+                break
     if path is None or not os.path.exists(path):
         return None, None
     k = json.load(open(path))["kernels"].get(kernel)
     if not k or not k.get("hbm_bytes_per_launch"):
-        return None, None
+        return None, os.path.relpath(path, ROOT)
     return k["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
 
 
@@ -502,14 +589,45 @@ def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=2):
         eng.close()
 
 
+def dry_dist(a, rank, world):
+    """--dry-dist: the multi-rank plumbing alone on gloo (no GPU): every rank
+    takes part in a barrier and the max-over-ranks timing, and rank 0 prints
+    the contract's JSON line with n_gpus = the world size
+    (tests/test_bench_launch.py runs `bench.py --gpus 2 --dry-dist`)"""
+    import torch.distributed as dist
+    from slo_amd import dist as sdist
+    if rank == a.dry_fail_rank:   # the launcher must stop the ranks left waiting for this one
+        sys.exit(3)
+    dist.init_process_group("gloo")
+    try:
+        dist.barrier()
+        el = sdist.max_over_ranks(0.01 * (rank + 1))
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "value": 0.0, "unit": "scans/s", "n_gpus": world, "steps": a.steps,
+                              "warmup": a.warmup, "ms_per_step": round(el * 1e3, 3), "dry_dist": True,
+                              "ranks_seen": world}), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 def main():
     a = parse()
+    from slo_amd import dist as sdist
+    if a.gpus > 1 and "RANK" not in os.environ:
+        # one process per GPU (the driver may also start them itself with
+        # torch.distributed.run): nothing here has touched a GPU yet
+        sys.exit(sdist.launch_ranks(a.gpus, sys.argv[1:], os.path.abspath(__file__)))
+    rank, world, local = sdist.env_rank()
+    if world != a.gpus and not (a.gpus == 1 and a.force_gather):
+        print(f"bench.py: --gpus {a.gpus} but the launcher started {world} rank(s)", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if a.dry_dist:
+        dry_dist(a, rank, world)
+        return
     import torch
     import torch.distributed as dist
     import slo_amd
-    from slo_amd import dist as sdist
 
-    rank, world, local = sdist.env_rank()
     torch.cuda.set_device(local)
     gather = world > 1 or a.force_gather
     if gather:
@@ -653,9 +771,11 @@ def main():
         parts = [stream_counts(c, c.n_streams) for c in ctxs]
         counts = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
         counts["pcl_work"] = sum(c.get(0, "pcl_work").astype(np.int64) - w0 for c, w0 in zip(ctxs, pw0))
-        counts["sc_pairs"] = int(sum(c.get(0, "work").astype(np.int64)[0] - w0[0] for c, w0 in zip(ctxs, wk0)))
+        wk = sum(c.get(0, "work").astype(np.int64) - w0 for c, w0 in zip(ctxs, wk0))
+        counts["sc_pairs"] = int(wk[0])
+        counts["long_items"], counts["long_voxels"] = int(wk[1]), int(wk[2])
         workload = {k: round(float(v.mean()), 1) for k, v in counts.items()
-                    if k not in ("pcl_work", "sc_pairs") and v.ndim == 1}
+                    if k not in ("pcl_work", "sc_pairs", "long_items", "long_voxels") and v.ndim == 1}
     # the largest single kernel by device time (vg_sort:<filter> entries time groups of launches)
     dominant = max(((kn, v) for kn, v in kt.items() if not kn.startswith("vg_sort:")),
                    key=lambda kv: kv[1][0])[0] if kt else None
@@ -743,7 +863,7 @@ def main():
                         "share_of_device_time": round(rms / total_ms, 4) if total_ms else None,
                         "note": "issued MFMA flop (64 x 64 padded Gram, ceil(NR/16) k-steps per Eigen accumulator) "
                                 "per distance pair; the kernel's other work (ring-key K-NN, sector-key alignment) is VALU"}
-            traffic, tsrc = pmc_traffic(a.traffic_from, rk)
+            traffic, tsrc = pmc_traffic(a.traffic_from, rk, a.profile_tag)
             return {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
                     "traffic": traffic, "traffic_source": tsrc, "kernel": rk,

@@ -645,6 +645,18 @@ static int modes_copy(slo_ctx* ctx, const std::vector<ModesSlab>& sl, char* buf,
     }
     return 0;
 }
+// Mode S carries no IMU ring (the deskew of a front context and the
+// initial guess of the odometry context would read rings fed elsewhere), so a
+// context that ingested IMU messages refuses the Mode S entry points, and
+// slo_batch_imu / slo_imu_handler refuse a context Mode S ran on
+int modes_enter(slo_ctx* ctx) {
+    if (ctx->imu_fed) {
+        ctx->err = "Mode S entry point on a context fed IMU messages (Mode S carries no IMU ring)";
+        return SLO_E_STATE;
+    }
+    ctx->modes_used = true;
+    return 0;
+}
 // after imageProjection: the cloud_info tails past this scan's points and, for
 // a scan without a finite point, the orientations come from the carry
 __global__ void k_modes_merge(DevView v, const uint32_t* col, const uint8_t* gnd, const float* rng, const float* orient) {
@@ -684,6 +696,7 @@ int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
                       const void* d_carry_in, void* d_carry_out, void* d_features_out) {
     if (!ctx || !d_points || !d_counts || !d_features_out) return SLO_E_ARG;
     if (ctx->cfg.use_cloud_ring && !ctx->v.rings) { ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings"; return SLO_E_STATE; }
+    if (int r = slo::modes_enter(ctx)) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     if (int r = slo::ip_run(ctx)) return r;
@@ -714,6 +727,7 @@ int slo_front_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
 int slo_back_process(slo_ctx* ctx, const void* d_features, const void* d_points, const int32_t* d_counts,
                      double t_scan) {
     if (!ctx || !d_features || !d_points || !d_counts) return SLO_E_ARG;
+    if (int r = slo::modes_enter(ctx)) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     int32_t* cnt;
@@ -773,7 +787,7 @@ int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points,
                      double t_scan, void* d_odom_out) {
     if (!ctx || !d_features || !d_points || !d_counts || !d_odom_out) return SLO_E_ARG;
     SLO_CHECK(hipSetDevice(ctx->dev));
-    ctx->odo_stage = true;   // the mapping context computes /integrated_to_init (k_modes_odom)
+    if (int r = slo::modes_enter(ctx)) return r;
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     int32_t* cnt;
     const auto feat = slo::modes_features(ctx, &cnt);
@@ -782,7 +796,8 @@ int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points,
     SLO_LAUNCH(ctx, "modes_counts", slo::k_modes_counts, dim3((ctx->S + 255) / 256), dim3(256), 0, ctx->v,
                (int32_t*)((char*)d_features + oc), 0);
     const bool first = !ctx->fa_inited;
-    if (int r = slo::fa_odometry_run(ctx, first)) return r;
+    // transformFusion is the mapping context's (k_modes_odom), in scan order after its mapping step
+    if (int r = slo::fa_odometry_run(ctx, first, false)) return r;
     slo::fa_advance(ctx, first);
     const auto od = slo::modes_odom(ctx);   // after the swap: the clouds just published
     if (int r = slo::modes_copy(ctx, od, (char*)d_odom_out, true, 0, 3)) return r;
@@ -795,6 +810,7 @@ int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points,
 
 int slo_map_process(slo_ctx* ctx, const void* d_odom, const void* d_points, const int32_t* d_counts, double t_scan) {
     if (!ctx || !d_odom || !d_points || !d_counts) return SLO_E_ARG;
+    if (int r = slo::modes_enter(ctx)) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     if (int r = slo::set_io_time(ctx, d_points, d_counts, t_scan, 3)) return r;
     const auto od = slo::modes_odom(ctx);
@@ -953,6 +969,22 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
         const int32_t a[7] = {st.n_corner_map, st.n_surf_map, raw, st.cornerLastNum, st.surfLastNum,
                               st.outlier_count, st.n_st};
         tmp.resize(sizeof(a)); memcpy(tmp.data(), a, sizeof(a)); count = 7; esz = 4;
+    }
+    else if (name == "counts") {   // the stream's cloud sizes in one read (bench.py's algorithmic-byte models):
+        // [0] segmented, [1] outliers, [2] sharp, [3] less sharp, [4] flat, [5] less flat (after the ring
+        // VoxelGrid), [6] less-flat ring points before it (FA:779 input), [7] cornerLast, [8] surfLast,
+        // [9] kd corner, [10] kd surf, [11] corner DS, [12] surf-total DS, [13] map corner DS, [14] map surf
+        // DS, [15] raw DS, [16..16+R] the less-flat ring offsets of the current scan (x-sorts' segments)
+        std::vector<int32_t> lf(R);
+        SLO_CHECK(hipMemcpy(lf.data(), v.r_lf_n + s * R, 4 * R, hipMemcpyDeviceToHost));
+        int32_t lfn = 0;
+        for (size_t i = 0; i < R; ++i) lfn += lf[i];
+        std::vector<int32_t> a{st.seg_count, st.outlier_count, st.n_sharp, st.n_less_sharp, st.n_flat, st.n_less_flat,
+                               lfn, st.cornerLastNum, st.surfLastNum, st.kdCornerNum, st.kdSurfNum, st.n_corner_ds,
+                               st.n_surf_total_ds, st.n_cmap_ds, st.n_smap_ds, st.n_raw_ds};
+        a.resize(16 + R + 1);
+        SLO_CHECK(hipMemcpy(a.data() + 16, v.roff_cur + (s * 2 + 1) * (R + 1), 4 * (R + 1), hipMemcpyDeviceToHost));
+        tmp.resize(4 * a.size()); memcpy(tmp.data(), a.data(), tmp.size()); count = a.size(); esz = 4;
     }
     else if (name == "map_raw_n") {   // laserCloudCornerFromMap / laserCloudSurfFromMap sizes before their VoxelGrids
         int32_t a[2] = {st.n_corner_map, st.n_surf_map}; tmp.resize(8); memcpy(tmp.data(), a, 8); count = 2; esz = 4;

@@ -31,6 +31,16 @@ int imu_init(slo_ctx* ctx) {
     return 0;
 }
 
+// a context Mode S ran on takes no IMU messages (slo_ctx.hip modes_enter)
+int imu_enter(slo_ctx* ctx) {
+    if (ctx->modes_used) {
+        ctx->err = "IMU messages on a context a Mode S entry point ran on (Mode S carries no IMU ring)";
+        return SLO_E_STATE;
+    }
+    ctx->imu_fed = true;
+    return 0;
+}
+
 }  // namespace slo
 
 extern "C" {
@@ -38,6 +48,7 @@ extern "C" {
 int slo_batch_imu(slo_ctx* ctx, const slo_imu_msg* d_msgs, int msgs_per_stream, const int32_t* d_counts) {
     if (!ctx || msgs_per_stream < 0 || (msgs_per_stream > 0 && (!d_msgs || !d_counts))) return SLO_E_ARG;
     if (msgs_per_stream == 0) return SLO_OK;
+    if (int r = slo::imu_enter(ctx)) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     SLO_LAUNCH(ctx, "imu_ingest", slo::k_imu_ingest, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v, d_msgs,
                msgs_per_stream, d_counts);
@@ -48,6 +59,7 @@ int slo_batch_imu(slo_ctx* ctx, const slo_imu_msg* d_msgs, int msgs_per_stream, 
 int slo_imu_handler(slo_ctx* ctx, const slo_imu_msg* msg) {
     if (!ctx || !msg) return SLO_E_ARG;
     if (ctx->S != 1) { ctx->err = "slo_imu_handler needs a context with n_streams == 1"; return SLO_E_STATE; }
+    if (int r = slo::imu_enter(ctx)) return r;
     SLO_CHECK(hipSetDevice(ctx->dev));
     slo_imu_msg* d = nullptr;
     SLO_CHECK(hipMallocAsync((void**)&d, sizeof(slo_imu_msg) + sizeof(int32_t), ctx->stream));

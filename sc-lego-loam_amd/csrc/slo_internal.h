@@ -193,7 +193,8 @@ struct DevView {
     StreamState* st;     // [S]
     ImuState* imu;       // [S] (slo_batch_imu / slo_imu_handler)
     unsigned long long* wctr;   // [8] cumulative work counters (slo_get "work"): [0] Scan Context pairs whose
-                                // distance was evaluated (k_sc_detect; the bench prices sc_detect's MFMA work)
+                                // distance was evaluated (k_sc_detect; the bench prices sc_detect's MFMA work),
+                                // [1] / [2] points / voxels of the VoxelGrids' long voxels (k_vg_long)
     // ---- mapping (mapOptmization.cpp)
     int KFR;             // keyframe cloud ring slots (>= surroundingKeyframeSearchNum + 2)
     int KFMAX;           // keyframe pose / Scan Context history capacity
@@ -555,8 +556,9 @@ struct slo_ctx {
     float* d_pg_poses = nullptr;
     size_t pg_cap = 0;
     bool mapped_now = false;            // this batch step ran the mapping stage
-    bool odo_stage = false;             // Mode S odometry context (slo_odom_process): its transformFusion
-                                        // output is recomputed by the mapping context, so k_fa_odo_finish skips it
+    bool imu_fed = false;               // slo_batch_imu / slo_imu_handler ran on this context
+    bool modes_used = false;            // a Mode S entry point ran on it (Mode S carries no IMU ring: the two
+                                        // refuse each other, SLO_E_STATE)
     // the input slot (DevView::io) and the captured steps of slo_batch_process
     // (slo_ctx.hip): step kind (0: no mapping, 1: mapping) x the layout of
     // the odometry ping-pong halves (fa_swap_last)
@@ -583,7 +585,7 @@ int pg_after_mapping(slo_ctx* ctx);
 int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
-int fa_odometry_run(slo_ctx* ctx, bool first_scan);
+int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse = true);
 void fa_swap_last(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);

@@ -1069,7 +1069,9 @@ void fa_swap_last(slo_ctx* ctx) {
     std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
 }
 
-int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
+// fuse: transformFusion's /integrated_to_init in k_fa_odo_finish (false on a
+// Mode S odometry context, slo_odom_process: the mapping context computes it)
+int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse) {
     DevView& v = ctx->v;
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
@@ -1088,7 +1090,7 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan) {
         }
     }
     SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v, ctx->odo_stage ? 0 : 1);
+    SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v, fuse ? 1 : 0);
     const int R = v.cfg.n_scan;
     if (!SLO_SURF_LINEAR)
     {

@@ -738,7 +738,8 @@ __global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, const unsigned
 // stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
 // intensity chains over them in order.
 __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int* vals, const int32_t* off,
-                                                 const int32_t* meta, const int4* longv, int nlong_cap) {
+                                                 const int32_t* meta, const int4* longv, int nlong_cap,
+                                                 unsigned long long* work) {
     __shared__ float4 buf[4][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nlong = min(meta[2], nlong_cap);
@@ -771,7 +772,11 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int*
         }
         const float sx = __shfl(acc, 0, 64), sy = __shfl(acc, 1, 64), sz = __shfl(acc, 2, 64),
                     si = __shfl(acc, 3, 64);
-        if (lane == 0) vg_store(srcv.out_row(s), r, sx, sy, sz, si, e - a);
+        if (lane == 0) {
+            vg_store(srcv.out_row(s), r, sx, sy, sz, si, e - a);
+            atomicAdd(&work[1], (unsigned long long)(e - a));   // DevView::wctr [1] long-voxel items, [2] voxels
+            atomicAdd(&work[2], 1ull);
+        }
     }
 }
 
@@ -1062,7 +1067,8 @@ int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G) {
                    dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src, v0,
                    w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap);
     }
-    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, v0, w.off, w.meta, w.longv, (int)w.nlong_cap);
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, v0, w.off, w.meta, w.longv, (int)w.nlong_cap,
+               ctx->v.wctr);
     SLO_CHECK(hipGetLastError());
     return 0;
 }

@@ -77,7 +77,8 @@ using slo_pcl::u64;
 // items of the ranges k_pc_tail stepped, [8] pairs it swapped, [9 + 3 list + q]
 // finish cycles of list `list` in streamed steps, register steps, lane tasks
 enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_TAIL = 7, PW_TAIL_PAIRS = 8, PW_PROF = 9,
-       PW_FINX = 20 };   // [20]: items of list 5 (the 4 Ki entries too wide for 32-bit items, k_pc_finish on 64-bit)
+       PW_FINX = 20,     // [20]: items of list 5 (the 4 Ki entries too wide for 32-bit items, k_pc_finish on 64-bit)
+       PW_FALL = 21 };   // [21]: items of the spent-depth ranges k_pc_fallback heapsorts
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
@@ -996,11 +997,12 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
 // a full stack; never seen) is finished by one lane with the sequential
 // restatement.
 __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
-                                                      int* cstat, u64* scratch) {
+                                                      int* cstat, u64* scratch, unsigned long long* pst) {
     const int nw = ctr[PCC_NW + 4];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl[e];
         const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
+        if (threadIdx.x == 0) atomicAdd(&pst[PW_FALL], (unsigned long long)n);
         for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
         if (d == 0 && n > 16) {
@@ -1126,7 +1128,8 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     const int FG = std::max(256, std::min(8192, S * 16));
     SLO_LAUNCH(ctx, "pc_tail", (k_pc_tail<512, PT_MAXT, 3>), dim3(std::max(64, std::min(4096, S * 8))), dim3(512), 0,
                K, V, PB, L, w.ctr, w.pstat, w.cstat, off, S, w.serr);
-    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare);
+    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare,
+               w.pstat);
     // 32-bit items first (lists 2 and 1); the entries too wide for them (list 5) after, on 64-bit items
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,

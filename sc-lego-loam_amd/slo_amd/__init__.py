@@ -45,7 +45,9 @@ _DT["imu"] = np.float64
 _DT["vg_in"] = np.int32
 _DT["vg_stats"] = np.int32
 _DT["pcl_work"] = np.uint64
-_DT["work"] = np.uint64      # DevView::wctr: [0] Scan Context pairs whose distance was evaluated
+_DT["work"] = np.uint64      # DevView::wctr: [0] Scan Context pairs whose distance was evaluated, [1] / [2] long-voxel
+                             # points / voxels (k_vg_long)
+_DT["counts"] = np.int32     # the stream's cloud sizes in one read (slo_get "counts", csrc/slo_ctx.hip)
 
 
 class SloError(RuntimeError):

@@ -14,12 +14,17 @@ the other ranks' (17.8 MB at 8 ranks), on the order of 0.1 ms of ring time on
 xGMI against a ~21 ms step; measured at world size 1 (pack + gather + store
 ingest + query) the exchange costs 0.73 ms per step, mostly the query.
 """
+import os
+import socket
+import subprocess
+import sys
+import time
+
 import torch
 import torch.distributed as dist
 
 
 def env_rank():
-    import os
     return (int(os.environ.get("RANK", "0")), int(os.environ.get("WORLD_SIZE", "1")),
             int(os.environ.get("LOCAL_RANK", "0")))
 
@@ -68,3 +73,51 @@ def max_over_ranks(seconds, device="cpu"):
     t = torch.tensor([float(seconds)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, script, poll_s=0.2):
+    """Run `n` copies of `python script argv` as ranks 0 .. n-1 of one node
+    (one process per GPU: RANK = LOCAL_RANK = r, WORLD_SIZE = n,
+    MASTER_ADDR = 127.0.0.1 and a free MASTER_PORT), the way
+    `torch.distributed.run --nproc-per-node n` would; the children inherit
+    stdout / stderr, so rank 0's output is the command's.  The caller never
+    touches a GPU.  Returns 0 when every rank exits 0; otherwise the first
+    failing rank's exit code, after the other ranks are stopped (their own
+    PIDs, SIGTERM then SIGKILL)."""
+    port = str(free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c if c > 0 else 128 - c
+                print(f"launch_ranks: rank {procs.index(p)} exited with {c}; stopping the others", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    q.terminate()
+                t_end = time.time() + 30
+                for q in live:
+                    try:
+                        q.wait(timeout=max(0.1, t_end - time.time()))
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                        q.wait()
+                live = []
+                break
+        time.sleep(poll_s)
+    return rc

@@ -1,4 +1,4 @@
-"""Mode S: one vehicle's stream over several ranks.
+"""Mode S: one vehicle's stream over several contexts or ranks.
 
 The reference deploys one stream as a pipeline of processes
 (imageProjection | featureAssociation | mapOptimization,
@@ -10,71 +10,67 @@ Per scan two buffers travel (include/slo_abi.h "Mode S"):
 - the carry, from scan k's front rank to scan k+1's: the stale state a front
   end inherits from the previous scan (SURVEY Appendix A Q5);
 - the features, from scan k's front rank to the owner.
+`run_rank3` splits the back end once more, the reference's third process
+boundary: odometry on rank 1, mapping + transformFusion + Scan Context on
+rank 0, a third buffer (the odometry hand-off) between them.
+
+The rank drivers (`run_rank`, `run_rank3`) are written against an engine
+interface that both engines implement:
+- `rank_front(scan, t, carry_in, need_carry)` -> (carry or None, features);
+  carry_in None = the previous scan's front end ran on this engine;
+- `rank_back(features, scan, t)` -> flags; `rank_odometry(features, scan, t)`
+  -> the odometry buffer; `rank_mapping(odom, scan, t)` -> flags;
+- `recv_buffer(tag)` -> a buffer to receive that tag into (None: the
+  transport allocates);
+`SloEngine` here (libslo contexts, device buffers: RCCL moves them between
+GPUs with `DistTransport`, `LocalTransport` between threads of one process)
+and the oracle engine of the CPU rehearsal (tests/mode_engines.py, gloo).
 The owner's poses, keyframes and loop ids are bit-identical to a one-context
-run (tests/test_modes_gloo.py on the oracle, tests/test_gpu_modes.py on the
-GPU).
+run (tests/test_modes_gloo.py, tests/test_gpu_modes.py).
 
 What it can buy is bounded by the owner (Amdahl): the front ends leave the
 owner, the back ends do not, and the carry chain serialises the feature
 extraction of consecutive scans (each waits for the previous scan's carry);
 only imageProjection runs fully in parallel.  DESIGN.md §8 gives the bound
-from the measured stage split.
-
-Engines: `SloEngine` (libslo contexts on one GPU: the front contexts and the
-owner) and `OracleEngine` (the CPU restatement, for the gloo rehearsal).  The
-protocol is the same for both: `run_rank_oracle` over torch.distributed
-point-to-point (gloo), `run_local_slo` with the buffers handed over inside one
-process.
+from the measured stage split and the bytes per scan.
 """
 import numpy as np
 
 
-class OracleEngine:
-    """the oracle's OracleStream.front / back (oracle/oracle_api.cpp), CPU"""
-
-    def __init__(self, cfg, fronts=1, split_back=False):
-        import oracle_py as O
-        self.O = O
-        self.fronts = [O.OracleStream(cfg) for _ in range(fronts)]
-        self.owner = O.OracleStream(cfg)
-        # split_back: odometry on self.odo, mapping on self.owner (OracleStream.odom / mapstage)
-        self.odo = O.OracleStream(cfg) if split_back else None
-
-    def front(self, slot, pts, t, carry):
-        c, f = self.fronts[slot].front(pts, t, carry)
-        return c, f
-
-    def back(self, features, pts, t):
-        if self.odo is not None:
-            return self.mapping(self.odometry(features, t), pts, t)
-        return self.owner.back(features, pts, t)
-
-    def odometry(self, features, t):
-        return self.odo.odom(features, t)
-
-    def mapping(self, odom, pts, t):
-        return self.owner.mapstage(odom, pts, t)
-
-
 class SloEngine:
-    """libslo on one GPU: `fronts` front contexts and one owner context, each
-    one stream (or n_streams vehicles split the same way), buffers as torch
-    uint8 device tensors"""
+    """libslo on one GPU: `fronts` front contexts, an owner context and (with
+    split_back) an odometry context, each one stream (or n_streams vehicles
+    split the same way); buffers are torch uint8 device tensors.  owner=False
+    leaves the owner out (a front-only rank of run_rank3)."""
 
-    def __init__(self, cfg, fronts=1, device=0, n_streams=1, split_back=False):
+    def __init__(self, cfg, fronts=1, device=0, n_streams=1, split_back=False, owner=True, read_flags=True):
         import torch
         import slo_amd
         self.torch = torch
         self.L = slo_amd._abi.lib()
         self.fronts = [slo_amd.Context(cfg, device, n_streams) for _ in range(fronts)]
-        self.owner = slo_amd.Context(cfg, device, n_streams)
+        self.owner = slo_amd.Context(cfg, device, n_streams) if owner else None
         # split_back: the back end on two contexts, odometry (self.odo) and
         # mapping (self.owner, which then holds the results)
         self.odo = slo_amd.Context(cfg, device, n_streams) if split_back else None
-        self.cbytes = int(self.L.slo_modes_carry_bytes(self.owner.h))
-        self.fbytes = int(self.L.slo_modes_features_bytes(self.owner.h))
-        self.obytes = int(self.L.slo_modes_odom_bytes(self.owner.h))
+        any_ctx = next(c for c in self.fronts + [self.owner, self.odo] if c is not None)
+        self.cbytes = int(self.L.slo_modes_carry_bytes(any_ctx.h))
+        self.fbytes = int(self.L.slo_modes_features_bytes(any_ctx.h))
+        self.obytes = int(self.L.slo_modes_odom_bytes(any_ctx.h))
         self.dev = torch.device("cuda", device)
+        self.read_flags = read_flags
+        self._ring = {}
+
+    @classmethod
+    def for_rank(cls, cfg, rank, world, split_back=False, device=0, n_streams=1, read_flags=True):
+        """the contexts rank `rank` of run_rank (split_back False) or
+        run_rank3 (True) needs: every rank of run_rank runs front ends, rank 0
+        also the owner; in run_rank3 rank 0 maps, rank 1 runs the odometry,
+        the others the front ends"""
+        if not split_back:
+            return cls(cfg, fronts=1, device=device, n_streams=n_streams, owner=rank == 0, read_flags=read_flags)
+        return cls(cfg, fronts=1 if rank >= 2 else 0, device=device, n_streams=n_streams, split_back=rank == 1,
+                   owner=rank == 0, read_flags=read_flags)
 
     def buffers(self):
         t = self.torch
@@ -110,9 +106,50 @@ class SloEngine:
         self.owner._ok(self.L.slo_map_process(self.owner.h, odom.data_ptr(), d_points, d_counts, float(t)),
                        "slo_map_process")
 
+    # ---- the rank interface (run_rank / run_rank3); scan = (device points, device counts)
+    def _buf(self, name, nbytes):
+        """two alternating buffers per kind: a buffer handed out for scan k is
+        not written again before scan k + 2 (the drivers drain the sends of
+        each scan before the next)"""
+        pair = self._ring.get(name)
+        if pair is None:
+            pair = self._ring[name] = [[self.torch.empty(nbytes, dtype=self.torch.uint8, device=self.dev) for _ in
+                                        range(2)], 0]
+        b = pair[0][pair[1]]
+        pair[1] ^= 1
+        return b
+
+    def recv_buffer(self, tag):
+        return self._buf(("recv", tag), {TAG_CARRY: self.cbytes, TAG_FEATURES: self.fbytes, TAG_ODOM: self.obytes}[tag])
+
+    def _flags(self):
+        return int(self.owner.get(0, "flags")[0]) if self.read_flags else None
+
+    def rank_front(self, scan, t, carry_in, need_carry):
+        cout = self._buf("carry", self.cbytes) if need_carry else None
+        feat = self._buf("features", self.fbytes)
+        self.front(0, scan[0], scan[1], t, carry_in, cout, feat)
+        return cout, feat
+
+    def rank_back(self, features, scan, t):
+        self.back(features, scan[0], scan[1], t)
+        self.owner.synchronize()   # the features buffer is read before the next recv reuses it
+        return self._flags()
+
+    def rank_odometry(self, features, scan, t):
+        o = self._buf("odom", self.obytes)
+        self.odometry(features, scan[0], scan[1], t, o)
+        return o
+
+    def rank_mapping(self, odom, scan, t):
+        self.mapping(odom, scan[0], scan[1], t)
+        self.owner.synchronize()
+        return self._flags()
+
     def close(self):
-        for c in self.fronts + [self.owner] + ([self.odo] if self.odo is not None else []):
-            c.close()
+        for c in self.fronts + [self.owner, self.odo]:
+            if c is not None:
+                c.close()
 
 
 def front_rank(k, world):
@@ -120,12 +157,13 @@ def front_rank(k, world):
     return k % world
 
 
-TAG_CARRY, TAG_FEATURES, TAG_ODOM = 1, 2, 3   # a front rank sends two of them to one rank in one scan
+TAG_CARRY, TAG_FEATURES, TAG_ODOM = 1, 2, 3
 
 
 class DistTransport:
     """torch.distributed point-to-point (gloo on CPU tensors, RCCL on device
-    tensors); variable-size blobs go as (length, bytes)"""
+    tensors); variable-size blobs go as (length, bytes).  RCCL ignores tags:
+    the drivers order each pair of ranks' messages the same way on both sides."""
 
     def __init__(self):
         import torch
@@ -147,7 +185,11 @@ class DistTransport:
         self.d.recv(n, src, tag=tag)
         x = t.empty(int(n.item()), dtype=t.uint8, device=dev) if like is None else like[:int(n.item())]
         self.d.recv(x, src, tag=tag)
-        return x.numpy() if like is None else x
+        if like is None:
+            return x.numpy()
+        if x.is_cuda:   # the engine's own HIP stream reads it next
+            t.cuda.current_stream(x.device).synchronize()
+        return x
 
     def drain(self):
         for r in self.pending:
@@ -155,30 +197,75 @@ class DistTransport:
         self.pending, self.keep = [], []
 
 
-def run_rank_oracle(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
-    """Mode S on the oracle engine: this rank's part of scans 0 .. n_scans-1.
-    scan_fn(k) -> (points, t).  The owner (rank 0) calls on_back(k, flags)
-    after each back end; returns the owner's flags."""
-    carry = None
+class LocalTransport:
+    """the ranks as threads of one process (one GPU, or CPU engines): one
+    mailbox per (source, destination, tag); a sent buffer is copied, so the
+    sender may reuse it at once.  `boxes` is shared by every rank's transport
+    (LocalTransport.group(world))."""
+
+    def __init__(self, rank, boxes, timeout=300.0):
+        self.rank, self.boxes, self.timeout = rank, boxes, timeout
+
+    @staticmethod
+    def group(world):
+        import queue
+        boxes = {(a, b, g): queue.Queue() for a in range(world) for b in range(world)
+                 for g in (TAG_CARRY, TAG_FEATURES, TAG_ODOM)}
+        return [LocalTransport(r, boxes) for r in range(world)]
+
+    def send(self, x, dst, tag):
+        if isinstance(x, np.ndarray):
+            y = x.copy()
+        else:
+            import torch
+            y = x.clone()
+            if y.is_cuda:
+                torch.cuda.current_stream(y.device).synchronize()
+        self.boxes[(self.rank, dst, tag)].put(y)
+
+    def recv(self, src, tag, like=None):
+        y = self.boxes[(src, self.rank, tag)].get(timeout=self.timeout)
+        if like is None:
+            return y
+        import torch
+        x = like[:y.numel()]
+        x.copy_(y)
+        if x.is_cuda:
+            torch.cuda.current_stream(x.device).synchronize()
+        return x
+
+    def drain(self):
+        pass
+
+
+def run_rank(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
+    """Mode S, this rank's part of scans 0 .. n_scans-1: scan k's front end
+    on rank k % world, every back end on rank 0 (the owner).  scan_fn(k) ->
+    (scan, t), scan in the engine's own form.  The owner calls on_back(k,
+    flags) after each back end; returns the owner's flags.  Per pair of ranks
+    the messages go in one order (features of scan k, then its carry), so a
+    transport without tags (RCCL) pairs them as well as one with (gloo)."""
     flags = []
     for k in range(n_scans):
         f = front_rank(k, world)
-        pts, t = scan_fn(k)
+        scan, t = scan_fn(k)
         feat = None
         if rank == f:
             prev = front_rank(k - 1, world) if k > 0 else None
+            carry_in = None   # the previous scan's front end ran here (its state is this engine's), or none ran
             if prev is not None and prev != rank:
-                carry = transport.recv(prev, TAG_CARRY)
-            carry, feat = engine.front(0, pts, t, carry)
+                carry_in = transport.recv(prev, TAG_CARRY, engine.recv_buffer(TAG_CARRY))
             nxt = front_rank(k + 1, world)
-            if k + 1 < n_scans and nxt != rank:
-                transport.send(carry, nxt, TAG_CARRY)
+            need = k + 1 < n_scans and nxt != rank
+            carry, feat = engine.rank_front(scan, t, carry_in, need)
             if rank != 0:
                 transport.send(feat, 0, TAG_FEATURES)
+            if need:
+                transport.send(carry, nxt, TAG_CARRY)
         if rank == 0:
             if f != 0:
-                feat = transport.recv(f, TAG_FEATURES)
-            fl = engine.back(feat, pts, t)
+                feat = transport.recv(f, TAG_FEATURES, engine.recv_buffer(TAG_FEATURES))
+            fl = engine.rank_back(feat, scan, t)
             flags.append(fl)
             if on_back:
                 on_back(k, fl)
@@ -186,34 +273,35 @@ def run_rank_oracle(engine, rank, world, scan_fn, n_scans, transport, on_back=No
     return flags
 
 
-def run_rank_oracle3(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
+def run_rank3(engine, rank, world, scan_fn, n_scans, transport, on_back=None):
     """Mode S with the back end split over two ranks, the reference's three
     processes (launch/run.launch:14-17) as ranks: rank 0 the mapping stage
     (transformFusion, mapOptimization, Scan Context: the owner), rank 1 the
     odometry, ranks 2 .. world-1 the front ends in turn (world >= 3).  Scan
-    k's features go from its front rank to rank 1, its odometry blob from
-    rank 1 to rank 0.  The engine needs split_back=True on ranks 0 and 1.
-    Returns the owner's flags (rank 0), as run_rank_oracle."""
+    k's features go from its front rank to rank 1, its odometry buffer from
+    rank 1 to rank 0.  Returns the owner's flags (rank 0), as run_rank."""
     assert world >= 3, "a front rank, the odometry rank and the owner"
     nf = world - 2
-    carry = None
     flags = []
     for k in range(n_scans):
         f = 2 + k % nf
-        pts, t = scan_fn(k)
+        scan, t = scan_fn(k)
         if rank == f:
             prev = 2 + (k - 1) % nf if k > 0 else None
+            carry_in = None
             if prev is not None and prev != rank:
-                carry = transport.recv(prev, TAG_CARRY)
-            carry, feat = engine.front(0, pts, t, carry)
+                carry_in = transport.recv(prev, TAG_CARRY, engine.recv_buffer(TAG_CARRY))
             nxt = 2 + (k + 1) % nf
-            if k + 1 < n_scans and nxt != rank:
-                transport.send(carry, nxt, TAG_CARRY)
+            need = k + 1 < n_scans and nxt != rank
+            carry, feat = engine.rank_front(scan, t, carry_in, need)
             transport.send(feat, 1, TAG_FEATURES)
+            if need:
+                transport.send(carry, nxt, TAG_CARRY)
         elif rank == 1:
-            transport.send(engine.odometry(transport.recv(f, TAG_FEATURES), t), 0, TAG_ODOM)
+            feat = transport.recv(f, TAG_FEATURES, engine.recv_buffer(TAG_FEATURES))
+            transport.send(engine.rank_odometry(feat, scan, t), 0, TAG_ODOM)
         elif rank == 0:
-            fl = engine.mapping(transport.recv(1, TAG_ODOM), pts, t)
+            fl = engine.rank_mapping(transport.recv(1, TAG_ODOM, engine.recv_buffer(TAG_ODOM)), scan, t)
             flags.append(fl)
             if on_back:
                 on_back(k, fl)
@@ -261,6 +349,9 @@ def run_pipelined_slo(engine, world, d_scans, d_counts, times, depth=3, on_back=
         try:
             for k in range(n):
                 slot = free.get()
+                if slot is None:   # the owner stopped
+                    ready.put(None)
+                    return
                 t0 = time.perf_counter()
                 cin = carry[(k + 1) & 1] if (k > 0 and world > 1) else None
                 engine.front(k % world, d_scans[k], d_counts, times[k], cin, carry[k & 1], feats[slot])
@@ -286,6 +377,9 @@ def run_pipelined_slo(engine, world, d_scans, d_counts, times, depth=3, on_back=
             free.put(slot)
             if on_back:
                 on_back(k)
+    except BaseException:
+        free.put(None)   # a front thread waiting for a slot stops instead of waiting forever
+        raise
     finally:
         th.join()
     if err:

@@ -149,3 +149,163 @@ def test_mode_s_three_stage_pipeline_matches_one_context():
     finally:
         eng.close()
         one.close()
+
+
+@pytest.mark.parametrize("world,split,preset,config,scans", [
+    (1, False, 0, 1, 80),    # world 1: the owner runs every front end itself, nothing travels
+    (3, False, 6, 3, 40),    # three ranks: carry from rank to rank, features to the owner
+    (4, True, 6, 3, 40),     # the three processes as ranks: mapping 0, odometry 1, front ends 2 and 3
+])
+def test_rank_drivers_match_one_context(world, split, preset, config, scans):
+    """the multi-GPU drivers (modes.run_rank / run_rank3, the ones the gloo
+    rehearsal runs on the oracle) with SloEngine ranks as threads of one
+    process on one GPU, the buffers moved by modes.LocalTransport: the
+    owner's poses, key poses, descriptors and detects equal a one-context run
+    bit for bit at every scan"""
+    import threading
+    torch = _torch()
+    cfg = slo_amd.preset(preset)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(preset, config, 0, 1)
+    buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    one = slo_amd.Context(cfg, 0, 1)
+    engs = [modes.SloEngine.for_rank(cfg, r, world, split_back=split) for r in range(world)]
+    tr = modes.LocalTransport.group(world)
+    run = modes.run_rank3 if split else modes.run_rank
+    bad, errs, out = [], [], {}
+
+    def check(k, fl):
+        one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        ref = int(one.get(0, "flags")[0])
+        if ref != fl:
+            bad.append((k, "flags", ref, fl))
+        names = ["transform_sum", "integrated", "err"] + (["mapped", "keyposes"] if ref & 2 else []) + \
+                (["sc_desc", "ring_key"] if ref & 4 else []) + (["detect", "detect_f"] if ref & 8 else [])
+        for name in names:
+            a, b = one.get(0, name), engs[0].owner.get(0, name)
+            if a.shape != b.shape or not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+                bad.append((k, name))
+
+    def go(r):
+        try:
+            out[r] = run(engs[r], r, world, lambda k: ((buf[k].data_ptr(), cnt.data_ptr()), 0.1 * k), scans, tr[r],
+                         on_back=check if r == 0 else None)
+        except BaseException as e:   # noqa: BLE001
+            errs.append((r, e))
+            for q in tr:   # unblock the others: their receives time out
+                q.timeout = 1.0
+
+    try:
+        ths = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+        assert not errs, errs
+        assert bad == [], bad[:5]
+        assert len(out[0]) == scans
+    finally:
+        for e in engs:
+            e.close()
+        one.close()
+
+
+def test_mode_s_three_streams_ragged_matches_one_context():
+    """n_streams vehicles split the same way: a context of three
+    streams with different point counts (so each stream's carry tail past its
+    own seg_count differs), front ends over two front contexts, every stream
+    against a three-stream one-context run bit for bit"""
+    torch = _torch()
+    preset, config, scans, S = 6, 3, 30, 3
+    cfg = slo_amd.preset(preset)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(preset, config, 0, S)
+    buf = torch.empty((scans, S, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.tensor([P, P - 20011, P // 2 + 7], dtype=torch.int32, device="cuda")
+    one = slo_amd.Context(cfg, 0, S)
+    eng = modes.SloEngine(cfg, fronts=2, n_streams=S)
+    bad = []
+    try:
+        def check(k):
+            one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            for s in range(S):
+                fl = int(one.get(s, "flags")[0])
+                names = ["transform_sum", "integrated", "err", "flags"] + (["mapped", "keyposes"] if fl & 2 else [])
+                for name in names:
+                    a, b = one.get(s, name), eng.owner.get(s, name)
+                    if a.shape != b.shape or not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+                        bad.append((k, s, name))
+
+        modes.run_local_slo(eng, 2, [buf[k].data_ptr() for k in range(scans)], cnt.data_ptr(),
+                            [0.1 * k for k in range(scans)], on_back=check)
+        assert bad == [], bad[:5]
+        assert len({int(one.get(s, "seg_pts").shape[0]) for s in range(S)}) == S   # the streams differ
+    finally:
+        eng.close()
+        one.close()
+
+
+def test_pipelined_raises_when_the_back_end_fails():
+    """run_pipelined_slo with a back end that raises: the error
+    surfaces instead of the front thread waiting for a free slot forever"""
+    torch = _torch()
+    cfg = slo_amd.preset(0)
+    P = cfg.max_points
+    scans = 12
+    gen = slo_amd.DeviceGenerator(0, 1, 0, 1)
+    buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    eng = modes.SloEngine(cfg, fronts=1)
+    try:
+        def boom(k):
+            if k == 1:
+                raise RuntimeError("back end failed")
+
+        with pytest.raises(RuntimeError, match="back end failed"):
+            modes.run_pipelined_slo(eng, 1, [buf[k].data_ptr() for k in range(scans)], cnt.data_ptr(),
+                                    [0.1 * k for k in range(scans)], depth=2, on_back=boom)
+    finally:
+        eng.close()
+
+
+def test_mode_s_and_imu_refuse_each_other():
+    """Mode S carries no IMU ring: a context fed IMU messages
+    refuses slo_front_process / slo_back_process (SLO_E_STATE, with the
+    reason in the error text), and a context Mode S ran on refuses IMU
+    messages — instead of odometry that silently differs from one context"""
+    torch = _torch()
+    from slo_amd import _abi
+    cfg = slo_amd.preset(0)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(0, 1, 0, 1)
+    buf = torch.empty((1, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, 1, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    msg = np.zeros(1, _abi.IMU_DTYPE)
+    eng = modes.SloEngine(cfg, fronts=1)
+    try:
+        eng.fronts[0].imu_handler(msg)   # fed IMU: Mode S refused
+        c, f = eng.buffers()
+        with pytest.raises(slo_amd.SloError, match="IMU"):
+            eng.front(0, buf[0].data_ptr(), cnt.data_ptr(), 0.0, None, c, f)
+        # the owner ran Mode S: IMU refused
+        g = eng.buffers()[1]
+        eng2 = modes.SloEngine(cfg, fronts=1)
+        try:
+            eng2.front(0, buf[0].data_ptr(), cnt.data_ptr(), 0.0, None, None, g)
+            eng2.back(g, buf[0].data_ptr(), cnt.data_ptr(), 0.0)
+            for ctx in (eng2.fronts[0], eng2.owner):
+                with pytest.raises(slo_amd.SloError, match="IMU"):
+                    ctx.imu_handler(msg)
+        finally:
+            eng2.close()
+    finally:
+        eng.close()

@@ -4,7 +4,8 @@ on rank 0, the carry and the features sent point to point.  The restatement
 runs the compute (oracle OracleStream.front / back), so this checks the
 protocol — what travels, in which order — against a one-process run of the
 same stream: odometry and mapped poses, keyframes and Scan Context detects
-bit for bit at every scan.  tests/test_gpu_modes.py checks libslo's own
+bit for bit at every scan.  The rank drivers are the product's
+(modes.run_rank / run_rank3); the oracle engine is tests/mode_engines.py.  tests/test_gpu_modes.py checks libslo's own
 front / back split the same way on the GPU."""
 import os
 import socket
@@ -15,6 +16,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 import oracle_py as O
+from mode_engines import OracleEngine
 from slo_amd import modes
 
 PID, CID, N = 0, 1, 220   # C1 VLP-16; >= 51 keyframes by the end, so Scan Context detects run
@@ -35,7 +37,7 @@ def _worker(rank, world, port, q, split=False):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         cfg = O.preset(PID)
-        eng = modes.OracleEngine(cfg, split_back=split)
+        eng = OracleEngine(cfg, split_back=split)
         ref = O.OracleStream(cfg) if rank == 0 else None
         bad, detects, kf = [], 0, 0
 
@@ -54,7 +56,7 @@ def _worker(rank, world, port, q, split=False):
             detects += int(bool(fr & 8))
             kf = len(ref.get("keyposes")) // 6
 
-        run = modes.run_rank_oracle3 if split else modes.run_rank_oracle
+        run = modes.run_rank3 if split else modes.run_rank
         run(eng, rank, world, _scan, N, modes.DistTransport(), on_back=check if rank == 0 else None)
         q.put((rank, bad, detects, kf))
     finally:
@@ -63,7 +65,7 @@ def _worker(rank, world, port, q, split=False):
 
 @pytest.mark.parametrize("world,split", [(2, False), (3, False), (3, True), (4, True)])
 def test_mode_s_owner_matches_one_process(world, split):
-    """split: the reference's three processes as ranks (modes.run_rank_oracle3:
+    """split: the reference's three processes as ranks (modes.run_rank3:
     mapping on rank 0, odometry on rank 1, front ends on the rest)"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -84,7 +86,7 @@ def test_split_back_end_matches_one_object():
     """OracleStream.odom / mapstage on two objects equal back() on one: flags,
     odometry, fused and mapped poses, keyframes at every scan (C1, 120 scans)"""
     cfg = O.preset(PID)
-    one, two = modes.OracleEngine(cfg), modes.OracleEngine(cfg, split_back=True)
+    one, two = OracleEngine(cfg), OracleEngine(cfg, split_back=True)
     for k in range(120):
         pts, t = _scan(k)
         _, f = one.front(0, pts, t, None)
@@ -104,7 +106,7 @@ def test_carry_is_the_one_object_state():
     scans, measured with and without the carry — so the carry buys
     exactness in the Q5 corner cases, not a visible difference here.)"""
     cfg = O.preset(PID)
-    one, two = modes.OracleEngine(cfg, fronts=1), modes.OracleEngine(cfg, fronts=2)
+    one, two = OracleEngine(cfg, fronts=1), OracleEngine(cfg, fronts=2)
     c = None
     for k in range(5):   # front object 1 first sees another stream
         c, _ = two.fronts[1].front(O.gen_scan(PID, CID, 7, k), 0.1 * k, c)
@@ -115,3 +117,35 @@ def test_carry_is_the_one_object_state():
         c2, f2 = two.front(k % 2, pts, t, c2)
         assert np.array_equal(c1, c2), k
         assert np.array_equal(f1, f2), k
+
+
+@pytest.mark.parametrize("world,split", [(2, False), (4, True)])
+def test_mode_s_threads_local_transport(world, split):
+    """the same drivers with the ranks as threads of one process
+    (modes.LocalTransport), the form tests/test_gpu_modes.py runs on one GPU"""
+    import threading
+    cfg = O.preset(PID)
+    n = 60
+    tr = modes.LocalTransport.group(world)
+    engs = [OracleEngine(cfg, split_back=split) for _ in range(world)]
+    run = modes.run_rank3 if split else modes.run_rank
+    out, errs = {}, []
+
+    def go(r):
+        try:
+            out[r] = run(engs[r], r, world, _scan, n, tr[r])
+        except BaseException as e:   # noqa: BLE001
+            errs.append(e)
+
+    ths = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    assert not errs, errs
+    ref = O.OracleStream(cfg)
+    for k in range(n):
+        pts, t = _scan(k)
+        assert ref.step(pts, t) == out[0][k], k
+    for name in ("transform_sum", "integrated", "mapped", "keyposes"):
+        assert np.array_equal(ref.get(name).view(np.uint8), engs[0].owner.get(name).view(np.uint8)), name

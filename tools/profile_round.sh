@@ -21,7 +21,7 @@ OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 SHORT="--cpu-scans 0 --single-steps 0 --steps 12 --profile-steps 0 --icp-jobs 0 --extra none --trace-marker $*"
-PMC_KERNELS=${PMC_KERNELS:-"spin|sleep|k_pc_|k_mo_knn|k_mo_corr|k_vg_|k_fa_ring_ds|k_fa_search|k_fa_sort|k_fa_sx|k_ip_tile|k_grid"}
+PMC_KERNELS=${PMC_KERNELS:-"spin|sleep|k_"}   # every libslo kernel (the config lines price each one ≥ 1 %)
 
 # run "$@" under its own limit ($LIM s), printing a line every 30 s; returns its status
 hb() {
