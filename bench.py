@@ -131,7 +131,7 @@ def parse(argv=None):
     ap.add_argument("--keyframe-ring", type=int, default=0, help="slo_config.keyframe_ring; 0 = default")
     ap.add_argument("--workload", default="C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 "
                                           "K=10, steady state")
-    ap.add_argument("--extra", default="c2,c5",
+    ap.add_argument("--extra", default="c2,c5,c4",
                     help="further BASELINE.json configs measured at 1 GPU after the headline, each by its own bench.py "
                          "process, reported under config_lines (outside value); 'none' = none")
     return ap.parse_args(argv)
@@ -143,6 +143,10 @@ EXTRA = {
            "--keyframe-ring", "128", "--workload",
            "C2 Ouster-64 synthetic 64x1800 stream, segmentation + features + LM, Scan Context off (radius-search "
            "local map, MO:1167-1222), steady state"],
+    "c4": ["--profile-tag", "c4", "--preset", "os1_64", "--config-id", "4", "--streams", "512", "--force-gather",
+           "--workload",
+           "C4 Ouster OS1-64 64x1024 streams (MulRan-shaped), full pipeline + Scan Context K=10, per-step RCCL "
+           "all-gather of the pose / SC-key records into the cross-stream store (1 GPU, one-rank group), steady state"],
     "c5": ["--profile-tag", "c5", "--preset", "dense128", "--config-id", "5", "--sc-k", "50", "--streams", "128", "--keyframe-cap", "65536",
            "--workload",
            "C5 128-ring x 2048-col dense synthetic scan, Scan Context K=50, LM against the ~1M-point raw local "

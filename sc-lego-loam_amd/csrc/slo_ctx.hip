@@ -310,7 +310,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // slo_vg.hip); the sparse corner cloud is searched by brute force.
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << SLO_MAP_TLOG2, v.cap_mc, SLO_MAP_CELL) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << SLO_MAP_TLOG2, v.cap_ms, SLO_MAP_CELL) ||
-        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL)) {
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL) || slo::map_ws_presize(ctx)) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }

@@ -1001,11 +1001,21 @@ __global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW
     }
 #endif
     if (tid == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
-    // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan
+    // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan;
+    // the chunk's points are gathered into registers first, every load in
+    // flight at once (only a voxel running past the chunk's end loads more)
+    constexpr int CHM = (PMAX + NT - 1) / NT;   // the longest chunk
     const int chunk = (n + NT - 1) / NT;
     const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
+    float4 q[CHM];
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) q[u] = in[(unsigned int)keys[min(i0 + u, n - 1)]];
     int heads = 0;
-    for (int i = i0; i < i1; ++i) heads += (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32));
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) {
+        const int i = i0 + u;
+        heads += i < i1 && (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32));
+    }
     int incl = heads;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -1020,18 +1030,33 @@ __global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW
         total += wsum[w];
     }
     int rank = before + incl - heads;
-    for (int i = i0; i < i1; ++i) {   // each voxel that starts in the chunk, summed in the sorted order
-        if (!(i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32))) continue;
-        const unsigned int vid = (unsigned int)(keys[i] >> 32);
-        float sx = 0, sy = 0, sz = 0, si = 0;
-        int e = i;
-        while (e < n && (unsigned int)(keys[e] >> 32) == vid) {
+    // each voxel that starts in the chunk, summed in the sorted order (PCL's
+    // in-order float chains); items before the chunk's first head belong to
+    // the previous chunk's last voxel
+    float sx = 0, sy = 0, sz = 0, si = 0;
+    int cnt = 0;
+    bool open = false;
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) {
+        const int i = i0 + u;
+        if (i < i1) {
+            if (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32)) {
+                if (open) out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
+                sx = sy = sz = si = 0;
+                cnt = 0;
+                open = true;
+            }
+            if (open) { sx += q[u].x; sy += q[u].y; sz += q[u].z; si += q[u].w; ++cnt; }
+        }
+    }
+    if (open) {   // the chunk's last voxel, possibly running on past it
+        const unsigned int vid = (unsigned int)(keys[i1 - 1] >> 32);
+        for (int e = i1; e < n && (unsigned int)(keys[e] >> 32) == vid; ++e) {
             const float4 p = in[(unsigned int)keys[e]];
             sx += p.x; sy += p.y; sz += p.z; si += p.w;
-            ++e;
+            ++cnt;
         }
-        const float cnt = (float)(e - i);
-        out[rank++] = make_float4(sx / cnt, sy / cnt, sz / cnt, si / cnt);
+        out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
     }
     if (tid == 0) v.ring_cnt[rr * 4 + 3] = total;
 #undef RING_STAMP

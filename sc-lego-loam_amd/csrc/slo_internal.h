@@ -600,6 +600,10 @@ GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx);
+int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces, at creation (slo_map.hip)
+struct VgGroup;
+int vg_presize(slo_ctx* ctx, const VgGroup* groups, int G);
+int pcl_presize(slo_ctx* ctx, int SV, size_t items, size_t maxT);
 void graphs_drop(slo_ctx* ctx);
 int imu_init(slo_ctx* ctx);
 int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n, int n_stride, int n_streams);

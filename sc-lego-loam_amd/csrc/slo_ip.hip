@@ -176,10 +176,36 @@ __device__ inline int find_root(int* par, int x) {
     while (y != x) { x = y; y = ld_parent(par, x); }
     return x;
 }
+// find_root with path halving above the first hop: every node passed on the
+// way up is relinked to its grandparent, so the next find over the same chain
+// is half as long.  A component spanning many tiles otherwise leaves a chain
+// of tile-local roots, one per tile (k_cc_merge links each tile's root under
+// its neighbour's), that every find walks in full: 64 dependent loads on a
+// 2048-column scan.  Only roots and tile-local roots are relinked — a
+// pixel's own parent stays its tile-local root (k_cc_stats relies on it) —
+// and only ever to an ancestor, by a CAS from the parent it read, so
+// concurrent finds, the CAS links of unite and k_cc_stats' final stores of
+// the root (which a stale relink must not overwrite: k_ip_rowcount reads a
+// pixel's root two hops up) stay correct; the roots (smallest index of each
+// component) are the same as without it.
+__device__ inline void st_parent(int* a, int x, int expect, int v) { atomicCAS(&a[x], expect, v); }
+__device__ inline int find_root_h(int* par, int x) {
+    int y = ld_parent(par, x);
+    if (y == x) return x;
+    x = y;   // the tile-local root (or a root): halving starts here
+    for (;;) {
+        y = ld_parent(par, x);
+        if (y == x) return x;
+        const int z = ld_parent(par, y);
+        if (z == y) return y;
+        st_parent(par, x, y, z);
+        x = z;
+    }
+}
 __device__ inline void unite(int* par, int a, int b) {
     while (true) {
-        a = find_root(par, a);
-        b = find_root(par, b);
+        a = find_root_h(par, a);
+        b = find_root_h(par, b);
         if (a == b) return;
         if (a < b) { int t = a; a = b; b = t; }
         int old = atomicCAS(&par[a], a, b);
@@ -338,7 +364,7 @@ __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
         if (par[p] >= 0) {
             code = IP_NOT_ROOT;
             if (v.csize[base + p] & IP_LROOT) {
-                const int fr = find_root(par, p);
+                const int fr = find_root_h(par, p);
                 const int k = atomicAdd(&n_slots, 1);
                 code = IP_OVERFLOW;
                 if (k < IP_STAT_SLOTS) { code = (uint16_t)k; l_fr[k] = fr; l_lr[k] = p; }
@@ -364,7 +390,7 @@ __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
             atomicAdd(&l_cnt[k], 1);
             if (p != l_fr[k]) atomicOr(&l_rows[k][i >> 6], bit);
         } else {
-            const int fr = find_root(par, lr == l ? p : par[p]);
+            const int fr = find_root_h(par, lr == l ? p : par[p]);
             atomicAdd(&v.csize[base + fr], 1);
             if (p != fr) atomicOr(&v.crows[2 * (base + fr) + (i >> 6)], bit);
         }

@@ -950,6 +950,59 @@ __device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nr
     if (threadIdx.x == 0) { st.sc_count = kfid + 1; st.sc_wrote = 1; }
 }
 
+// The mapping step's six VoxelGrid filters (MO:1224-1263) as one batched
+// call's groups.  One call sorts S * (sum of the six strides) items; item
+// positions are 32-bit, so a context whose sum passes INT32_MAX runs them as
+// two calls (the local maps, then the current scan's four): map_vg_split.
+static void map_groups(slo_ctx* ctx, VgGroup gs[6]) {
+    DevView& v = ctx->v;
+    const int SS = ST_STRIDE;
+    StreamState* st0 = v.st;
+    auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
+    const VgGroup g[6] = {
+        {v.map_c, (size_t)v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner, v.map_c_ds,
+         (size_t)v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc},
+        {v.map_s, (size_t)v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf, v.map_s_ds,
+         (size_t)v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms},
+        {nullptr, (size_t)v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, (size_t)v.P,
+         fld(&StreamState::n_raw_ds), SS, v.P},
+        {v.corner_last, (size_t)v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS, v.cfg.leaf_corner,
+         v.cur_c_ds, (size_t)v.cap_less_sharp, fld(&StreamState::n_corner_ds), SS, v.cap_less_sharp},
+        {v.surf_last, (size_t)v.cap_less_flat, fld(&StreamState::surfLastNum), SS, v.cfg.leaf_surf, v.cur_s_ds,
+         (size_t)v.H, fld(&StreamState::n_surf_ds), SS, v.H},
+        {v.outl_cam, (size_t)v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier, v.cur_o_ds,
+         (size_t)v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko}};
+    for (int k = 0; k < 6; ++k) gs[k] = g[k];
+}
+static bool map_vg_split(slo_ctx* ctx, const VgGroup gs[6]) {
+    size_t items = 0;
+    for (int k = 0; k < 6; ++k) items += (size_t)ctx->S * gs[k].stride;
+    return items > (size_t)INT32_MAX;
+}
+static VgGroup map_total_group(slo_ctx* ctx) {
+    DevView& v = ctx->v;
+    StreamState* st0 = v.st;
+    return {v.cur_st, (size_t)v.cap_st, &st0->n_st, ST_STRIDE, v.cfg.leaf_surf, v.cur_st_ds, (size_t)v.cap_st,
+            &st0->n_surf_total_ds, ST_STRIDE, v.cap_st};
+}
+
+// Every workspace a mapping step's VoxelGrids and sorts will use, allocated
+// at context creation from the capacities (the sizes depend on the strides
+// alone), so no step allocates: an out-of-memory shows at slo_create, and a
+// captured step graph's pointers never move.
+int map_ws_presize(slo_ctx* ctx) {
+    VgGroup gs[6];
+    map_groups(ctx, gs);
+    int r;
+    if (map_vg_split(ctx, gs)) {
+        if ((r = vg_presize(ctx, gs, 2)) || (r = vg_presize(ctx, gs + 2, 4))) return r;
+    } else if ((r = vg_presize(ctx, gs, 6))) {
+        return r;
+    }
+    const VgGroup t = map_total_group(ctx);
+    return vg_presize(ctx, &t, 1);
+}
+
 int map_run(slo_ctx* ctx) {
     DevView& v = ctx->v;
     const int S = ctx->S;
@@ -967,20 +1020,13 @@ int map_run(slo_ctx* ctx) {
 #endif
     const bool fork = !SLO_MAP_BATCHED_VG && S <= SLO_VG_FORK_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
     if (SLO_MAP_BATCHED_VG) {
-        const VgGroup gs[6] = {
-            {v.map_c, (size_t)v.cap_mc, fld(&StreamState::n_corner_map), SS, v.cfg.leaf_corner, v.map_c_ds,
-             (size_t)v.cap_mc, fld(&StreamState::n_cmap_ds), SS, v.cap_mc},
-            {v.map_s, (size_t)v.cap_ms, fld(&StreamState::n_surf_map), SS, v.cfg.leaf_surf, v.map_s_ds,
-             (size_t)v.cap_ms, fld(&StreamState::n_smap_ds), SS, v.cap_ms},
-            {nullptr, (size_t)v.P, nullptr, 1, v.cfg.leaf_sc, v.cur_raw_ds, (size_t)v.P,
-             fld(&StreamState::n_raw_ds), SS, v.P},
-            {v.corner_last, (size_t)v.cap_less_sharp, fld(&StreamState::cornerLastNum), SS, v.cfg.leaf_corner,
-             v.cur_c_ds, (size_t)v.cap_less_sharp, fld(&StreamState::n_corner_ds), SS, v.cap_less_sharp},
-            {v.surf_last, (size_t)v.cap_less_flat, fld(&StreamState::surfLastNum), SS, v.cfg.leaf_surf, v.cur_s_ds,
-             (size_t)v.H, fld(&StreamState::n_surf_ds), SS, v.H},
-            {v.outl_cam, (size_t)v.H, fld(&StreamState::outlier_count), SS, v.cfg.leaf_outlier, v.cur_o_ds,
-             (size_t)v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko}};
-        if ((r = vg_run_groups(ctx, "map_step", gs, 6))) return r;
+        VgGroup gs[6];
+        map_groups(ctx, gs);
+        if (map_vg_split(ctx, gs)) {   // over 2^31 items in one call: the local maps, then the rest
+            if ((r = vg_run_groups(ctx, "map_step", gs, 2)) || (r = vg_run_groups(ctx, "map_step", gs + 2, 4))) return r;
+        } else if ((r = vg_run_groups(ctx, "map_step", gs, 6))) {
+            return r;
+        }
     } else {
     // (round 3's form: one call per filter; with a few streams the two
     // local-map filters run on a side stream while the current scan's run here)
@@ -1013,8 +1059,10 @@ int map_run(slo_ctx* ctx) {
     if (fork) SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));   // k_mo_concat's map_ok reads the map DS sizes
     }
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
-    if ((r = vg_run(ctx, "surf_total", v.cur_st, v.cap_st, fld(&StreamState::n_st), SS, v.cfg.leaf_surf, v.cur_st_ds,
-                    v.cap_st, fld(&StreamState::n_surf_total_ds), SS, v.cap_st))) return r;
+    {
+        const VgGroup t = map_total_group(ctx);
+        if ((r = vg_run_groups(ctx, "surf_total", &t, 1))) return r;
+    }
     if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(1024), 0, v);
     // hash grids over the DS maps (on the side stream when forked, above)
     if (!fork && (r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;

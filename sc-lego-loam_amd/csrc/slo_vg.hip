@@ -734,49 +734,69 @@ __global__ void __launch_bounds__(VG_T) k_vg_centroid(VgSrc srcv, const unsigned
     }
 }
 
-// Long voxels, one wave each (persistent grid over the list): the wave
-// stages 256 points at a time in LDS and lanes 0..3 run the x, y, z and
-// intensity chains over them in order.
+// Long voxels, one wave each (persistent grid over the list).  The wave
+// gathers 256 points at a time into LDS — the next chunk's index and point
+// loads are issued before the current chunk is summed (two LDS buffers per
+// wave), so the gathers' latency hides behind the chains — and lanes 0..3 run
+// the x, y, z and intensity chains over the chunk in order, eight LDS values
+// loaded ahead of each eight dependent adds.  (A wave's LDS operations run in
+// program order, so one buffer per wave serves both chunks.)  The sum is
+// PCL's in-order float chain (CentroidPoint), exactly.
+#define VG_LONG_G 1024   // workgroups of k_vg_long (4 waves each, 16 KB of LDS)
 __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int* vals, const int32_t* off,
                                                  const int32_t* meta, const int4* longv, int nlong_cap,
                                                  unsigned long long* work) {
     __shared__ float4 buf[4][256];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nlong = min(meta[2], nlong_cap);
-    float4* b = buf[w];
+    unsigned long long witems = 0, wvox = 0;   // this wave's work, added to DevView::wctr once at the end
     for (int t = blockIdx.x * 4 + w; t < nlong; t += gridDim.x * 4) {
         const int4 L = longv[t];
         const int s = L.x, a = L.y, r = L.z, e = L.w;
         const unsigned int* v = vals + off[s];
         const float4* src = srcv.row(s);
         float acc = 0.0f;
+        // a chunk of 256 items from c0: its indices, then its points, all loads in flight
+        auto gather = [&](int c0, float4& p0, float4& p1, float4& p2, float4& p3) {
+            const int mg = min(256, e - c0);
+            const unsigned int i0 = v[c0 + min(lane, mg - 1)], i1 = v[c0 + min(64 + lane, mg - 1)],
+                               i2 = v[c0 + min(128 + lane, mg - 1)], i3 = v[c0 + min(192 + lane, mg - 1)];
+            p0 = src[i0]; p1 = src[i1]; p2 = src[i2]; p3 = src[i3];
+        };
+        float4 p0, p1, p2, p3;
+        gather(a, p0, p1, p2, p3);
+        float4* b = buf[w];
         for (int c0 = a; c0 < e; c0 += 256) {
             const int m = min(256, e - c0);
-            unsigned int ix[4];
-            float4 pt[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) ix[u] = v[c0 + min(u * 64 + lane, m - 1)];   // all loads in flight
-#pragma unroll
-            for (int u = 0; u < 4; ++u) pt[u] = src[ix[u]];
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (u * 64 + lane < m) b[u * 64 + lane] = pt[u];
+            if (lane < m) b[lane] = p0;
+            if (64 + lane < m) b[64 + lane] = p1;
+            if (128 + lane < m) b[128 + lane] = p2;
+            if (192 + lane < m) b[192 + lane] = p3;
             __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
             __builtin_amdgcn_wave_barrier();
+            if (c0 + 256 < e) gather(c0 + 256, p0, p1, p2, p3);   // the next chunk's loads, in flight during the chains
             if (lane < 4) {
                 const float* f = reinterpret_cast<const float*>(b) + lane;
-                for (int q = 0; q < m; ++q) acc += f[4 * q];
+                int q = 0;
+                for (; q + 8 <= m; q += 8) {
+                    const float x0 = f[4 * q], x1 = f[4 * q + 4], x2 = f[4 * q + 8], x3 = f[4 * q + 12],
+                                x4 = f[4 * q + 16], x5 = f[4 * q + 20], x6 = f[4 * q + 24], x7 = f[4 * q + 28];
+                    acc += x0; acc += x1; acc += x2; acc += x3; acc += x4; acc += x5; acc += x6; acc += x7;
+                }
+                for (; q < m; ++q) acc += f[4 * q];
             }
-            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");   // this wave's LDS traffic drained
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
             __builtin_amdgcn_wave_barrier();
         }
         const float sx = __shfl(acc, 0, 64), sy = __shfl(acc, 1, 64), sz = __shfl(acc, 2, 64),
                     si = __shfl(acc, 3, 64);
-        if (lane == 0) {
-            vg_store(srcv.out_row(s), r, sx, sy, sz, si, e - a);
-            atomicAdd(&work[1], (unsigned long long)(e - a));   // DevView::wctr [1] long-voxel items, [2] voxels
-            atomicAdd(&work[2], 1ull);
-        }
+        if (lane == 0) vg_store(srcv.out_row(s), r, sx, sy, sz, si, e - a);
+        witems += (unsigned long long)(e - a);
+        ++wvox;
+    }
+    if (lane == 0 && wvox) {   // DevView::wctr [1] long-voxel items, [2] voxels (one atomic per wave: a
+        atomicAdd(&work[1], witems);   // device-scope atomic per voxel on one address serialises)
+        atomicAdd(&work[2], wvox);
     }
 }
 
@@ -1067,9 +1087,25 @@ int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G) {
                    dim3(std::max(1, std::min(64, (int)((out_cap + VG_T - 1) / VG_T))), S), dim3(VG_T), 0, src, v0,
                    w.off, w.nvox, starts, ends, w.meta, w.longv, (int)w.nlong_cap);
     }
-    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(256), dim3(256), 0, src, v0, w.off, w.meta, w.longv, (int)w.nlong_cap,
+    SLO_LAUNCH(ctx, "vg_long", k_vg_long, dim3(VG_LONG_G), dim3(256), 0, src, v0, w.off, w.meta, w.longv, (int)w.nlong_cap,
                ctx->v.wctr);
     SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+// The workspaces a vg_run_groups call over these groups needs, allocated now
+// (sizes from the strides alone; map_ws_presize at context creation)
+int vg_presize(slo_ctx* ctx, const VgGroup* groups, int G) {
+    if (G < 1 || G > VG_MAXG) { ctx->err = "vg_presize: 1..VG_MAXG filters"; return SLO_E_ARG; }
+    VgSrc src;
+    src.io = ctx->v.io;
+    src.S = ctx->S;
+    src.G = G;
+    for (int g = 0; g < VG_MAXG; ++g) src.g[g] = groups[std::min(g, G - 1)];
+    const VgShape h = vg_shape(src);
+    if (int r = ensure_ws(ctx, h.items, (size_t)h.SV * h.maxT)) return r;
+    if (ctx->cfg.voxel_order == SLO_VOXEL_PCL && h.items <= (size_t)INT32_MAX)
+        return pcl_presize(ctx, h.SV, h.items, (size_t)h.maxT);
     return 0;
 }
 

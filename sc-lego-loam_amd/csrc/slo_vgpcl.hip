@@ -1065,6 +1065,8 @@ static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
     return 0;
 }
 
+int pcl_presize(slo_ctx* ctx, int SV, size_t items, size_t maxT) { return pcl_ws(ctx, SV, items, maxT); }
+
 // global levels for ranges of up to `stride` items: enough that what is left
 // is mostly at most PC_TAIL items (median-of-three quicksort's depth runs to
 // ~1.5 log2(n / PC_TAIL) on the configs' clouds); whatever is larger after the

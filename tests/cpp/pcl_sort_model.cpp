@@ -18,9 +18,10 @@
 //
 //   pcl_sort_model <points.f32 file> <leaf> [T]   -> stats + "OK" / "MISMATCH"
 //   pcl_sort_model --random <seed> <n> <nkeys>   -> same, random keys
-//   pcl_sort_model --killer <n> <out.u32>        -> writes n keys that drive
+//   pcl_sort_model --killer <n> <out.u32> [div] -> writes n keys that drive
 //       libstdc++'s introsort into its depth limit (heapsort), by McIlroy's
-//       "killer adversary" run against the host std::sort, then checks them
+//       "killer adversary" run against the host std::sort, then checks them;
+//       with div, every key divided by div (ties inside the heapsort)
 #include <stdio.h>
 #include <stdlib.h>
 #include <stdint.h>
@@ -129,6 +130,8 @@ int main(int argc, char** argv) {
     if (argc >= 4 && !strcmp(argv[1], "--killer")) {
         const int n = atoi(argv[2]);
         std::vector<unsigned int> k = killer(n);
+        if (argc >= 5)
+            for (auto& x : k) x /= (unsigned)std::max(1, atoi(argv[4]));
         FILE* fo = fopen(argv[3], "wb");
         if (!fo) return 2;
         fwrite(k.data(), 4, k.size(), fo);

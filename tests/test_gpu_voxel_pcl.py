@@ -38,9 +38,10 @@ def model(tmp_path_factory):
     return exe
 
 
-def killer_keys(model, n, tmp):
-    out = tmp / f"killer{n}.u32"
-    r = subprocess.run([str(model), "--killer", str(n), str(out)], capture_output=True, text=True)
+def killer_keys(model, n, tmp, div=1):
+    out = tmp / f"killer{n}_{div}.u32"
+    r = subprocess.run([str(model), "--killer", str(n), str(out)] + ([str(div)] if div > 1 else []),
+                       capture_output=True, text=True)
     assert r.returncode == 0 and "heapsorts=1" in r.stdout and "OK" in r.stdout, r.stdout
     return np.fromfile(out, np.uint32)
 
@@ -246,3 +247,25 @@ def test_stable_order_switch():
     big = big[np.isfinite(big[:, :3]).all(1)]
     got, _ = run_batch([big], 0.3, voxel_order=1)
     assert mismatch(got[0], O.voxel_grid(big, 0.3, stable=True)) == 0
+
+
+def test_spent_depth_heapsort_paths(model, tmp_path):
+    """k_pc_fallback (slo_vgpcl.hip): spent-depth ranges over 4 Ki items,
+    heapsorted by one wave in global memory — a 12 000-item killer, a
+    7 000-item killer with its keys spread x97 (a key span over 2^18) and the
+    100 000-item killer, several ranges in one call (each workgroup's scratch
+    slots must stay its own range's) — each bit for bit against std::sort's
+    order.  Every killer key is halved, so the heaps hold pairs of equal keys
+    (two points of one voxel) whose order the heapsort decides."""
+    rng = np.random.default_rng(14)
+    k12 = killer_keys(model, 12000, tmp_path, 2)
+    k7 = killer_keys(model, 7000, tmp_path, 2) * np.uint32(97)
+    k100 = killer_keys(model, 100000, tmp_path, 2)
+    assert int(k7.max() - k7.min()) >= (1 << 18) and int(k12.max() - k12.min()) < (1 << 18)
+    clouds = [cloud_from_keys(k, rng) for k in (k12, k7, k100)]
+    got, stats = run_batch(clouds, 1.0)
+    for s, c in enumerate(clouds):
+        want = O.voxel_grid(c, 1.0, stable=False)
+        assert len(got[s]) == len(want) and mismatch(got[s], want) == 0, s
+    assert stats[0] >= 3, stats.tolist()   # each stream sent its spent range to the fallback
+    assert stats[2] == 0 and stats[3] == 0 and stats[4] == 0, stats.tolist()

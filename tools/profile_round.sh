@@ -63,7 +63,7 @@ LIM=600 hb rocprofv3 --pmc FETCH_SIZE --kernel-include-regex "$PMC_KERNELS" --ou
 echo "[profile] WRITE_SIZE"
 LIM=600 hb rocprofv3 --pmc WRITE_SIZE --kernel-include-regex "$PMC_KERNELS" --output-format csv \
     -d "$OUT/pmc_write" -o pmc -- python3 bench.py $SHORT > "$OUT/pmc_write.log" 2>&1
-python3 tools/pmc_summary.py "$OUT" "$OUT/summary" > "$OUT/summary.txt"
+python3 tools/pmc_summary.py "$OUT" "$OUT" > "$OUT/summary.txt"
 rm -rf "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/kt"
 head -30 "$OUT/summary.txt"
 echo "[profile] SQ"
