@@ -902,6 +902,110 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #ifndef RING_W
 #define RING_W 4            // waves per ring (170 streams: 1.13 ms per launch against 1.53 with one wave,
 #endif                      // since block_sort's pool); 16 when the context has a few streams
+// the ring VoxelGrid after its bounds (k_fa_ring_ds_pcl): the items into
+// LDS, std::sort's order (slo_pcl::block_sort), the voxel heads and the
+// centroids.  It: 64-bit (voxel << 32 | point) or 32-bit (voxel << 12 |
+// point) items.  Returns the voxel count.
+struct RingVg {
+    const float4* in;
+    float4* out;
+    int n;
+    float inv;
+    int minbx, minby, minbz, mul1, mul2, tid, lane, wv;
+};
+__device__ inline unsigned long long ring_item(unsigned long long, unsigned int idx, int i) {
+    return ((unsigned long long)idx << 32) | (unsigned int)i;
+}
+__device__ inline unsigned int ring_item(unsigned int, unsigned int idx, int i) {
+    return (idx << slo_pcl::kPosBits) | (unsigned int)i;
+}
+__device__ inline unsigned int ring_point(unsigned long long it) { return (unsigned int)it; }
+__device__ inline unsigned int ring_point(unsigned int it) { return it & ((1u << slo_pcl::kPosBits) - 1u); }
+template <int PMAX, int RW, class It>
+__device__ __forceinline__ int ring_vg_tail(const RingVg& g, It* keys, unsigned short* tbl, slo_pcl::WaveSmem* ws,
+                                            slo_pcl::BlockQ<RW>& bq, int* serr, long long* rp, int* wsum) {
+    constexpr int NT = 64 * RW;
+    const int n = g.n, tid = g.tid, lane = g.lane, wv = g.wv;
+    const float4* in = g.in;
+    float4* out = g.out;
+    const float inv = g.inv;
+    for (int b = 0; b < n; b += 8 * NT) {
+        float4 pp[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * NT + tid, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int i = b + u * NT + tid;
+            const int ijk0 = (int)(floorf(pp[u].x * inv) - (float)g.minbx);
+            const int ijk1 = (int)(floorf(pp[u].y * inv) - (float)g.minby);
+            const int ijk2 = (int)(floorf(pp[u].z * inv) - (float)g.minbz);
+            const unsigned int idx = (unsigned int)(ijk0 + ijk1 * g.mul1 + ijk2 * g.mul2);
+            if (i < n) keys[i] = ring_item(It(0), idx, i);
+        }
+    }
+    __syncthreads();
+    slo_pcl::block_sort<RING_TLANE, RW>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, serr, rp);
+    // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan;
+    // the chunk's points are gathered into registers first, every load in
+    // flight at once (only a voxel running past the chunk's end loads more)
+    constexpr int CHM = (PMAX + NT - 1) / NT;   // the longest chunk
+    const int chunk = (n + NT - 1) / NT;
+    const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
+    auto key = [&](int i) { return slo_pcl::vkey(keys[i]); };
+    float4 q[CHM];
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) q[u] = in[ring_point(keys[min(i0 + u, n - 1)])];
+    int heads = 0;
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) {
+        const int i = i0 + u;
+        heads += i < i1 && (i == 0 || key(i) != key(i - 1));
+    }
+    int incl = heads;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < RW; ++w) {
+        if (w < wv) before += wsum[w];
+        total += wsum[w];
+    }
+    int rank = before + incl - heads;
+    // each voxel that starts in the chunk, summed in the sorted order (PCL's
+    // in-order float chains); items before the chunk's first head belong to
+    // the previous chunk's last voxel
+    float sx = 0, sy = 0, sz = 0, si = 0;
+    int cnt = 0;
+    bool open = false;
+#pragma unroll
+    for (int u = 0; u < CHM; ++u) {
+        const int i = i0 + u;
+        if (i < i1) {
+            if (i == 0 || key(i) != key(i - 1)) {
+                if (open) out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
+                sx = sy = sz = si = 0;
+                cnt = 0;
+                open = true;
+            }
+            if (open) { sx += q[u].x; sy += q[u].y; sz += q[u].z; si += q[u].w; ++cnt; }
+        }
+    }
+    if (open) {   // the chunk's last voxel, possibly running on past it
+        const unsigned int vid = key(i1 - 1);
+        for (int e = i1; e < n && key(e) == vid; ++e) {
+            const float4 p = in[ring_point(keys[e])];
+            sx += p.x; sy += p.y; sz += p.z; si += p.w;
+            ++cnt;
+        }
+        out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
+    }
+    return total;
+}
+
 template <int PMAX, int RW>
 __global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW == 4 ? RING_OCC : 1))) k_fa_ring_ds_pcl(DevView v) {
     constexpr int NT = 64 * RW;
@@ -967,97 +1071,25 @@ __global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW
         return;
     }
     const int minbx = (int)floorf(mnx * inv), minby = (int)floorf(mny * inv), minbz = (int)floorf(mnz * inv);
-    const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv);
+    const int maxbx = (int)floorf(mxx * inv), maxby = (int)floorf(mxy * inv), maxbz = (int)floorf(mxz * inv);
     const int divx = maxbx - minbx + 1, divy = maxby - minby + 1;
     const int mul1 = divx, mul2 = divx * divy;
-    for (int b = 0; b < n; b += 8 * NT) {
-        float4 pp[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) pp[u] = in[min(b + u * NT + tid, n - 1)];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int i = b + u * NT + tid;
-            const int ijk0 = (int)(floorf(pp[u].x * inv) - (float)minbx);
-            const int ijk1 = (int)(floorf(pp[u].y * inv) - (float)minby);
-            const int ijk2 = (int)(floorf(pp[u].z * inv) - (float)minbz);
-            const unsigned int idx = (unsigned int)(ijk0 + ijk1 * mul1 + ijk2 * mul2);
-            if (i < n) keys[i] = ((unsigned long long)idx << 32) | (unsigned int)i;
-        }
-    }
-    __syncthreads();
-#if SLO_DIAG_RING
-    t_r = clock64();
-#endif
-    slo_pcl::block_sort<RING_TLANE, RW>(keys, n, 2 * slo_pcl::lg2(n), tbl, ws, bq, &serr, rp);
-#if SLO_DIAG_RING
-    if (tid == 0) atomicMax(&v.st[s].dbg[1], clock64() - t_r);
-#endif
-    RING_STAMP(0)
+    // 32-bit items (voxel << 12 | point) when every voxel index of the ring's
+    // box fits 20 bits (the near rings; the sort's LDS traffic and registers
+    // halve), else 64-bit (voxel << 32 | point): the same comparisons, so the
+    // same std::sort order
+    const RingVg g{in, out, n, inv, minbx, minby, minbz, mul1, mul2, tid, lane, wv};
+    int total;
+    if ((long long)divx * divy * ((long long)maxbz - minbz + 1) <= (1LL << 20))
+        total = ring_vg_tail<PMAX, RW>(g, reinterpret_cast<unsigned int*>(keys), tbl, ws, bq, &serr, rp, wsum);
+    else
+        total = ring_vg_tail<PMAX, RW>(g, keys, tbl, ws, bq, &serr, rp, wsum);
 #if SLO_DIAG_RING
     if (tid == 0) {   // thread 0's phases of block_sort
         for (int k = 4; k < 8; ++k) atomicAdd(&v.st[s].dbg[k - 2], (unsigned long long)rprof[k]);
-        atomicMax(&v.st[s].dbg[6], ((unsigned long long)(clock64() - t_r) << 16) | ((unsigned)n << 4) | 0);
-        atomicMax(&v.st[s].dbg[7], ((unsigned long long)(clock64() - t_r) << 8) | (unsigned)ring);
     }
 #endif
     if (tid == 0 && serr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
-    // voxel heads: a thread per contiguous chunk, ranks by a workgroup scan;
-    // the chunk's points are gathered into registers first, every load in
-    // flight at once (only a voxel running past the chunk's end loads more)
-    constexpr int CHM = (PMAX + NT - 1) / NT;   // the longest chunk
-    const int chunk = (n + NT - 1) / NT;
-    const int i0 = min(n, tid * chunk), i1 = min(n, i0 + chunk);
-    float4 q[CHM];
-#pragma unroll
-    for (int u = 0; u < CHM; ++u) q[u] = in[(unsigned int)keys[min(i0 + u, n - 1)]];
-    int heads = 0;
-#pragma unroll
-    for (int u = 0; u < CHM; ++u) {
-        const int i = i0 + u;
-        heads += i < i1 && (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32));
-    }
-    int incl = heads;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[wv] = incl;
-    __syncthreads();
-    int before = 0, total = 0;
-    for (int w = 0; w < RW; ++w) {
-        if (w < wv) before += wsum[w];
-        total += wsum[w];
-    }
-    int rank = before + incl - heads;
-    // each voxel that starts in the chunk, summed in the sorted order (PCL's
-    // in-order float chains); items before the chunk's first head belong to
-    // the previous chunk's last voxel
-    float sx = 0, sy = 0, sz = 0, si = 0;
-    int cnt = 0;
-    bool open = false;
-#pragma unroll
-    for (int u = 0; u < CHM; ++u) {
-        const int i = i0 + u;
-        if (i < i1) {
-            if (i == 0 || (keys[i] >> 32) != (keys[i - 1] >> 32)) {
-                if (open) out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
-                sx = sy = sz = si = 0;
-                cnt = 0;
-                open = true;
-            }
-            if (open) { sx += q[u].x; sy += q[u].y; sz += q[u].z; si += q[u].w; ++cnt; }
-        }
-    }
-    if (open) {   // the chunk's last voxel, possibly running on past it
-        const unsigned int vid = (unsigned int)(keys[i1 - 1] >> 32);
-        for (int e = i1; e < n && (unsigned int)(keys[e] >> 32) == vid; ++e) {
-            const float4 p = in[(unsigned int)keys[e]];
-            sx += p.x; sy += p.y; sz += p.z; si += p.w;
-            ++cnt;
-        }
-        out[rank++] = make_float4(sx / (float)cnt, sy / (float)cnt, sz / (float)cnt, si / (float)cnt);
-    }
     if (tid == 0) v.ring_cnt[rr * 4 + 3] = total;
 #undef RING_STAMP
 }

@@ -339,10 +339,15 @@ __global__ void k_cc_merge(DevView v, int ntiles) {
 // root as its own parent, so every pixel's root is parent[parent[p]].
 // (k_cc_merge only relinks roots, so a non-root pixel's parent is still its
 // tile-local root; local roots are flagged in csize.)
-#define IP_STAT_SLOTS 512
+// Slots (tile-local roots counted in LDS) per workgroup: a dense scan's tile
+// holds many small components — 1 200 local roots per 128 x 32 tile on C5's
+// 128 x 2048 scans, up to ~950 per 64 x 64 tile on C2 / C3 — and a tile past
+// its slots takes the slow path, per-pixel device atomics; so 1024 slots for
+// up to 64 rows, 1536 beyond (24 B each, 32 / 44 KB of LDS per workgroup).
 #define IP_NOT_CAND 0xfffd
 #define IP_NOT_ROOT 0xfffe
 #define IP_OVERFLOW 0xffff
+template <int SLOTS>
 __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
     const int s = blockIdx.y, R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     const int TC = ip_tile_cols(R), c0 = blockIdx.x * TC, nc = min(TC, C - c0), npx = R * TC;
@@ -350,11 +355,11 @@ __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
     int* par = v.parent + base;
     const int tid = threadIdx.x;
     __shared__ uint16_t l_slot[IP_TILE_PX];
-    __shared__ int l_cnt[IP_STAT_SLOTS], l_fr[IP_STAT_SLOTS], l_lr[IP_STAT_SLOTS];
-    __shared__ unsigned long long l_rows[IP_STAT_SLOTS][2];
+    __shared__ int l_cnt[SLOTS], l_fr[SLOTS];
+    __shared__ unsigned long long l_rows[SLOTS][2];
     __shared__ int n_slots;
     if (tid == 0) n_slots = 0;
-    for (int k = tid; k < IP_STAT_SLOTS; k += 256) { l_cnt[k] = 0; l_rows[k][0] = 0ull; l_rows[k][1] = 0ull; }
+    for (int k = tid; k < SLOTS; k += 256) { l_cnt[k] = 0; l_rows[k][0] = 0ull; l_rows[k][1] = 0ull; }
     __syncthreads();
     for (int l = tid; l < npx; l += 256) {
         const int i = l / TC, jj = l - i * TC;
@@ -367,7 +372,7 @@ __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
                 const int fr = find_root_h(par, p);
                 const int k = atomicAdd(&n_slots, 1);
                 code = IP_OVERFLOW;
-                if (k < IP_STAT_SLOTS) { code = (uint16_t)k; l_fr[k] = fr; l_lr[k] = p; }
+                if (k < SLOTS) { code = (uint16_t)k; l_fr[k] = fr; }
             }
         }
         l_slot[l] = code;
@@ -396,23 +401,23 @@ __global__ void __launch_bounds__(256) k_cc_stats(DevView v) {
         }
     }
     __syncthreads();
-    const int ns = min(n_slots, IP_STAT_SLOTS);
+    const int ns = min(n_slots, SLOTS);
     for (int k = tid; k < ns; k += 256) {
         const int fr = l_fr[k];
         atomicAdd(&v.csize[base + fr], l_cnt[k]);
         if (l_rows[k][0]) atomicOr(&v.crows[2 * (base + fr)], l_rows[k][0]);
         if (l_rows[k][1]) atomicOr(&v.crows[2 * (base + fr) + 1], l_rows[k][1]);
     }
-    __syncthreads();
     // compress: the local roots point at their component roots (every find
     // of this workgroup has finished; other workgroups only follow parent
     // links, which this keeps valid)
-    for (int k = tid; k < ns; k += 256) par[l_lr[k]] = l_fr[k];
     for (int l = tid; l < npx; l += 256) {
         const int i = l / TC, jj = l - i * TC;
-        if (jj >= nc || l_slot[l] != IP_OVERFLOW) continue;
+        if (jj >= nc) continue;
+        const int code = l_slot[l];
+        if (code == IP_NOT_CAND || code == IP_NOT_ROOT) continue;
         const int p = i * C + c0 + jj;
-        par[p] = find_root(par, p);
+        par[p] = code == IP_OVERFLOW ? find_root(par, p) : l_fr[code];
     }
 }
 
@@ -572,7 +577,8 @@ int ip_run(slo_ctx* ctx) {
     const int ntiles = (v.cfg.horizon_scan + ip_tile_cols(v.cfg.n_scan) - 1) / ip_tile_cols(v.cfg.n_scan);
     SLO_LAUNCH(ctx, "ip_tile", k_ip_tile, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_cc_merge", k_cc_merge, dim3((ntiles * v.cfg.n_scan + T - 1) / T, S), dim3(T), 0, v, ntiles);
-    SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats, dim3(ntiles, S), dim3(T), 0, v);
+    if (v.cfg.n_scan <= 64) SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<1024>, dim3(ntiles, S), dim3(T), 0, v);
+    else SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<1536>, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_rowcount", k_ip_rowcount, gr, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_compact", k_ip_compact, gr, dim3(T), 0, v);
     SLO_CHECK(hipGetLastError());

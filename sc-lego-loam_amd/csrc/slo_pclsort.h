@@ -555,6 +555,111 @@ __device__ inline void wave_heap_sort(It* a, int n) {
     heap_fence<Global>();
 }
 
+// wave_heap_sort with the heap in global memory (k_pc_fallback: spent-depth
+// ranges over 4 Ki items) and its levels 6 .. 10 (nodes 63 .. 2046) cached in
+// LDS for the sort_heap phase: a pop's path then costs one LDS round trip for
+// those five levels and one L2 round trip for the five below (up to 2^16
+// items), against two L2 round trips with the whole path in global memory.
+// mid: this wave's LDS array of kMidN items (nodes [0, kMidN); the first 63
+// are held in registers as in wave_heap_sort).  Same moves, same result.
+constexpr int kMidN = 2047;
+template <class It>
+__device__ inline void wave_heap_sort_cached(It* a, int n, It* mid) {
+    const int lane = threadIdx.x & 63;
+    if (n < 2) return;
+    const int P = (n - 2) / 2;   // the last parent
+    for (int L = lg2(P + 1); L >= 0; --L) {   // make_heap in global memory, a tree level at a time
+        const int lo = (1 << L) - 1, hi = min((1 << (L + 1)) - 2, P);
+        for (int x = lo + lane; x <= hi; x += 64) slo_sort::adjust_heap_(a, x, n, a[x], LessT<It>());
+        heap_fence<true>();
+    }
+    constexpr int TOPN = 63;
+    const int nm = min(n, kMidN);
+    for (int x = TOPN + lane; x < nm; x += 64) mid[x] = a[x];
+    It top = lane < min(n, TOPN) ? a[lane] : (It)0;
+    wave_fence();
+    const int tlev = 31 - __builtin_clz(lane + 1);        // tree level of node `lane`
+    const int cj = 31 - __builtin_clz(lane + 2), cq = lane + 2 - (1 << cj);   // chunk slot: level cj, position cq
+    // node x's item: registers (x < 63), LDS (x < kMidN), else global
+    auto at = [&](int x) -> It { return x < kMidN ? mid[x] : a[x]; };
+    for (int len = n - 1; len >= 1; --len) {
+        const It mx = irl(top, 0);
+        It v;
+        if (len < TOPN) {
+            v = irl(top, len);
+            if (lane == len) top = mx;
+        } else {
+            v = at(len);
+            if (lane == 0) {
+                if (len < kMidN) mid[len] = mx;
+                else a[len] = mx;
+            }
+        }
+        const int lim = (len - 1) / 2;   // nodes below lim have two children
+        int h = 0, k = 0, ph = 0;
+        It pv = 0;
+        // The path takes the larger child at every level (ties: the right
+        // one).  Every node's choice is computed at once — lane t compares
+        // its node's two children — and the walk reads them from a ballot:
+        // scalar bit steps instead of a chain of lane reads and compares.
+        {
+            const It cl = ishfl(top, min(2 * lane + 1, 63)), cr = ishfl(top, min(2 * lane + 2, 63));
+            const unsigned long long BR = __ballot(lane < 31 && !(vkey(cr) < vkey(cl)));
+            while (h < lim && 2 * h + 2 < TOPN) {   // the register levels
+                h = 2 * h + 1 + (int)((BR >> h) & 1ull);
+                ++k;
+                if (lane == k) ph = h;
+            }
+            const It tv = ishfl(top, min(ph, 63));
+            if (lane >= 1 && lane <= k) pv = tv;
+        }
+        while (h < lim) {   // deeper: the five levels below h in one load (LDS for levels 6 .. 10)
+            const int node = (h + 1) * (1 << cj) - 1 + cq;
+            const It sub = (lane < 62 && node < len) ? at(node) : (It)0;
+            // chunk slot (level j, position q) = 2^j - 2 + q; its children: slots 2^(j+1) - 2 + 2q, + 1
+            const int cs = (1 << (cj + 1)) - 2 + 2 * cq;
+            const It sl = ishfl(sub, min(cs, 63)), sr = ishfl(sub, min(cs + 1, 63));
+            const unsigned long long BC = __ballot(lane < 30 && !(vkey(sr) < vkey(sl)));
+            const bool r0 = !(vkey(irl(sub, 1)) < vkey(irl(sub, 0)));   // h's own children: slots 0, 1
+            const int k0 = k;
+            int rel = r0 ? 1 : 0, pslot = 0;
+            h = 2 * h + 1 + rel;
+            ++k;
+            if (lane == k) { ph = h; pslot = rel; }
+            for (int j = 2; j <= 5 && h < lim; ++j) {
+                const int b = (int)((BC >> ((1 << (j - 1)) - 2 + rel)) & 1ull);
+                rel = 2 * rel + b;
+                h = 2 * h + 1 + b;
+                ++k;
+                if (lane == k) { ph = h; pslot = (1 << j) - 2 + rel; }
+            }
+            const It sv = ishfl(sub, min(pslot, 63));
+            if (lane > k0 && lane <= k) pv = sv;
+        }
+        if ((len & 1) == 0 && h == (len - 2) / 2) {   // the last parent's only child
+            const int c = 2 * h + 1;
+            const It cv = c < TOPN ? irl(top, c) : at(c);
+            ++k;
+            if (lane == k) { ph = c; pv = cv; }
+        }
+        const unsigned int kv = vkey(v);
+        const int m = __popcll(__ballot(lane >= 1 && lane <= k && !(vkey(pv) < kv)));
+        const It up = ishfl(pv, min(lane + 1, 63));
+        const It w = lane < m ? up : v;
+        const int phl = __shfl(ph, min(tlev, 63), 64);
+        const It wl = ishfl(w, min(tlev, 63));
+        if (lane <= m && ph >= TOPN) {
+            if (ph < kMidN) mid[ph] = w;
+            else a[ph] = w;
+        }
+        if (lane < TOPN && tlev <= m && phl == lane) top = wl;
+        heap_fence<true>();   // the global stores (and the LDS ones) before the next pop's loads
+    }
+    if (lane < min(n, TOPN)) a[lane] = top;
+    for (int x = TOPN + lane; x < nm; x += 64) a[x] = mid[x];
+    heap_fence<true>();
+}
+
 // the queued lane tasks, one per lane, through the sequential restatement
 template <class It>
 __device__ __forceinline__ void lane_flush(It* items, const unsigned int* q, int nq) {

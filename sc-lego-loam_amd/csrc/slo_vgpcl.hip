@@ -987,17 +987,21 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
 }
 
 // list 4 — a range over PC_T items whose depth budget is spent (std::sort's
-// heapsort; the dense C5 maps send a few hundred per run here): the first
-// wave heapsorts it in global memory (slo_pclsort.h wave_heap_sort: one round
-// trip per pop instead of two dependent loads per tree level on one lane).
-// (Staging ranges of up to 12 Ki items in LDS measured 1 % faster on C5, but
-// its 96 KB of LDS held every launch of the kernel — nearly always empty —
-// until a CU had that much free beside the other contexts' finish kernels:
-// 3 ms per launch in the live trace.)  A range that came here for another reason (over PT_MAXT tiles,
+// heapsort; the dense C5 maps send a few hundred per run here, two or three
+// per launch): the first wave heapsorts it in global memory, the heap's
+// levels 6 .. 10 cached in 16 KB of LDS (slo_pclsort.h wave_heap_sort_cached:
+// per pop one LDS and one L2 round trip for the path below the register
+// levels, instead of two L2 round trips).  (Staging whole ranges in LDS —
+// 96 KB in round 4, 64 KB of 32-bit items in round 5 — held every launch of
+// the kernel, nearly always empty, until a CU had that much free beside the
+// other contexts' finish kernels: 3-4 ms per launch, and on a graph branch of
+// its own the join stalled the context instead: C3 19.2 k -> 16.1 k scans/s.)
+// A range that came here for another reason (over PT_MAXT tiles,
 // a full stack; never seen) is finished by one lane with the sequential
 // restatement.
 __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
                                                       int* cstat, u64* scratch, unsigned long long* pst) {
+    __shared__ u64 mid[slo_pcl::kMidN];   // heap levels 6 .. 10 (wave_heap_sort_cached)
     const int nw = ctr[PCC_NW + 4];
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl[e];
@@ -1006,7 +1010,7 @@ __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned i
         for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
         __syncthreads();
         if (d == 0 && n > 16) {
-            if (threadIdx.x < 64) slo_pcl::wave_heap_sort<u64, true>(scratch + f, n);
+            if (threadIdx.x < 64) slo_pcl::wave_heap_sort_cached<u64>(scratch + f, n, mid);
             if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
         } else if (threadIdx.x == 0) {
             atomicAdd(&cstat[0], 1);
