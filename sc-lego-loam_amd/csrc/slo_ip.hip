@@ -342,8 +342,8 @@ __global__ void k_cc_merge(DevView v, int ntiles) {
 // Slots (tile-local roots counted in LDS) per workgroup: a dense scan's tile
 // holds many small components — 1 200 local roots per 128 x 32 tile on C5's
 // 128 x 2048 scans, up to ~950 per 64 x 64 tile on C2 / C3 — and a tile past
-// its slots takes the slow path, per-pixel device atomics; so 1024 slots for
-// up to 64 rows, 1536 beyond (24 B each, 32 / 44 KB of LDS per workgroup).
+// its slots takes the slow path, per-pixel device atomics; so 768 slots for
+// up to 64 rows, 1536 beyond (24 B each, 26 / 44 KB of LDS per workgroup).
 #define IP_NOT_CAND 0xfffd
 #define IP_NOT_ROOT 0xfffe
 #define IP_OVERFLOW 0xffff
@@ -577,7 +577,7 @@ int ip_run(slo_ctx* ctx) {
     const int ntiles = (v.cfg.horizon_scan + ip_tile_cols(v.cfg.n_scan) - 1) / ip_tile_cols(v.cfg.n_scan);
     SLO_LAUNCH(ctx, "ip_tile", k_ip_tile, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_cc_merge", k_cc_merge, dim3((ntiles * v.cfg.n_scan + T - 1) / T, S), dim3(T), 0, v, ntiles);
-    if (v.cfg.n_scan <= 64) SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<1024>, dim3(ntiles, S), dim3(T), 0, v);
+    if (v.cfg.n_scan <= 64) SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<768>, dim3(ntiles, S), dim3(T), 0, v);
     else SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<1536>, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_rowcount", k_ip_rowcount, gr, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_compact", k_ip_compact, gr, dim3(T), 0, v);

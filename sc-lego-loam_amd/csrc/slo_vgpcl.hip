@@ -598,13 +598,20 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
     }
 }
 
-// ---- the same with 32-bit items, for an entry whose keys span less than
-// 2^20: (key - min) << 12 | position in the entry (slo_pclsort.h kPosBits).
+// ---- the same with 32-bit items: (key - min) << 12 | position in the entry
+// (slo_pclsort.h kPosBits) for an entry whose keys span less than 2^20.
 // Half the LDS of the 64-bit items — 25 KB per 4 Ki entry at four waves, six
 // workgroups per CU instead of three — and the same comparisons, so the same
 // order.  The point indices stay in global memory and follow their items at
 // the write-back (gathered into the items' LDS slots, written back after a
-// barrier).  A wider entry goes to list 5 (k_pc_finish).
+// barrier).  A wider entry (sparse map regions: a range of 4 Ki items over
+// several z slabs of a 0.4 m grid) takes the keys' ranks instead of the keys:
+// a bitonic sort of its raw keys in the items' LDS, then each position's rank
+// = the first sorted index of its key (a binary search), which orders the
+// items exactly as their keys do, in 12 bits; the original keys then follow
+// their items at the write-back like the point indices.  (Round 4 sent such
+// entries to a 64-bit finish kernel, k_pc_finish — 41 KB of LDS, three
+// workgroups per CU: 6.9 % of C2's and 8.3 % of C5's device time.)
 #ifndef PC_F32_OCC
 #define PC_F32_OCC 6      // waves per SIMD k_pc_finish32 is built for (25 KB of LDS: six 4-wave workgroups per CU;
                           // pc_finish_b 32.0 -> 31.0 ms per 6 mapping steps against five)
@@ -649,12 +656,44 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
         if (lane == 0) { kmn[wv] = mn; kmx[wv] = mx; }
         __syncthreads();
         for (int q = 0; q < W; ++q) { mn = min(mn, kmn[q]); mx = max(mx, kmx[q]); }
-        if (mx - mn >= (1u << (32 - slo_pcl::kPosBits))) {   // too wide for 32-bit items (uniform)
-            if (tid == 0) wl.l[5][atomicAdd(&ctr[PCC_NW + 5], 1)] = w;
-            __syncthreads();   // kmn / kmx and items are rewritten by the next entry
-            continue;
+        const bool wide = mx - mn >= (1u << (32 - slo_pcl::kPosBits));   // uniform
+        if (wide) {
+            // ranks: the raw keys sorted (bitonic, padded to a power of two
+            // with the largest key), then each position's key searched
+            int np = 1;
+            while (np < n) np <<= 1;
+            for (int i = n + tid; i < np; i += NT) items[i] = 0xffffffffu;
+            __syncthreads();
+            for (int size = 2; size <= np; size <<= 1)
+                for (int stride = size >> 1; stride > 0; stride >>= 1) {
+                    for (int t = tid; t < np / 2; t += NT) {
+                        const int lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+                        const unsigned int a = items[lo], b = items[hi];
+                        if ((a > b) == ((lo & size) == 0)) { items[lo] = b; items[hi] = a; }
+                    }
+                    __syncthreads();
+                }
+            constexpr int RK = (NMAX + NT - 1) / NT;   // positions per thread
+            unsigned int rk[RK];
+#pragma unroll
+            for (int u = 0; u < RK; ++u) {   // lower_bound of each position's key, all searches side by side
+                const int i = u * NT + tid;
+                const unsigned int key = K[f + min(i, n - 1)];
+                int lo = 0;
+#pragma unroll
+                for (int step = NMAX >> 1; step > 0; step >>= 1)
+                    if (lo + step <= np && items[lo + step - 1] < key) lo += step;
+                rk[u] = (unsigned int)lo;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RK; ++u) {
+                const int i = u * NT + tid;
+                if (i < n) items[i] = (rk[u] << slo_pcl::kPosBits) | (unsigned int)i;
+            }
+        } else {
+            for (int i = tid; i < n; i += NT) items[i] = ((items[i] - mn) << slo_pcl::kPosBits) | (unsigned int)i;
         }
-        for (int i = tid; i < n; i += NT) items[i] = ((items[i] - mn) << slo_pcl::kPosBits) | (unsigned int)i;
         __syncthreads();
         slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, prof);
         __syncthreads();
@@ -662,12 +701,32 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
             atomicAdd(&cstat[1], ferr);
             pc_flag(serr, off, S, f, SLO_ERR_SORT);
         }
-        // the keys out at once; each position's point index gathered into its
-        // LDS slot, written out only after every gather of the entry is done
-        for (int i = tid; i < n; i += NT) {
-            const unsigned int it = items[i];
-            K[f + i] = (it >> slo_pcl::kPosBits) + mn;
-            items[i] = V[f + (it & ((1u << slo_pcl::kPosBits) - 1u))];
+        if (wide) {   // the keys and the point indices gathered by position (all reads before any write)
+            constexpr int RK = (NMAX + NT - 1) / NT;
+            unsigned int pos[RK];
+#pragma unroll
+            for (int u = 0; u < RK; ++u) {
+                const int i = u * NT + tid;
+                pos[u] = i < n ? items[i] & ((1u << slo_pcl::kPosBits) - 1u) : 0u;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RK; ++u)
+                if (u * NT + tid < n) items[u * NT + tid] = K[f + pos[u]];
+            __syncthreads();
+            for (int i = tid; i < n; i += NT) K[f + i] = items[i];
+            __syncthreads();
+#pragma unroll
+            for (int u = 0; u < RK; ++u)
+                if (u * NT + tid < n) items[u * NT + tid] = V[f + pos[u]];
+        } else {
+            // the keys out at once; each position's point index gathered into its
+            // LDS slot, written out only after every gather of the entry is done
+            for (int i = tid; i < n; i += NT) {
+                const unsigned int it = items[i];
+                K[f + i] = (it >> slo_pcl::kPosBits) + mn;
+                items[i] = V[f + (it & ((1u << slo_pcl::kPosBits) - 1u))];
+            }
         }
         __syncthreads();
         for (int i = tid; i < n; i += NT) V[f + i] = items[i];
@@ -1136,20 +1195,16 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
                K, V, PB, L, w.ctr, w.pstat, w.cstat, off, S, w.serr);
     SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare,
                w.pstat);
-    // 32-bit items first (lists 2 and 1); the entries too wide for them (list 5) after, on 64-bit items
+    // 32-bit items (lists 2 and 1; entries whose keys span 2^20 or more take their keys' ranks)
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
                    w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
                    w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 5, w.pstat,
-                   w.cstat, off, S, w.serr);
     } else {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
                    w.pstat, w.cstat, off, S, w.serr);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
-                   w.pstat, w.cstat, off, S, w.serr);
-        SLO_LAUNCH(ctx, "pc_finish_bx", (k_pc_finish<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 5,
                    w.pstat, w.cstat, off, S, w.serr);
     }
     SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat, off, S, w.serr);
