@@ -321,7 +321,11 @@ __device__ inline float sqd(const P4& q, float x, float y, float z) {
 #ifndef SLO_KNN_UNROLL
 #define SLO_KNN_UNROLL 2   // entry loads in flight per walk step: 4 costs occupancy (110 VGPRs -> 4 waves)
 #endif
-__device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float* od) {
+// bw: a bound on the walk known before it starts (the squared distance of
+// five map points, so at least the 5th-NN distance; 1 = none): rows and
+// cells past it are skipped, every point within it is still visited, so the
+// five found are the same.
+__device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float* od, float bw = 1.0f) {
     // sorted top-5 by (distance, index); empty slots are (1, INT_MAX).
     // Insertion is unrolled with constant indices so the lists stay in
     // registers (a data-dependent index would put them in scratch memory).
@@ -330,7 +334,7 @@ __device__ inline int knn5(const GridView& g, int s, const P4& q, int* oi, float
     if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z))) return 0;
     auto less = [](float da, int ia, float db, int ib) { return da < db || (da == db && ia < ib); };
     int n = 0;
-    grid_ball<SLO_MAP_R, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return od[4]; }, [&](const float4& p) {
+    grid_ball<SLO_MAP_R, SLO_KNN_UNROLL>(g, s, q.x, q.y, q.z, [&]() { return fminf(od[4], bw); }, [&](const float4& p) {
         const float d = sqd(q, p.x, p.y, p.z);
         const int idx = __float_as_int(p.w);
         if (!less(d, idx, od[4], oi[4])) return;
@@ -474,7 +478,26 @@ __global__ void __launch_bounds__(256) k_mo_knn(DevView v) {
         const P4 sel = mo_query(v, s, st, q, g, po);
         int ind[5];
         float dis[5];
-        const int n = q < nc ? knn5(v.g_mc, s, sel, ind, dis) : knn5(v.g_ms, s, sel, ind, dis);
+        // warm start (LM iterations after the first, same map): the previous
+        // iteration's five neighbours, seen from the moved query, bound the
+        // walk before it starts
+        float bw = 1.0f;
+        if (st.mo_iters > 0) {
+            int pi[5];
+#pragma unroll
+            for (int k = 0; k < 5; ++k) pi[k] = nn[(size_t)q * 5 + k];
+            if (pi[0] >= 0) {
+                const float4* mp = q < nc ? v.map_c_ds + (size_t)s * v.cap_mc : v.map_s_ds + (size_t)s * v.cap_ms;
+                float4 m[5];
+#pragma unroll
+                for (int k = 0; k < 5; ++k) m[k] = mp[pi[k]];
+                bw = 0.0f;
+#pragma unroll
+                for (int k = 0; k < 5; ++k) bw = fmaxf(bw, sqd(sel, m[k].x, m[k].y, m[k].z));
+                bw = fminf(bw, 1.0f);
+            }
+        }
+        const int n = q < nc ? knn5(v.g_mc, s, sel, ind, dis, bw) : knn5(v.g_ms, s, sel, ind, dis, bw);
         const bool ok = n == 5 && dis[4] < 1.0;   // MO:1281 / 1364
 #pragma unroll
         for (int k = 0; k < 5; ++k) nn[(size_t)q * 5 + k] = ok ? ind[k] : -1;
