@@ -544,6 +544,10 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(int tail_min, const PSeg* seg
 #ifndef PC_FW
 #define PC_FW 4           // waves per entry of the two larger size classes
 #endif
+#ifndef PC_PROF
+#define PC_PROF 0         // 1: the finishes count their cycles per step kind (pcl_work [9..17], a diagnostic build:
+                          // the clock reads wait for the wave's LDS traffic at every step)
+#endif
 template <int NMAX, int W>
 __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned int* V, PcLists wl, int* ctr, int list,
                                                        unsigned long long* pst, int* cstat, const int32_t* off,
@@ -573,7 +577,7 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
                 if (i0 + u * 64 * W + tid < n) items[i0 + u * 64 * W + tid] = ((u64)kk[u] << 32) | vv[u];
         }
         __syncthreads();
-        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, prof);
+        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, PC_PROF ? prof : nullptr);
         __syncthreads();
         if (tid == 0 && ferr) {   // never expected: counted and the stream flagged
             atomicAdd(&cstat[1], ferr);
@@ -695,7 +699,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
             for (int i = tid; i < n; i += NT) items[i] = ((items[i] - mn) << slo_pcl::kPosBits) | (unsigned int)i;
         }
         __syncthreads();
-        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, prof);
+        slo_pcl::block_sort<PC_TLANE, W>(items, n, d, tbl, ws, bq, &ferr, PC_PROF ? prof : nullptr);
         __syncthreads();
         if (tid == 0 && ferr) {   // never expected: counted and the stream flagged
             atomicAdd(&cstat[1], ferr);
