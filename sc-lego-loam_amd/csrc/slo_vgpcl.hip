@@ -124,6 +124,10 @@ __device__ inline void pc_flag(int32_t* serr, const int32_t* off, int S, int pos
     atomicOr(&serr[pc_stream_of(off, S, pos)], bit);
 }
 
+__device__ __forceinline__ int lane_prefix64(unsigned long long b) {   // set bits of b below this lane
+    return (int)__builtin_amdgcn_mbcnt_hi((unsigned int)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned int)b, 0u));
+}
+
 // ---- items: finite points first, in input order
 __global__ void __launch_bounds__(VG_T) k_pc_count(VgSrc src, const int32_t* off,
                                                     const VgParams* prm, int* tcnt, int maxT, int S, int* ctr) {
@@ -198,41 +202,62 @@ __global__ void __launch_bounds__(1024) k_pc_scan(int tail_min, const int32_t* o
     }
 }
 
+// Striped: thread tid takes items a + k * VG_T + tid (k = 0 .. VG_IPT - 1),
+// so every load and store instruction of a wave touches 64 consecutive items
+// (the blocked layout, a + tid * VG_IPT + k, made each instruction 64 separate
+// lines: k_pc_write waited on instruction issue 80 % of its cycles).  The
+// tile's input order is k-major, then wave, then lane: per (stripe, wave)
+// finite counts by ballot, one prefix over them, and the lane's rank by mbcnt.
 __global__ void __launch_bounds__(VG_T) __attribute__((amdgpu_waves_per_eu(PC_WOCC))) k_pc_write(VgSrc src, const int32_t* off,
                                                     const VgParams* prm, const int* tcnt, const int32_t* nfin,
                                                     int maxT, unsigned int* K, unsigned int* V, int S) {
-    __shared__ unsigned int wsum[VG_W];
+    __shared__ int wc[VG_IPT * VG_W];   // finite items per (stripe, wave), then their exclusive prefixes
     const int s = blockIdx.y;
     if (s >= S) return;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const VgParams p = prm[s];
     const int base = off[s], n = off[s + 1] - base, nf = nfin[s];
     const float4* in = src.row(s);
     for (int t = blockIdx.x; t < p.ntiles; t += gridDim.x) {
         const int a = t * VG_TILE, m = min(VG_TILE, n - a);
-        // blocked: thread tid holds items a + tid*VG_IPT + k, so the block scan keeps input order
-        const int j0 = threadIdx.x * VG_IPT;
         float4 q[VG_IPT];
 #pragma unroll
-        for (int k = 0; k < VG_IPT; ++k) q[k] = in[a + min(j0 + k, m - 1)];
-        unsigned int key[VG_IPT], fin = 0, c = 0;
+        for (int k = 0; k < VG_IPT; ++k) q[k] = in[a + min(k * VG_T + tid, m - 1)];
+        unsigned int key[VG_IPT], fin = 0;
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
-            key[k] = vg_key(q[k], p, a + j0 + k);
-            const bool ok = j0 + k < m && key[k] != vg_none(p);
+            key[k] = vg_key(q[k], p, a + k * VG_T + tid);
+            const bool ok = k * VG_T + tid < m && key[k] != vg_none(p);
             fin |= (unsigned int)ok << k;
-            c += ok;
+            const unsigned long long b = __ballot(ok);
+            if (lane == 0) wc[k * VG_W + w] = __popcll(b);
         }
-        unsigned int total;
-        const unsigned int ex = vg_block_scan<VG_W>(c, wsum, &total);
-        int r = tcnt[(size_t)s * maxT + t] + (int)ex;        // finite items before this thread's first
-        int rn = nf + (a + j0) - r;                            // non-finite items before it
+        __syncthreads();
+        if (tid < 64) {   // exclusive prefix over the VG_IPT * VG_W (stripe, wave) counts, in input order
+            static_assert(VG_IPT * VG_W == 64, "one lane per (stripe, wave)");
+            const int x = wc[tid];
+            int incl = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const int y = __shfl_up(incl, o, 64);
+                if (lane >= o) incl += y;
+            }
+            wc[tid] = incl - x;
+        }
+        __syncthreads();
+        const int r0 = tcnt[(size_t)s * maxT + t];   // finite items of the stream before the tile
 #pragma unroll
         for (int k = 0; k < VG_IPT; ++k) {
-            if (j0 + k >= m) break;
-            const int o = ((fin >> k) & 1) ? r++ : rn++;
-            K[base + o] = key[k];
-            V[base + o] = (unsigned int)(a + j0 + k);
+            const int j = k * VG_T + tid;
+            const bool ok = (fin >> k) & 1u;
+            const int fb = r0 + wc[k * VG_W + w] + lane_prefix64(__ballot(ok));   // finite items before item j
+            if (j < m) {
+                const int o = ok ? fb : nf + (a + j) - fb;
+                K[base + o] = key[k];
+                V[base + o] = (unsigned int)(a + j);
+            }
         }
+        __syncthreads();   // wc is the next tile's
     }
 }
 
