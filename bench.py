@@ -99,7 +99,7 @@ def parse(argv=None):
                     help="extra Scan Context history per stream (scans before scan 0, a KITTI-00 mid-drive history: "
                          "detects search ~1000 keyframes, SCc:264-289); the pre-roll builds the recent part")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="mo_knn,pc_tail,pc_lpairs,fa_search_corner,sc_detect",
+    ap.add_argument("--roofline-also", default="fa_ring_ds,mo_knn,pc_tail,pc_lpairs,fa_search_corner,pc_fallback,sc_detect",
                     help="further kernels timed live the same way, reported under roofline_also (comma list)")
     ap.add_argument("--roofline-kernel", default="auto",
                     help="kernel timed inside the timed region (the roofline's kernel); auto = the largest kernel by "

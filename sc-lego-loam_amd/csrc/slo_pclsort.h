@@ -377,16 +377,19 @@ __device__ __forceinline__ unsigned int ishfl(unsigned int v, int src) {
     return (unsigned int)__shfl((int)v, src, 64);
 }
 
-// items[f, f + n), n <= 64; tw: 128 bytes of this wave's LDS.  Returns the
-// lanes that start a spent-depth segment (bit lo), the segment's end in *hend
-// (per lane) for the caller's lane tasks.
+// items[f, f + n), n <= 64, as one or more adjacent ranges: lane i's range is
+// [lo0, hi0) (relative to f) with depth dd0 — several small ranges sorted in
+// one call (wave_sort_range merges the adjacent ones off its stack); tw: 128
+// bytes of this wave's LDS.  Returns the lanes that start a spent-depth
+// segment (bit lo), the segment's end in *hend (per lane) for the caller's
+// lane tasks.
 template <class It>
-__device__ __forceinline__ unsigned long long wave_small_sort(It* items, int f, int n, int depth, unsigned char* tw,
-                                                              int* hend) {
+__device__ __forceinline__ unsigned long long wave_small_sort(It* items, int f, int n, int lo0, int hi0, int dd0,
+                                                              unsigned char* tw, int* hend) {
     const int i = threadIdx.x & 63;
     const bool live = i < n;
     It it = items[f + min(i, n - 1)];
-    int lo = 0, hi = n, dd = depth;
+    int lo = lo0, hi = hi0, dd = dd0;
     for (;;) {
         const bool act = live && hi - lo > 16 && dd > 0;
         if (__ballot(act) == 0) break;
@@ -752,7 +755,23 @@ __device__ __forceinline__ void wave_sort_range(It* items, int f0, int l0, int d
             const long long t0 = prof ? clock64() : 0;
             const bool small = len >= 2 && len <= 64 && d > 0 && !stepped;
             const bool heap = !small && !stepped && d == 0 && len > 16;   // introsort_range's heapsort, by the wave
-            if (small) hs = wave_small_sort(items, f, len, d, ws.tw, &hend);
+            int ln = l;   // the end of the ranges sorted together
+            if (small) {
+                // the stack's top ranges that follow this one (depth first, left half first: its right
+                // sibling, then the right siblings of its ancestors) join it while the whole stays within
+                // 64 items: one register sort for several small ranges (most are leaves of <= 16)
+                int mlo = 0, mhi = len, mdd = d;
+                wave_fence();
+                while (sp > 0) {
+                    const unsigned int e2 = __builtin_amdgcn_readfirstlane(ws.stk[sp - 1]);
+                    const int f2 = (int)(e2 & 0x1fffu), l2 = (int)((e2 >> 13) & 0x1fffu), d2 = (int)(e2 >> 26);
+                    if (f2 != ln || d2 == 0 || l2 - f > 64) break;
+                    --sp;
+                    if (lane >= f2 - f && lane < l2 - f) { mlo = f2 - f; mhi = l2 - f; mdd = d2; }
+                    ln = l2;
+                }
+                hs = wave_small_sort(items, f, ln - f, mlo, mhi, mdd, ws.tw, &hend);
+            }
             else if (heap) wave_heap_sort(items + f, len);
             else if (len >= 2) hs = 1ull;   // the whole range
             if (prof) {

@@ -769,6 +769,11 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
             atomicAdd(&pst[PW_ENTRIES], we);
         }
         for (int q = 0; q < 3; ++q) atomicAdd(&pst[PW_PROF + 3 * list + q], (unsigned long long)prof[q]);
+#if PC_PROF
+        // block_sort's phases (thread 0 of each workgroup): group levels, -, pool entry, pool ([22 + q])
+        if (tid == 0)
+            for (int q = 4; q < 8; ++q) atomicAdd(&pst[22 + q - 4], (unsigned long long)prof[q]);
+#endif
     }
 }
 

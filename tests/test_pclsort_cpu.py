@@ -81,11 +81,16 @@ def ballot(flags):
     return sum(1 << i for i, f in enumerate(flags) if f)
 
 
-def wave_small_sort(items, depth):
-    """slo_pclsort.h wave_small_sort, lane by lane (64 lanes, n <= 64 items)"""
+def wave_small_sort(items, depth, segs=None):
+    """slo_pclsort.h wave_small_sort, lane by lane (64 lanes, n <= 64 items);
+    segs: adjacent ranges [(lo, hi, depth), ...] covering the items, sorted in
+    one call (wave_sort_range merges a small range with the stack's next ones)"""
     n, L = len(items), 64
     it = [items[min(i, n - 1)] for i in range(L)]
     lo, hi, dd = [0] * L, [n] * L, [depth] * L
+    for a, b, d in segs or []:
+        for i in range(a, b):
+            lo[i], hi[i], dd[i] = a, b, d
     live = [i < n for i in range(L)]
     while True:
         act = [live[i] and hi[i] - lo[i] > 16 and dd[i] > 0 for i in range(L)]
@@ -171,3 +176,32 @@ def test_small_sort_is_std_sort_order(seed):
         assert wave_small_sort(items, depth) == want, items
         checked += 1
     assert checked > 500
+
+
+@pytest.mark.parametrize("seed", [4, 5])
+def test_small_sort_merged_ranges(seed):
+    """several adjacent small ranges (each with its own depth budget) sorted in
+    one register call equal each range sorted alone"""
+    rng = random.Random(seed)
+    checked = 0
+    for trial in range(400):
+        segs, a = [], 0
+        while a < 64:
+            n = rng.choice([1, 2, 3, 7, 12, 16, 17, 25, 33, 40])
+            if a + n > 64:
+                break
+            d = rng.randint(1, 12)
+            segs.append((a, a + n, d))
+            a += n
+        if not segs:
+            continue
+        items = [(rng.randrange(rng.choice([1, 2, 4, 9])), i) for i in range(a)]
+        try:
+            want = []
+            for lo, hi, d in segs:
+                want += introsort(items[lo:hi], d)
+        except OverflowError:
+            continue
+        assert wave_small_sort(items, 0, segs) == want, (segs, items)
+        checked += 1
+    assert checked > 300
