@@ -396,45 +396,46 @@ __device__ inline P4 mo_query(const DevView& v, int s, const StreamState& st, in
 // of their body-frame 4 m cell (corner queries first), in LDS, one workgroup
 // per stream — so the lanes of a wave walk neighbouring rows of the map grid.
 // Only the work order changes: mo_nn is indexed by query.
-#define MO_PERM_B 16384  // buckets per query kind (14-bit Morton codes)
+#define MO_PERM_B 4096   // buckets per query kind (12-bit Morton codes): 32 KB of LDS, so the
+                         // block finds a CU next to the other contexts' sort blocks
 #ifndef MO_PERM_INV
 #define MO_PERM_INV 0.25f   // 1 / cell edge (4 m)
 #endif
 #ifndef SLO_MO_PERM
 #define SLO_MO_PERM 1
 #endif
-__global__ void __launch_bounds__(1024) k_mo_perm(DevView v) {
+__global__ void __launch_bounds__(256) k_mo_perm(DevView v) {
     __shared__ int cnt[2 * MO_PERM_B];
-    __shared__ int wsum[16];
+    __shared__ int wsum[4];
     const int s = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const StreamState& st = v.st[s];
     if (!st.mo_ran) return;
     const int nc = st.n_corner_ds, nq = nc + st.n_surf_total_ds;
     const float4* qc = v.cur_c_ds + (size_t)s * v.cap_less_sharp;
     const float4* qs = v.cur_st_ds + (size_t)s * v.cap_st;
-    // Morton code of the body-frame cell: x, z 5 bits, y 4 bits (clamped
-    // around the sensor), interleaved x z y from the top -> 14 bits
+    // Morton code of the body-frame cell: x, z, y 4 bits each (clamped to
+    // +-32 m around the sensor), interleaved x z y from the top -> 12 bits
     auto bucket = [&](int q) {
         const float4 p = q < nc ? qc[q] : qs[q - nc];
         unsigned int h = 0;
         if (isfinite(p.x) && isfinite(p.y) && isfinite(p.z)) {
-            const unsigned int a = (unsigned int)min(max(grid_cell(p.x, MO_PERM_INV) + 16, 0), 31);
+            const unsigned int a = (unsigned int)min(max(grid_cell(p.x, MO_PERM_INV) + 8, 0), 15);
             const unsigned int b = (unsigned int)min(max(grid_cell(p.y, MO_PERM_INV) + 8, 0), 15);
-            const unsigned int c = (unsigned int)min(max(grid_cell(p.z, MO_PERM_INV) + 16, 0), 31);
+            const unsigned int c = (unsigned int)min(max(grid_cell(p.z, MO_PERM_INV) + 8, 0), 15);
 #pragma unroll
-            for (int k = 4; k >= 0; --k) {
+            for (int k = 3; k >= 0; --k) {
                 h = (h << 1) | ((a >> k) & 1u);
                 h = (h << 1) | ((c >> k) & 1u);
-                if (k < 4) h = (h << 1) | ((b >> k) & 1u);
+                h = (h << 1) | ((b >> k) & 1u);
             }
         }
         return (q < nc ? 0 : MO_PERM_B) + (int)h;
     };
-    for (int b = tid; b < 2 * MO_PERM_B; b += 1024) cnt[b] = 0;
+    for (int b = tid; b < 2 * MO_PERM_B; b += 256) cnt[b] = 0;
     __syncthreads();
-    for (int q = tid; q < nq; q += 1024) atomicAdd(&cnt[bucket(q)], 1);
+    for (int q = tid; q < nq; q += 256) atomicAdd(&cnt[bucket(q)], 1);
     __syncthreads();
-    constexpr int PER = 2 * MO_PERM_B / 1024;
+    constexpr int PER = 2 * MO_PERM_B / 256;
     int c[PER], sum = 0;
 #pragma unroll
     for (int k = 0; k < PER; ++k) { c[k] = cnt[tid * PER + k]; sum += c[k]; }
@@ -451,7 +452,7 @@ __global__ void __launch_bounds__(1024) k_mo_perm(DevView v) {
     for (int k = 0; k < PER; ++k) { cnt[tid * PER + k] = run; run += c[k]; }
     __syncthreads();
     int32_t* perm = v.mo_perm + (size_t)s * v.cap_q;
-    for (int q = tid; q < nq; q += 1024) perm[atomicAdd(&cnt[bucket(q)], 1)] = q;
+    for (int q = tid; q < nq; q += 256) perm[atomicAdd(&cnt[bucket(q)], 1)] = q;
 }
 
 // The 5-NN of every query, one thread per query, into mo_nn (index -1 in the
@@ -1086,7 +1087,7 @@ int map_run(slo_ctx* ctx) {
         const VgGroup t = map_total_group(ctx);
         if ((r = vg_run_groups(ctx, "surf_total", &t, 1))) return r;
     }
-    if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(1024), 0, v);
+    if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(256), 0, v);
     // hash grids over the DS maps (on the side stream when forked, above)
     if (!fork && (r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
     if (!fork && (r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;

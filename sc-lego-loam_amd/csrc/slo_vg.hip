@@ -629,17 +629,20 @@ __global__ void __launch_bounds__(VG_T) k_vg_heads(const unsigned int* keys, con
     }
 }
 
-__global__ void __launch_bounds__(1024) k_vg_hscan(VgSrc src, const VgParams* prm, int* hcnt, int maxT, int32_t* nvox,
-                                                   int32_t* errflag) {
-    __shared__ int wsum[16];
+// 256 threads: a 1024-thread block needs 16 free wave slots on one CU, which
+// the other contexts' LDS-heavy sort blocks rarely leave (1.1 ms per launch
+// in the live window against 8 us isolated, round-5 C3 profile)
+__global__ void __launch_bounds__(256) k_vg_hscan(VgSrc src, const VgParams* prm, int* hcnt, int maxT, int32_t* nvox,
+                                                  int32_t* errflag) {
+    __shared__ int wsum[4];
     const int s = blockIdx.x, tid = threadIdx.x;
     const int nt = prm[s].ntiles;
     int* h = hcnt + (size_t)s * maxT;
-    const int L = (nt + 1023) / 1024, t0 = min(nt, tid * L), t1 = min(nt, t0 + L);
+    const int L = (nt + 255) / 256, t0 = min(nt, tid * L), t1 = min(nt, t0 + L);
     int sum = 0;
     for (int t = t0; t < t1; ++t) sum += h[t];
     int total;
-    int run = vg_block_scan<16>(sum, wsum, &total);
+    int run = vg_block_scan<4>(sum, wsum, &total);
     for (int t = t0; t < t1; ++t) {
         const int x = h[t];
         h[t] = run;
@@ -1077,7 +1080,7 @@ int vg_run_groups(slo_ctx* ctx, const char* tag, const VgGroup* groups, int G) {
     int* starts = (int*)k1;
     int* ends = (int*)v1;
     SLO_LAUNCH(ctx, "vg_heads", k_vg_heads, grid, dim3(VG_T), 0, k0, w.off, w.prm, w.hcnt, maxT, S);
-    SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(1024), 0, src, w.prm, w.hcnt, maxT, w.nvox, w.errflag);
+    SLO_LAUNCH(ctx, "vg_hscan", k_vg_hscan, dim3(S), dim3(256), 0, src, w.prm, w.hcnt, maxT, w.nvox, w.errflag);
     if (SLO_VG_FUSED) {
         SLO_LAUNCH(ctx, "vg_reduce", k_vg_reduce, grid, dim3(VG_T), 0, src, k0, v0, w.off, w.prm, w.hcnt, maxT, w.meta,
                    w.longv, (int)w.nlong_cap, S);
@@ -1178,9 +1181,20 @@ __global__ void __launch_bounds__(1024) k_grid_build_lds(const float4* pts, size
     int32_t* O = off + (size_t)s * (T + 1);
     for (int k = tid; k < T; k += 1024) cnt[k] = 0;
     __syncthreads();
-    for (int i = tid; i < m; i += 1024) {
-        const float4 p = P[i];
-        atomicAdd(&cnt[grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T)], 1);
+    // GB_U points per thread in flight: the loop was one dependent global load
+    // per iteration (97 us per launch isolated at C3's ~20k points)
+    constexpr int GB_U = 8;
+    for (int i0 = 0; i0 < m; i0 += 1024 * GB_U) {
+        float4 q[GB_U];
+#pragma unroll
+        for (int u = 0; u < GB_U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            if (i < m) q[u] = P[i];
+        }
+#pragma unroll
+        for (int u = 0; u < GB_U; ++u)
+            if (i0 + u * 1024 + tid < m)
+                atomicAdd(&cnt[grid_hash(grid_cell(q[u].x, inv), grid_cell(q[u].y, inv), grid_cell(q[u].z, inv), T)], 1);
     }
     __syncthreads();
     const int per = (T + 1023) / 1024, k0 = tid * per, k1 = min(T, k0 + per);
@@ -1203,10 +1217,21 @@ __global__ void __launch_bounds__(1024) k_grid_build_lds(const float4* pts, size
     }
     if (tid == 1023) O[T] = run;   // == m: the stream's closing (empty) bucket
     __syncthreads();
-    for (int i = tid; i < m; i += 1024) {
-        const float4 p = P[i];
-        const int b = (int)grid_hash(grid_cell(p.x, inv), grid_cell(p.y, inv), grid_cell(p.z, inv), T);
-        ent[(size_t)s * ent_stride + atomicAdd(&cnt[b], 1)] = make_float4(p.x, p.y, p.z, __int_as_float(i));
+    for (int i0 = 0; i0 < m; i0 += 1024 * GB_U) {
+        float4 q[GB_U];
+#pragma unroll
+        for (int u = 0; u < GB_U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            if (i < m) q[u] = P[i];
+        }
+#pragma unroll
+        for (int u = 0; u < GB_U; ++u) {
+            const int i = i0 + u * 1024 + tid;
+            if (i < m) {
+                const int b = (int)grid_hash(grid_cell(q[u].x, inv), grid_cell(q[u].y, inv), grid_cell(q[u].z, inv), T);
+                ent[(size_t)s * ent_stride + atomicAdd(&cnt[b], 1)] = make_float4(q[u].x, q[u].y, q[u].z, __int_as_float(i));
+            }
+        }
     }
 }
 
