@@ -349,6 +349,7 @@ void slo_destroy(slo_ctx* ctx) {
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
     slo::graphs_drop(ctx);
     slo::vg_side_free(ctx);
+    slo::fa_prep_free(ctx);
     slo::vg_free(ctx);
     slo::pcl_free(ctx);
     slo::grid_free(ctx->grid_c);
@@ -491,10 +492,21 @@ namespace slo {
 // features, odometry, the mapping step when `map`, Scan Context detect.
 // Launches only (the host state is advanced by the caller), so the same
 // calls can be captured into a graph.
+// With at most SLO_PREP_DEFER_STREAMS streams the odometry's preparation of
+// the next scan's searches (fa_prep_*, slo_odom.hip) is left to the next step,
+// forked beside its projection and features: it leaves a scan's critical path.
+#ifndef SLO_PREP_DEFER_STREAMS
+#define SLO_PREP_DEFER_STREAMS 8
+#endif
 static int step_launches(slo_ctx* ctx, bool map) {
-    int r = ip_run(ctx);
+    // (not with a kernel-name timing filter: its in-stream stamps pair up per stream, as map_run's fork)
+    const bool defer = ctx->S <= SLO_PREP_DEFER_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
+    const bool forked = ctx->prep_pending && defer;
+    int r = forked ? fa_prep_fork(ctx) : 0;
+    if (!r) r = ip_run(ctx);
     if (!r) r = fa_features_run(ctx);
-    if (!r) r = fa_odometry_run(ctx, false);
+    if (!r && forked) r = fa_prep_join(ctx);
+    if (!r) r = fa_odometry_run(ctx, false, true, defer);
     if (r) return r;
     SLO_LAUNCH(ctx, "clear_flags", k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
     if (map && (r = map_run(ctx))) return r;

@@ -901,7 +901,10 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #endif
 #ifndef RING_W
 #define RING_W 4            // waves per ring (170 streams: 1.13 ms per launch against 1.53 with one wave,
-#endif                      // since block_sort's pool); 16 when the context has a few streams
+#endif                      // since block_sort's pool); RING_FEW_W when the context has a few streams
+#ifndef RING_FEW_W
+#define RING_FEW_W 16
+#endif
 // the ring VoxelGrid after its bounds (k_fa_ring_ds_pcl): the items into
 // LDS, std::sort's order (slo_pcl::block_sort), the voxel heads and the
 // centroids.  It: 64-bit (voxel << 32 | point) or 32-bit (voxel << 12 |
@@ -1150,10 +1153,10 @@ int fa_features_run(slo_ctx* ctx) {
     if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // RING_W waves per ring; slo_create refuses rings over 4096 points
         const bool few = S <= 8;
         if (v.cfg.horizon_scan <= 2048) {
-            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<2048, 16>), dim3(R, S), dim3(64 * 16), 0, v);
+            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<2048, RING_FEW_W>), dim3(R, S), dim3(64 * RING_FEW_W), 0, v);
             else SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<2048, RING_W>), dim3(R, S), dim3(64 * RING_W), 0, v);
         } else {
-            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<4096, 16>), dim3(R, S), dim3(64 * 16), 0, v);
+            if (few) SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<4096, RING_FEW_W>), dim3(R, S), dim3(64 * RING_FEW_W), 0, v);
             else SLO_LAUNCH(ctx, "fa_ring_ds", (k_fa_ring_ds_pcl<4096, RING_W>), dim3(R, S), dim3(64 * RING_W), 0, v);
         }
     } else {

@@ -74,6 +74,7 @@ struct StreamState {
     int32_t iters_surf, iters_corner;
     int32_t first_half;                   // deskew: first index with halfPassed
     int32_t odo_phase;                    // odometry control between launches (slo_odom.hip)
+    int32_t kd_set;                       // this scan's odometry (re)built the "trees" (k_fa_sx_kd's gate)
     int32_t seg_count, outlier_count;
     int32_t n_sharp, n_less_sharp, n_flat, n_less_flat;
     // mapping
@@ -571,6 +572,14 @@ struct slo_ctx {
     unsigned int ws_gen = 0;            // bumped whenever a workspace behind a captured pointer moves
     const float4* pp_corner0 = nullptr; // corner_last of layout 0
     bool vg_onesweep = false;           // VoxelGrid sort by single-pass scatters (env SLO_VG_ONESWEEP=1 at creation)
+    // the odometry's preparation of the next scan's search structures (the
+    // surf rings' x-order, the corner tree's x-order, the surf hash grid;
+    // slo_odom.hip fa_prep_*): a batched step of a few streams defers it to
+    // the next step, which runs it on prep_stream beside its projection and
+    // features; any other odometry entry runs a pending one in-stream first
+    bool prep_pending = false;
+    hipStream_t prep_stream = nullptr;
+    hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
 };
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -585,8 +594,11 @@ int pg_after_mapping(slo_ctx* ctx);
 int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx);
-int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse = true);
+int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse = true, bool defer = false);
 void fa_swap_last(slo_ctx* ctx);
+int fa_prep_fork(slo_ctx* ctx);    // a pending preparation on prep_stream (forked from / joined to ctx->stream)
+int fa_prep_join(slo_ctx* ctx);
+void fa_prep_free(slo_ctx* ctx);
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 int vg_ws_reinit(slo_ctx* ctx);    // the stream-ordered initialisation of the VoxelGrid workspaces, again

@@ -61,6 +61,76 @@ __device__ inline void nn1_grid(const GridView& g, int s, float gate, const P4& 
     if (bi == INT_MAX) { bi = -1; bd = FLT_MAX; }
 }
 
+// The same 1-NN by an aligned group of G lanes of one query (the few-stream
+// surf search, where one stream's queries leave most of the chip idle and a
+// query's latency is its chain of dependent loads): the walk of nn1_grid —
+// the probed cell, then the rows of the (2R+1)^2 box nearest first — with
+// each cell's / row's entry run dealt over the group (G x U loads in flight)
+// and the group's best (d, index) taken after each, so every row is cut by
+// the bound of all points seen so far.  Exact: rows and points are skipped
+// only when strictly farther than a distance already found, and the
+// (distance, index) minimum does not depend on the visiting order.
+template <int G>
+__device__ inline void nn1_grid_group(const GridView& g, int s, float gate, const P4& q, bool act, int sub, int& bi,
+                                      float& bd) {
+    constexpr int R = SLO_ODO_SURF_R, N = GridRows<R>::N, U = 2;
+    bi = INT_MAX; bd = gate;
+    if (act && isfinite(q.x) && isfinite(q.y) && isfinite(q.z)) {
+        const float inv = g.inv, cell = g.cell, c2 = cell * cell;
+        const int cx = grid_cell(q.x, inv), cy = grid_cell(q.y, inv), cz = grid_cell(q.z, inv);
+        const size_t gb = (size_t)s * (g.T + 1);
+        const int base = g.off[gb];
+        const float4* E = g.ent + (size_t)s * g.es;
+        auto run = [&](int e0, int e1, int yy, int zz, int xa, int xb, bool skip_cx) {   // entries [e0, e1)
+            for (int e = e0 + sub; e < e1; e += G * U) {
+                float4 p[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) p[u] = E[min(e + u * G, e1 - 1)];
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    if (e + u * G >= e1) break;
+                    const int px = grid_cell(p[u].x, inv);
+                    if (grid_cell(p[u].y, inv) != yy || grid_cell(p[u].z, inv) != zz || px < xa || px > xb ||
+                        (skip_cx && px == cx)) continue;
+                    const float d = sqdist_flann(q, p[u]);
+                    const int idx = __float_as_int(p[u].w);
+                    if (d < bd || (d == bd && idx < bi)) { bd = d; bi = idx; }
+                }
+            }
+#pragma unroll
+            for (int o = 1; o < G; o <<= 1) {
+                const float d2 = __shfl_xor(bd, o, 64);
+                const int i2 = __shfl_xor(bi, o, 64);
+                if (d2 < bd || (d2 == bd && i2 < bi)) { bd = d2; bi = i2; }
+            }
+        };
+        {   // the probed cell
+            const int h0 = (int)grid_hash(cx, cy, cz, g.T);
+            run(g.off[gb + h0] - base, g.off[gb + h0 + 1] - base, cy, cz, cx, cx, false);
+        }
+        for (int k = 0; k < N; ++k) {   // bd, bi: the same in the group's lanes here
+            const float b = bd;
+            if ((float)kGridRows<R>.gap[k] * c2 > b) break;
+            const int dy = kGridRows<R>.dy[k], dz = kGridRows<R>.dz[k];
+            const int yy = cy + dy, zz = cz + dz;
+            const float ey = dy > 0 ? (float)yy * cell - q.y : (dy < 0 ? q.y - (float)(yy + 1) * cell : 0.0f);
+            const float ez = dz > 0 ? (float)zz * cell - q.z : (dz < 0 ? q.z - (float)(zz + 1) * cell : 0.0f);
+            float lb = ey * ey;
+            lb += ez * ez;
+            if (lb > b) continue;
+            const float rx = sqrtf((b - lb) * 1.0001f + 1e-5f * b) + 1e-3f;
+            const int xa = max(cx - R, grid_cell(q.x - rx, inv)), xb = min(cx + R, grid_cell(q.x + rx, inv));
+            const int h = (int)grid_hash(xa, yy, zz, g.T), len = xb - xa + 1;
+            const int h2 = min(h + len, g.T), w1 = h + len - h2;   // w1: buckets wrapped to the table start
+            const int e0 = g.off[gb + h] - base, e1 = g.off[gb + h2] - base;
+            const int f1 = w1 > 0 ? g.off[gb + w1] - base : 0;
+            run(e0, e1, yy, zz, xa, xb, k == 0);   // k == 0: the probed cell's row
+            if (w1 > 0) run(0, f1, yy, zz, xa, xb, k == 0);
+        }
+    }
+    if (bi == INT_MAX) { bi = -1; bd = FLT_MAX; }
+}
+
 // block-wide double-double sum of NV terms + one int (slo_ddsum.h); result
 // valid in lane 0 of wave 0
 template <int NV>
@@ -272,6 +342,7 @@ __global__ void __launch_bounds__(256) k_fa_odo_begin(DevView v, int first_scan)
         if (tid == 0) {
             st.cornerLastNum = nLS; st.surfLastNum = nLF;
             st.kdCornerNum = nLS; st.kdSurfNum = nLF;
+            st.kd_set = 1;
             st.iters_surf = st.iters_corner = 0;
             st.odo_phase = 3;
             st.transformSum[0] += v.imu[s].pitchStart;   // FA:1633-1634
@@ -382,7 +453,7 @@ __global__ void __launch_bounds__(256) k_fa_sx_rings(DevView v, int nb) {
     const int R = v.cfg.n_scan;
     const int lane = threadIdx.x & 63, r = chunk * 4 + (threadIdx.x >> 6);
     if (r >= R) return;
-    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + 1) * (R + 1);   // == roff_cur after k_fa_odo_finish
     const int a = rf[r], n = rf[r + 1] - a;
     if (n <= 0) return;
     const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
@@ -405,7 +476,7 @@ __global__ void __launch_bounds__(256) k_fa_sx_long(DevView v, int nb) {
     xcd_stream_chunk(blockIdx.x, nb, s, r);
     if (s >= v.S) return;
     const int R = v.cfg.n_scan;
-    const int32_t* rf = v.roff_cur + ((size_t)s * 2 + 1) * (R + 1);
+    const int32_t* rf = v.roff_last + ((size_t)s * 2 + 1) * (R + 1);
     const int a = rf[r], n = rf[r + 1] - a;
     if (n <= 512) return;
     const float4* in = v.surf_next + (size_t)s * v.cap_less_flat;
@@ -462,7 +533,7 @@ template <int NP>
 __global__ void __launch_bounds__(1024) k_fa_sx_kd(DevView v) {
     const int s = blockIdx.x;
     const StreamState& st = v.st[s];
-    if (!(st.odo_phase == 3 || (st.n_less_sharp > 10 && st.n_less_flat > 100))) return;
+    if (!st.kd_set) return;
     const int n = st.kdCornerNum;
     const float4* in = v.kd_corner + (size_t)s * v.cap_less_sharp;
     float4* out = v.sx_kd_corner + (size_t)s * v.cap_less_sharp;
@@ -663,15 +734,19 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
 
 // The same for a context of a few streams, where one stream's queries leave
 // most of the chip idle and the search is the odometry's latency: eight lanes
-// per query.  Each lane finds the 1-NN (the same walk as k_fa_search_surf's
-// thread; dealing the grid rows over the lanes measured twice as slow, every
-// lane pruning by its own, looser bound), then the five ring walks run one
+// per query.  The lanes find the 1-NN together, eight grid rows per round
+// with the bound shared after each (nn1_grid_group; dealing the rows with
+// every lane pruning by its own, looser bound measured twice as slow as one
+// lane's walk), then the five ring walks run one
 // per lane — lane 0 the closest point's ring (the 2nd point), lanes 1-4 rings
 // cscan - 2, - 1, + 1, + 2 (the 3rd) — and the 3rd point's four bests merge
 // in WalkBest's order, a strict total order on (distance, class, index): the
 // minimum over all offers, whatever the order of the rings.  Same results as
 // k_fa_search_surf.
 #define SURF_QL 8
+#ifndef SLO_SURF_GROUP_NN
+#define SLO_SURF_GROUP_NN 1   // the 1-NN by the query's eight lanes with a shared bound (nn1_grid_group)
+#endif
 #ifndef SLO_ODO_FEW
 #define SLO_ODO_FEW 8   // at most this many streams: k_fa_search_surf_few
 #endif
@@ -699,7 +774,19 @@ __global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
     auto ring_first = [&](int r) { return rf[min(max(r, 0), R)]; };
     int ci = -1;
     float cd = FLT_MAX;
+#if SLO_DIAG_ODO
+    // per wave: [4] / [5] the slowest wave's 1-NN / walk cycles, [6] / [7] their sums, [0] waves
+    unsigned long long t_d = clock64(), t_nn = 0;
+#endif
+#if SLO_SURF_GROUP_NN
+    nn1_grid_group<SURF_QL>(v.g_os, s, gate, sel, active, sub, ci, cd);
+#else
     if (active) nn1_grid(v.g_os, s, gate, sel, ci, cd);
+#endif
+#if SLO_DIAG_ODO
+    t_nn = clock64() - t_d;
+    t_d = clock64();
+#endif
     const float4* sx = v.sx_surf_last + (size_t)s * v.cap_less_flat;
     const float4* slast = v.surf_last + (size_t)s * v.cap_less_flat;
     const int surfLastNum = st.surfLastNum;
@@ -729,6 +816,13 @@ __global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
         const int c2 = __shfl_xor(w3.cls, o, 64), t2 = __shfl_xor(w3.t, o, 64);
         if (walk_better(d2, c2, t2, w3)) { w3.d = d2; w3.cls = c2; w3.t = t2; }
     }
+#if SLO_DIAG_ODO
+    if ((threadIdx.x & 63) == 0) {
+        const unsigned long long t_w = clock64() - t_d;
+        atomicMax(&v.st[s].dbg[4], t_nn); atomicMax(&v.st[s].dbg[5], t_w);
+        atomicAdd(&v.st[s].dbg[6], t_nn); atomicAdd(&v.st[s].dbg[7], t_w); atomicAdd(&v.st[s].dbg[0], 1ull);
+    }
+#endif
     if (!active || sub != 0) return;
     int32_t* ind = v.ind_surf + (size_t)s * v.cap_flat * 3;
     ind[3 * i] = found ? ci : -1;
@@ -1056,7 +1150,8 @@ __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v, int fuse) {
         const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;
-        if (nLS > 10 && nLF > 100) { st.kdCornerNum = nLS; st.kdSurfNum = nLF; }
+        st.kd_set = nLS > 10 && nLF > 100;
+        if (st.kd_set) { st.kdCornerNum = nLS; st.kdSurfNum = nLF; }
     }
 }
 
@@ -1069,9 +1164,75 @@ void fa_swap_last(slo_ctx* ctx) {
     std::swap(ctx->v.sx_surf_last, ctx->v.sx_surf_next);
 }
 
+// The preparation of the next scan's searches: the surf rings' x-order, the
+// corner tree's x-order (both read the clouds this scan's odometry wrote: the
+// ping-pong halves before fa_swap_last, prep_view) and the hash grid over the
+// surf tree cloud (setInputCloud; the corner tree is a windowed brute force
+// over its x-sorted copy).  Nothing before the next scan's searches reads
+// them, and nothing the next scan's projection and features write feeds them
+// (the ring offsets come from roff_last, the gate from StreamState::kd_set).
+static DevView prep_view(const DevView& v) {
+    DevView p = v;
+    std::swap(p.corner_last, p.corner_next);
+    std::swap(p.surf_last, p.surf_next);
+    std::swap(p.sx_surf_last, p.sx_surf_next);
+    return p;
+}
+static int fa_prep_launch(slo_ctx* ctx) {
+    const DevView v = prep_view(ctx->v);
+    const int S = ctx->S, R = v.cfg.n_scan;
+    ctx->prep_pending = false;
+    if (!SLO_SURF_LINEAR) {
+        SLO_LAUNCH(ctx, "fa_sx_rings", k_fa_sx_rings, dim3(xcd_grid(S, (R + 3) / 4)), dim3(256), 0, v, (R + 3) / 4);
+        if (v.cfg.horizon_scan > 512)
+            SLO_LAUNCH(ctx, "fa_sx_long", k_fa_sx_long, dim3(xcd_grid(S, R)), dim3(256), 0, v, R);
+    }
+    if (v.cap_less_sharp <= 4096) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<4096>, dim3(S), dim3(1024), 0, v);
+    else if (v.cap_less_sharp <= 8192) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<8192>, dim3(S), dim3(1024), 0, v);
+    else SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<16384>, dim3(S), dim3(1024), 0, v);
+    SLO_CHECK(hipGetLastError());
+    const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
+    return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
+}
+
+int fa_prep_fork(slo_ctx* ctx) {
+    if (!ctx->prep_pending) return 0;
+    if (!ctx->prep_stream) {
+        SLO_CHECK(hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking));
+        SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
+        SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pjoin, hipEventDisableTiming));
+    }
+    SLO_CHECK(hipEventRecord(ctx->ev_pfork, ctx->stream));
+    SLO_CHECK(hipStreamWaitEvent(ctx->prep_stream, ctx->ev_pfork, 0));
+    std::swap(ctx->stream, ctx->prep_stream);
+    const int r = fa_prep_launch(ctx);
+    std::swap(ctx->stream, ctx->prep_stream);
+    if (r) return r;
+    SLO_CHECK(hipEventRecord(ctx->ev_pjoin, ctx->prep_stream));
+    return 0;
+}
+
+int fa_prep_join(slo_ctx* ctx) {
+    if (ctx->prep_stream) SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_pjoin, 0));
+    return 0;
+}
+
+void fa_prep_free(slo_ctx* ctx) {
+    if (!ctx->prep_stream) return;
+    hipStreamSynchronize(ctx->prep_stream);
+    hipEventDestroy(ctx->ev_pfork);
+    hipEventDestroy(ctx->ev_pjoin);
+    hipStreamDestroy(ctx->prep_stream);
+    ctx->prep_stream = nullptr;
+}
+
 // fuse: transformFusion's /integrated_to_init in k_fa_odo_finish (false on a
-// Mode S odometry context, slo_odom_process: the mapping context computes it)
-int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse) {
+// Mode S odometry context, slo_odom_process: the mapping context computes it).
+// defer: leave the next scan's preparation pending (the batched step of a few
+// streams forks it beside its next projection and features, fa_prep_fork)
+int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse, bool defer) {
+    if (ctx->prep_pending)
+        if (int r = fa_prep_launch(ctx)) return r;   // the last scan's, in-stream
     DevView& v = ctx->v;
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
@@ -1091,22 +1252,10 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse) {
     }
     SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v, fuse ? 1 : 0);
-    const int R = v.cfg.n_scan;
-    if (!SLO_SURF_LINEAR)
-    {
-        SLO_LAUNCH(ctx, "fa_sx_rings", k_fa_sx_rings, dim3(xcd_grid(S, (R + 3) / 4)), dim3(256), 0, v, (R + 3) / 4);
-        if (v.cfg.horizon_scan > 512)
-            SLO_LAUNCH(ctx, "fa_sx_long", k_fa_sx_long, dim3(xcd_grid(S, R)), dim3(256), 0, v, R);
-    }
-    if (v.cap_less_sharp <= 4096) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<4096>, dim3(S), dim3(1024), 0, v);
-    else if (v.cap_less_sharp <= 8192) SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<8192>, dim3(S), dim3(1024), 0, v);
-    else SLO_LAUNCH(ctx, "fa_sx_kd", k_fa_sx_kd<16384>, dim3(S), dim3(1024), 0, v);
     SLO_CHECK(hipGetLastError());
     fa_swap_last(ctx);
-    // setInputCloud: hash grid over the (possibly unchanged) surf tree cloud
-    // (the corner tree by a windowed brute force over its x-sorted copy, k_fa_sx_kd)
-    const int SS = (int)(sizeof(StreamState) / sizeof(int32_t));
-    return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
+    ctx->prep_pending = true;
+    return defer ? 0 : fa_prep_launch(ctx);
 }
 
 }  // namespace slo
