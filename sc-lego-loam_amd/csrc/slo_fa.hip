@@ -199,7 +199,7 @@ __device__ void extract_ring_global(const DevView& v, int s, int ring) {
     const int tid = threadIdx.x;
     if (tid < 6) {
         const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
-        if (sp < ep) slo_sort::std_sort(sm + sp, ep - sp, SmoothLess());
+        if (sp < ep) slo_sort::std_sort_small(sm + sp, ep - sp, SmoothLess());
     }
     __syncthreads();
     if (tid != 0) return;
@@ -469,7 +469,7 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     SORT_STAMP(1)
     if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
         const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
-        slo_sort::std_sort(&lsm[sp - lo], ep - sp, SmoothLess());
+        slo_sort::std_sort_small(&lsm[sp - lo], ep - sp, SmoothLess());
     }
     __syncthreads();
     SORT_STAMP(2)

@@ -201,4 +201,54 @@ SLO_SORT_HD void introsort_range(T* first, int n, int depth, Less less) {
     insertion_sort_(first, first + n, less);
 }
 
+// The two loops above for n <= 8191 (the GPU's lane tasks: PCL-sort ranges
+// of an LDS finish entry, featureAssociation's sector sorts), with the stack
+// packed one entry per 32-bit word (lo 13 | hi 13 | depth 6 bits): 256 B of
+// private memory per lane instead of 768.  The depths on the stack strictly
+// decrease from bottom to top (a push stores the decremented depth of the
+// range in hand, and a popped range's pushes store less again), so it holds
+// at most depth + 1 <= 64 entries.  The same steps in the same order.
+template <class T, class Less>
+SLO_SORT_HD void introsort_loop_small_(T* first, int n, int depth, Less less) {
+    unsigned int st[64];
+    int sp = 0;
+    st[sp++] = (unsigned int)n << 13 | (unsigned int)depth << 26;
+    while (sp > 0) {
+        const unsigned int e = st[--sp];
+        int lo = (int)(e & 0x1fffu), hi = (int)((e >> 13) & 0x1fffu), dep = (int)(e >> 26);
+        while (hi - lo > 16) {
+            if (dep == 0) {
+                heap_sort_(first + lo, hi - lo, less);
+                break;
+            }
+            --dep;
+            T* f = first + lo;
+            T* l = first + hi;
+            T* mid = f + (hi - lo) / 2;
+            move_median_to_first_(f, f + 1, mid, l - 1, less);
+            T* cut = unguarded_partition_(f + 1, l, f, less);
+            const int c = (int)(cut - first);
+            st[sp++] = (unsigned int)c | (unsigned int)hi << 13 | (unsigned int)dep << 26;
+            hi = c;
+        }
+    }
+}
+template <class T, class Less>
+SLO_SORT_HD void std_sort_small(T* first, int n, Less less) {   // std_sort, n <= 8191
+    if (n <= 1) return;
+    introsort_loop_small_(first, n, 2 * lg_(n), less);
+    if (n > 16) {
+        insertion_sort_(first, first + 16, less);
+        for (T* i = first + 16; i != first + n; ++i) unguarded_linear_insert_(i, less);
+    } else {
+        insertion_sort_(first, first + n, less);
+    }
+}
+template <class T, class Less>
+SLO_SORT_HD void introsort_range_small(T* first, int n, int depth, Less less) {   // introsort_range, n <= 8191
+    if (n <= 1) return;
+    introsort_loop_small_(first, n, depth, less);
+    insertion_sort_(first, first + n, less);
+}
+
 }  // namespace slo_sort

@@ -671,7 +671,7 @@ __device__ __forceinline__ void lane_flush(It* items, const unsigned int* q, int
     if (lane < nq) {
         const unsigned int e = q[lane];
         const int f = (int)(e & 0x1fffu), l = (int)((e >> 13) & 0x1fffu), d = (int)(e >> 26);
-        slo_sort::introsort_range(items + f, l - f, d, LessT<It>());
+        slo_sort::introsort_range_small(items + f, l - f, d, LessT<It>());
     }
     wave_fence();
 }

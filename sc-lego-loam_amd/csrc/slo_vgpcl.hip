@@ -1107,7 +1107,7 @@ __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned i
             if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
         } else if (threadIdx.x == 0) {
             atomicAdd(&cstat[0], 1);
-            slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());
+            slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());   // any n (a range over PT_MAXT tiles)
         }
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += 256) {

@@ -1,4 +1,4 @@
-// introsort_check.cpp — compares slo_sort::std_sort (the restatement the GPU
+// introsort_check.cpp — compares slo_sort::std_sort and std_sort_small (the restatements the GPU
 // feature extraction runs per lane) with the host libstdc++ std::sort on
 // cloudSmoothness-like arrays full of ties (FA:699 sorts by value only, so the
 // permutation of equal keys is implementation-defined and must match).
@@ -24,14 +24,30 @@ int main() {
             if (rep % 7 == 1) std::sort(a.begin(), a.end(), [](const Smooth& x, const Smooth& y) { return x.ind > y.ind; });
             if (rep % 11 == 2)   // sorted / reverse-sorted inputs drive the depth limit
                 std::sort(a.begin(), a.end(), [](const Smooth& x, const Smooth& y) { return x.value > y.value; });
-            std::vector<Smooth> b = a;
+            std::vector<Smooth> b = a, c = a;
             auto less = [](const Smooth& x, const Smooth& y) { return x.value < y.value; };
             std::sort(a.begin(), a.end(), less);
             slo_sort::std_sort(b.data(), n, less);
+            slo_sort::std_sort_small(c.data(), n, less);   // the packed-stack form the GPU lanes run
             ++cases;
             for (int i = 0; i < n; ++i)
-                if (a[i].ind != b[i].ind || a[i].value != b[i].value) { ++bad; break; }
+                if (a[i].ind != b[i].ind || a[i].value != b[i].value || a[i].ind != c[i].ind) { ++bad; break; }
         }
+    // introsort_range_small against introsort_range (the PCL-sort lane tasks:
+    // a sub-range with `depth` levels of budget left, depth 0 included)
+    for (int rep = 0; rep < 3000; ++rep) {
+        const int n = (int)(nx() % 300), depth = (int)(nx() % 27), levels = 1 + (int)(nx() % 12);
+        std::vector<Smooth> a(n);
+        for (int i = 0; i < n; ++i) a[i] = {(float)(nx() % levels), i};
+        if (rep % 5 == 1) std::sort(a.begin(), a.end(), [](const Smooth& x, const Smooth& y) { return x.value > y.value; });
+        std::vector<Smooth> b = a;
+        auto less = [](const Smooth& x, const Smooth& y) { return x.value < y.value; };
+        slo_sort::introsort_range(a.data(), n, depth, less);
+        slo_sort::introsort_range_small(b.data(), n, depth, less);
+        ++cases;
+        for (int i = 0; i < n; ++i)
+            if (a[i].ind != b[i].ind) { ++bad; break; }
+    }
     printf("%ld %ld\n", bad, cases);
     return 0;
 }
