@@ -903,7 +903,7 @@ __global__ void __launch_bounds__(256) k_fa_ring_ds(DevView v) {
 #define RING_W 4            // waves per ring (170 streams: 1.13 ms per launch against 1.53 with one wave,
 #endif                      // since block_sort's pool); RING_FEW_W when the context has a few streams
 #ifndef RING_FEW_W
-#define RING_FEW_W 16
+#define RING_FEW_W 8        // one stream: 182 us per launch against 199 with 16 waves and 180 with 4 (r05)
 #endif
 // the ring VoxelGrid after its bounds (k_fa_ring_ds_pcl): the items into
 // LDS, std::sort's order (slo_pcl::block_sort), the voxel heads and the
