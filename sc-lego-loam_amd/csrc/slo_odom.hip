@@ -18,6 +18,7 @@
 #include "slo_internal.h"
 #include "slo_libm.h"
 #include "slo_pose.h"
+#include "slo_pose_wave.h"
 #include "slo_linalg.h"
 #include <float.h>
 
@@ -1126,27 +1127,52 @@ __global__ void __launch_bounds__(256) k_fa_to_end(DevView v) {
     }
 }
 
-// integrate (FA:1697-1725) and the *Last / tree bookkeeping, per stream
+// integrate (FA:1697-1725) and the *Last / tree bookkeeping, per stream.
+// One wave: the trig of integrateTransformation and of transformFusion's
+// hand-off runs on its lanes side by side (slo_pose_wave.h; 53 -> ~15 us on
+// one stream), lane 0 stores.
 __global__ void __launch_bounds__(64) k_fa_odo_finish(DevView v, int fuse) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
     if (st.odo_phase == 3) return;
     copy_ring_offsets(v, s);
-    if (threadIdx.x == 0) {
-        float tc[6];
-        for (int k = 0; k < 6; ++k) tc[k] = st.transformCur[k];
-        const ImuState& m = v.imu[s];
-        const float imu[9] = {m.shiftFromStart[0], m.shiftFromStart[1], m.shiftFromStart[2], m.pitchStart, m.yawStart,
-                              m.rollStart, m.pitchLast, m.yawLast, m.rollLast};
-        slo_pose::integrate(st.transformSum, tc, imu);
-        // TransformFusion::laserOdometryHandler (TF:186-219): this scan's
-        // odometry through the tf round trip, associated to the map with the
-        // last published mapping result (this scan's mapping comes after)
-        if (fuse) {
-            float sum[6], incre[6];
-            slo_pose::odom_handoff(st.transformSum, sum);
-            slo_pose::associate_to_map(sum, st.tf_bef, st.tf_aft, incre, st.integrated);
-        }
+    const bool w0 = threadIdx.x == 0;
+    float tc[6], sum0[6], sum[6];
+    for (int k = 0; k < 6; ++k) { tc[k] = st.transformCur[k]; sum0[k] = st.transformSum[k]; }
+    const ImuState& m = v.imu[s];
+    const float imu[9] = {m.shiftFromStart[0], m.shiftFromStart[1], m.shiftFromStart[2], m.pitchStart, m.yawStart,
+                          m.rollStart, m.pitchLast, m.yawLast, m.rollLast};
+#ifdef SLO_DIAG_FIN   // [0] integrate, [1] odom_handoff, [2] associate_to_map cycles, [3] calls
+    unsigned long long t0 = clock64();
+#endif
+    slo_pose::integrate_w(sum0, tc, imu, sum);
+#ifdef SLO_DIAG_FIN
+    unsigned long long t1 = clock64();
+    if (w0) { st.dbg[0] += t1 - t0; st.dbg[3] += 1; }
+#endif
+    // TransformFusion::laserOdometryHandler (TF:186-219): this scan's
+    // odometry through the tf round trip, associated to the map with the
+    // last published mapping result (this scan's mapping comes after)
+    float tbm[6];
+    if (fuse) {
+        float h[6], incre[6];
+#ifdef SLO_DIAG_FIN
+        unsigned long long t2 = clock64();
+#endif
+        slo_pose::odom_handoff_w(sum, h);
+#ifdef SLO_DIAG_FIN
+        unsigned long long t3 = clock64();
+#endif
+        slo_pose::associate_to_map_w(h, st.tf_bef, st.tf_aft, incre, tbm);
+#ifdef SLO_DIAG_FIN
+        unsigned long long t4 = clock64();
+        if (w0) { st.dbg[1] += t3 - t2; st.dbg[2] += t4 - t3; }
+#endif
+    }
+    if (w0) {
+        for (int k = 0; k < 6; ++k) st.transformSum[k] = sum[k];
+        if (fuse)
+            for (int k = 0; k < 6; ++k) st.integrated[k] = tbm[k];
         const int nLS = st.n_less_sharp, nLF = st.n_less_flat;
         st.cornerLastNum = nLS;
         st.surfLastNum = nLF;
