@@ -89,15 +89,16 @@ SLO_LA_HD void solve_qr(const float* A, const float* b, int m, int n, float* x) 
     else solve_qr_t<6, 6>(A, b, x);
 }
 
-// Jacobi eigen-decomposition of a symmetric n x n (n <= 6)
+// Jacobi eigen-decomposition of a symmetric n x n (n <= 6).  The rotation
+// indices are data-dependent, so on the GPU the matrix, W, V and the row /
+// column maxima live in memory: eigen_sym_ws takes them from the caller
+// (LDS in the one-lane solves, where private arrays went to scratch memory).
 template <int N>
-SLO_LA_HD void eigen_sym_t(const float* S, float* W, float* V) {
+SLO_LA_HD void eigen_sym_ws(const float* S, float* W, float* V, float* A, int* indR, int* indC) {
     constexpr int n = N;
-    float A[N * N];
 #pragma unroll
     for (int i = 0; i < n * n; ++i) A[i] = S[i];
     const float eps = FLT_EPSILON;
-    int indR[6], indC[6];
     for (int i = 0; i < n; i++) {
         for (int j = 0; j < n; j++) V[i * n + j] = 0.0f;
         V[i * n + i] = 1.0f;
@@ -163,11 +164,18 @@ SLO_LA_HD void eigen_sym_t(const float* S, float* W, float* V) {
         }
     }
 }
+template <int N>
+SLO_LA_HD void eigen_sym_t(const float* S, float* W, float* V) {
+    float A[N * N];
+    int indR[6], indC[6];
+    eigen_sym_ws<N>(S, W, V, A, indR, indC);
+}
 SLO_LA_HD void eigen_sym(const float* S, int n, float* W, float* V) {
     if (n == 3) eigen_sym_t<3>(S, W, V);
     else eigen_sym_t<6>(S, W, V);
 }
 
+SLO_LA_HD void inv_ws(const float* S, int n, float* D, float* A, float* b);
 SLO_LA_HD void inv(const float* S, int n, float* D) {
     if (n == 3) {
         double s00 = S[0], s01 = S[1], s02 = S[2], s10 = S[3], s11 = S[4], s12 = S[5], s20 = S[6], s21 = S[7], s22 = S[8];
@@ -186,6 +194,10 @@ SLO_LA_HD void inv(const float* S, int n, float* D) {
         return;
     }
     float A[36], b[36];
+    inv_ws(S, n, D, A, b);
+}
+// the n > 3 LU inverse with the caller's workspaces A, b (n * n each)
+SLO_LA_HD void inv_ws(const float* S, int n, float* D, float* A, float* b) {
     for (int i = 0; i < n * n; ++i) { A[i] = S[i]; b[i] = 0; }
     for (int i = 0; i < n; ++i) b[i * n + i] = 1;
     const float eps = FLT_EPSILON * 10;

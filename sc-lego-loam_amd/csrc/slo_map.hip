@@ -646,6 +646,9 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
     __shared__ slo_dd::DD s_acc[27];
     __shared__ int s_nsel;
     const int lane = threadIdx.x;
+#ifdef SLO_DIAG_FIN   // [4] fold, [5] solve_qr, [6] degeneracy (iteration 0), [7] the rest, cycles
+    unsigned long long tq0 = clock64();
+#endif
     if (lane < 27) {
         slo_dd::DD a = slo_dd::zero();
         const double* part = v.mo_part + (size_t)s * SLO_MO_BLOCKS * SLO_MO_PART + 2 * lane;
@@ -673,10 +676,19 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
             AtA[i * 6 + j] = f; AtA[j * 6 + i] = f;
         }
     for (int i = 0; i < 6; ++i) AtB[i] = slo_dd::to_float(acc[21 + i]);
+#ifdef SLO_DIAG_FIN
+    unsigned long long tq1 = clock64();
+#endif
     slo_la::solve_qr(AtA, AtB, 6, 6, X);
+#ifdef SLO_DIAG_FIN
+    unsigned long long tq2 = clock64();
+#endif
     if (iterCount == 0) {
-        float E[6], V[36], V2[36], Vi[36];
-        slo_la::eigen_sym(AtA, 6, E, V);
+        // the data-indexed matrices in LDS (as private arrays they lived in
+        // scratch memory: ~100 us of this one lane per mapping step)
+        __shared__ float E[6], V[36], V2[36], Vi[36], wa[36], wb[36];
+        __shared__ int wr[6], wc[6];
+        slo_la::eigen_sym_ws<6>(AtA, E, V, wa, wr, wc);
         for (int i = 0; i < 36; ++i) V2[i] = V[i];
         st.isDegenerate_mo = 0;
         for (int i = 5; i >= 0; i--) {
@@ -685,9 +697,12 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
                 st.isDegenerate_mo = 1;
             } else break;
         }
-        slo_la::inv(V, 6, Vi);
+        slo_la::inv_ws(V, 6, Vi, wa, wb);
         slo_la::mul(Vi, V2, 6, 6, 6, st.matP_mo);
     }
+#ifdef SLO_DIAG_FIN
+    unsigned long long tq3 = clock64();
+#endif
     if (st.isDegenerate_mo) {
         float X2[6];
         for (int i = 0; i < 6; ++i) X2[i] = X[i];
@@ -700,6 +715,10 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
     float deltaR = (float)sqrt(r0 * r0 + r1 * r1 + r2 * r2);
     float deltaT = (float)sqrt(t0 * t0 + t1 * t1 + t2 * t2);
     if (deltaR < 0.05 && deltaT < 0.05) st.mo_converged = 1;
+#ifdef SLO_DIAG_FIN
+    unsigned long long tq4 = clock64();
+    st.dbg[4] += tq1 - tq0; st.dbg[5] += tq2 - tq1; st.dbg[6] += tq3 - tq2; st.dbg[7] += tq4 - tq3;
+#endif
 }
 
 // ---------------------------------------------------------------- keyframe + Scan Context make

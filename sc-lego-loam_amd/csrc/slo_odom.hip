@@ -175,8 +175,10 @@ __device__ inline bool solve_step(StreamState& st, const slo_dd::DD* acc, int it
     float AtB[3] = {r[6], r[7], r[8]};
     slo_la::solve_qr(AtA, AtB, 3, 3, X);
     if (iterCount == 0) {
-        float E[3], V[9], V2[9], Vi[9];
-        slo_la::eigen_sym(AtA, 3, E, V);
+        // the data-indexed arrays in LDS (private ones went to scratch memory)
+        __shared__ float E[3], V[9], V2[9], Vi[9], wa[9];
+        __shared__ int wr[6], wc[6];
+        slo_la::eigen_sym_ws<3>(AtA, E, V, wa, wr, wc);
         for (int i = 0; i < 9; ++i) V2[i] = V[i];
         st.isDegenerate_fa = 0;
         for (int i = 2; i >= 0; i--) {
