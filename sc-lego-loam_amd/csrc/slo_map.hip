@@ -25,6 +25,7 @@
 #include <memory>
 #include "slo_libm.h"
 #include "slo_pose.h"
+#include "slo_pose_wave.h"
 #include "slo_linalg.h"
 #include "slo_scdist.h"
 #include <float.h>
@@ -187,15 +188,33 @@ __global__ void k_mo_prepare(DevView v) {
     // extractSurroundingKeyFrames without loop closure: the radius branch
     // reads the pose of the last run, before associate_to_map below
     if (!v.cfg.loop_closure_enable && st.n_keyframes > 0) mo_surrounding_radius(v, s, st);
-    if (threadIdx.x != 0) return;
+    if (threadIdx.x >= 64) return;
+    // laserOdometryHandler (via the tf round trip), transformAssociateToMap
+    // and pointAssociateToMap's sin/cos, their trig side by side on wave 0's
+    // lanes (slo_pose_wave.h); lane 0 stores
+    {
+        float ts[6], bef[6], aft[6], sum[6], inc[6], tbm[6];
+        for (int k = 0; k < 6; ++k) {
+            ts[k] = st.transformSum[k]; bef[k] = st.transformBefMapped[k]; aft[k] = st.transformAftMapped[k];
+        }
+        slo_pose::odom_handoff_w(ts, sum);
+        slo_pose::associate_to_map_w(sum, bef, aft, inc, tbm);
+        const float a3[3] = {tbm[0], tbm[1], tbm[2]};
+        float sn[3], cs[3];
+        slo_pose::wave_sincos<3>(a3, sn, cs);
+        if (threadIdx.x != 0) return;
+        for (int k = 0; k < 6; ++k) {
+            st.mo_sum[k] = sum[k]; st.transformTobeMapped[k] = tbm[k];
+        }
+        for (int k = 3; k < 6; ++k) st.transformIncre[k] = inc[k];   // associate_to_map writes incre[3..5]
+        float* o = st.mo_trig;   // mo_store_trig
+        o[0] = sn[0]; o[1] = cs[0]; o[2] = sn[1]; o[3] = cs[1]; o[4] = sn[2]; o[5] = cs[2];
+        o[6] = tbm[3]; o[7] = tbm[4]; o[8] = tbm[5];
+    }
     st.mo_ran = 1;
     st.kf_saved = 0;
     st.mo_iters = 0;
     st.mo_converged = 0;
-    slo_pose::odom_handoff(st.transformSum, st.mo_sum);   // laserOdometryHandler, via the tf round trip
-    slo_pose::associate_to_map(st.mo_sum, st.transformBefMapped, st.transformAftMapped, st.transformIncre,
-                               st.transformTobeMapped);
-    mo_store_trig(st);
     // extractSurroundingKeyFrames: recent keyframe deque
     const int nk = st.n_keyframes;
     const int N = v.cfg.surrounding_keyframe_search_num;
