@@ -64,6 +64,10 @@ using slo_pcl::u64;
                           // 3 / 6 / 9 / 12: the tail 39.9 / 27.1 / 21.3 / 21.1 ms, the levels 21.0 / 23.3 / 24.9 /
                           // 26.4 ms per 6 mapping steps; 18.8k / 19.0k / 19.1k / 19.0k scans/s
 #endif
+#ifndef PC_XLEV_FEW
+#define PC_XLEV_FEW 0     // a few streams: no extra levels (an empty level is five launches of latency; the tail's
+                          // workgroups step what is left): one stream's mapping sorts 2.27 -> 2.02 ms (r05)
+#endif
 #ifndef PC_LOCC
 #define PC_LOCC 8         // waves per SIMD k_pc_lrank is built for (latency-bound streaming)
 #endif
@@ -1173,7 +1177,7 @@ static int pcl_levels(size_t stride, int tail_min, bool few) {
     int g = 0;
     size_t x = (size_t)tail_min;
     while (x < stride) { x <<= 1; ++g; }
-    return g ? g + (few ? 3 : PC_XLEV) : 0;   // (a few streams: each level is five launches of latency)
+    return g ? g + (few ? PC_XLEV_FEW : PC_XLEV) : 0;   // (a few streams: each level is five launches of latency)
 }
 
 int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, const VgParams* prm,
