@@ -672,6 +672,9 @@ def main():
     maxlag = max(lag(g) for g in range(len(groups)))
     nwin = a.profile_steps + a.warmup + a.steps + maxlag
     dev = torch.empty((max(nwin, a.chunk), S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+    free_after = torch.cuda.mem_get_info(local)[0]   # what is left for the runtime's scratch and the legs after
+    if free_after < 2**30:
+        print(f"bench: only {free_after / 2**20:.0f} MiB of HBM left after the input window", file=sys.stderr)
     cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
     gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
     rec_n = ctxs[0].L.slo_record_floats()
@@ -959,7 +962,7 @@ def main():
             "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
             "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
             "setup_seconds": round(t_gen, 1), "preroll_seconds": round(t_pre, 1),
-            "context_hbm_gb": round(ctx_bytes / 2**30, 2),
+            "context_hbm_gb": round(ctx_bytes / 2**30, 2), "hbm_free_after_window_gb": round(free_after / 2**30, 2),
             "loop_verify_icp": icp,
         }
         if world == 1 and a.extra not in ("", "none"):   # the other BASELINE configs at 1 GPU, each by its own process

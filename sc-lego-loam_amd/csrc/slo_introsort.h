@@ -172,11 +172,12 @@ SLO_SORT_HD void std_sort(T* first, int n, Less less) {
 // only passes strictly greater ones), so restricting it to the sub-range —
 // and making it guarded — changes nothing.  Used by the PCL-order VoxelGrid
 // (slo_pclsort.h) for the sub-ranges one lane finishes.
+// (st_lo / st_hi / st_d: the caller's stack of 64 entries each, e.g. LDS on
+// the GPU, where a private one is 768 B of scratch memory per lane)
 template <class T, class Less>
-SLO_SORT_HD void introsort_range(T* first, int n, int depth, Less less) {
+SLO_SORT_HD void introsort_range_ws(T* first, int n, int depth, Less less, int* st_lo, int* st_hi, int* st_d) {
     if (n <= 1) return;
     const int threshold = 16;
-    int st_lo[64], st_hi[64], st_d[64];
     int sp = 0;
     st_lo[sp] = 0; st_hi[sp] = n; st_d[sp] = depth; sp++;
     while (sp > 0) {
@@ -199,6 +200,11 @@ SLO_SORT_HD void introsort_range(T* first, int n, int depth, Less less) {
         }
     }
     insertion_sort_(first, first + n, less);
+}
+template <class T, class Less>
+SLO_SORT_HD void introsort_range(T* first, int n, int depth, Less less) {
+    int st_lo[64], st_hi[64], st_d[64];
+    introsort_range_ws(first, n, depth, less, st_lo, st_hi, st_d);
 }
 
 // The two loops above for n <= 8191 (the GPU's lane tasks: PCL-sort ranges

@@ -741,8 +741,8 @@ __global__ void __launch_bounds__(64) k_mo_solve(DevView v, int iterCount) {
 }
 
 // ---------------------------------------------------------------- keyframe + Scan Context make
-__device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
-__device__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc);
+__device__ __forceinline__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw);
+__device__ __forceinline__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc);
 
 
 __device__ inline float sc_xy2theta(float x, float y, int atan_float) {
@@ -957,7 +957,7 @@ int sc_make_run(slo_ctx* ctx, const float4* pts, size_t stride, const int32_t* n
 // SCManager::makeScancontext (Scancontext.cpp:151-195) of nraw points into
 // desc[NR * NS] (LDS, row-major: ring, sector), one workgroup; cell is LDS
 // scratch of the same size
-__device__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc) {
+__device__ __forceinline__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw, unsigned int* cell, double* desc) {
     const int NR = cfg.sc_num_ring, NS = cfg.sc_num_sector;
     for (int i = threadIdx.x; i < NR * NS; i += blockDim.x) cell[i] = ford(-1000.0f);
     __syncthreads();
@@ -984,7 +984,9 @@ __device__ void sc_desc_block(const slo_config& cfg, const float4* raw, int nraw
 
 // SCManager::makeScancontext + makeRingkey/SectorkeyFromScancontext +
 // history append (Scancontext.cpp:151-244), one workgroup
-__device__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw) {
+// (inlined into its kernels: a call would take the address of the kernel's
+// by-value DevView, which then gets a 1.2 KB private copy in scratch memory)
+__device__ __forceinline__ void sc_make_block(const DevView& v, int s, const float4* raw, int nraw) {
     StreamState& st = v.st[s];
     const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
     __shared__ unsigned int cell[20 * 60];

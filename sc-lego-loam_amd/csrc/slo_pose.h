@@ -17,7 +17,7 @@
 #include "slo_libm_d.h"
 
 #if defined(__HIPCC__)
-#define SLO_P_HD __host__ __device__ inline
+#define SLO_P_HD __host__ __device__ inline __attribute__((always_inline))
 #else
 #define SLO_P_HD inline
 #endif

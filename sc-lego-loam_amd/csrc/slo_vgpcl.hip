@@ -1111,7 +1111,8 @@ __global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned i
             if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
         } else if (threadIdx.x == 0) {
             atomicAdd(&cstat[0], 1);
-            slo_sort::introsort_range(scratch + f, n, d, slo_pcl::Less());   // any n (a range over PT_MAXT tiles)
+            __shared__ int st_lo[64], st_hi[64], st_d[64];   // any n (a range over PT_MAXT tiles)
+            slo_sort::introsort_range_ws(scratch + f, n, d, slo_pcl::Less(), st_lo, st_hi, st_d);
         }
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += 256) {
