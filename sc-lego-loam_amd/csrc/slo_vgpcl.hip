@@ -65,8 +65,9 @@ using slo_pcl::u64;
                           // 26.4 ms per 6 mapping steps; 18.8k / 19.0k / 19.1k / 19.0k scans/s
 #endif
 #ifndef PC_XLEV_FEW
-#define PC_XLEV_FEW 0     // a few streams: no extra levels (an empty level is five launches of latency; the tail's
-                          // workgroups step what is left): one stream's mapping sorts 2.27 -> 2.02 ms (r05)
+#define PC_XLEV_FEW 3     // a few streams: 0 extra levels shortened the sorts of young local maps (2.27 -> 2.02 ms per
+                          // mapping step over scans 0-200) but not steady-state ones (the bench's one-stream legs
+                          // after its 210-scan pre-roll: 569 / 731 / 1 155 scans/s against 578 / 765 / 1 240 with 3)
 #endif
 #ifndef PC_LOCC
 #define PC_LOCC 8         // waves per SIMD k_pc_lrank is built for (latency-bound streaming)
