@@ -1,7 +1,8 @@
 """Per-kernel times of one C3 stream in ONE context (bench.py's single_stream
 leg), from the context's launch timing, beside the graph-mode latency of the
 same scans: where a lone stream's per-scan time goes.  GPU.
-python tools/single_profile.py [scans]"""
+python tools/single_profile.py [scans] [preroll]   (preroll: untimed scans first, e.g.
+210 for the bench's steady state with 50-keyframe local maps)"""
 import os
 import sys
 import time
@@ -16,16 +17,18 @@ import slo_amd  # noqa: E402
 
 def main():
     scans = int(sys.argv[1]) if len(sys.argv) > 1 else 160
+    pre = int(sys.argv[2]) if len(sys.argv) > 2 else 0
     cfg = slo_amd.preset(6)
     P = cfg.max_points
     gen = slo_amd.DeviceGenerator(6, 3, 0, 1)
+    scans += pre
     buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
     gen.scans(0, scans, buf.data_ptr())
     gen.close()
     cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
     ctx = slo_amd.Context(cfg, 0, 1)
     ctx.graph_mode(True)
-    warm = 60
+    warm = 60 + pre
     for k in range(warm):
         ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
     ctx.synchronize()
