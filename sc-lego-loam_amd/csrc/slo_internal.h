@@ -108,6 +108,10 @@ struct StreamState {
     int32_t det_valid, det_loop_id, det_nn_idx, det_cand[64];
     float det_yaw;
     double det_min_dist;
+    // a few streams: detect split over launches (slo_sc.hip) — the candidates'
+    // distances, one workgroup each, and whether the pick is still to come
+    double det_cdist[64];
+    int32_t det_calign[64], det_pending;
     int32_t flags;
     int32_t err;
     unsigned long long dbg[8];            // diagnostic counters (slo_get "dbg"), not part of the algorithm

@@ -16,6 +16,10 @@
 
 namespace slo {
 
+// SPLIT (a context of a few streams, where one workgroup's ten candidate
+// distances in a row are the detect's latency): the K-NN here, then
+// k_sc_pairs (a workgroup per candidate) and k_sc_pick (the first minimum)
+template <bool SPLIT>
 __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
@@ -77,6 +81,11 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
         prev = best;
         __syncthreads();
     }
+    if (SPLIT) {
+        if (tid < K) st.det_cand[tid] = cands[tid];
+        if (tid == 0) st.det_pending = 1;
+        return;
+    }
     const double* sc1 = v.sc_desc + (hb + N - 1) * NR * NS;
     const double* vk1 = v.sc_sect + (hb + N - 1) * NS;
     for (int c = 0; c < K; ++c) {
@@ -98,8 +107,50 @@ __global__ void __launch_bounds__(256) k_sc_detect(DevView v) {
     }
 }
 
+// candidate c of stream s (grid K x S): distanceBtnScanContext into det_cdist / det_calign
+__global__ void __launch_bounds__(256) k_sc_pairs(DevView v) {
+    const int c = blockIdx.x, s = blockIdx.y;
+    StreamState& st = v.st[s];
+    if (!(st.kf_saved && st.det_pending)) return;
+    __shared__ ScPairLds pl;
+    const int NR = v.cfg.sc_num_ring, NS = v.cfg.sc_num_sector;
+    const size_t hb = (size_t)s * v.KFMAX;
+    const int N = st.sc_count, ci = st.det_cand[c];
+    sc_pair_distance(v.sc_desc + (hb + N - 1) * NR * NS, v.sc_sect + (hb + N - 1) * NS, v.sc_desc + (hb + ci) * NR * NS,
+                     v.sc_sect + (hb + ci) * NS, NR, NS, v.cfg.sc_search_ratio, pl, &st.det_cdist[c], &st.det_calign[c]);
+}
+
+// the first minimum over the K distances, in candidate order (as k_sc_detect)
+__global__ void k_sc_pick(DevView v) {
+    const int s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= v.S) return;
+    StreamState& st = v.st[s];
+    if (!(st.kf_saved && st.det_pending)) return;
+    st.det_pending = 0;
+    const int K = v.cfg.sc_num_candidates, NS = v.cfg.sc_num_sector;
+    double min_dist = 10000000;
+    int nn_align = 0, nn_idx = 0;
+    for (int c = 0; c < K; ++c)
+        if (st.det_cdist[c] < min_dist) { min_dist = st.det_cdist[c]; nn_align = st.det_calign[c]; nn_idx = st.det_cand[c]; }
+    st.det_loop_id = min_dist < v.cfg.sc_dist_thres ? nn_idx : -1;
+    float deg = (float)(nn_align * (360.0 / (double)NS));
+    st.det_yaw = (float)(deg * M_PI / 180.0);
+    st.det_min_dist = min_dist;
+    st.det_nn_idx = nn_idx;
+}
+
+#ifndef SLO_SC_SPLIT_STREAMS
+#define SLO_SC_SPLIT_STREAMS 8
+#endif
 int sc_detect_run(slo_ctx* ctx) {
-    SLO_LAUNCH(ctx, "sc_detect", k_sc_detect, dim3(ctx->S), dim3(256), 0, ctx->v);
+    const int S = ctx->S, K = ctx->cfg.sc_num_candidates;
+    if (S <= SLO_SC_SPLIT_STREAMS && K > 0) {
+        SLO_LAUNCH(ctx, "sc_detect", k_sc_detect<true>, dim3(S), dim3(256), 0, ctx->v);
+        SLO_LAUNCH(ctx, "sc_pairs", k_sc_pairs, dim3(K, S), dim3(256), 0, ctx->v);
+        SLO_LAUNCH(ctx, "sc_pick", k_sc_pick, dim3((S + 63) / 64), dim3(64), 0, ctx->v);
+    } else {
+        SLO_LAUNCH(ctx, "sc_detect", k_sc_detect<false>, dim3(S), dim3(256), 0, ctx->v);
+    }
     SLO_CHECK(hipGetLastError());
     return 0;
 }
@@ -109,7 +160,7 @@ __global__ void k_sc_force(DevView v) { v.st[0].kf_saved = 1; }
 // detectLoopClosureID on stream 0 only (single-scan API)
 int sc_detect_run_one(slo_ctx* ctx) {
     SLO_LAUNCH(ctx, "sc_force", k_sc_force, dim3(1), dim3(1), 0, ctx->v);
-    SLO_LAUNCH(ctx, "sc_detect", k_sc_detect, dim3(1), dim3(256), 0, ctx->v);
+    SLO_LAUNCH(ctx, "sc_detect", k_sc_detect<false>, dim3(1), dim3(256), 0, ctx->v);
     SLO_CHECK(hipGetLastError());
     return 0;
 }
