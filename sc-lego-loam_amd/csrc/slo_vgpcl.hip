@@ -59,6 +59,9 @@ using slo_pcl::u64;
 #define PC_TAIL_FEW 16384
 #endif
 #define PC_G 2048         // workgroups of the grid-stride level kernels
+#ifndef PC_G_FEW
+#define PC_G_FEW PC_G     // the same with a few streams
+#endif
 #ifndef PC_XLEV
 #define PC_XLEV 9         // global levels past log2(stride / tail size), for the uneven splits median-of-three leaves:
                           // 3 / 6 / 9 / 12: the tail 39.9 / 27.1 / 21.3 / 21.1 ms, the levels 21.0 / 23.3 / 24.9 /
@@ -1216,7 +1219,8 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
         const int cur = lv & 1;
         // the grid-stride kernels take whatever the level holds; past the first
         // levels most items have left for the finish lists: smaller grids
-        const int GG = lv < 8 ? PC_G : PC_G / 4, GS = PC_G / 4;
+        const int G0 = few ? PC_G_FEW : PC_G;
+        const int GG = lv < 8 ? G0 : G0 / 4, GS = G0 / 4;
         SLO_LAUNCH(ctx, "pc_lcount", k_pc_lcount, dim3(GG), dim3(PC_CT), 0, K, w.seg[cur], w.cseg[cur], w.ccnt,
                    w.ctr, cur);
         SLO_LAUNCH(ctx, "pc_lscan", k_pc_lscan, dim3(GS), dim3(PC_CT), 0, K, w.seg[cur], w.ccnt, w.res, w.ctr, cur,
