@@ -131,7 +131,9 @@ __global__ void k_ip_project(DevView v) {
 // k_ip_tile, k_cc_stats: one workgroup per tile of all R rows x TC columns
 // (IP_TILE_PX pixels, local index l = i * TC + jj, row-major like the global
 // pixel index p = i * C + j, so local and global orders agree).
+#ifndef IP_TILE_PX
 #define IP_TILE_PX 4096
+#endif
 #define IP_TILE_MAXC 256
 #define IP_LROOT (1 << 30)   // csize flag: the pixel is a tile-local root (k_ip_tile)
 __host__ __device__ inline int ip_tile_cols(int R) { return min(IP_TILE_MAXC, max(1, IP_TILE_PX / R)); }
