@@ -132,8 +132,8 @@ __global__ void k_ip_project(DevView v) {
 // (IP_TILE_PX pixels, local index l = i * TC + jj, row-major like the global
 // pixel index p = i * C + j, so local and global orders agree).
 #ifndef IP_TILE_PX
-#define IP_TILE_PX 4096
-#endif
+#define IP_TILE_PX 2048   // 2048: 42 KB -> 22 KB of LDS, seven workgroups per CU instead of three; C3 ip_tile 10.5 -> 7.6 ms
+#endif                    // per 24 launches (k_cc_merge +0.5 ms), 20.04 k -> 20.20 k and 19.95 k -> 20.43 k scans/s (r05)
 #define IP_TILE_MAXC 256
 #define IP_LROOT (1 << 30)   // csize flag: the pixel is a tile-local root (k_ip_tile)
 __host__ __device__ inline int ip_tile_cols(int R) { return min(IP_TILE_MAXC, max(1, IP_TILE_PX / R)); }
