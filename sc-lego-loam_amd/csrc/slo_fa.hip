@@ -260,6 +260,9 @@ __device__ void extract_ring_global(const DevView& v, int s, int ring) {
 }
 
 #define SLO_RING_STAGE 2080
+#ifndef SLO_SORT_LCV
+#define SLO_SORT_LCV 0   // 1: k_fa_sort stages the window's curvature in LDS too (27 KB: five workgroups per CU against eight;
+#endif                   // the kernel alone the same, C3 live +0.6 % and +1.8 % in two A/B pairs with 0, r05)
 
 // A ring's sorts, picks and marks stay inside its window [rs-5, re+5) when
 // every entry of its sectors is one of its own points.  That holds for every
@@ -426,7 +429,13 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Smooth* sm = v.smooth + base;
     __shared__ Smooth lsm[SLO_RING_STAGE];
+#if SLO_SORT_LCV
     __shared__ float lcv[SLO_RING_STAGE];
+#define SORT_CV(ind) lcv[(ind) - lo]
+#else
+    const float* gcv = v.curv + base;   // the list predicates read curvature from L2: 27 -> 19 KB of LDS
+#define SORT_CV(ind) gcv[ind]
+#endif
     __shared__ uint8_t lgf[SLO_RING_STAGE];
     __shared__ int s_tie[6];
 #if SLO_DIAG
@@ -437,7 +446,9 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
 #endif
     for (int k = tid; k < hi - lo; k += blockDim.x) {
         lsm[k] = sm[lo + k];
+#if SLO_SORT_LCV
         lcv[k] = v.curv[base + lo + k];
+#endif
         lgf[k] = v.seg_ground[base + lo + k];
     }
     if (tid < 6) s_tie[tid] = 0;
@@ -451,7 +462,7 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
             Smooth* a = &lsm[sp - lo];
             // the list predicates of the candidate pass below (FA:704-705, 737-738)
             auto cand = [&](int ind) __attribute__((always_inline)) {
-                const float c = lcv[ind - lo];
+                const float c = SORT_CV(ind);
                 const int g = lgf[ind - lo];
                 return ind < S && ((c > v.cfg.edge_threshold && g == 0) || (c < v.cfg.surf_threshold && g == 1));
             };
@@ -488,11 +499,11 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
                 int is = 0, iff = 0;
                 if (ks >= sp) {
                     is = lsm[ks - lo].ind;
-                    es = is < S && lcv[is - lo] > v.cfg.edge_threshold && lgf[is - lo] == 0;
+                    es = is < S && SORT_CV(is) > v.cfg.edge_threshold && lgf[is - lo] == 0;
                 }
                 if (kf <= ep) {
                     iff = lsm[kf - lo].ind;
-                    ef = iff < S && lcv[iff - lo] < v.cfg.surf_threshold && lgf[iff - lo] == 1;
+                    ef = iff < S && SORT_CV(iff) < v.cfg.surf_threshold && lgf[iff - lo] == 1;
                 }
                 const unsigned long long ms = __ballot(es), mf = __ballot(ef);
                 const unsigned long long below = (1ull << lane) - 1;
@@ -510,6 +521,7 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
 #endif
     SORT_STAMP(4)
 #undef SORT_STAMP
+#undef SORT_CV
 }
 
 __global__ void __launch_bounds__(64) k_fa_pick(DevView v) {
