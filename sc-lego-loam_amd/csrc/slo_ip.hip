@@ -579,8 +579,11 @@ int ip_run(slo_ctx* ctx) {
     const int ntiles = (v.cfg.horizon_scan + ip_tile_cols(v.cfg.n_scan) - 1) / ip_tile_cols(v.cfg.n_scan);
     SLO_LAUNCH(ctx, "ip_tile", k_ip_tile, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_cc_merge", k_cc_merge, dim3((ntiles * v.cfg.n_scan + T - 1) / T, S), dim3(T), 0, v, ntiles);
+    // slots for a tile's local roots (more go through device atomics): C5's
+    // 128-row tiles hold ~1 200 at 4 096 pixels, ~600 at 2 048
+    constexpr int kWide = IP_TILE_PX <= 2048 ? 768 : 1536;
     if (v.cfg.n_scan <= 64) SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<768>, dim3(ntiles, S), dim3(T), 0, v);
-    else SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<1536>, dim3(ntiles, S), dim3(T), 0, v);
+    else SLO_LAUNCH(ctx, "ip_cc_stats", k_cc_stats<kWide>, dim3(ntiles, S), dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_rowcount", k_ip_rowcount, gr, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "ip_compact", k_ip_compact, gr, dim3(T), 0, v);
     SLO_CHECK(hipGetLastError());
