@@ -816,7 +816,8 @@ __global__ void __launch_bounds__(256) k_vg_long(VgSrc srcv, const unsigned int*
 #endif
 #ifndef SLO_VG_LV
 #define SLO_VG_LV 1   // the slice's point indices staged in LDS for the gathers (32.8 KB, four waves per SIMD; without
-                      // them eight, measured slower: 13.8 against 12.6 ms per 6 mapping steps)
+                      // them eight, measured slower: 13.8 against 12.6 ms per 6 mapping steps; r05, live
+                      // in the mix: 20.50 k / 20.19 k against 20.19 k / 20.18 k scans/s, not taken)
 #endif
 __global__ void __launch_bounds__(VG_T) k_vg_reduce(VgSrc srcv, const unsigned int* keys, const unsigned int* vals,
                                                     const int32_t* off, const VgParams* prm, const int* hcnt, int maxT,
