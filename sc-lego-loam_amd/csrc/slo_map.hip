@@ -258,26 +258,40 @@ __global__ void k_mo_assemble(DevView v) {
     const StreamState& st = v.st[s];
     if (!st.mo_ran || e >= st.recent_n) return;
     const int32_t* ids = mo_map_ids(v, s, st);
-    int oc = 0, os = 0;
-    for (int k = 0; k < e; ++k) {
-        const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + ids[k] % v.KFR) * 3;
-        oc += kn[0];
-        os += kn[1] + kn[2];
+    // the clouds before this keyframe's: their sizes summed by the block
+    // (integer sums: any order), not by every thread in a row
+    __shared__ int s_oc, s_os;
+    __shared__ float tr[9];
+    if (threadIdx.x == 0) { s_oc = 0; s_os = 0; }
+    __syncthreads();
+    {
+        int a = 0, b = 0;
+        for (int k = threadIdx.x; k < e; k += blockDim.x) {
+            const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + ids[k] % v.KFR) * 3;
+            a += kn[0];
+            b += kn[1] + kn[2];
+        }
+        if (a) atomicAdd(&s_oc, a);
+        if (b) atomicAdd(&s_os, b);
     }
     const int slot = ids[e] % v.KFR;
     const int32_t* kn = v.kf_n + ((size_t)s * v.KFR + slot) * 3;
     const size_t ks = (size_t)s * v.KFR + slot;
     // transformPointCloud with cloudKeyPoses6D[id] (MO:566-596): the ring
-    // keeps body-frame clouds, so a pose correctPoses rewrote is used as is
-    __shared__ float tr[9];
-    if (threadIdx.x == 0) {
+    // keeps body-frame clouds, so a pose correctPoses rewrote is used as is;
+    // its three sin / cos pairs on three lanes of wave 0 (slo_pose_wave.h)
+    if (threadIdx.x < 64) {
         const float* kp = v.kf_pose + ((size_t)s * v.KFMAX + ids[e]) * 6;
-        tr[0] = slo_libm::cosf_(kp[3]); tr[1] = slo_libm::sinf_(kp[3]);
-        tr[2] = slo_libm::cosf_(kp[4]); tr[3] = slo_libm::sinf_(kp[4]);
-        tr[4] = slo_libm::cosf_(kp[5]); tr[5] = slo_libm::sinf_(kp[5]);
-        tr[6] = kp[0]; tr[7] = kp[1]; tr[8] = kp[2];
+        const float a3[3] = {kp[3], kp[4], kp[5]};
+        float sn[3], cs[3];
+        slo_pose::wave_sincos<3>(a3, sn, cs);
+        if (threadIdx.x == 0) {
+            tr[0] = cs[0]; tr[1] = sn[0]; tr[2] = cs[1]; tr[3] = sn[1]; tr[4] = cs[2]; tr[5] = sn[2];
+            tr[6] = kp[0]; tr[7] = kp[1]; tr[8] = kp[2];
+        }
     }
     __syncthreads();
+    const int oc = s_oc, os = s_os;
     const float ctRoll = tr[0], stRoll = tr[1], ctPitch = tr[2], stPitch = tr[3], ctYaw = tr[4], stYaw = tr[5];
     auto xf = [&](const float4 p) {
         const float x1 = ctYaw * p.x - stYaw * p.y, y1 = stYaw * p.x + ctYaw * p.y, z1 = p.z;
