@@ -73,8 +73,9 @@ def parse(argv=None):
         name = argv[i + 1]
         argv = argv[:i] + argv[i + 2:] + (EXTRA[name] if name != "c3" else [])
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1,
-                    help="GPUs of this node: N > 1 starts N ranks (one process per GPU) unless a launcher did")
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs of this node: N > 1 starts N ranks (one process per GPU) unless a launcher did; "
+                         "default: the launcher's WORLD_SIZE, else 1")
     ap.add_argument("--dry-dist", action="store_true",
                     help="only the rank plumbing on gloo (no GPU): launch, barrier, max-over-ranks, rank 0's JSON line")
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help="--dry-dist: this rank exits with 3 (launcher test)")
@@ -133,10 +134,24 @@ def parse(argv=None):
     ap.add_argument("--keyframe-ring", type=int, default=0, help="slo_config.keyframe_ring; 0 = default")
     ap.add_argument("--workload", default="C3 KITTI-shaped HDL-64 64x1800 stream, full pipeline + Scan Context 20x60 "
                                           "K=10, steady state")
+    ap.add_argument("--window", type=int, default=0,
+                    help="steps of input resident at once (0 = as many as the HBM budget allows); more steps than "
+                         "that are timed in segments, each segment's scans generated untimed before it")
+    ap.add_argument("--hbm-reserve-gb", type=float, default=8.0,
+                    help="HBM left free after the contexts, the cross-stream store and the input window")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="side file (relative to the repo root) for the per-kernel detail the JSON line leaves out")
+    ap.add_argument("--modes-steps", type=int, default=100,
+                    help="timed scans of the Mode S leg (one C3 stream over the ranks, single_stream_ranks; 0 = skip)")
+    ap.add_argument("--modes-leg", action="store_true",
+                    help="internal: run only the Mode S leg as one rank of a launch_ranks group and print its JSON")
     ap.add_argument("--extra", default="c2,c5,c4",
                     help="further BASELINE.json configs measured at 1 GPU after the headline, each by its own bench.py "
                          "process, reported under config_lines (outside value); 'none' = none")
-    return ap.parse_args(argv)
+    a = ap.parse_args(argv)
+    if a.gpus is None:   # a launcher (torch.distributed.run) without --gpus: its world size
+        a.gpus = int(os.environ.get("WORLD_SIZE", "1"))
+    return a
 
 
 # BASELINE.json configs measured beside the headline (C3) at 1 GPU: bench.py arguments
@@ -175,8 +190,8 @@ def extra_lines(a):
     out = {}
     for name in [x for x in a.extra.split(",") if x and x != "none"]:
         cmd = [sys.executable, os.path.abspath(__file__), "--extra", "none", "--single-steps", "0", "--icp-jobs", "0",
-               "--steps", "12", "--warmup", "3", "--profile-steps", "4", "--cpu-scans", "4", "--cpu-distinct", "4",
-               "--config", name]
+               "--modes-steps", "0", "--steps", "12", "--warmup", "3", "--profile-steps", "4", "--cpu-scans", "4",
+               "--cpu-distinct", "4", "--detail-out", detail_path(a, name), "--config", name]
         t0 = time.time()
         try:
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
@@ -188,12 +203,111 @@ def extra_lines(a):
             out[name] = {"error": f"rc={getattr(r, 'returncode', 'timeout')}",
                          "stderr_tail": (r.stderr[-600:] if r else "")}
             continue
-        keep = ("value", "unit", "ms_per_step", "steps", "warmup", "config", "roofline", "roofline_also",
-                "cpu_baseline", "speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors", "sort_guards", "dtype",
-                "setup_seconds", "preroll_seconds", "context_hbm_gb", "kernels_ms", "kernels_algo_gbs")
-        out[name] = {k: j.get(k) for k in keep}
+        out[name] = j   # the child's own contract line; its per-kernel detail is in its side file
         out[name]["wall_seconds"] = round(time.time() - t0, 1)
     return out
+
+
+def detail_path(a, tag=None):
+    """the side file for the per-kernel detail (relative to the repo root unless absolute)"""
+    p = a.detail_out if os.path.isabs(a.detail_out) else os.path.join(ROOT, a.detail_out)
+    if tag:
+        b, e = os.path.splitext(p)
+        p = f"{b}_{tag}{e or '.json'}"
+    return p
+
+
+def write_detail(a, out):
+    """the whole result (per-kernel times and byte rates, every roofline, the
+    legs' full records) to the side file; returns its path for the line"""
+    p = detail_path(a)
+    try:
+        os.makedirs(os.path.dirname(p), exist_ok=True)
+        with open(p, "w") as f:
+            json.dump(out, f, indent=1)
+        return os.path.relpath(p, ROOT)
+    except OSError as e:
+        print(f"bench.py: could not write {p}: {e}", file=sys.stderr)
+        return None
+
+
+def _pick(d, keys):
+    return {k: d[k] for k in keys if k in d} if isinstance(d, dict) else d
+
+
+def compact_roofline(r):
+    """a roofline record without its notes: the contract's fields, the live
+    launch, the isolated rate, the compulsory-bytes rate and the whole path"""
+    if not isinstance(r, dict):
+        return r
+    o = _pick(r, ("bound", "dtype", "achieved", "peak", "unit", "frac", "traffic", "traffic_source", "kernel",
+                  "avg_launch_us", "launches_timed", "bytes_per_launch", "flop_per_launch",
+                  "share_of_device_time"))
+    if isinstance(r.get("isolated"), dict):
+        o["isolated"] = _pick(r["isolated"], ("achieved", "frac", "avg_launch_us"))
+    if isinstance(r.get("compulsory"), dict):
+        o["compulsory"] = _pick(r["compulsory"], ("bytes_per_launch", "achieved", "frac"))
+    if isinstance(r.get("path"), dict):
+        o["path"] = _pick(r["path"], ("achieved", "unit", "bytes_per_step", "frac_of_spec_8000",
+                                      "frac_of_measured_copy_6290"))
+    return o
+
+
+def contract_line(out):
+    """the one JSON line the driver parses: the contract's fields, the
+    roofline and cpu_baseline, the one-stream legs' headline numbers and one
+    small record per extra config; everything else stays in the side file
+    (tests/test_bench_line.py bounds its size)"""
+    line = {k: out[k] for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config") if k in out}
+    line["roofline"] = compact_roofline(out.get("roofline"))
+    also = out.get("roofline_also") or {}
+    if isinstance(also.get("sc_detect"), dict):   # north_star: MFMA utilisation of the Scan Context Gram
+        line["mfma"] = compact_roofline(also["sc_detect"])
+    cpu = out.get("cpu_baseline")
+    if isinstance(cpu, dict):
+        c = _pick(cpu, ("value", "unit", "cores", "kind", "sample", "seconds", "one_stream_scans_per_s"))
+        if isinstance(cpu.get("A_reference_topology"), dict):
+            c["A_reference_topology"] = _pick(cpu["A_reference_topology"], ("value", "unit", "cores",
+                                                                            "stage_ms_per_scan"))
+        if isinstance(cpu.get("host"), dict):
+            c["host"] = _pick(cpu["host"], ("nproc", "cgroup_cpu_quota", "cpu_model", "glibc"))
+        line["cpu_baseline"] = c
+    else:
+        line["cpu_baseline"] = cpu
+    for k in ("speedup_vs_cpu", "speedup_vs_cpu_A", "stream_errors"):
+        if k in out:
+            line[k] = out[k]
+    one = out.get("single_stream")
+    if isinstance(one, dict):
+        line["single_stream"] = _pick(one, ("value", "unit", "latency_ms", "err"))
+    for k in ("single_stream_pipelined", "single_stream_pipelined3", "single_stream_ranks"):
+        v = out.get(k)
+        if isinstance(v, dict):
+            line[k] = _pick(v, ("value", "unit", "ranks", "transport", "stage_ms_per_scan", "owner_ms_per_scan",
+                                "bit_exact_vs_one_context", "err", "error"))
+    for k in ("single_stream_speedup_vs_cpu_A", "single_stream_pipelined3_speedup_vs_cpu_A",
+              "single_stream_ranks_speedup_vs_cpu_A"):
+        if out.get(k) is not None:
+            line[k] = out[k]
+    if isinstance(out.get("hbm"), dict):
+        line["hbm"] = out["hbm"]
+    cl = out.get("config_lines")
+    if isinstance(cl, dict):
+        line["config_lines"] = {}
+        for name, j in cl.items():
+            if not isinstance(j, dict) or "error" in j:
+                line["config_lines"][name] = j
+                continue
+            r = j.get("roofline") or {}
+            line["config_lines"][name] = {
+                "workload": (j.get("config") or {}).get("workload"), "value": j.get("value"), "unit": j.get("unit"),
+                "ms_per_step": j.get("ms_per_step"), "steps": j.get("steps"),
+                "roofline": _pick(r, ("kernel", "achieved", "frac", "avg_launch_us", "traffic")),
+                "cpu_baseline_value": (j.get("cpu_baseline") or {}).get("value"),
+                "speedup_vs_cpu": j.get("speedup_vs_cpu"), "stream_errors": j.get("stream_errors"),
+                "wall_seconds": j.get("wall_seconds")}
+    return line
 
 
 # slo_get "counts" (csrc/slo_ctx.hip): the stream's cloud sizes in one read
@@ -361,6 +475,21 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
     if name == "sc_detect" and c.get("sc_pairs") is not None:   # MFMA flop (bound "mfma")
         return int(c["sc_pairs"]) * sc_pair_mfma_flop(cfg.sc_num_ring)
     return None
+
+
+PCL_SORT_FAMILY = ("pc_count", "pc_write", "pc_lcount", "pc_lrank", "pc_lpairs", "pc_lscan", "pc_lsplit", "pc_tail",
+                   "pc_finish_w", "pc_finish_s", "pc_finish_b", "pc_finish_bx", "pc_fallback", "vg_reduce")
+
+
+def compulsory_bytes(name, c):
+    """SURVEY §8(d) compulsory bytes of the PCL-order VoxelGrid family over the
+    instrumented window: every filter input point read once (16 B); the
+    implementation's own passes (algo_bytes) come on top.  None outside the
+    family or without the work counters."""
+    pw = c.get("pcl_work") if c else None
+    if name not in PCL_SORT_FAMILY or pw is None or not int(pw[5]):
+        return None
+    return int(16 * pw[5])
 
 
 def pmc_traffic(path, kernel, tag=None):
@@ -595,6 +724,145 @@ def single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=2):
         eng.close()
 
 
+MODES_STATE = ("transform_sum", "integrated", "mapped", "keyposes", "n_keyframes", "ring_key", "err")
+
+
+def modes_leg_run(torch, slo_amd, a, cfg, pid, local, engine, rank, world, transport):
+    """one C3 stream through modes.run_rank (world 2) or run_rank3 (world >= 3):
+    scans [0, preroll + warmup + modes_steps) generated on this rank's device,
+    the owner (rank 0) timing the last modes_steps back ends; then rank 0 runs
+    the same scans through one context and compares the owner's final state
+    and every scan's flags bit for bit.  Returns rank 0's record (None on the
+    other ranks)."""
+    from slo_amd import modes
+    P = cfg.max_points
+    n = a.preroll + a.warmup + a.modes_steps
+    k0 = a.preroll + a.warmup
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
+    buf = torch.empty((n, 1, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+    gen.scans(0, n, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device=f"cuda:{local}")
+    torch.cuda.synchronize()
+    stamps = {}
+
+    def on_back(k, fl):
+        if k in (k0 - 1, n - 1):
+            stamps[k] = time.perf_counter()
+
+    run = modes.run_rank3 if world >= 3 else modes.run_rank
+    flags = run(engine, rank, world, lambda k: ((buf[k].data_ptr(), cnt.data_ptr()), 0.1 * k), n, transport,
+                on_back=on_back if rank == 0 else None)
+    if rank != 0:
+        return None
+    el = stamps[n - 1] - stamps[k0 - 1]
+    got = {nm: engine.owner.get(0, nm).copy() for nm in MODES_STATE}
+    one = slo_amd.Context(cfg, local, 1)
+    try:
+        ref_flags = []
+        for k in range(n):
+            one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            ref_flags.append(int(one.get(0, "flags")[0]))
+        ref = {nm: one.get(0, nm).copy() for nm in MODES_STATE}
+    finally:
+        one.close()
+    same = ref_flags == list(flags) and all(
+        ref[nm].shape == got[nm].shape and np.array_equal(ref[nm].view(np.uint8), got[nm].view(np.uint8))
+        for nm in MODES_STATE)
+    return {"value": round(a.modes_steps / el, 2), "unit": "scans/s", "ranks": world, "streams": 1,
+            "scans_timed": a.modes_steps, "owner_ms_per_scan": round(el / a.modes_steps * 1e3, 3),
+            "bit_exact_vs_one_context": bool(same), "keyframes_at_end": int(got["n_keyframes"][0]),
+            "err": int(got["err"][0]),
+            "layout": ("rank 0 mapping + Scan Context (owner), rank 1 odometry, ranks 2.. front ends in turn "
+                       "(modes.run_rank3)" if world >= 3 else
+                       "front ends on ranks 0 and 1 in turn, back end on rank 0 (modes.run_rank)")}
+
+
+def modes_leg_local(torch, slo_amd, a, cfg, pid, local, world=3):
+    """Mode S at N = 1: the ranks of run_rank3 as threads of this process on
+    one GPU, the carry / features / odometry buffers moved by LocalTransport"""
+    import threading
+    from slo_amd import modes
+    engs = [modes.SloEngine.for_rank(cfg, r, world, split_back=True, device=local, read_flags=r == 0)
+            for r in range(world)]
+    tr = modes.LocalTransport.group(world)
+    res, errs = {}, []
+
+    def go(r):
+        try:
+            res[r] = modes_leg_run(torch, slo_amd, a, cfg, pid, local, engs[r], r, world, tr[r])
+        except BaseException as e:   # noqa: BLE001
+            errs.append(f"rank {r}: {e!r}")
+            for q in tr:   # the others' receives time out instead of waiting forever
+                q.timeout = 1.0
+
+    try:
+        ths = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+        for th in ths:
+            th.start()
+        for th in ths:
+            th.join()
+    finally:
+        for e in engs:
+            e.close()
+    if errs or res.get(0) is None:
+        return {"error": "; ".join(errs)[:400] or "no result"}
+    out = res[0]
+    out["transport"] = "LocalTransport: 3 ranks as threads on 1 GPU"
+    return out
+
+
+def modes_leg_launch(a, world, timeout_s=420):
+    """Mode S at N > 1: a fresh group of `world` processes, one per GPU
+    (bench.py --modes-leg, slo_amd.dist.launch_ranks), the buffers moved by
+    RCCL point-to-point (modes.DistTransport); rank 0's JSON record, or the
+    failure"""
+    import tempfile
+    from slo_amd import dist as sdist
+    argv = ["--modes-leg", "--gpus", str(world), "--preset", a.preset, "--config-id", str(a.config_id),
+            "--preroll", str(a.preroll), "--warmup", str(a.warmup), "--modes-steps", str(a.modes_steps)]
+    if a.sc_k:
+        argv += ["--sc-k", str(a.sc_k)]
+    if a.sc_off:
+        argv.append("--sc-off")
+    with tempfile.TemporaryFile("w+") as f:
+        rc = sdist.launch_ranks(world, argv, os.path.abspath(__file__), stdout=f, timeout_s=timeout_s)
+        f.seek(0)
+        lines = [x for x in f.read().splitlines() if x.startswith("{")]
+    if rc != 0 or not lines:
+        return {"error": f"Mode S ranks exited with {rc}", "ranks": world}
+    out = json.loads(lines[-1])
+    out["transport"] = f"RCCL point-to-point over {world} GPUs (modes.DistTransport)"
+    return out
+
+
+def modes_leg_rank(a):
+    """bench.py --modes-leg: this process is one rank of the Mode S group"""
+    import torch
+    import torch.distributed as dist
+    import slo_amd
+    from slo_amd import dist as sdist
+    from slo_amd import modes
+    rank, world, local = sdist.env_rank()
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    try:
+        cfg = slo_amd.preset(a.preset)
+        cfg_edit(cfg, a)
+        pid = slo_amd.PRESETS[a.preset]
+        eng = modes.SloEngine.for_rank(cfg, rank, world, split_back=world >= 3, device=local, read_flags=rank == 0)
+        try:
+            dist.barrier()
+            rec = modes_leg_run(torch, slo_amd, a, cfg, pid, local, eng, rank, world, modes.DistTransport())
+            dist.barrier()
+        finally:
+            eng.close()
+        if rank == 0:
+            print(json.dumps(rec), flush=True)
+    finally:
+        dist.destroy_process_group()
+
+
 def dry_dist(a, rank, world):
     """--dry-dist: the multi-rank plumbing alone on gloo (no GPU): every rank
     takes part in a barrier and the max-over-ranks timing, and rank 0 prints
@@ -630,9 +898,13 @@ def main():
     if a.dry_dist:
         dry_dist(a, rank, world)
         return
+    if a.modes_leg:
+        modes_leg_rank(a)
+        return
     import torch
     import torch.distributed as dist
     import slo_amd
+    from slo_amd import budget
 
     torch.cuda.set_device(local)
     gather = world > 1 or a.force_gather
@@ -672,21 +944,31 @@ def main():
     # contexts as the mapping period the contexts map on different steps
     lag = (lambda g: g) if a.stagger else (lambda g: 0)
     maxlag = max(lag(g) for g in range(len(groups)))
-    nwin = a.profile_steps + a.warmup + a.steps + maxlag
-    dev = torch.empty((max(nwin, a.chunk), S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
-    free_after = torch.cuda.mem_get_info(local)[0]   # what is left for the runtime's scratch and the legs after
-    if free_after < 2**30:
-        print(f"bench: only {free_after / 2**20:.0f} MiB of HBM left after the input window", file=sys.stderr)
-    cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
-    gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
-    rec_n = ctxs[0].L.slo_record_floats()
-    rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
-    gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
+    total = a.profile_steps + a.warmup + a.steps
+    # HBM budget (slo_amd.budget): the cross-stream store first, then as many
+    # steps of resident input as fit beside it with --hbm-reserve-gb left free
+    xsc_b = budget.xsc_bytes(world * S, a.xsc_cap, cfg.sc_num_ring, cfg.sc_num_sector) if gather else 0
+    free_ctx = torch.cuda.mem_get_info(local)[0]
+    step_b = budget.step_bytes(S, P)
+    try:
+        wscans = budget.window_scans(free_ctx, step_b, max(total, a.chunk), maxlag, xsc_b,
+                                     int(a.hbm_reserve_gb * budget.GIB), a.window)
+    except MemoryError as e:
+        print(f"bench.py: {e}", file=sys.stderr, flush=True)
+        sys.exit(4)
+    seg_len = wscans - maxlag   # steps per timed segment
     xsc, matches = None, None
     if gather:   # cross-stream Scan Context store over every rank's streams
         from slo_amd import xsc as X
         xsc = X.CrossSession(cfg, world * S, a.xsc_cap, local)
         matches = torch.zeros((S, X.MATCH_DTYPE.itemsize // 4), dtype=torch.int32, device=f"cuda:{local}")
+    dev = torch.empty((wscans, S, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+    free_after = torch.cuda.mem_get_info(local)[0]   # what is left for the runtime's scratch and the legs after
+    cnt = torch.full((S,), P, dtype=torch.int32, device=f"cuda:{local}")
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, stream0, S, local)
+    rec_n = ctxs[0].L.slo_record_floats()
+    rec = torch.zeros((S, rec_n), dtype=torch.float32, device=f"cuda:{local}")
+    gathered = torch.zeros((world * S, rec_n), dtype=torch.float32, device=f"cuda:{local}") if gather else None
     exts = [torch.cuda.ExternalStream(c.stream_handle) for c in ctxs]
     pool = ThreadPoolExecutor(max_workers=len(ctxs)) if len(ctxs) > 1 else None
 
@@ -702,8 +984,9 @@ def main():
         each(lambda g, c, o, n: c.synchronize())
 
     # optional extra Scan Context history (makeAndSaveScancontextAndKeys of scans before 0)
-    for h0 in range(-a.history, 0, a.chunk):
-        nh = min(a.chunk, -h0)
+    chunk = min(a.chunk, wscans)
+    for h0 in range(-a.history, 0, chunk):
+        nh = min(chunk, -h0)
         gen.scans(h0, nh, dev.data_ptr())
         for h in range(nh):
             each(lambda g, c, o, n: c.batch_sc_make(dev[h, o].data_ptr(), cnt[o].data_ptr()))
@@ -712,8 +995,8 @@ def main():
 
     # ---- pre-roll: scans [0, preroll), generated on the device a chunk at a time
     t_pre = time.time()
-    for k0 in range(0, a.preroll + maxlag, a.chunk):
-        nk = min(a.chunk, a.preroll + maxlag - k0)
+    for k0 in range(0, a.preroll + maxlag, chunk):
+        nk = min(chunk, a.preroll + maxlag - k0)
         sync_all()
         gen.scans(k0, nk, dev.data_ptr())
         for j in range(nk):
@@ -722,19 +1005,33 @@ def main():
     sync_all()
     t_pre = time.time() - t_pre
     base = a.preroll
-    t1 = time.time()
-    gen.scans(base, nwin, dev.data_ptr())
-    gen.close()
-    t_gen += time.time() - t1
+    win = [0, 0]   # the resident window holds steps [win[0], win[0] + win[1]) (+ maxlag scans for the lags)
 
-    def step(k, serial=False):   # k = index into the resident window; context g processes scan base + lag(g) + k
+    def load(k0, n):
+        """generate steps [k0, k0 + n) of every stream into the window (untimed)"""
+        sync_all()
+        t1 = time.time()
+        gen.scans(base + k0, n + maxlag, dev.data_ptr())
+        torch.cuda.synchronize()
+        win[0], win[1] = k0, n
+        return time.time() - t1
+
+    def ensure(k0, n):   # make steps [k0, k0 + n) resident; the window starts at k0 when it is reloaded
+        if not (win[0] <= k0 and k0 + n <= win[0] + win[1]):
+            return load(k0, min(seg_len, total - k0))
+        return 0.0
+
+    t_gen += ensure(0, min(seg_len, total))
+
+    def step(k, serial=False):   # k = step index; context g processes scan base + lag(g) + k
+        j = k - win[0]   # its slot in the resident window
         if serial:   # instrumented pass: one context at a time, so its kernels have the device alone
             for g, c in enumerate(ctxs):
-                c.batch_process(dev[k + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
+                c.batch_process(dev[j + lag(g), groups[g][0]].data_ptr(), cnt[groups[g][0]].data_ptr(),
                                 0.1 * (base + lag(g) + k))
                 c.synchronize()
         else:
-            each(lambda g, c, o, n: c.batch_process(dev[k + lag(g), o].data_ptr(), cnt[o].data_ptr(),
+            each(lambda g, c, o, n: c.batch_process(dev[j + lag(g), o].data_ptr(), cnt[o].data_ptr(),
                                                     0.1 * (base + lag(g) + k)))
         if gather:   # records of every group, then one all-gather after all of them
             evs = []
@@ -769,6 +1066,7 @@ def main():
         pw0 = [c.get(0, "pcl_work").astype(np.int64) for c in ctxs]
         wk0 = [c.get(0, "work").astype(np.int64) for c in ctxs]
         for k in range(P0):
+            t_gen += ensure(k, 1)
             step(k, serial=True)
             sync_all()
             map_steps += int(int(ctxs[0].get(0, "flags")[0]) & 2 != 0)
@@ -792,11 +1090,10 @@ def main():
     rks = ([rk0] if rk0 else []) + [k for k in a.roofline_also.split(",") if k and k != rk0]
 
     for k in range(P0, P0 + a.warmup):
+        t_gen += ensure(k, 1)
         step(k)
     sync_all()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
     # the roofline kernels alone are timed inside the timed region: two
     # in-stream device timestamps per launch on its context's stream (captured
     # into the step graphs), nothing else
@@ -807,14 +1104,26 @@ def main():
     if a.trace_marker:   # a torch spin kernel on either side of the timed steps (tools/trace_window.py)
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(P0 + a.warmup, P0 + a.warmup + a.steps):
-        step(k)
-    sync_all()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
+    # the timed steps, in segments of what the window holds (one segment
+    # unless --steps exceeds the HBM budget): each segment's scans resident
+    # before it, the segment bracketed by barrier + synchronize on both sides,
+    # the job's time = the sum over segments of the slowest rank's
+    el, n_seg = 0.0, 0
+    for k0, n in budget.segments(P0 + a.warmup, total, seg_len):
+        t_gen += ensure(k0, n)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for k in range(k0, k0 + n):
+            step(k)
+        sync_all()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el += sdist.max_over_ranks(time.perf_counter() - t0, f"cuda:{local}")
+        n_seg += 1
+    gen.close()
     if a.trace_marker:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
@@ -851,7 +1160,7 @@ def main():
         def roof_of(rk):
             rms, rn = kt.get(rk, (0.0, 0))
             rb = algo_bytes(rk, counts, cfg, S, P0, map_steps)
-            bpl = rb / rn if (rb is not None and rn) else None
+            bpl = rb / rn if (rb and rn) else None   # an empty work counter prices nothing: null, not 0
             lms, ln = live.get(rk, (0.0, 0))
             live_s = lms / 1e3 / ln if ln else None
             ach = bpl / live_s / 1e9 if (bpl is not None and live_s) else None
@@ -873,7 +1182,18 @@ def main():
                         "note": "issued MFMA flop (64 x 64 padded Gram, ceil(NR/16) k-steps per Eigen accumulator) "
                                 "per distance pair; the kernel's other work (ring-key K-NN, sector-key alignment) is VALU"}
             traffic, tsrc = pmc_traffic(a.traffic_from, rk, a.profile_tag)
+            comp = None
+            cb = compulsory_bytes(rk, counts)
+            if cb and rn:   # SURVEY §8(d)'s compulsory bytes: the sort family's VoxelGrid input once (16 B / item)
+                cpl = cb / rn
+                cach = cpl / live_s / 1e9 if live_s else None
+                comp = {"bytes_per_launch": int(cpl), "achieved": round(cach, 2) if cach else None,
+                        "frac": round(cach / HBM_PEAK_GBS, 5) if cach else None,
+                        "note": "16 B x the PCL-order VoxelGrid input items of the window / this kernel's launches "
+                                "(a lower bound: the filter's input read once); bytes_per_launch above models "
+                                "the implementation's passes"}
             return {"bound": "hbm", "achieved": round(ach, 2) if ach is not None else None, "peak": HBM_PEAK_GBS,
+                    "compulsory": comp,
                     "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 5) if ach is not None else None,
                     "traffic": traffic, "traffic_source": tsrc, "kernel": rk,
                     "avg_launch_us": round(live_s * 1e6, 2) if live_s else None, "launches_timed": ln,
@@ -905,14 +1225,32 @@ def main():
         c.close()
     ctxs = []
     del dev
+    if pool is not None:
+        pool.shutdown()
+    if xsc is not None:
+        xsc.close()
     torch.cuda.empty_cache()
+    if gather:
+        if world > 1:
+            dist.barrier()
+        dist.destroy_process_group()
+    if rank != 0:   # the other ranks are done: their GPUs are free for rank 0's Mode S leg
+        return
 
     # ---- one stream alone (C3 is defined on one KITTI replay)
     one = one_p = one_p3 = None
-    if rank == 0 and a.single_steps > 0:
+    if a.single_steps > 0:
         one = single_stream(torch, slo_amd, a, cfg, pid, local)
         one_p = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local)
         one_p3 = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=3)
+
+    # ---- Mode S over the ranks: one stream, front ends dealt over the GPUs,
+    # the back end on the owner; at N = 1 the ranks are threads
+    # of this process on one GPU (LocalTransport), at N > 1 a fresh group of N
+    # processes over RCCL, started once every rank has released its GPU
+    ranks_leg = None
+    if a.modes_steps > 0:
+        ranks_leg = modes_leg_local(torch, slo_amd, a, cfg, pid, local) if world == 1 else modes_leg_launch(a, world)
 
     # ---- loop verification (MO:964-1110), measured apart
     # from the headline (not part of the metric): a batch of --icp-jobs ICP
@@ -920,62 +1258,60 @@ def main():
     # displaced by a loop-closure-sized drift (<= 0.3 m, 0.02 rad) onto every
     # 4th point of the same scan (~29k points, a voxelised submap's density)
     icp = None
-    if rank == 0 and a.icp_jobs > 0:
+    if a.icp_jobs > 0:
         icp = icp_bench(torch, slo_amd, pid, a, local, gthreads)
 
     # ---- CPU baseline (oracle = C++ restatement of the reference), rank 0, N = 1
     cpu = None
-    if rank == 0 and world == 1 and a.cpu_scans > 0:
+    if world == 1 and a.cpu_scans > 0:
         cpu = cpu_baseline(a, pid, ncpu, a.preroll + P0 + a.warmup)
 
-    if rank == 0:
-        out = {
-            "metric": METRIC, "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps,
-            "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-            "config": {"workload": a.workload, "sc_candidates": cfg.sc_num_candidates,
-                       "loop_closure": bool(cfg.loop_closure_enable),
-                       "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
-                       "scans_per_step": S * world, "preroll_scans": a.preroll,
-                       "context_phase_lag": [lag(g) for g in range(n_ctx)],
-                       "timed_scans": [base + P0 + a.warmup, base + P0 + a.warmup + a.steps - 1],
-                       "voxel_order": "pcl std::sort (reference)" if a.voxel_order == 0 else "stable",
-                       "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
-                       "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),
-                       "sc_history_seed": a.history,
-                       "launch": "eager" if a.no_graphs else "one HIP graph per context and step",
-                       "parallelism": f"streams sharded over {world} GPU(s)"},
-            "roofline": roof,
-            "roofline_also": roof_also,
-            "cpu_baseline": cpu,
-            "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
-            "speedup_vs_cpu_A": round(value / cpu["A_reference_topology"]["value"], 2) if cpu else None,
-            "single_stream": one,
-            "single_stream_speedup_vs_cpu_A": (round(one["value"] / cpu["A_reference_topology"]["value"], 2)
-                                               if (one and cpu) else None),
-            "single_stream_pipelined": one_p,
-            "single_stream_pipelined_speedup_vs_cpu_A": (round(one_p["value"] / cpu["A_reference_topology"]["value"],
-                                                               2) if (one_p and cpu) else None),
-            "single_stream_pipelined3": one_p3,
-            "single_stream_pipelined3_speedup_vs_cpu_A": (
-                round(one_p3["value"] / cpu["A_reference_topology"]["value"], 2) if (one_p3 and cpu) else None),
-            "stream_errors": errs,
-            "sort_guards": guards,
-            "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
-            "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
-            "setup_seconds": round(t_gen, 1), "preroll_seconds": round(t_pre, 1),
-            "context_hbm_gb": round(ctx_bytes / 2**30, 2), "hbm_free_after_window_gb": round(free_after / 2**30, 2),
-            "loop_verify_icp": icp,
-        }
-        if world == 1 and a.extra not in ("", "none"):   # the other BASELINE configs at 1 GPU, each by its own process
-            out["config_lines"] = extra_lines(a)
-        print(json.dumps(out), flush=True)
-    if pool is not None:
-        pool.shutdown()
-    if xsc is not None:
-        xsc.close()
-    if gather:
-        dist.destroy_process_group()
+    A = cpu["A_reference_topology"]["value"] if cpu else None
+    vs_a = lambda leg: round(leg["value"] / A, 2) if (leg and A and leg.get("value")) else None  # noqa: E731
+    out = {
+        "metric": METRIC, "value": round(value, 2), "unit": "scans/s", "n_gpus": world, "steps": a.steps,
+        "warmup": a.warmup, "ms_per_step": round(el / a.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "config": {"workload": a.workload, "sc_candidates": cfg.sc_num_candidates,
+                   "loop_closure": bool(cfg.loop_closure_enable),
+                   "preset": a.preset, "streams_per_gpu": S, "contexts_per_gpu": n_ctx,
+                   "scans_per_step": S * world, "preroll_scans": a.preroll,
+                   "context_phase_lag": [lag(g) for g in range(n_ctx)],
+                   "timed_scans": [base + P0 + a.warmup, base + P0 + a.warmup + a.steps - 1],
+                   "timed_segments": n_seg, "resident_steps": seg_len,
+                   "voxel_order": "pcl std::sort (reference)" if a.voxel_order == 0 else "stable",
+                   "keyframes_per_stream_at_end": {"min": int(kfs.min()), "mean": round(float(kfs.mean()), 1)},
+                   "local_map_keyframes": min(int(kfs.min()), cfg.surrounding_keyframe_search_num),
+                   "sc_history_seed": a.history,
+                   "launch": "eager" if a.no_graphs else "one HIP graph per context and step",
+                   "parallelism": f"streams sharded over {world} GPU(s)"},
+        "roofline": roof,
+        "roofline_also": roof_also,
+        "cpu_baseline": cpu,
+        "speedup_vs_cpu": round(value / cpu["value"], 2) if cpu else None,
+        "speedup_vs_cpu_A": vs_a({"value": value}),
+        "single_stream": one,
+        "single_stream_speedup_vs_cpu_A": vs_a(one),
+        "single_stream_pipelined": one_p,
+        "single_stream_pipelined_speedup_vs_cpu_A": vs_a(one_p),
+        "single_stream_pipelined3": one_p3,
+        "single_stream_pipelined3_speedup_vs_cpu_A": vs_a(one_p3),
+        "single_stream_ranks": ranks_leg,
+        "single_stream_ranks_speedup_vs_cpu_A": vs_a(ranks_leg),
+        "stream_errors": errs,
+        "sort_guards": guards,
+        "kernels_ms": {k: [round(v[0], 3), int(v[1])] for k, v in sorted(kt.items(), key=lambda kv: -kv[1][0])},
+        "kernels_algo_gbs": gbs, "workload_mean_last_step": workload,
+        "setup_seconds": round(t_gen, 1), "preroll_seconds": round(t_pre, 1),
+        "hbm": {"context_gb": round(ctx_bytes / 2**30, 2), "window_gb": round(wscans * step_b / 2**30, 2),
+                "xsc_store_gb": round(xsc_b / 2**30, 3), "free_after_window_gb": round(free_after / 2**30, 2)},
+        "loop_verify_icp": icp,
+    }
+    if world == 1 and a.extra not in ("", "none"):   # the other BASELINE configs at 1 GPU, each by its own process
+        out["config_lines"] = extra_lines(a)
+    line = contract_line(out)
+    line["detail"] = write_detail(a, out)
+    print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":

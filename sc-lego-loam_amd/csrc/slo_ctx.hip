@@ -310,7 +310,8 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     // slo_vg.hip); the sparse corner cloud is searched by brute force.
     if (slo::vg_alloc(ctx) || slo::grid_alloc(ctx, ctx->grid_c, 1 << SLO_MAP_TLOG2, v.cap_mc, SLO_MAP_CELL) ||
         slo::grid_alloc(ctx, ctx->grid_s, 1 << SLO_MAP_TLOG2, v.cap_ms, SLO_MAP_CELL) ||
-        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL) || slo::map_ws_presize(ctx)) {
+        slo::grid_alloc(ctx, ctx->grid_os, 1 << 15, v.cap_less_flat, SLO_ODO_SURF_CELL) ||
+        (S <= SLO_PREP_DEFER_STREAMS && slo::fa_prep_init(ctx))) {
         slo_destroy(ctx);
         return SLO_E_HIP;
     }
@@ -470,7 +471,8 @@ int slo_batch_map_optimization(slo_ctx* ctx, const void* d_points, const int32_t
     if (int r = slo::set_io(ctx, d_points, d_counts)) return r;
     SLO_LAUNCH(ctx, "clear_flags", slo::k_clear_flags, dim3((ctx->S + 63) / 64), dim3(64), 0, ctx->v);
     if (!slo::map_gate(ctx, t_scan)) return SLO_OK;
-    int r = slo::map_run(ctx);
+    int r = slo::map_ws_ensure(ctx);
+    if (!r) r = slo::map_run(ctx);
     if (r) return r;
     ctx->mapped_now = true;
     // the graph half of saveKeyFramesAndFactor, then correctPoses (MO:1697-1699)
@@ -495,9 +497,6 @@ namespace slo {
 // With at most SLO_PREP_DEFER_STREAMS streams the odometry's preparation of
 // the next scan's searches (fa_prep_*, slo_odom.hip) is left to the next step,
 // forked beside its projection and features: it leaves a scan's critical path.
-#ifndef SLO_PREP_DEFER_STREAMS
-#define SLO_PREP_DEFER_STREAMS 8
-#endif
 static int step_launches(slo_ctx* ctx, bool map) {
     // (not with a kernel-name timing filter: its in-stream stamps pair up per stream, as map_run's fork)
     const bool defer = ctx->S <= SLO_PREP_DEFER_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
@@ -597,6 +596,8 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
         ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings";
         return SLO_E_STATE;
     }
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::map_ws_ensure(ctx)) return r;   // before step_graph may capture
     int r = slo::step_graph(ctx, d_points, d_counts, t_scan);
     if (r <= 0) return r;
     if ((r = slo_batch_scan_time(ctx, t_scan))) return r;

@@ -584,7 +584,17 @@ struct slo_ctx {
     bool prep_pending = false;
     hipStream_t prep_stream = nullptr;
     hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+    // the mapping step's workspaces are sized on the first entry that can map
+    // (map_ws_ensure), so a Mode S front or odometry context never holds them
+    bool map_ws_ready = false;
 };
+
+// With at most SLO_PREP_DEFER_STREAMS streams a batched step defers the
+// odometry's preparation of the next scan's searches to the next step, forked
+// beside its projection and features (slo_ctx.hip step_launches)
+#ifndef SLO_PREP_DEFER_STREAMS
+#define SLO_PREP_DEFER_STREAMS 8
+#endif
 
 // launch helpers with optional per-kernel HIP-event timing
 namespace slo {
@@ -603,6 +613,7 @@ void fa_swap_last(slo_ctx* ctx);
 int fa_prep_fork(slo_ctx* ctx);    // a pending preparation on prep_stream (forked from / joined to ctx->stream)
 int fa_prep_join(slo_ctx* ctx);
 void fa_prep_free(slo_ctx* ctx);
+int fa_prep_init(slo_ctx* ctx);    // prep_stream and its two events (at creation, never inside a capture)
 int vg_alloc(slo_ctx* ctx);
 void vg_free(slo_ctx* ctx);
 int vg_ws_reinit(slo_ctx* ctx);    // the stream-ordered initialisation of the VoxelGrid workspaces, again
@@ -616,7 +627,8 @@ GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx);
-int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces, at creation (slo_map.hip)
+int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces (slo_map.hip)
+int map_ws_ensure(slo_ctx* ctx);   // map_ws_presize once, from an entry point that can map, before any capture
 struct VgGroup;
 int vg_presize(slo_ctx* ctx, const VgGroup* groups, int G);
 int pcl_presize(slo_ctx* ctx, int SV, size_t items, size_t maxT);

@@ -1065,9 +1065,11 @@ static VgGroup map_total_group(slo_ctx* ctx) {
 }
 
 // Every workspace a mapping step's VoxelGrids and sorts will use, allocated
-// at context creation from the capacities (the sizes depend on the strides
-// alone), so no step allocates: an out-of-memory shows at slo_create, and a
-// captured step graph's pointers never move.
+// from the capacities (the sizes depend on the strides alone) by the first
+// entry point that can map, before anything is captured (map_ws_ensure), so no
+// step allocates: an out-of-memory shows at that call, a captured step
+// graph's pointers never move, and a context that never maps (a Mode S front
+// or odometry context) never holds them.
 int map_ws_presize(slo_ctx* ctx) {
     VgGroup gs[6];
     map_groups(ctx, gs);
@@ -1079,6 +1081,13 @@ int map_ws_presize(slo_ctx* ctx) {
     }
     const VgGroup t = map_total_group(ctx);
     return vg_presize(ctx, &t, 1);
+}
+
+int map_ws_ensure(slo_ctx* ctx) {
+    if (ctx->map_ws_ready) return 0;
+    if (int r = map_ws_presize(ctx)) return r;
+    ctx->map_ws_ready = true;
+    return 0;
 }
 
 int map_run(slo_ctx* ctx) {

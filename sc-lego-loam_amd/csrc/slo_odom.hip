@@ -1223,13 +1223,19 @@ static int fa_prep_launch(slo_ctx* ctx) {
     return grid_build(ctx, ctx->grid_os, v.kd_surf, v.cap_less_flat, &v.st->kdSurfNum, SS);
 }
 
+int fa_prep_init(slo_ctx* ctx) {
+    if (ctx->prep_stream) return 0;
+    SLO_CHECK(hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pjoin, hipEventDisableTiming));
+    return 0;
+}
+
+// (prep_stream exists from slo_create: only contexts of at most
+// SLO_PREP_DEFER_STREAMS streams defer, so nothing is created mid-capture)
 int fa_prep_fork(slo_ctx* ctx) {
     if (!ctx->prep_pending) return 0;
-    if (!ctx->prep_stream) {
-        SLO_CHECK(hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking));
-        SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
-        SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pjoin, hipEventDisableTiming));
-    }
+    if (int r = fa_prep_init(ctx)) return r;
     SLO_CHECK(hipEventRecord(ctx->ev_pfork, ctx->stream));
     SLO_CHECK(hipStreamWaitEvent(ctx->prep_stream, ctx->ev_pfork, 0));
     std::swap(ctx->stream, ctx->prep_stream);

@@ -476,7 +476,7 @@ __device__ __forceinline__ u64 irl(u64 x, int i) { return rl64(x, i); }
 __device__ __forceinline__ unsigned int irl(unsigned int x, int i) {
     return (unsigned int)__builtin_amdgcn_readlane((int)x, __builtin_amdgcn_readfirstlane(i));
 }
-// Global: `a` in global memory (k_pc_fallback's scratch): the lanes' stores
+// Global: `a` in global memory (pc_fallback_entry's scratch): the lanes' stores
 // are ordered before the next reads by a workgroup-scope fence instead of the
 // LDS wave fence.
 template <bool Global>
@@ -558,7 +558,7 @@ __device__ inline void wave_heap_sort(It* a, int n) {
     heap_fence<Global>();
 }
 
-// wave_heap_sort with the heap in global memory (k_pc_fallback: spent-depth
+// wave_heap_sort with the heap in global memory (pc_fallback_entry: spent-depth
 // ranges over 4 Ki items) and its levels 6 .. 10 (nodes 63 .. 2046) cached in
 // LDS for the sort_heap phase: a pop's path then costs one LDS round trip for
 // those five levels and one L2 round trip for the five below (up to 2^16

@@ -33,8 +33,8 @@
 //     down to ranges of at most PC_T (the same step, barriers for launches);
 //   k_pc_finish: one wave per range of at most PC_T items sorts it in LDS to
 //     the end (slo_pcl::wave_sort);
-//   k_pc_fallback: a range over PC_T items with its depth budget spent
-//     (adversarial inputs only; counted in vg_stats) is heapsorted by one lane.
+//   pc_fallback_entry: a range over PC_T items with its depth budget spent
+//     (counted in vg_stats) is heapsorted by one wave, inside k_pc_finish32.
 #include "slo_vgcommon.h"
 #include "slo_pclsort.h"
 
@@ -86,7 +86,7 @@ using slo_pcl::u64;
 // finish cycles of list `list` in streamed steps, register steps, lane tasks
 enum { PW_ACTIVE = 0, PW_PAIRS = 1, PW_FIN = 2, PW_INPUT = 5, PW_ENTRIES = 6, PW_TAIL = 7, PW_TAIL_PAIRS = 8, PW_PROF = 9,
        PW_FINX = 20,     // [20]: items of list 5 (the 4 Ki entries too wide for 32-bit items, k_pc_finish on 64-bit)
-       PW_FALL = 21 };   // [21]: items of the spent-depth ranges k_pc_fallback heapsorts
+       PW_FALL = 21 };   // [21]: items of the spent-depth ranges pc_fallback_entry heapsorts
 
 struct PSeg { int f, l, d, c0; };
 struct PRes { unsigned int piv, vmed; int med, m, TR, cutA, cutB; };
@@ -96,7 +96,7 @@ enum { PCC_NSEG = 0, PCC_NCH = 2, PCC_NW = 6 };   // [cur] per level parity; PCC
 
 // Range lists: finish entries by size class, list 0 <= PC_WT items, 1 <= PC_ST,
 // 2 <= PC_T (k_pc_finish32, then k_pc_finish<size>); 3 larger (k_pc_tail); 4 a spent depth budget
-// over PC_T items (k_pc_fallback: heapsort); 5 the list-2 entries whose keys span 2^20 or more (filled by
+// over PC_T items (pc_fallback_entry: heapsort); 5 the list-2 entries whose keys span 2^20 or more (filled by
 // k_pc_finish32, sorted by k_pc_finish on 64-bit items); 6 the list-3 ranges over PT_SMAXT tiles (filled by the
 // small-table k_pc_tail, stepped by the large-table one).  An entry is (first position, size | depth << 24).
 struct PcLists { int2* l[7]; };
@@ -568,6 +568,46 @@ __global__ void __launch_bounds__(256) k_pc_lsplit(int tail_min, const PSeg* seg
     }
 }
 
+// list 4 — a range over PC_T items whose depth budget is spent (std::sort's
+// heapsort; the dense C5 maps send a few hundred per run here, two or three
+// per sort): taken first by the low workgroups of the 4 Ki finish
+// (k_pc_finish32<PC_T>, one range per workgroup, so the ranges run side by side
+// and beside the finish entries instead of in a launch of their own before
+// them — round 5's k_pc_fallback was 11.4 % of C5's device time on the
+// mapping step's critical path); the first wave heapsorts it in global memory, the heap's
+// levels 6 .. 10 cached in the finish's 16 KB item array (slo_pclsort.h wave_heap_sort_cached:
+// per pop one LDS and one L2 round trip for the path below the register
+// levels, instead of two L2 round trips).  (Staging whole ranges in LDS —
+// 96 KB in round 4, 64 KB of 32-bit items in round 5 — held every launch of
+// the kernel, nearly always empty, until a CU had that much free beside the
+// other contexts' finish kernels: 3-4 ms per launch, and on a graph branch of
+// its own the join stalled the context instead: C3 19.2 k -> 16.1 k scans/s.)
+// A range that came here for another reason (over PT_MAXT tiles,
+// a full stack; never seen) is finished by one lane with the sequential
+// restatement.
+__device__ __forceinline__ void pc_fallback_entry(unsigned int* K, unsigned int* V, int2 w, int* cstat, u64* scratch,
+                                                  unsigned long long* pst, u64* mid) {
+    const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24, NT = blockDim.x;
+    if (threadIdx.x == 0) atomicAdd(&pst[PW_FALL], (unsigned long long)n);
+    for (int i = threadIdx.x; i < n; i += NT) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
+    __syncthreads();
+    if (d == 0 && n > 16) {
+        if (threadIdx.x < 64) slo_pcl::wave_heap_sort_cached<u64>(scratch + f, n, mid);
+        if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
+    } else if (threadIdx.x == 0) {
+        atomicAdd(&cstat[0], 1);
+        __shared__ int st_lo[64], st_hi[64], st_d[64];   // any n (a range over PT_MAXT tiles)
+        slo_sort::introsort_range_ws(scratch + f, n, d, slo_pcl::Less(), st_lo, st_hi, st_d);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += NT) {
+        const u64 it = scratch[f + i];
+        K[f + i] = (unsigned int)(it >> 32);
+        V[f + i] = (unsigned int)it;
+    }
+    __syncthreads();
+}
+
 // ---- finish: PC_FW waves per entry (slo_pcl::block_sort; one for the
 // smallest class), the entry's items staged in LDS; lane tasks take the
 // ranges of <= PC_TLANE items
@@ -656,10 +696,10 @@ __global__ void __launch_bounds__(64 * W) k_pc_finish(unsigned int* K, unsigned 
 template <int NMAX, int W>
 __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >= 4 ? PC_F32_OCC : 1))) k_pc_finish32(unsigned int* K, unsigned int* V, PcLists wl, int* ctr,
                                                          int list, unsigned long long* pst, int* cstat,
-                                                         const int32_t* off, int S, int32_t* serr) {
+                                                         const int32_t* off, int S, int32_t* serr, u64* fall) {
     constexpr int NT = 64 * W;
     static_assert(NMAX <= (1 << slo_pcl::kPosBits), "positions fit kPosBits");
-    __shared__ unsigned int items[NMAX];
+    __shared__ __attribute__((aligned(16))) unsigned int items[NMAX];
     __shared__ unsigned short tbl[NMAX / 2 + 1];
     __shared__ slo_pcl::WaveSmem ws[W];
     __shared__ slo_pcl::BlockQ<W> bq;
@@ -668,6 +708,13 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
     const int nw = ctr[PCC_NW + list], tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     unsigned long long wn = 0, we = 0;
     long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if constexpr (NMAX * sizeof(unsigned int) >= slo_pcl::kMidN * sizeof(u64)) {
+        if (fall) {   // list 4 first (the spent-depth ranges: heapsort, the item array as its LDS cache)
+            const int n4 = ctr[PCC_NW + 4];
+            for (int e = blockIdx.x; e < n4; e += gridDim.x)
+                pc_fallback_entry(K, V, wl.l[4][e], cstat, fall, pst, reinterpret_cast<u64*>(items));
+        }
+    }
     for (int e = blockIdx.x; e < nw; e += gridDim.x) {
         const int2 w = wl.l[list][e];
         const int f = w.x, n = min(w.y & 0xffffff, NMAX), d = w.y >> 24;
@@ -792,7 +839,7 @@ __global__ void __launch_bounds__(64 * W) __attribute__((amdgpu_waves_per_eu(W >
 // wave's (PT_ROWS rows of 64), the tile counts and their prefixes sit in LDS,
 // and barriers separate the passes instead of launches.  Halves of at most
 // PC_T items go to the finish lists, larger ones onto the workgroup's stack;
-// a range whose depth budget is spent goes to list 4 (k_pc_fallback,
+// a range whose depth budget is spent goes to list 4 (pc_fallback_entry,
 // heapsort).  Ranges over PT_MAXT tiles go to list 4 as well (one lane
 // finishes them exactly; never seen: the map clouds' strides are ~1.6 M).
 
@@ -1087,47 +1134,6 @@ __global__ void __launch_bounds__(PT_NT) __attribute__((amdgpu_waves_per_eu(PT_O
     }
 }
 
-// list 4 — a range over PC_T items whose depth budget is spent (std::sort's
-// heapsort; the dense C5 maps send a few hundred per run here, two or three
-// per launch): the first wave heapsorts it in global memory, the heap's
-// levels 6 .. 10 cached in 16 KB of LDS (slo_pclsort.h wave_heap_sort_cached:
-// per pop one LDS and one L2 round trip for the path below the register
-// levels, instead of two L2 round trips).  (Staging whole ranges in LDS —
-// 96 KB in round 4, 64 KB of 32-bit items in round 5 — held every launch of
-// the kernel, nearly always empty, until a CU had that much free beside the
-// other contexts' finish kernels: 3-4 ms per launch, and on a graph branch of
-// its own the join stalled the context instead: C3 19.2 k -> 16.1 k scans/s.)
-// A range that came here for another reason (over PT_MAXT tiles,
-// a full stack; never seen) is finished by one lane with the sequential
-// restatement.
-__global__ void __launch_bounds__(256) k_pc_fallback(unsigned int* K, unsigned int* V, const int2* wl, const int* ctr,
-                                                      int* cstat, u64* scratch, unsigned long long* pst) {
-    __shared__ u64 mid[slo_pcl::kMidN];   // heap levels 6 .. 10 (wave_heap_sort_cached)
-    const int nw = ctr[PCC_NW + 4];
-    for (int e = blockIdx.x; e < nw; e += gridDim.x) {
-        const int2 w = wl[e];
-        const int f = w.x, n = w.y & 0xffffff, d = w.y >> 24;
-        if (threadIdx.x == 0) atomicAdd(&pst[PW_FALL], (unsigned long long)n);
-        for (int i = threadIdx.x; i < n; i += 256) scratch[f + i] = ((u64)K[f + i] << 32) | V[f + i];
-        __syncthreads();
-        if (d == 0 && n > 16) {
-            if (threadIdx.x < 64) slo_pcl::wave_heap_sort_cached<u64>(scratch + f, n, mid);
-            if (threadIdx.x == 0) atomicAdd(&cstat[0], 1);
-        } else if (threadIdx.x == 0) {
-            atomicAdd(&cstat[0], 1);
-            __shared__ int st_lo[64], st_hi[64], st_d[64];   // any n (a range over PT_MAXT tiles)
-            slo_sort::introsort_range_ws(scratch + f, n, d, slo_pcl::Less(), st_lo, st_hi, st_d);
-        }
-        __syncthreads();
-        for (int i = threadIdx.x; i < n; i += 256) {
-            const u64 it = scratch[f + i];
-            K[f + i] = (unsigned int)(it >> 32);
-            V[f + i] = (unsigned int)it;
-        }
-        __syncthreads();
-    }
-}
-
 // ---- workspace and driver
 static int pcl_ws(slo_ctx* ctx, int SV, size_t items, size_t maxT) {
     PclWs& w = ctx->pws;
@@ -1237,19 +1243,17 @@ int vg_pcl_sort(slo_ctx* ctx, const VgSrc& src, size_t in_stride, size_t items, 
     const int FG = std::max(256, std::min(8192, S * 16));
     SLO_LAUNCH(ctx, "pc_tail", (k_pc_tail<512, PT_MAXT, 3>), dim3(std::max(64, std::min(4096, S * 8))), dim3(512), 0,
                K, V, PB, L, w.ctr, w.pstat, w.cstat, off, S, w.serr);
-    SLO_LAUNCH(ctx, "pc_fallback", k_pc_fallback, dim3(64), dim3(256), 0, K, V, L.l[4], w.ctr, w.cstat, (u64*)spare,
-               w.pstat);
     // 32-bit items (lists 2 and 1; entries whose keys span 2^20 or more take their keys' ranks)
     if (few) {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, 16>), dim3(FG), dim3(64 * 16), 0, K, V, L, w.ctr, 2, w.pstat,
-                   w.cstat, off, S, w.serr);
+                   w.cstat, off, S, w.serr, (u64*)spare);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, 8>), dim3(FG), dim3(64 * 8), 0, K, V, L, w.ctr, 1, w.pstat,
-                   w.cstat, off, S, w.serr);
+                   w.cstat, off, S, w.serr, (u64*)nullptr);
     } else {
         SLO_LAUNCH(ctx, "pc_finish_b", (k_pc_finish32<PC_T, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 2,
-                   w.pstat, w.cstat, off, S, w.serr);
+                   w.pstat, w.cstat, off, S, w.serr, (u64*)spare);
         SLO_LAUNCH(ctx, "pc_finish_s", (k_pc_finish32<PC_ST, PC_FW>), dim3(FG), dim3(64 * PC_FW), 0, K, V, L, w.ctr, 1,
-                   w.pstat, w.cstat, off, S, w.serr);
+                   w.pstat, w.cstat, off, S, w.serr, (u64*)nullptr);
     }
     SLO_LAUNCH(ctx, "pc_finish_w", (k_pc_finish<PC_WT, 1>), dim3(FG), dim3(64), 0, K, V, L, w.ctr, 0, w.pstat, w.cstat, off, S, w.serr);
     SLO_CHECK(hipGetLastError());

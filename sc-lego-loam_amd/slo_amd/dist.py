@@ -81,24 +81,46 @@ def free_port():
         return s.getsockname()[1]
 
 
-def launch_ranks(n, argv, script, poll_s=0.2):
+def _stop(procs):
+    """SIGTERM the given processes (their own PIDs), SIGKILL what is left after 30 s"""
+    for q in procs:
+        q.terminate()
+    t_end = time.time() + 30
+    for q in procs:
+        try:
+            q.wait(timeout=max(0.1, t_end - time.time()))
+        except subprocess.TimeoutExpired:
+            q.kill()
+            q.wait()
+
+
+def launch_ranks(n, argv, script, poll_s=0.2, stdout=None, timeout_s=None):
     """Run `n` copies of `python script argv` as ranks 0 .. n-1 of one node
     (one process per GPU: RANK = LOCAL_RANK = r, WORLD_SIZE = n,
     MASTER_ADDR = 127.0.0.1 and a free MASTER_PORT), the way
     `torch.distributed.run --nproc-per-node n` would; the children inherit
-    stdout / stderr, so rank 0's output is the command's.  The caller never
-    touches a GPU.  Returns 0 when every rank exits 0; otherwise the first
+    stdout / stderr (or write stdout to `stdout`, a file), so rank 0's output
+    is the command's.  The caller's own launcher variables (TORCHELASTIC_*)
+    are not passed on.  Returns 0 when every rank exits 0; otherwise the first
     failing rank's exit code, after the other ranks are stopped (their own
-    PIDs, SIGTERM then SIGKILL)."""
+    PIDs, SIGTERM then SIGKILL); 124 when `timeout_s` passes first (every
+    rank stopped)."""
     port = str(free_port())
     procs = []
+    base = {k: v for k, v in os.environ.items() if not k.startswith("TORCHELASTIC_")}
     for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+        env = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, script] + list(argv), env=env, stdout=stdout))
     rc = 0
     live = list(procs)
+    t_end = time.time() + timeout_s if timeout_s else None
     while live:
+        if t_end is not None and time.time() > t_end:
+            print(f"launch_ranks: {len(live)} rank(s) still running after {timeout_s} s; stopping them",
+                  file=sys.stderr, flush=True)
+            _stop(live)
+            return 124
         for p in list(live):
             c = p.poll()
             if c is None:
@@ -108,15 +130,7 @@ def launch_ranks(n, argv, script, poll_s=0.2):
                 rc = c if c > 0 else 128 - c
                 print(f"launch_ranks: rank {procs.index(p)} exited with {c}; stopping the others", file=sys.stderr,
                       flush=True)
-                for q in live:
-                    q.terminate()
-                t_end = time.time() + 30
-                for q in live:
-                    try:
-                        q.wait(timeout=max(0.1, t_end - time.time()))
-                    except subprocess.TimeoutExpired:
-                        q.kill()
-                        q.wait()
+                _stop(live)
                 live = []
                 break
         time.sleep(poll_s)

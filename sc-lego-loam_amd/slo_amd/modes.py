@@ -192,8 +192,16 @@ class DistTransport:
         return x
 
     def drain(self):
+        """every send of this scan complete before its buffers are handed out
+        again: Work.wait() on an RCCL send only orders the current stream
+        after it, so for device tensors the host then waits on that stream too
+        (libslo's own HIP stream, which writes the buffers next, is not
+        ordered against RCCL's)"""
         for r in self.pending:
             r.wait()
+        cuda = sorted({x.device.index for x in self.keep if x.is_cuda})
+        for d in cuda:
+            self.t.cuda.current_stream(d).synchronize()
         self.pending, self.keep = [], []
 
 
