@@ -100,7 +100,7 @@ def parse(argv=None):
                     help="extra Scan Context history per stream (scans before scan 0, a KITTI-00 mid-drive history: "
                          "detects search ~1000 keyframes, SCc:264-289); the pre-roll builds the recent part")
     ap.add_argument("--profile-steps", type=int, default=8, help="instrumented steps for the per-kernel roofline")
-    ap.add_argument("--roofline-also", default="fa_ring_ds,mo_knn,pc_tail,pc_fallback,sc_detect",
+    ap.add_argument("--roofline-also", default="fa_ring_ds,mo_knn,pc_tail,sc_detect",
                     help="further kernels timed live the same way, reported under roofline_also (comma list; each "
                          "launch of a timed kernel adds two one-thread stamp kernels to the timed steps, so the "
                          "many-launch pc_lpairs / fa_search_corner are left to kernels_algo_gbs unless named here)")
@@ -145,6 +145,9 @@ def parse(argv=None):
                     help="timed scans of the Mode S leg (one C3 stream over the ranks, single_stream_ranks; 0 = skip)")
     ap.add_argument("--modes-leg", action="store_true",
                     help="internal: run only the Mode S leg as one rank of a launch_ranks group and print its JSON")
+    ap.add_argument("--modes-transport", default="nccl", choices=("nccl", "gloo"),
+                    help="the Mode S leg's point-to-point backend at N > 1: RCCL on device buffers, or gloo through "
+                         "pinned host copies (the fallback when the RCCL group fails)")
     ap.add_argument("--extra", default="c2,c5,c4",
                     help="further BASELINE.json configs measured at 1 GPU after the headline, each by its own bench.py "
                          "process, reported under config_lines (outside value); 'none' = none")
@@ -825,15 +828,22 @@ def modes_leg_launch(a, world, timeout_s=420):
         argv += ["--sc-k", str(a.sc_k)]
     if a.sc_off:
         argv.append("--sc-off")
-    with tempfile.TemporaryFile("w+") as f:
-        rc = sdist.launch_ranks(world, argv, os.path.abspath(__file__), stdout=f, timeout_s=timeout_s)
-        f.seek(0)
-        lines = [x for x in f.read().splitlines() if x.startswith("{")]
-    if rc != 0 or not lines:
-        return {"error": f"Mode S ranks exited with {rc}", "ranks": world}
-    out = json.loads(lines[-1])
-    out["transport"] = f"RCCL point-to-point over {world} GPUs (modes.DistTransport)"
-    return out
+    failed = None
+    for tr in ("nccl", "gloo"):   # RCCL first; gloo through host copies if the RCCL group fails
+        with tempfile.TemporaryFile("w+") as f:
+            rc = sdist.launch_ranks(world, argv + ["--modes-transport", tr], os.path.abspath(__file__), stdout=f,
+                                    timeout_s=timeout_s)
+            f.seek(0)
+            lines = [x for x in f.read().splitlines() if x.startswith("{")]
+        if rc == 0 and lines:
+            out = json.loads(lines[-1])
+            out["transport"] = (f"RCCL point-to-point over {world} GPUs (modes.DistTransport)" if tr == "nccl" else
+                                f"gloo point-to-point over {world} GPUs through pinned host copies (modes.HostTransport)")
+            if failed:
+                out["rccl_error"] = failed
+            return out
+        failed = f"{tr} ranks exited with {rc}"
+    return {"error": failed, "ranks": world}
 
 
 def modes_leg_rank(a):
@@ -844,8 +854,13 @@ def modes_leg_rank(a):
     from slo_amd import dist as sdist
     from slo_amd import modes
     rank, world, local = sdist.env_rank()
+    if a.modes_transport == "gloo":   # host-staged messages: ranks may share a GPU (the 1-GPU rehearsal)
+        local %= max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    if a.modes_transport == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
     try:
         cfg = slo_amd.preset(a.preset)
         cfg_edit(cfg, a)
@@ -853,7 +868,8 @@ def modes_leg_rank(a):
         eng = modes.SloEngine.for_rank(cfg, rank, world, split_back=world >= 3, device=local, read_flags=rank == 0)
         try:
             dist.barrier()
-            rec = modes_leg_run(torch, slo_amd, a, cfg, pid, local, eng, rank, world, modes.DistTransport())
+            tr = modes.DistTransport() if a.modes_transport == "nccl" else modes.HostTransport()
+            rec = modes_leg_run(torch, slo_amd, a, cfg, pid, local, eng, rank, world, tr)
             dist.barrier()
         finally:
             eng.close()
@@ -938,6 +954,7 @@ def main():
     ctxs = [slo_amd.Context(cfg, local, n) for _, n in groups]
     for c in ctxs:
         c.graph_mode(not a.no_graphs)
+        c.prepare_mapping()   # the mapping workspaces now, so the budget below sees them
     ctx_bytes = free0 - torch.cuda.mem_get_info(local)[0]
     n_ctx = len(ctxs)
     # --stagger: context g runs lag(g) = g scans ahead, so with as many

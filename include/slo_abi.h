@@ -53,6 +53,12 @@ const char* slo_last_error(const slo_ctx* ctx);
 void* slo_stream(slo_ctx* ctx);
 /* Block until all queued work of the context is done. */
 int slo_synchronize(slo_ctx* ctx);
+/* Allocate now every workspace a mapping step will use (the VoxelGrid and
+ * PCL-order sort workspaces of mapOptimization, MO:1224-1263), sized from the
+ * configured capacities; otherwise the first call that can map does it.  A
+ * caller budgeting device memory calls it right after slo_create; a Mode S
+ * front or odometry context never maps and never holds them. */
+int slo_prepare_mapping(slo_ctx* ctx);
 
 /* ---------------------------------------------------------------- batched
  * d_points: device array [n_streams][cfg.max_points] of (x,y,z,intensity)

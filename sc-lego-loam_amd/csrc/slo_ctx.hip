@@ -367,6 +367,14 @@ void slo_destroy(slo_ctx* ctx) {
     delete ctx;
 }
 
+int slo_prepare_mapping(slo_ctx* ctx) {
+    if (!ctx) return SLO_E_ARG;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    if (int r = slo::map_ws_ensure(ctx)) return r;
+    SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    return SLO_OK;
+}
+
 int slo_synchronize(slo_ctx* ctx) {
     if (!ctx) return SLO_E_ARG;
     hipSetDevice(ctx->dev);

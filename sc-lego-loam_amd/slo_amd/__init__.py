@@ -151,6 +151,11 @@ class Context:
     def synchronize(self):
         self._ok(self.L.slo_synchronize(self.h), "slo_synchronize")
 
+    def prepare_mapping(self):
+        """slo_prepare_mapping: the mapping step's workspaces now (a caller
+        budgeting HBM measures free memory after this)"""
+        self._ok(self.L.slo_prepare_mapping(self.h), "slo_prepare_mapping")
+
     # batched, device pointers (int addresses)
     def batch_image_projection(self, d_pts, d_cnt):
         self._ok(self.L.slo_batch_image_projection(self.h, d_pts, d_cnt), "slo_batch_image_projection")

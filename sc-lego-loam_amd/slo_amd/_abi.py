@@ -112,6 +112,7 @@ REC = {"pose": 0, "mapped": 6, "n_keyframes": 12, "kf_saved": 13, "loop_id": 14,
 # symbols declared in include/slo_abi.h (tests check every one is exported)
 EXPORTS = [
     "slo_config_preset", "slo_create", "slo_destroy", "slo_last_error", "slo_stream", "slo_synchronize",
+    "slo_prepare_mapping",
     "slo_batch_image_projection", "slo_batch_feature_association", "slo_batch_map_optimization",
     "slo_batch_sc_detect", "slo_batch_process", "slo_graph_mode", "slo_batch_imu", "slo_batch_scan_time",
     "slo_imu_handler", "slo_image_projection", "slo_feature_association",
@@ -161,6 +162,7 @@ def lib():
     L.slo_stream.argtypes = [P]
     L.slo_stream.restype = P
     L.slo_synchronize.argtypes = [P]
+    L.slo_prepare_mapping.argtypes = [P]
     L.slo_batch_image_projection.argtypes = [P, P, P]
     L.slo_batch_feature_association.argtypes = [P]
     L.slo_batch_map_optimization.argtypes = [P, P, P, ctypes.c_double]

@@ -50,6 +50,8 @@ class SloEngine:
         self.L = slo_amd._abi.lib()
         self.fronts = [slo_amd.Context(cfg, device, n_streams) for _ in range(fronts)]
         self.owner = slo_amd.Context(cfg, device, n_streams) if owner else None
+        if self.owner is not None:   # the one context here that maps: its workspaces up front
+            self.owner.prepare_mapping()
         # split_back: the back end on two contexts, odometry (self.odo) and
         # mapping (self.owner, which then holds the results)
         self.odo = slo_amd.Context(cfg, device, n_streams) if split_back else None
@@ -203,6 +205,27 @@ class DistTransport:
         for d in cuda:
             self.t.cuda.current_stream(d).synchronize()
         self.pending, self.keep = [], []
+
+
+class HostTransport(DistTransport):
+    """DistTransport for a group whose backend moves host tensors only
+    (gloo): a device buffer is staged through pinned host memory on both
+    sides — the fallback of bench.py's Mode S leg when RCCL point-to-point is
+    not available; the drivers and their message order are the same"""
+
+    def send(self, x, dst, tag):
+        if not isinstance(x, np.ndarray) and x.is_cuda:
+            x = x.to("cpu")   # synchronous: the buffer is complete before it travels
+        super().send(x, dst, tag)
+
+    def recv(self, src, tag, like=None):
+        if like is None or not like.is_cuda:
+            return super().recv(src, tag, like)
+        host = super().recv(src, tag, None)   # a numpy array of the message's bytes
+        x = like[:host.size]
+        x.copy_(self.t.from_numpy(host))
+        self.t.cuda.current_stream(x.device).synchronize()
+        return x
 
 
 class LocalTransport:

@@ -48,3 +48,23 @@ def test_a_failing_rank_fails_the_job():
     assert r.returncode == 3
     assert "rank 1 exited with 3" in r.stderr
     assert not [x for x in r.stdout.splitlines() if x.startswith("{")]
+
+
+def test_launch_ranks_stdout_file_and_time_limit(tmp_path):
+    """the Mode S leg's launcher (bench.py modes_leg_launch): every rank's
+    stdout into one file, and a group still running at the time limit is
+    stopped with 124 instead of holding the bench"""
+    import tempfile
+    sys.path.insert(0, os.path.join(ROOT, "sc-lego-loam_amd"))
+    from slo_amd import dist as sdist
+    script = tmp_path / "rank.py"
+    script.write_text("import os, sys, time\n"
+                      "print('{\"rank\": %s, \"world\": %s}' % (os.environ['RANK'], os.environ['WORLD_SIZE']), flush=True)\n"
+                      "time.sleep(float(sys.argv[1]))\n")
+    with tempfile.TemporaryFile("w+") as f:
+        assert sdist.launch_ranks(3, ["0"], str(script), stdout=f, timeout_s=60) == 0
+        f.seek(0)
+        got = sorted(json.loads(x)["rank"] for x in f.read().splitlines())
+    assert got == [0, 1, 2]
+    with tempfile.TemporaryFile("w+") as f:
+        assert sdist.launch_ranks(2, ["600"], str(script), stdout=f, timeout_s=3) == 124

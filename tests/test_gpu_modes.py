@@ -309,3 +309,29 @@ def test_mode_s_and_imu_refuse_each_other():
             eng2.close()
     finally:
         eng.close()
+
+
+def test_mode_s_leg_as_processes_gloo(tmp_path):
+    """bench.py's Mode S leg as separate processes (bench.py --modes-leg,
+    slo_amd.dist.launch_ranks): three ranks of run_rank3 — mapping, odometry,
+    front end — moving device buffers through modes.HostTransport over gloo
+    (the leg's fallback when RCCL is unavailable; RCCL itself needs one GPU per
+    rank), all three on this GPU; the owner's final state and every scan's
+    flags equal one context's bit for bit"""
+    import json
+    import os
+    import sys
+    import tempfile
+    from slo_amd import dist as sdist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    argv = ["--modes-leg", "--gpus", "3", "--preset", "hdl64_1800", "--config-id", "3", "--preroll", "24",
+            "--warmup", "2", "--modes-steps", "16", "--modes-transport", "gloo"]
+    with tempfile.TemporaryFile("w+") as f:
+        rc = sdist.launch_ranks(3, argv, os.path.join(root, "bench.py"), stdout=f, timeout_s=240)
+        f.seek(0)
+        lines = [x for x in f.read().splitlines() if x.startswith("{")]
+    assert rc == 0 and lines, rc
+    rec = json.loads(lines[-1])
+    assert rec["bit_exact_vs_one_context"] is True, rec
+    assert rec["ranks"] == 3 and rec["err"] == 0 and rec["value"] > 0
+    print(rec, file=sys.stderr)

@@ -32,7 +32,7 @@ def _scan(k):
     return O.gen_scan(PID, CID, 0, k), 0.1 * k
 
 
-def _worker(rank, world, port, q, split=False):
+def _worker(rank, world, port, q, split=False, transport="dist"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -57,20 +57,23 @@ def _worker(rank, world, port, q, split=False):
             kf = len(ref.get("keyposes")) // 6
 
         run = modes.run_rank3 if split else modes.run_rank
-        run(eng, rank, world, _scan, N, modes.DistTransport(), on_back=check if rank == 0 else None)
+        tr = modes.DistTransport() if transport == "dist" else modes.HostTransport()
+        run(eng, rank, world, _scan, N, tr, on_back=check if rank == 0 else None)
         q.put((rank, bad, detects, kf))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,split", [(2, False), (3, False), (3, True), (4, True)])
-def test_mode_s_owner_matches_one_process(world, split):
+@pytest.mark.parametrize("world,split,transport", [(2, False, "dist"), (3, False, "dist"), (3, True, "dist"),
+                                                   (4, True, "dist"), (3, True, "host")])
+def test_mode_s_owner_matches_one_process(world, split, transport):
     """split: the reference's three processes as ranks (modes.run_rank3:
-    mapping on rank 0, odometry on rank 1, front ends on the rest)"""
+    mapping on rank 0, odometry on rank 1, front ends on the rest); "host":
+    modes.HostTransport, bench.py's gloo fallback for the Mode S leg"""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, q, split)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, q, split, transport)) for r in range(world)]
     for p in ps:
         p.start()
     res = sorted([q.get(timeout=300) for _ in range(world)])

@@ -20,7 +20,7 @@ shift || true
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
-SHORT="--cpu-scans 0 --single-steps 0 --steps 12 --profile-steps 0 --icp-jobs 0 --extra none --trace-marker $*"
+SHORT="--cpu-scans 0 --single-steps 0 --modes-steps 0 --steps 12 --profile-steps 0 --icp-jobs 0 --extra none --trace-marker $*"
 PMC_KERNELS=${PMC_KERNELS:-"spin|sleep|k_"}   # every libslo kernel (the config lines price each one ≥ 1 %)
 
 # run "$@" under its own limit ($LIM s), printing a line every 30 s; returns its status
