@@ -69,10 +69,10 @@ def test_line_survives_missing_legs():
     assert len(json.dumps(line)) < LIMIT
 
 
-# measured context HBM per GPU (round 5's bench: C3 512 streams 186.48 GiB, C5 128 streams 92.48 GiB), the
-# runtime's own ~1 GiB, 288 GB of HBM
+# measured context HBM per GPU (rounds 5-6: C3 512 streams 186.48 GiB, C4 512 OS1-64 streams 153.81 GiB, C5 128
+# streams 92.48 GiB, the mapping workspaces included), the runtime's own ~1 GiB, 288 GB of HBM
 HBM = 288e9
-CASES = {"c3": (186.48, 512, 115200, 64), "c5": (92.48, 128, 262144, 64)}
+CASES = {"c3": (186.48, 512, 115200, 64), "c4": (153.81, 512, 65536, 64), "c5": (92.48, 128, 262144, 64)}
 
 
 @pytest.mark.parametrize("cfg", sorted(CASES))
