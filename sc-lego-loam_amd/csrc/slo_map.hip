@@ -1097,10 +1097,7 @@ int map_run(slo_ctx* ctx) {
     StreamState* st0 = v.st;
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
     SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
-#ifndef SLO_EXP_SKIP_ASM
-#define SLO_EXP_SKIP_ASM 0   // experiment builds only: 1 leaves the local maps unassembled (wrong results; an upper bound)
-#endif
-    if (!SLO_EXP_SKIP_ASM) SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
     // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263): the six
     // filters as one batched VoxelGrid call (vg_run_groups: (filter, stream)
     // pairs as the sort's units), so a scan waits for one sort chain, not six
