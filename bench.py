@@ -284,13 +284,13 @@ def contract_line(out):
     one = out.get("single_stream")
     if isinstance(one, dict):
         line["single_stream"] = _pick(one, ("value", "unit", "latency_ms", "err"))
-    for k in ("single_stream_pipelined", "single_stream_pipelined3", "single_stream_ranks"):
+    for k in ("single_stream_ctx_pipeline", "single_stream_pipelined", "single_stream_pipelined3", "single_stream_ranks"):
         v = out.get(k)
         if isinstance(v, dict):
-            line[k] = _pick(v, ("value", "unit", "ranks", "transport", "stage_ms_per_scan", "owner_ms_per_scan",
-                                "bit_exact_vs_one_context", "err", "error"))
-    for k in ("single_stream_speedup_vs_cpu_A", "single_stream_pipelined3_speedup_vs_cpu_A",
-              "single_stream_ranks_speedup_vs_cpu_A"):
+            line[k] = _pick(v, ("value", "unit", "ranks", "contexts", "depth", "transport", "stage_ms_per_scan",
+                                "owner_ms_per_scan", "bit_exact_vs_one_context", "err", "error"))
+    for k in ("single_stream_speedup_vs_cpu_A", "single_stream_ctx_pipeline_speedup_vs_cpu_A",
+              "single_stream_pipelined3_speedup_vs_cpu_A", "single_stream_ranks_speedup_vs_cpu_A"):
         if out.get(k) is not None:
             line[k] = out[k]
     if isinstance(out.get("hbm"), dict):
@@ -678,10 +678,47 @@ def single_stream(torch, slo_amd, a, cfg, pid, local):
             lat.append(time.perf_counter() - t1)
         lat = np.array(lat) * 1e3
         kf = int(ctx.get(0, "n_keyframes")[0])
+        state = {nm: ctx.get(0, nm).copy() for nm in MODES_STATE}
         return {"value": round(thr, 2), "unit": "scans/s", "streams": 1, "scans_timed": half,
                 "latency_ms": {"mean": round(float(lat.mean()), 3), "p50": round(float(np.median(lat)), 3),
                                "p99": round(float(np.percentile(lat, 99)), 3), "scans": len(lat)},
-                "keyframes_at_end": kf, "err": int(ctx.get(0, "err")[0])}
+                "keyframes_at_end": kf, "err": int(ctx.get(0, "err")[0])}, state
+    finally:
+        gen.close()
+        ctx.close()
+
+
+def single_stream_ctx_pipeline(torch, slo_amd, a, cfg, pid, local, ref_state, depth=6):
+    """one C3 stream in ONE context with slo_pipeline: its front end, odometry
+    and mapping stage on three HIP streams of the context (the reference's
+    three processes), the host only enqueuing slo_batch_process calls; the
+    scans of single_stream, the last half timed back to back, the final state
+    compared bit for bit with single_stream's plain context"""
+    P = cfg.max_points
+    ctx = slo_amd.Context(cfg, local, 1)
+    ctx.pipeline(depth)
+    gen = slo_amd.DeviceGenerator(pid, a.config_id, 0, 1, local)
+    n = a.preroll + a.warmup + a.single_steps
+    try:
+        buf = torch.empty((n, 1, P, 4), dtype=torch.float32, device=f"cuda:{local}")
+        gen.scans(0, n, buf.data_ptr())
+        cnt = torch.full((1,), P, dtype=torch.int32, device=f"cuda:{local}")
+        k0 = a.preroll + a.warmup + a.single_steps // 2
+        for k in range(k0):
+            ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        ctx.synchronize()
+        t0 = time.perf_counter()
+        for k in range(k0, n):
+            ctx.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        ctx.synchronize()
+        el = time.perf_counter() - t0
+        got = {nm: ctx.get(0, nm) for nm in MODES_STATE}
+        same = ref_state is not None and all(
+            ref_state[nm].shape == got[nm].shape and np.array_equal(ref_state[nm].view(np.uint8), got[nm].view(np.uint8))
+            for nm in MODES_STATE)
+        return {"value": round((n - k0) / el, 2), "unit": "scans/s", "streams": 1, "contexts": 1, "depth": depth,
+                "scans_timed": n - k0, "bit_exact_vs_one_context": bool(same), "err": int(got["err"][0]),
+                "note": "one context, slo_pipeline: front end | odometry | mapping + Scan Context on three HIP streams"}
     finally:
         gen.close()
         ctx.close()
@@ -1255,9 +1292,10 @@ def main():
         return
 
     # ---- one stream alone (C3 is defined on one KITTI replay)
-    one = one_p = one_p3 = None
+    one = one_p = one_p3 = one_c = None
     if a.single_steps > 0:
-        one = single_stream(torch, slo_amd, a, cfg, pid, local)
+        one, one_state = single_stream(torch, slo_amd, a, cfg, pid, local)
+        one_c = single_stream_ctx_pipeline(torch, slo_amd, a, cfg, pid, local, one_state)
         one_p = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local)
         one_p3 = single_stream_pipelined(torch, slo_amd, a, cfg, pid, local, stages=3)
 
@@ -1309,6 +1347,8 @@ def main():
         "speedup_vs_cpu_A": vs_a({"value": value}),
         "single_stream": one,
         "single_stream_speedup_vs_cpu_A": vs_a(one),
+        "single_stream_ctx_pipeline": one_c,
+        "single_stream_ctx_pipeline_speedup_vs_cpu_A": vs_a(one_c),
         "single_stream_pipelined": one_p,
         "single_stream_pipelined_speedup_vs_cpu_A": vs_a(one_p),
         "single_stream_pipelined3": one_p3,

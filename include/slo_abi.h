@@ -254,6 +254,23 @@ int slo_odom_process(slo_ctx* ctx, const void* d_features, const void* d_points,
                      double t_scan, void* d_odom_out);
 int slo_map_process(slo_ctx* ctx, const void* d_odom, const void* d_points, const int32_t* d_counts, double t_scan);
 
+/* The same three-stage split inside ONE context (the reference's three
+ * processes, launch/run.launch:14-17, as three HIP streams): after
+ * slo_pipeline(ctx, depth >= 2) on a fresh context, slo_batch_process(ctx, ..)
+ * runs a scan's front end on an internal front context, its odometry on an
+ * internal odometry context and transformFusion + mapOptimization + Scan
+ * Context on ctx itself, each on its own HIP stream, the stages chained by
+ * events through rings of `depth` feature / odometry buffers and input copies —
+ * so scan k + 2's front end, scan k + 1's odometry and scan k's mapping step
+ * run at once, and the host only enqueues.  Results are bit-identical to the
+ * context without it (Mode S above).  slo_get reads each field from the stage
+ * that computes it; slo_synchronize waits for all three; slo_stream(ctx) is
+ * the mapping stage's stream, the last one a scan passes (its completion
+ * covers every stage of every scan issued).  depth 0 turns it off again (only
+ * before the first scan).  Not with IMU input, loop verification or the pose
+ * graph (their host round trips need the one-context path): SLO_E_STATE. */
+int slo_pipeline(slo_ctx* ctx, int depth);
+
 /* ---------------------------------------------------------------- loop-closure verification
  * mapOptmization.cpp:841-1110 (detectLoopClosure + performLoopClosure, minus
  * the GTSAM factors).  Needs cfg.loop_verify = 1 and

@@ -346,6 +346,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
 void slo_destroy(slo_ctx* ctx) {
     if (!ctx) return;
     hipSetDevice(ctx->dev);
+    slo::pipe_free(ctx);   // slo_pipeline's stage contexts and rings
     if (ctx->stream) hipStreamSynchronize(ctx->stream);
     for (auto& p : ctx->pending) { hipEventDestroy(p.second.first); hipEventDestroy(p.second.second); }
     slo::graphs_drop(ctx);
@@ -378,6 +379,8 @@ int slo_prepare_mapping(slo_ctx* ctx) {
 int slo_synchronize(slo_ctx* ctx) {
     if (!ctx) return SLO_E_ARG;
     hipSetDevice(ctx->dev);
+    if (ctx->pipe)   // slo_pipeline: the front and odometry stages too
+        for (slo_ctx* c : slo::pipe_stages(ctx)) SLO_CHECK(hipStreamSynchronize(c->stream));
     SLO_CHECK(hipStreamSynchronize(ctx->stream));
     return SLO_OK;
 }
@@ -600,6 +603,7 @@ extern "C" {
 
 int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
     if (!ctx || !d_points || !d_counts) return SLO_E_ARG;
+    if (ctx->pipe) return slo::pipe_step(ctx, d_points, d_counts, t_scan);   // slo_pipeline
     if (ctx->cfg.use_cloud_ring && !ctx->v.rings) {
         ctx->err = "cfg.use_cloud_ring needs slo_batch_set_rings";
         return SLO_E_STATE;
@@ -845,6 +849,135 @@ int slo_map_process(slo_ctx* ctx, const void* d_odom, const void* d_points, cons
     return slo_batch_sc_detect(ctx);
 }
 
+}  // extern "C"
+namespace slo {
+// slo_pipeline: the Mode S three-stage split (front end | odometry |
+// mapping) inside one context.  Per scan k, slot = k mod D of the rings:
+//   front stream:    [wait evM[slot] of scan k - D] copy the input -> raw / cnt[slot],
+//                    slo_front_process -> feat[slot], record evF[slot]
+//   odometry stream: wait evF[slot], slo_odom_process(feat[slot]) -> odom[slot], record evO[slot]
+//   mapping stream:  wait evO[slot], slo_map_process(odom[slot]), record evM[slot]
+// Scan k - D's mapping step has read raw / cnt / odom[slot], and before it
+// (evO) its odometry read feat[slot], so waiting on evM[slot] before the
+// copy protects every buffer of the slot; each stage's own state is ordered
+// by its stream.  The host never waits.
+struct SloPipe {
+    slo_ctx* front = nullptr;
+    slo_ctx* odo = nullptr;
+    int D = 0;
+    long long k = 0;
+    size_t fbytes = 0, obytes = 0, rbytes = 0;
+    std::vector<void*> feat, odom, raw, cnt;
+    std::vector<hipEvent_t> evF, evO, evM;
+};
+void pipe_free(slo_ctx* ctx) {
+    SloPipe* p = ctx->pipe;
+    if (!p) return;
+    for (slo_ctx* c : {p->front, p->odo})
+        if (c) hipStreamSynchronize(c->stream);
+    hipStreamSynchronize(ctx->stream);
+    for (auto* v : {&p->feat, &p->odom, &p->raw, &p->cnt})
+        for (void* q : *v)
+            if (q) hipFree(q);
+    for (auto* v : {&p->evF, &p->evO, &p->evM})
+        for (hipEvent_t e : *v)
+            if (e) hipEventDestroy(e);
+    slo_destroy(p->front);
+    slo_destroy(p->odo);
+    delete p;
+    ctx->pipe = nullptr;
+}
+// the stage whose context computes slo_get's field `name` (the mapping stage,
+// ctx itself, for everything mapOptimization, transformFusion and Scan
+// Context write, and for the fields the odometry buffer hands it)
+slo_ctx* pipe_stage_of(slo_ctx* ctx, const std::string& name) {
+    static const char* front[] = {"range", "label", "ground", "full_cloud", "seg_pts", "seg_ground", "seg_col",
+                                  "seg_range", "ring_start", "ring_end", "orient", "fa_seg_pts", "curvature",
+                                  "picked", "cloud_label", "smooth_ind", "sharp", "less_sharp", "flat", "less_flat"};
+    static const char* odom[] = {"transform_cur", "fa_iters", "imu"};
+    for (const char* f : front)
+        if (name == f) return ctx->pipe->front;
+    for (const char* f : odom)
+        if (name == f) return ctx->pipe->odo;
+    return ctx;
+}
+static int pipe_fail(slo_ctx* ctx, slo_ctx* stage, int r) {
+    if (stage != ctx) ctx->err = stage->err;
+    return r;
+}
+std::vector<slo_ctx*> pipe_stages(slo_ctx* ctx) { return {ctx->pipe->front, ctx->pipe->odo}; }
+int pipe_step(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan) {
+    SloPipe& p = *ctx->pipe;
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    const int slot = (int)(p.k % p.D);
+    slo_ctx* F = p.front;
+    slo_ctx* O = p.odo;
+    if (p.k >= p.D) SLO_CHECK(hipStreamWaitEvent(F->stream, p.evM[slot], 0));
+    SLO_CHECK(hipMemcpyAsync(p.raw[slot], d_points, p.rbytes, hipMemcpyDeviceToDevice, F->stream));
+    SLO_CHECK(hipMemcpyAsync(p.cnt[slot], d_counts, sizeof(int32_t) * ctx->S, hipMemcpyDeviceToDevice, F->stream));
+    const int32_t* cnt = (const int32_t*)p.cnt[slot];
+    int r = slo_front_process(F, p.raw[slot], cnt, t_scan, nullptr, nullptr, p.feat[slot]);
+    if (r) return pipe_fail(ctx, F, r);
+    SLO_CHECK(hipEventRecord(p.evF[slot], F->stream));
+    SLO_CHECK(hipStreamWaitEvent(O->stream, p.evF[slot], 0));
+    r = slo_odom_process(O, p.feat[slot], p.raw[slot], cnt, t_scan, p.odom[slot]);
+    if (r) return pipe_fail(ctx, O, r);
+    SLO_CHECK(hipEventRecord(p.evO[slot], O->stream));
+    SLO_CHECK(hipStreamWaitEvent(ctx->stream, p.evO[slot], 0));
+    r = slo_map_process(ctx, p.odom[slot], p.raw[slot], cnt, t_scan);
+    if (r) return r;
+    SLO_CHECK(hipEventRecord(p.evM[slot], ctx->stream));
+    ++p.k;
+    return SLO_OK;
+}
+}  // namespace slo
+extern "C" {
+
+int slo_pipeline(slo_ctx* ctx, int depth) {
+    if (!ctx || depth < 0 || depth == 1 || depth > 64) return SLO_E_ARG;
+    if (ctx->fa_inited || ctx->modes_used || (ctx->pipe && ctx->pipe->k > 0)) {
+        ctx->err = "slo_pipeline: only on a context that has not processed a scan";
+        return SLO_E_STATE;
+    }
+    if (ctx->imu_fed || ctx->cfg.loop_verify || ctx->cfg.pose_graph || ctx->cfg.use_cloud_ring) {
+        ctx->err = "slo_pipeline: not with IMU input, loop verification, the pose graph or useCloudRing";
+        return SLO_E_STATE;
+    }
+    SLO_CHECK(hipSetDevice(ctx->dev));
+    slo::pipe_free(ctx);
+    if (depth == 0) return SLO_OK;
+    slo::SloPipe* p = new (std::nothrow) slo::SloPipe();
+    if (!p) return SLO_E_CAPACITY;
+    ctx->pipe = p;
+    int r = slo_create(&ctx->cfg, ctx->dev, ctx->S, &p->front);
+    if (!r) r = slo_create(&ctx->cfg, ctx->dev, ctx->S, &p->odo);
+    if (!r) r = slo::map_ws_ensure(ctx);
+    if (r) {
+        slo::pipe_free(ctx);
+        return r;
+    }
+    p->D = depth;
+    p->fbytes = slo_modes_features_bytes(ctx);
+    p->obytes = slo_modes_odom_bytes(ctx);
+    p->rbytes = (size_t)ctx->S * ctx->v.P * sizeof(float4);
+    bool ok = true;
+    for (int i = 0; i < depth && ok; ++i) {
+        void *a = nullptr, *b = nullptr, *c = nullptr, *d = nullptr;
+        hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+        ok = hipMalloc(&a, p->fbytes) == hipSuccess && hipMalloc(&b, p->obytes) == hipSuccess &&
+             hipMalloc(&c, p->rbytes) == hipSuccess && hipMalloc(&d, sizeof(int32_t) * ctx->S) == hipSuccess;
+        for (int j = 0; j < 3 && ok; ++j) ok = hipEventCreateWithFlags(&e[j], hipEventDisableTiming) == hipSuccess;
+        p->feat.push_back(a); p->odom.push_back(b); p->raw.push_back(c); p->cnt.push_back(d);
+        p->evF.push_back(e[0]); p->evO.push_back(e[1]); p->evM.push_back(e[2]);
+    }
+    if (!ok) {
+        slo::pipe_free(ctx);
+        ctx->err = "slo_pipeline: out of device memory for the stage rings";
+        return SLO_E_HIP;
+    }
+    return SLO_OK;
+}
+
 int slo_batch_loop_closure(slo_ctx* ctx) {
     if (!ctx) return SLO_E_ARG;
     if (!ctx->cfg.loop_verify) { ctx->err = "loop verification needs cfg.loop_verify"; return SLO_E_STATE; }
@@ -879,6 +1012,10 @@ int slo_get(slo_ctx* ctx, int stream, const char* name_c, void* dst, size_t cap_
     if (!ctx || !name_c || stream < 0 || stream >= ctx->S) return SLO_E_ARG;
     SLO_CHECK(hipSetDevice(ctx->dev));
     SLO_CHECK(hipStreamSynchronize(ctx->stream));
+    if (ctx->pipe) {   // slo_pipeline: the field from the stage that computes it
+        slo_ctx* st = slo::pipe_stage_of(ctx, std::string(name_c));
+        if (st != ctx) return slo_get(st, stream, name_c, dst, cap_bytes);
+    }
     slo::timing_flush(ctx);
     const DevView& v = ctx->v;
     StreamState st;

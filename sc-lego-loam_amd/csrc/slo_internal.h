@@ -503,6 +503,7 @@ struct HashGrid {
 
 }  // namespace slo
 
+namespace slo { struct SloPipe; }
 struct slo_ctx {
     slo_config cfg;
     int dev = 0;
@@ -587,6 +588,9 @@ struct slo_ctx {
     // the mapping step's workspaces are sized on the first entry that can map
     // (map_ws_ensure), so a Mode S front or odometry context never holds them
     bool map_ws_ready = false;
+    // slo_pipeline: the front end and the odometry on two internal contexts,
+    // each on its own stream, this context the mapping stage (slo_ctx.hip)
+    slo::SloPipe* pipe = nullptr;
 };
 
 // With at most SLO_PREP_DEFER_STREAMS streams a batched step defers the
@@ -629,6 +633,12 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
 int map_run(slo_ctx* ctx);
 int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces (slo_map.hip)
 int map_ws_ensure(slo_ctx* ctx);   // map_ws_presize once, from an entry point that can map, before any capture
+// slo_pipeline (slo_ctx.hip): one scan through the three stages; the stage
+// contexts; the stage that computes a slo_get field; freeing it all
+int pipe_step(slo_ctx* ctx, const void* d_points, const int32_t* d_counts, double t_scan);
+std::vector<slo_ctx*> pipe_stages(slo_ctx* ctx);
+slo_ctx* pipe_stage_of(slo_ctx* ctx, const std::string& name);
+void pipe_free(slo_ctx* ctx);
 struct VgGroup;
 int vg_presize(slo_ctx* ctx, const VgGroup* groups, int G);
 int pcl_presize(slo_ctx* ctx, int SV, size_t items, size_t maxT);

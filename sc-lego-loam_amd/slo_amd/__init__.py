@@ -151,6 +151,12 @@ class Context:
     def synchronize(self):
         self._ok(self.L.slo_synchronize(self.h), "slo_synchronize")
 
+    def pipeline(self, depth=6):
+        """slo_pipeline: the front end, the odometry and the mapping stage of
+        every scan on three HIP streams of this one context (depth: the
+        buffer rings; 0 = off), bit-identical to the context without it"""
+        self._ok(self.L.slo_pipeline(self.h, int(depth)), "slo_pipeline")
+
     def prepare_mapping(self):
         """slo_prepare_mapping: the mapping step's workspaces now (a caller
         budgeting HBM measures free memory after this)"""

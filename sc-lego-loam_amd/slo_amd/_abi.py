@@ -127,7 +127,7 @@ EXPORTS = [
     "slo_gen_device_create", "slo_gen_device_scans", "slo_gen_device_destroy",
     # Mode S: one stream's front ends and back end on different contexts
     "slo_modes_carry_bytes", "slo_modes_features_bytes", "slo_front_process", "slo_back_process",
-    "slo_modes_odom_bytes", "slo_odom_process", "slo_map_process",
+    "slo_modes_odom_bytes", "slo_odom_process", "slo_map_process", "slo_pipeline",
     # pose-graph back end (csrc/slo_pg.hip, host side)
     "slo_pg_create", "slo_pg_destroy", "slo_pg_last_error", "slo_pg_size", "slo_pg_add_keyframe", "slo_pg_add_loop", "slo_pg_optimize", "slo_pg_get_key_poses", "slo_pg_last_transform", "slo_set_key_poses",
 ]
@@ -163,6 +163,7 @@ def lib():
     L.slo_stream.restype = P
     L.slo_synchronize.argtypes = [P]
     L.slo_prepare_mapping.argtypes = [P]
+    L.slo_pipeline.argtypes = [P, ctypes.c_int]
     L.slo_batch_image_projection.argtypes = [P, P, P]
     L.slo_batch_feature_association.argtypes = [P]
     L.slo_batch_map_optimization.argtypes = [P, P, P, ctypes.c_double]

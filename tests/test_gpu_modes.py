@@ -335,3 +335,97 @@ def test_mode_s_leg_as_processes_gloo(tmp_path):
     assert rec["bit_exact_vs_one_context"] is True, rec
     assert rec["ranks"] == 3 and rec["err"] == 0 and rec["value"] > 0
     print(rec, file=sys.stderr)
+
+
+def _pipe_names(fl):
+    n = ["transform_sum", "integrated", "err", "flags", "n_keyframes", "seg_pts", "curvature", "sharp", "less_flat",
+         "transform_cur", "fa_iters", "corner_last"]
+    if fl & 2:
+        n += ["mapped", "keyposes", "map_surf_ds", "surf_total_ds", "raw_ds"]
+    if fl & 4:
+        n += ["sc_desc", "ring_key"]
+    if fl & 8:
+        n += ["detect", "detect_f"]
+    return n
+
+
+@pytest.mark.parametrize("preset,config,scans,depth", [
+    (0, 1, 220, 2),   # C1 VLP-16 past 51 keyframes (Scan Context detects), the smallest rings
+    (6, 3, 60, 6),    # C3 hdl64_1800 at the bench's depth
+])
+def test_pipeline_one_context_matches_plain(preset, config, scans, depth):
+    """slo_pipeline: one context whose front end, odometry and mapping stage
+    run on three HIP streams (the reference's three processes inside one
+    context).  Scan by scan (read after each) every pose, flag, feature cloud,
+    keyframe, descriptor and detect equals a plain context's bit for bit —
+    each field read from the stage that computes it — and, enqueued back to
+    back with no host wait (the stages overlapping through the rings), the
+    final state is the same too."""
+    torch = _torch()
+    cfg = slo_amd.preset(preset)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(preset, config, 0, 1)
+    buf = torch.empty((scans, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, scans, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    one = slo_amd.Context(cfg, 0, 1)
+    pipe = slo_amd.Context(cfg, 0, 1)
+    pipe.pipeline(depth)
+    fast = slo_amd.Context(cfg, 0, 1)
+    fast.pipeline(depth)
+    bad, detects, ref = [], 0, None
+    try:
+        for k in range(scans):
+            one.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            pipe.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+            fl = int(one.get(0, "flags")[0])
+            detects += int(bool(fl & 8))
+            for name in _pipe_names(fl):
+                a, b = one.get(0, name), pipe.get(0, name)
+                if a.shape != b.shape or not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+                    bad.append((k, name))
+        ref = {n: one.get(0, n).copy() for n in _pipe_names(7)}
+        for k in range(scans):   # back to back: the host only enqueues
+            fast.batch_process(buf[k].data_ptr(), cnt.data_ptr(), 0.1 * k)
+        fast.synchronize()
+        for n, a in ref.items():
+            b = fast.get(0, n)
+            if a.shape != b.shape or not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+                bad.append(("async", n))
+        assert bad == [], bad[:8]
+        assert int(one.get(0, "n_keyframes")[0]) > 5
+        if preset == 0:
+            assert detects > 0
+    finally:
+        for c in (one, pipe, fast):
+            c.close()
+
+
+def test_pipeline_refusals():
+    """slo_pipeline only on a fresh context, and not with the paths whose host
+    round trips need one context (loop verification here)"""
+    torch = _torch()
+    cfg = slo_amd.preset(0)
+    P = cfg.max_points
+    gen = slo_amd.DeviceGenerator(0, 1, 0, 1)
+    buf = torch.empty((1, 1, P, 4), dtype=torch.float32, device="cuda")
+    gen.scans(0, 1, buf.data_ptr())
+    gen.close()
+    cnt = torch.full((1,), P, dtype=torch.int32, device="cuda")
+    a = slo_amd.Context(cfg, 0, 1)
+    try:
+        a.batch_process(buf[0].data_ptr(), cnt.data_ptr(), 0.0)
+        with pytest.raises(slo_amd.SloError, match="first scan|processed a scan"):
+            a.pipeline(4)
+    finally:
+        a.close()
+    cfg2 = slo_amd.preset(0)
+    cfg2.loop_verify = 1
+    cfg2.loop_archive_points = 4096
+    b = slo_amd.Context(cfg2, 0, 1)
+    try:
+        with pytest.raises(slo_amd.SloError, match="loop verification"):
+            b.pipeline(4)
+    finally:
+        b.close()
