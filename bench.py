@@ -852,7 +852,7 @@ def modes_leg_local(torch, slo_amd, a, cfg, pid, local, world=3):
     return out
 
 
-def modes_leg_launch(a, world, timeout_s=420):
+def modes_leg_launch(a, world, timeout_s=(150, 120)):
     """Mode S at N > 1: a fresh group of `world` processes, one per GPU
     (bench.py --modes-leg, slo_amd.dist.launch_ranks), the buffers moved by
     RCCL point-to-point (modes.DistTransport); rank 0's JSON record, or the
@@ -866,10 +866,13 @@ def modes_leg_launch(a, world, timeout_s=420):
     if a.sc_off:
         argv.append("--sc-off")
     failed = None
-    for tr in ("nccl", "gloo"):   # RCCL first; gloo through host copies if the RCCL group fails
+    # RCCL first; gloo through host copies if the RCCL group fails.  The leg
+    # takes ~40 s (process start, group init, 310 scans, the one-context
+    # replay); the limits keep a hung group from costing the bench its line
+    for tr, lim in zip(("nccl", "gloo"), timeout_s):
         with tempfile.TemporaryFile("w+") as f:
             rc = sdist.launch_ranks(world, argv + ["--modes-transport", tr], os.path.abspath(__file__), stdout=f,
-                                    timeout_s=timeout_s)
+                                    timeout_s=lim)
             f.seek(0)
             lines = [x for x in f.read().splitlines() if x.startswith("{")]
         if rc == 0 and lines:
