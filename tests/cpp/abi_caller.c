@@ -22,6 +22,8 @@ int main(void) {
     CHECK(slo_create(NULL, 0, 1, &ctx) == SLO_E_ARG);
     CHECK(slo_batch_process(NULL, NULL, NULL, 0.0) == SLO_E_ARG);
     CHECK(slo_graph_mode(NULL, 1) == SLO_E_ARG);
+    CHECK(slo_pipeline(NULL, 6) == SLO_E_ARG);
+    CHECK(slo_prepare_mapping(NULL) == SLO_E_ARG);
     CHECK(slo_record_floats() == SLO_RECORD_FLOATS);
     /* argument checks of the SCManager helpers and the batched VoxelGrid (no GPU call) */
     {
