@@ -462,15 +462,16 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
         if name == "pc_lpairs":   # per pair: both positions in, both items (key + index) read and written
             return int(40 * pw[1])
         if name in ("pc_finish_w", "pc_finish_s", "pc_finish_b"):   # a finish entry's items in and out
-            return int(16 * pw[2 + ("pc_finish_w", "pc_finish_s", "pc_finish_b").index(name)])
+            b = int(16 * pw[2 + ("pc_finish_w", "pc_finish_s", "pc_finish_b").index(name)])
+            if name == "pc_finish_b":   # + the spent-depth heapsorts it runs first (PW_FALL; std::sort's heapsort):
+                b += int(32 * pw[21])   # each item in, to the 8-B scratch, back, out
+            return b
         if name == "pc_finish_bx":   # the 4 Ki entries too wide for 32-bit items (PW_FINX)
             return int(16 * pw[20])
         if name == "pc_tail":     # per stepped item: its key counted (4 B) and read again on its side of the
             # crossing (4 B) plus the left side's index (4 B); per pair: partner position out and in, both
             # items read and written
             return int(12 * pw[7] + 40 * pw[8])
-        if name == "pc_fallback":   # the spent-depth ranges' items in and out (PW_FALL; std::sort's heapsort)
-            return int(16 * pw[21])
         if name == "pc_count":    # the points
             return int(16 * pw[5])
         if name == "pc_write":    # the points in, (key, index) out
@@ -481,7 +482,7 @@ def algo_bytes(name, c, cfg, S, steps, map_steps):
 
 
 PCL_SORT_FAMILY = ("pc_count", "pc_write", "pc_lcount", "pc_lrank", "pc_lpairs", "pc_lscan", "pc_lsplit", "pc_tail",
-                   "pc_finish_w", "pc_finish_s", "pc_finish_b", "pc_finish_bx", "pc_fallback", "vg_reduce")
+                   "pc_finish_w", "pc_finish_s", "pc_finish_b", "pc_finish_bx", "vg_reduce")
 
 
 def compulsory_bytes(name, c):

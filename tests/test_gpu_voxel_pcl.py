@@ -250,7 +250,7 @@ def test_stable_order_switch():
 
 
 def test_spent_depth_heapsort_paths(model, tmp_path):
-    """k_pc_fallback (slo_vgpcl.hip): spent-depth ranges over 4 Ki items,
+    """pc_fallback_entry (slo_vgpcl.hip, inside k_pc_finish32<4 Ki>): spent-depth ranges over 4 Ki items,
     heapsorted by one wave in global memory — a 12 000-item killer, a
     7 000-item killer with its keys spread x97 (a key span over 2^18) and the
     100 000-item killer, several ranges in one call (each workgroup's scratch
