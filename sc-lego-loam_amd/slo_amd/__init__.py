@@ -262,11 +262,11 @@ class Context:
         self._ok(self.L.slo_timing_reset(self.h), "slo_timing_reset")
 
     def timing_read(self):
-        cap = 64
-        buf = ctypes.create_string_buffer(8192)
+        cap = 256
+        buf = ctypes.create_string_buffer(32768)
         ms = (ctypes.c_double * cap)()
         cnt = (ctypes.c_int64 * cap)()
-        n = self.L.slo_timing_read(self.h, buf, 8192, ms, cnt, cap)
+        n = self.L.slo_timing_read(self.h, buf, 32768, ms, cnt, cap)
         names = buf.raw.split(b"\0")[:n]
         return {names[i].decode(): (ms[i], cnt[i]) for i in range(n)}
 
