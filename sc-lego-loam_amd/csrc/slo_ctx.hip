@@ -514,7 +514,7 @@ static int step_launches(slo_ctx* ctx, bool map) {
     const bool forked = ctx->prep_pending && defer;
     int r = forked ? fa_prep_fork(ctx) : 0;
     if (!r) r = ip_run(ctx);
-    if (!r) r = fa_features_run(ctx);
+    if (!r) r = fa_features_run(ctx, defer);   // its less-flat VoxelGrids beside the odometry
     if (!r && forked) r = fa_prep_join(ctx);
     if (!r) r = fa_odometry_run(ctx, false, true, defer);
     if (r) return r;

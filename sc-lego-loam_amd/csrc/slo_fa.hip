@@ -1110,13 +1110,17 @@ __global__ void __launch_bounds__(64 * RW) __attribute__((amdgpu_waves_per_eu(RW
 }
 
 // concatenate per-ring outputs in ring order: one block per (ring, stream),
-// each summing the counts of the rings before its own
-__global__ void __launch_bounds__(256) k_fa_gather(DevView v) {
+// each summing the counts of the rings before its own.  `part`: 0 all four
+// clouds; 1 sharp, less sharp and flat (fa_pick's); 2 less flat alone
+// (fa_ring_ds's) — the two halves of a forked step (fa_features_run), which
+// read and write disjoint counts
+__global__ void __launch_bounds__(256) k_fa_gather(DevView v, int part) {
     const int r = blockIdx.x, s = blockIdx.y;
     const int R = v.cfg.n_scan, C = v.cfg.horizon_scan;
     __shared__ int off[4], tot[4];
     const int* rc = v.ring_cnt + (size_t)s * R * 4;
-    if (threadIdx.x < 4) {
+    const bool pk = part != 2, ds = part != 1;
+    if (threadIdx.x < 4 && (threadIdx.x == 3 ? ds : pk)) {
         const int c = threadIdx.x;
         int a = 0, b = 0;
         for (int q = 0; q < R; ++q) {
@@ -1130,38 +1134,40 @@ __global__ void __launch_bounds__(256) k_fa_gather(DevView v) {
     __syncthreads();
     // ring boundaries of less_sharp / less_flat (the odometry's ring windows)
     if (threadIdx.x == 0) {
-        v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + r] = off[1];
-        v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + r] = min(off[3], v.cap_less_flat);
-        if (r == R - 1) {
-            v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + R] = tot[1];
-            v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + R] = min(tot[3], v.cap_less_flat);
-            StreamState& st = v.st[s];
-            st.n_sharp = tot[0]; st.n_less_sharp = tot[1]; st.n_flat = tot[2];
-            st.n_less_flat = min(tot[3], v.cap_less_flat);
+        StreamState& st = v.st[s];
+        if (pk) {
+            v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + r] = off[1];
+            if (r == R - 1) {
+                v.roff_cur[((size_t)s * 2 + 0) * (R + 1) + R] = tot[1];
+                st.n_sharp = tot[0]; st.n_less_sharp = tot[1]; st.n_flat = tot[2];
+            }
+        }
+        if (ds) {
+            v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + r] = min(off[3], v.cap_less_flat);
+            if (r == R - 1) {
+                v.roff_cur[((size_t)s * 2 + 1) * (R + 1) + R] = min(tot[3], v.cap_less_flat);
+                st.n_less_flat = min(tot[3], v.cap_less_flat);
+            }
         }
     }
     const size_t rr = (size_t)s * R + r;
-    for (int i = threadIdx.x; i < rc[4 * r + 0]; i += blockDim.x)
-        v.sharp[(size_t)s * v.cap_sharp + off[0] + i] = v.r_sharp[rr * 12 + i];
-    for (int i = threadIdx.x; i < rc[4 * r + 1]; i += blockDim.x)
-        v.less_sharp[(size_t)s * v.cap_less_sharp + off[1] + i] = v.r_less_sharp[rr * 120 + i];
-    for (int i = threadIdx.x; i < rc[4 * r + 2]; i += blockDim.x)
-        v.flat[(size_t)s * v.cap_flat + off[2] + i] = v.r_flat[rr * 24 + i];
-    for (int i = threadIdx.x; i < rc[4 * r + 3]; i += blockDim.x)
-        if (off[3] + i < v.cap_less_flat) v.less_flat[(size_t)s * v.cap_less_flat + off[3] + i] = v.r_lf_ds[rr * C + i];
+    if (pk) {
+        for (int i = threadIdx.x; i < rc[4 * r + 0]; i += blockDim.x)
+            v.sharp[(size_t)s * v.cap_sharp + off[0] + i] = v.r_sharp[rr * 12 + i];
+        for (int i = threadIdx.x; i < rc[4 * r + 1]; i += blockDim.x)
+            v.less_sharp[(size_t)s * v.cap_less_sharp + off[1] + i] = v.r_less_sharp[rr * 120 + i];
+        for (int i = threadIdx.x; i < rc[4 * r + 2]; i += blockDim.x)
+            v.flat[(size_t)s * v.cap_flat + off[2] + i] = v.r_flat[rr * 24 + i];
+    }
+    if (ds)
+        for (int i = threadIdx.x; i < rc[4 * r + 3]; i += blockDim.x)
+            if (off[3] + i < v.cap_less_flat) v.less_flat[(size_t)s * v.cap_less_flat + off[3] + i] = v.r_lf_ds[rr * C + i];
 }
 
-int fa_features_run(slo_ctx* ctx) {
+// the less-flat VoxelGrids and their gather (fa_features_run)
+static int fa_ring_ds_launch(slo_ctx* ctx, int part) {
     DevView& v = ctx->v;
     const int S = ctx->S, R = v.cfg.n_scan;
-    const int T = 256;
-    dim3 gh((v.H + T - 1) / T, S);
-    SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "fa_imu_start", k_fa_imu_start, dim3((S + 63) / 64), dim3(64), 0, v);
-    SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
-    SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     if (v.cfg.voxel_order == SLO_VOXEL_PCL) {   // RING_W waves per ring; slo_create refuses rings over 4096 points
         const bool few = S <= 8;
         if (v.cfg.horizon_scan <= 2048) {
@@ -1176,8 +1182,45 @@ int fa_features_run(slo_ctx* ctx) {
         while (ds_keys < v.cfg.horizon_scan) ds_keys <<= 1;
         SLO_LAUNCH(ctx, "fa_ring_ds", k_fa_ring_ds, dim3(R, S), dim3(256), ds_keys * sizeof(unsigned long long), v);
     }
-    SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v, part);
     SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+// fork: the less-flat VoxelGrids (the reference's surfPointsLessFlatScan
+// downsampling, FA:779-780) on ring_stream beside the odometry, which reads
+// none of their output before its end (k_fa_to_end): fa_odometry_run joins
+// there (fa_ring_join).  Contexts of at most SLO_PREP_DEFER_STREAMS streams,
+// whose step the latency of these sorts would otherwise lengthen.
+int fa_features_run(slo_ctx* ctx, bool fork) {
+    DevView& v = ctx->v;
+    const int S = ctx->S, R = v.cfg.n_scan;
+    const int T = 256;
+    dim3 gh((v.H + T - 1) / T, S);
+    SLO_LAUNCH(ctx, "fa_halfpass", k_fa_halfpass, gh, dim3(T), 0, v);
+    SLO_LAUNCH(ctx, "fa_imu_start", k_fa_imu_start, dim3((S + 63) / 64), dim3(64), 0, v);
+    SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
+    SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
+    if (!fork || !ctx->ring_stream) return fa_ring_ds_launch(ctx, 0);
+    SLO_CHECK(hipEventRecord(ctx->ev_rfork, ctx->stream));
+    SLO_CHECK(hipStreamWaitEvent(ctx->ring_stream, ctx->ev_rfork, 0));
+    std::swap(ctx->stream, ctx->ring_stream);
+    int r = fa_ring_ds_launch(ctx, 2);
+    std::swap(ctx->stream, ctx->ring_stream);
+    if (r) return r;
+    SLO_CHECK(hipEventRecord(ctx->ev_rjoin, ctx->ring_stream));
+    ctx->ring_pending = true;
+    SLO_LAUNCH(ctx, "fa_gather", k_fa_gather, dim3(R, S), dim3(256), 0, v, 1);
+    SLO_CHECK(hipGetLastError());
+    return 0;
+}
+
+int fa_ring_join(slo_ctx* ctx) {
+    if (!ctx->ring_pending) return 0;
+    ctx->ring_pending = false;
+    SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_rjoin, 0));
     return 0;
 }
 

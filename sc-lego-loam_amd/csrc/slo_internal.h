@@ -585,6 +585,12 @@ struct slo_ctx {
     bool prep_pending = false;
     hipStream_t prep_stream = nullptr;
     hipEvent_t ev_pfork = nullptr, ev_pjoin = nullptr;
+    // the less-flat VoxelGrids of a batched step of a few streams, forked
+    // beside its odometry on ring_stream (fa_features_run) and joined before
+    // the odometry's end (fa_ring_join); created with prep_stream
+    bool ring_pending = false;
+    hipStream_t ring_stream = nullptr;
+    hipEvent_t ev_rfork = nullptr, ev_rjoin = nullptr;
     // the mapping step's workspaces are sized on the first entry that can map
     // (map_ws_ensure), so a Mode S front or odometry context never holds them
     bool map_ws_ready = false;
@@ -611,7 +617,8 @@ void pg_free(slo_ctx* ctx);
 int pg_after_mapping(slo_ctx* ctx);
 int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
-int fa_features_run(slo_ctx* ctx);
+int fa_features_run(slo_ctx* ctx, bool fork = false);
+int fa_ring_join(slo_ctx* ctx);    // a forked step's less-flat VoxelGrids, joined to ctx->stream
 int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse = true, bool defer = false);
 void fa_swap_last(slo_ctx* ctx);
 int fa_prep_fork(slo_ctx* ctx);    // a pending preparation on prep_stream (forked from / joined to ctx->stream)

@@ -1228,6 +1228,9 @@ int fa_prep_init(slo_ctx* ctx) {
     SLO_CHECK(hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pjoin, hipEventDisableTiming));
+    SLO_CHECK(hipStreamCreateWithFlags(&ctx->ring_stream, hipStreamNonBlocking));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_rfork, hipEventDisableTiming));
+    SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_rjoin, hipEventDisableTiming));
     return 0;
 }
 
@@ -1258,6 +1261,13 @@ void fa_prep_free(slo_ctx* ctx) {
     hipEventDestroy(ctx->ev_pjoin);
     hipStreamDestroy(ctx->prep_stream);
     ctx->prep_stream = nullptr;
+    if (ctx->ring_stream) {
+        hipStreamSynchronize(ctx->ring_stream);
+        hipEventDestroy(ctx->ev_rfork);
+        hipEventDestroy(ctx->ev_rjoin);
+        hipStreamDestroy(ctx->ring_stream);
+        ctx->ring_stream = nullptr;
+    }
 }
 
 // fuse: transformFusion's /integrated_to_init in k_fa_odo_finish (false on a
@@ -1267,6 +1277,8 @@ void fa_prep_free(slo_ctx* ctx) {
 int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse, bool defer) {
     if (ctx->prep_pending)
         if (int r = fa_prep_launch(ctx)) return r;   // the last scan's, in-stream
+    if (first_scan)   // (k_fa_odo_begin's first-scan branch reads the less-flat cloud)
+        if (int r = fa_ring_join(ctx)) return r;
     DevView& v = ctx->v;
     const int S = ctx->S;
     SLO_LAUNCH(ctx, "fa_odo_begin", k_fa_odo_begin, dim3(S), dim3(256), 0, v, first_scan ? 1 : 0);
@@ -1284,6 +1296,7 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse, bool defer) {
             SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
         }
     }
+    if (int r = fa_ring_join(ctx)) return r;   // the less-flat cloud, forked by fa_features_run
     SLO_LAUNCH(ctx, "fa_to_end", k_fa_to_end, dim3(xcd_grid(S, SLO_TOEND_BLOCKS)), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_odo_finish", k_fa_odo_finish, dim3(S), dim3(64), 0, v, fuse ? 1 : 0);
     SLO_CHECK(hipGetLastError());
