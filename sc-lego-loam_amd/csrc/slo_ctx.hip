@@ -512,7 +512,9 @@ static int step_launches(slo_ctx* ctx, bool map) {
     // (not with a kernel-name timing filter: its in-stream stamps pair up per stream, as map_run's fork)
     const bool defer = ctx->S <= SLO_PREP_DEFER_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
     const bool forked = ctx->prep_pending && defer;
-    int r = forked ? fa_prep_fork(ctx) : 0;
+    ctx->map_forked = false;
+    int r = map && defer && map_fork_ok(ctx) ? map_side_fork(ctx) : 0;
+    if (!r && forked) r = fa_prep_fork(ctx);
     if (!r) r = ip_run(ctx);
     if (!r) r = fa_features_run(ctx, defer);   // its less-flat VoxelGrids beside the odometry
     if (!r && forked) r = fa_prep_join(ctx);

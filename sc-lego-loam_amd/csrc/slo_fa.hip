@@ -413,6 +413,13 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
 // wave ballot: a sector's picks only label that sector's own points, so
 // collecting after all six sectors equals the reference's interleaving.
 
+// WAVE_TIES (contexts of a few streams, whose scan waits for the slowest
+// ring): a tie sector is sorted by a whole wave with slo_pclsort.h's exact
+// std::sort restatement (wave_sort: the same introsort steps, partitions taken
+// lane-parallel) on (curvature order key << 32 | index) items in place of the
+// sector's entries — SmoothLess compares the curvature alone, as the PCL
+// sort's items compare their high words — instead of by one lane.
+template <bool WAVE_TIES>
 __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int s = blockIdx.y;
     const int ring = blockIdx.x;
@@ -428,7 +435,7 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int S = v.st[s].seg_count;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     Smooth* sm = v.smooth + base;
-    __shared__ Smooth lsm[SLO_RING_STAGE];
+    __shared__ Smooth lsm[SLO_RING_STAGE];   // (alignas(8): also the wave tie sort's u64 items)
 #if SLO_SORT_LCV
     __shared__ float lcv[SLO_RING_STAGE];
 #define SORT_CV(ind) lcv[(ind) - lo]
@@ -478,11 +485,43 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     }
     __syncthreads();
     SORT_STAMP(1)
-    if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
-        const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
-        slo_sort::std_sort_small(&lsm[sp - lo], ep - sp, SmoothLess());
+    if constexpr (WAVE_TIES) {   // ties (or a long sector): the exact sort, a wave each
+        constexpr int kTieMax = 2048;   // the wave path's longest sector
+        __shared__ unsigned short ttbl[4][kTieMax / 2 + 1];
+        __shared__ slo_pcl::WaveSmem tws[4];
+        __shared__ int s_terr;
+        if (tid == 0) s_terr = 0;
+        __syncthreads();
+        for (int j = wave; j < 6; j += 4) {
+            if (!s_tie[j]) continue;   // (uniform in the wave)
+            const int sp = sec_sp(rs, re, j), n = sec_ep(rs, re, j) - sp;
+            if (n > kTieMax) {
+                if (lane == 0) slo_sort::std_sort_small(&lsm[sp - lo], n, SmoothLess());
+                continue;
+            }
+            // each lane turns its own entries into items and back: no entry moves between the two
+            slo_pcl::u64* it = reinterpret_cast<slo_pcl::u64*>(&lsm[sp - lo]);
+            for (int k = lane; k < n; k += 64) {
+                const Smooth x = lsm[sp - lo + k];
+                it[k] = ((slo_pcl::u64)f2ord_fa(x.value) << 32) | (unsigned int)x.ind;
+            }
+            slo_pcl::wave_fence();
+            slo_pcl::wave_sort<64>(it, n, 2 * slo_pcl::lg2(n), ttbl[wave], tws[wave], &s_terr);
+            slo_pcl::wave_fence();
+            for (int k = lane; k < n; k += 64) {
+                const slo_pcl::u64 q = it[k];
+                lsm[sp - lo + k] = Smooth{ord2f_fa((unsigned int)(q >> 32)), (int)(unsigned int)q};
+            }
+        }
+        __syncthreads();
+        if (tid == 0 && s_terr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
+    } else {
+        if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
+            const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
+            slo_sort::std_sort_small(&lsm[sp - lo], ep - sp, SmoothLess());
+        }
+        __syncthreads();
     }
-    __syncthreads();
     SORT_STAMP(2)
     // ---- candidate lists: point indices as window offsets, in visiting order
     int16_t* l_sh = v.ex_list + (size_t)s * v.H * 2;
@@ -1201,7 +1240,8 @@ int fa_features_run(slo_ctx* ctx, bool fork) {
     SLO_LAUNCH(ctx, "fa_imu_start", k_fa_imu_start, dim3((S + 63) / 64), dim3(64), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
+    if (S <= SLO_PREP_DEFER_STREAMS) SLO_LAUNCH(ctx, "fa_sort", k_fa_sort<true>, dim3(R, S), dim3(256), 0, v);
+    else SLO_LAUNCH(ctx, "fa_sort", k_fa_sort<false>, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     if (!fork || !ctx->ring_stream) return fa_ring_ds_launch(ctx, 0);
     SLO_CHECK(hipEventRecord(ctx->ev_rfork, ctx->stream));

@@ -114,6 +114,7 @@ struct StreamState {
     int32_t det_calign[64], det_pending;
     int32_t flags;
     int32_t err;
+    int32_t err_map;   // the local-map selection's error bits until k_mo_concat folds them into err
     unsigned long long dbg[8];            // diagnostic counters (slo_get "dbg"), not part of the algorithm
 };
 
@@ -589,6 +590,9 @@ struct slo_ctx {
     // beside its odometry on ring_stream (fa_features_run) and joined before
     // the odometry's end (fa_ring_join); created with prep_stream
     bool ring_pending = false;
+    // the local map's half of this step's mapping, issued on `side` at the
+    // step's start (map_side_fork, slo_map.hip); map_run joins it
+    bool map_forked = false;
     hipStream_t ring_stream = nullptr;
     hipEvent_t ev_rfork = nullptr, ev_rjoin = nullptr;
     // the mapping step's workspaces are sized on the first entry that can map
@@ -604,6 +608,12 @@ struct slo_ctx {
 // beside its projection and features (slo_ctx.hip step_launches)
 #ifndef SLO_PREP_DEFER_STREAMS
 #define SLO_PREP_DEFER_STREAMS 8
+#endif
+#ifndef SLO_MAP_FORK
+#define SLO_MAP_FORK 1   // such a step also issues its mapping's local-map half at its start (map_side_fork)
+#endif
+#ifndef SLO_MAP_FORK_G
+#define SLO_MAP_FORK_G 3   // the forked half's VoxelGrids (map_groups order): both local maps and the raw scan
 #endif
 
 // launch helpers with optional per-kernel HIP-event timing
@@ -638,6 +648,8 @@ GridView grid_view(const HashGrid& g);
 void grid_free(HashGrid& g);
 int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, const int32_t* n, int n_stride);
 int map_run(slo_ctx* ctx);
+bool map_fork_ok(const slo_ctx* ctx);   // a few-stream PCL-order context: its steps fork the local map's half
+int map_side_fork(slo_ctx* ctx);        // (step_launches, before the projection)
 int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces (slo_map.hip)
 int map_ws_ensure(slo_ctx* ctx);   // map_ws_presize once, from an entry point that can map, before any capture
 // slo_pipeline (slo_ctx.hip): one scan through the three stages; the stage

@@ -113,7 +113,7 @@ __device__ void mo_surrounding_radius(const DevView& v, int s, StreamState& st) 
     const int minb0 = (int)floorf(mn[0] * inv), minb1 = (int)floorf(mn[1] * inv), minb2 = (int)floorf(mn[2] * inv);
     const int divx = (int)floorf(mx[0] * inv) - minb0 + 1, divy = (int)floorf(mx[1] * inv) - minb1 + 1;
     if (n > 0 && dx * dy * dz > 2147483647LL) {
-        if (threadIdx.x == 0) st.err |= SLO_ERR_MAP_CAPACITY;
+        if (threadIdx.x == 0) st.err_map |= SLO_ERR_MAP_CAPACITY;
         bad = 1;
     }
     // (voxel index << 32 | key index), padded to a power of two with ~0
@@ -168,31 +168,39 @@ __device__ void mo_surrounding_radius(const DevView& v, int s, StreamState& st) 
             for (int i = 0; i < ne; ++i) if (ex[i] == ds_id[j]) { have = true; break; }
             if (have) continue;
             if (ne < v.MAPK) ex[ne++] = ds_id[j];
-            else st.err |= SLO_ERR_MAP_CAPACITY;
+            else st.err_map |= SLO_ERR_MAP_CAPACITY;
         }
         st.recent_n = ne;
         // a keyframe whose cloud slot a newer keyframe reused
         for (int i = 0; i < ne; ++i)
-            if (ex[i] < nk - v.KFR) st.err |= SLO_ERR_MAP_CAPACITY;
+            if (ex[i] < nk - v.KFR) st.err_map |= SLO_ERR_MAP_CAPACITY;
     }
 }
 
-__global__ void k_mo_prepare(DevView v) {
+// part: 1 the current scan's half (the outlier cloud's axes, the odometry
+// hand-off and transformAssociateToMap), 2 the local map's half
+// (extractSurroundingKeyFrames' selection and the map sizes: state the last
+// mapping step left, none of the current scan's), 3 both.  A few-stream step
+// runs half 2 on the side stream from its start (map_side_fork); the halves
+// write disjoint StreamState fields, the map half's errors into err_map
+// (k_mo_concat folds them after the join)
+__global__ void k_mo_prepare(DevView v, int part) {
     const int s = blockIdx.x;
     StreamState& st = v.st[s];
     // adjustOutlierCloud (FA:1746-1757): lidar -> camera axes
-    for (int i = threadIdx.x; i < st.outlier_count; i += blockDim.x) {
-        float4 p = v.outlier[(size_t)s * v.H + i];
-        v.outl_cam[(size_t)s * v.H + i] = make_float4(p.y, p.z, p.x, p.w);
-    }
+    if (part & 1)
+        for (int i = threadIdx.x; i < st.outlier_count; i += blockDim.x) {
+            float4 p = v.outlier[(size_t)s * v.H + i];
+            v.outl_cam[(size_t)s * v.H + i] = make_float4(p.y, p.z, p.x, p.w);
+        }
     // extractSurroundingKeyFrames without loop closure: the radius branch
-    // reads the pose of the last run, before associate_to_map below
-    if (!v.cfg.loop_closure_enable && st.n_keyframes > 0) mo_surrounding_radius(v, s, st);
+    // reads the pose of the last run (transformAftMapped)
+    if ((part & 2) && !v.cfg.loop_closure_enable && st.n_keyframes > 0) mo_surrounding_radius(v, s, st);
     if (threadIdx.x >= 64) return;
     // laserOdometryHandler (via the tf round trip), transformAssociateToMap
     // and pointAssociateToMap's sin/cos, their trig side by side on wave 0's
     // lanes (slo_pose_wave.h); lane 0 stores
-    {
+    if (part & 1) {
         float ts[6], bef[6], aft[6], sum[6], inc[6], tbm[6];
         for (int k = 0; k < 6; ++k) {
             ts[k] = st.transformSum[k]; bef[k] = st.transformBefMapped[k]; aft[k] = st.transformAftMapped[k];
@@ -211,10 +219,14 @@ __global__ void k_mo_prepare(DevView v) {
         o[0] = sn[0]; o[1] = cs[0]; o[2] = sn[1]; o[3] = cs[1]; o[4] = sn[2]; o[5] = cs[2];
         o[6] = tbm[3]; o[7] = tbm[4]; o[8] = tbm[5];
     }
-    st.mo_ran = 1;
-    st.kf_saved = 0;
-    st.mo_iters = 0;
-    st.mo_converged = 0;
+    if (threadIdx.x != 0) return;
+    if (part & 1) {
+        st.mo_ran = 1;
+        st.kf_saved = 0;
+        st.mo_iters = 0;
+        st.mo_converged = 0;
+    }
+    if (!(part & 2)) return;
     // extractSurroundingKeyFrames: recent keyframe deque
     const int nk = st.n_keyframes;
     const int N = v.cfg.surrounding_keyframe_search_num;
@@ -246,17 +258,18 @@ __global__ void k_mo_prepare(DevView v) {
         nc += kn[0];
         ns += kn[1] + kn[2];
     }
-    if (nc > v.cap_mc) { nc = v.cap_mc; st.err |= SLO_ERR_MAP_CAPACITY; }
-    if (ns > v.cap_ms) { ns = v.cap_ms; st.err |= SLO_ERR_MAP_CAPACITY; }
+    if (nc > v.cap_mc) { nc = v.cap_mc; st.err_map |= SLO_ERR_MAP_CAPACITY; }
+    if (ns > v.cap_ms) { ns = v.cap_ms; st.err_map |= SLO_ERR_MAP_CAPACITY; }
     st.n_corner_map = nc;
     st.n_surf_map = ns;
 }
 
-// one block per deque entry (blockIdx.x) of stream blockIdx.y
-__global__ void k_mo_assemble(DevView v) {
+// one block per deque entry (blockIdx.x) of stream blockIdx.y (need_ran 0:
+// the side stream's, issued before this step's k_mo_prepare sets mo_ran)
+__global__ void k_mo_assemble(DevView v, int need_ran) {
     const int s = blockIdx.y, e = blockIdx.x;
     const StreamState& st = v.st[s];
-    if (!st.mo_ran || e >= st.recent_n) return;
+    if ((need_ran && !st.mo_ran) || e >= st.recent_n) return;
     const int32_t* ids = mo_map_ids(v, s, st);
     // the clouds before this keyframe's: their sizes summed by the block
     // (integer sums: any order), not by every thread in a row
@@ -326,6 +339,8 @@ __global__ void k_mo_concat(DevView v) {
     if (threadIdx.x == 0) {
         st.n_st = a + b;
         st.map_ok = st.n_cmap_ds > 10 && st.n_smap_ds > 100;
+        st.err |= st.err_map;   // the local-map selection's (k_mo_prepare half 2)
+        st.err_map = 0;
     }
 }
 
@@ -1079,6 +1094,11 @@ int map_ws_presize(slo_ctx* ctx) {
     } else if ((r = vg_presize(ctx, gs, 6))) {
         return r;
     }
+    if (map_fork_ok(ctx)) {   // the side stream and its workspaces (map_side_fork)
+        if ((r = vg_side_ready(ctx))) return r;
+        VgSide sd(ctx);
+        if ((r = vg_presize(ctx, gs, SLO_MAP_FORK_G))) return r;
+    }
     const VgGroup t = map_total_group(ctx);
     return vg_presize(ctx, &t, 1);
 }
@@ -1090,14 +1110,62 @@ int map_ws_ensure(slo_ctx* ctx) {
     return 0;
 }
 
+static int map_run_rest(slo_ctx* ctx, bool grids_built);
+
+bool map_fork_ok(const slo_ctx* ctx) {
+    return SLO_MAP_FORK && ctx->S <= SLO_PREP_DEFER_STREAMS && ctx->cfg.voxel_order == SLO_VOXEL_PCL;
+}
+
+// A few-stream step's mapping half that needs nothing of the current scan's
+// odometry, issued on the side stream at the step's start, beside its
+// projection, features and odometry: extractSurroundingKeyFrames' selection
+// (k_mo_prepare half 2; MO:1127-1166), the local map's assembly (MO:1168-1222)
+// and the VoxelGrids of the two local maps and of the raw scan (MO:1224-1230,
+// the Scan Context input), then the hash grids over the DS maps.  map_run's
+// current-scan half joins it before k_mo_concat.
+int map_side_fork(slo_ctx* ctx) {
+    DevView& v = ctx->v;
+    const int S = ctx->S;
+    const int SS = ST_STRIDE;
+    StreamState* st0 = v.st;
+    auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
+    int r;
+    if ((r = vg_side_ready(ctx))) return r;   // (map_ws_ensure made it: nothing is created here)
+    SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SLO_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    {
+        VgSide sd(ctx);
+        SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v, 2);
+        SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v, 0);
+        VgGroup gs[6];
+        map_groups(ctx, gs);
+        if ((r = vg_run_groups(ctx, "map_local", gs, SLO_MAP_FORK_G))) return r;
+        if ((r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
+        if ((r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
+    }
+    SLO_CHECK(hipEventRecord(ctx->ev_join, ctx->side));
+    ctx->map_forked = true;
+    return 0;
+}
+
 int map_run(slo_ctx* ctx) {
     DevView& v = ctx->v;
     const int S = ctx->S;
     const int SS = ST_STRIDE;
     StreamState* st0 = v.st;
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
-    SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v);
-    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v);
+    const bool forked = ctx->map_forked;   // map_side_fork issued the local map's half
+    ctx->map_forked = false;
+    SLO_LAUNCH(ctx, "mo_prepare", k_mo_prepare, dim3(S), dim3(256), 0, v, forked ? 1 : 3);
+    if (forked) {
+        VgGroup gs[6];
+        map_groups(ctx, gs);
+        int r = vg_run_groups(ctx, "map_step", gs + SLO_MAP_FORK_G, 6 - SLO_MAP_FORK_G);   // corner, surf, outlier (MO:1233-1263)
+        if (r) return r;
+        SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+        return map_run_rest(ctx, true);
+    }
+    SLO_LAUNCH(ctx, "mo_assemble", k_mo_assemble, dim3(v.MAPK, S), dim3(256), 0, v, 1);
     // local map DS (MO:1224-1230) and current scan DS (MO:1233-1263): the six
     // filters as one batched VoxelGrid call (vg_run_groups: (filter, stream)
     // pairs as the sort's units), so a scan waits for one sort chain, not six
@@ -1145,6 +1213,18 @@ int map_run(slo_ctx* ctx) {
                     v.cur_o_ds, v.cap_ko, fld(&StreamState::n_outl_ds), SS, v.cap_ko))) return r;
     if (fork) SLO_CHECK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));   // k_mo_concat's map_ok reads the map DS sizes
     }
+    return map_run_rest(ctx, fork);
+}
+
+// k_mo_concat onwards; grids_built: the hash grids over the DS maps were
+// built on the side stream
+static int map_run_rest(slo_ctx* ctx, bool grids_built) {
+    DevView& v = ctx->v;
+    const int S = ctx->S;
+    const int SS = ST_STRIDE;
+    StreamState* st0 = v.st;
+    auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
+    int r;
     SLO_LAUNCH(ctx, "mo_concat", k_mo_concat, dim3(S), dim3(256), 0, v);
     {
         const VgGroup t = map_total_group(ctx);
@@ -1152,8 +1232,8 @@ int map_run(slo_ctx* ctx) {
     }
     if (SLO_MO_PERM) SLO_LAUNCH(ctx, "mo_perm", k_mo_perm, dim3(S), dim3(256), 0, v);
     // hash grids over the DS maps (on the side stream when forked, above)
-    if (!fork && (r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
-    if (!fork && (r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
+    if (!grids_built && (r = grid_build(ctx, ctx->grid_c, v.map_c_ds, v.cap_mc, fld(&StreamState::n_cmap_ds), SS))) return r;
+    if (!grids_built && (r = grid_build(ctx, ctx->grid_s, v.map_s_ds, v.cap_ms, fld(&StreamState::n_smap_ds), SS))) return r;
     for (int it = 0; it < 10; ++it) {
         SLO_LAUNCH(ctx, "mo_knn", k_mo_knn, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);
         SLO_LAUNCH(ctx, "mo_corr", k_mo_corr, dim3(xcd_grid(S, SLO_MO_BLOCKS)), dim3(256), 0, v);

@@ -52,7 +52,7 @@ def main():
     out = {}
     lat, cls, _ = run(True, False, n0, n, buf, cnt, cfg, pid)
     out["graph"] = {"lat_ms": [round(x, 3) for x in lat], "flags": cls}
-    lat2, cls2, ker = run(False, True, n0, n, buf, cnt, cfg, pid)
+    lat2, cls2, ker = run(False, True, n0, n, buf, cnt, cfg, pid) if os.environ.get("EAGER", "1") == "1" else ([], [], [])
     out["eager"] = {"lat_ms": [round(x, 3) for x in lat2], "flags": cls2}
     by = {}
     for f, kt in zip(cls2, ker):
@@ -71,7 +71,7 @@ def main():
     l = np.array(lat)
     print(f"all: mean {l.mean():.3f} p50 {np.median(l):.3f} p99 {np.percentile(l, 99):.3f}", flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    json.dump(out, open(os.path.join(ROOT, "gpurun_out", "single_trace.json"), "w"))
+    json.dump(out, open(os.environ.get("TRACE_OUT") or os.path.join(ROOT, "gpurun_out", "single_trace.json"), "w"))
 
 
 if __name__ == "__main__":
