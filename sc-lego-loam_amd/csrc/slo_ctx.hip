@@ -513,7 +513,7 @@ static int step_launches(slo_ctx* ctx, bool map) {
     const bool defer = ctx->S <= SLO_PREP_DEFER_STREAMS && !(ctx->timing && !ctx->timing_only.empty());
     const bool forked = ctx->prep_pending && defer;
     ctx->map_forked = false;
-    int r = map && defer && map_fork_ok(ctx) ? map_side_fork(ctx) : 0;
+    int r = map && defer && ctx->map_fork_ready ? map_side_fork(ctx) : 0;
     if (!r && forked) r = fa_prep_fork(ctx);
     if (!r) r = ip_run(ctx);
     if (!r) r = fa_features_run(ctx, defer);   // its less-flat VoxelGrids beside the odometry
@@ -612,6 +612,10 @@ int slo_batch_process(slo_ctx* ctx, const void* d_points, const int32_t* d_count
     }
     SLO_CHECK(hipSetDevice(ctx->dev));
     if (int r = slo::map_ws_ensure(ctx)) return r;   // before step_graph may capture
+    if (ctx->S <= SLO_PREP_DEFER_STREAMS) {   // the few-stream step's forks (step_launches)
+        if (int r = slo::fa_ring_init(ctx)) return r;
+        if (int r = slo::map_fork_prepare(ctx)) return r;
+    }
     int r = slo::step_graph(ctx, d_points, d_counts, t_scan);
     if (r <= 0) return r;
     if ((r = slo_batch_scan_time(ctx, t_scan))) return r;

@@ -593,6 +593,7 @@ struct slo_ctx {
     // the local map's half of this step's mapping, issued on `side` at the
     // step's start (map_side_fork, slo_map.hip); map_run joins it
     bool map_forked = false;
+    bool map_fork_ready = false;   // map_fork_prepare made the side stream and sized its workspaces
     hipStream_t ring_stream = nullptr;
     hipEvent_t ev_rfork = nullptr, ev_rjoin = nullptr;
     // the mapping step's workspaces are sized on the first entry that can map
@@ -629,6 +630,7 @@ int pg_after_loops(slo_ctx* ctx);
 int ip_run(slo_ctx* ctx);
 int fa_features_run(slo_ctx* ctx, bool fork = false);
 int fa_ring_join(slo_ctx* ctx);    // a forked step's less-flat VoxelGrids, joined to ctx->stream
+int fa_ring_init(slo_ctx* ctx);    // ring_stream and its events (slo_batch_process, outside captures)
 int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse = true, bool defer = false);
 void fa_swap_last(slo_ctx* ctx);
 int fa_prep_fork(slo_ctx* ctx);    // a pending preparation on prep_stream (forked from / joined to ctx->stream)
@@ -650,6 +652,7 @@ int grid_build(slo_ctx* ctx, HashGrid& g, const float4* pts, size_t stride, cons
 int map_run(slo_ctx* ctx);
 bool map_fork_ok(const slo_ctx* ctx);   // a few-stream PCL-order context: its steps fork the local map's half
 int map_side_fork(slo_ctx* ctx);        // (step_launches, before the projection)
+int map_fork_prepare(slo_ctx* ctx);     // its side stream and workspaces (slo_batch_process, outside captures)
 int map_ws_presize(slo_ctx* ctx);  // the mapping step's VoxelGrid / sort workspaces (slo_map.hip)
 int map_ws_ensure(slo_ctx* ctx);   // map_ws_presize once, from an entry point that can map, before any capture
 // slo_pipeline (slo_ctx.hip): one scan through the three stages; the stage

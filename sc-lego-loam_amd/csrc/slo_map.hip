@@ -1094,11 +1094,7 @@ int map_ws_presize(slo_ctx* ctx) {
     } else if ((r = vg_presize(ctx, gs, 6))) {
         return r;
     }
-    if (map_fork_ok(ctx)) {   // the side stream and its workspaces (map_side_fork)
-        if ((r = vg_side_ready(ctx))) return r;
-        VgSide sd(ctx);
-        if ((r = vg_presize(ctx, gs, SLO_MAP_FORK_G))) return r;
-    }
+
     const VgGroup t = map_total_group(ctx);
     return vg_presize(ctx, &t, 1);
 }
@@ -1116,6 +1112,22 @@ bool map_fork_ok(const slo_ctx* ctx) {
     return SLO_MAP_FORK && ctx->S <= SLO_PREP_DEFER_STREAMS && ctx->cfg.voxel_order == SLO_VOXEL_PCL;
 }
 
+// the side stream and its workspaces for map_side_fork (slo_batch_process,
+// never inside a capture; only contexts that step through it)
+int map_fork_prepare(slo_ctx* ctx) {
+    if (ctx->map_fork_ready || !map_fork_ok(ctx)) return 0;
+    if (int r = map_ws_ensure(ctx)) return r;
+    if (int r = vg_side_ready(ctx)) return r;
+    VgGroup gs[6];
+    map_groups(ctx, gs);
+    {
+        VgSide sd(ctx);
+        if (int r = vg_presize(ctx, gs, SLO_MAP_FORK_G)) return r;
+    }
+    ctx->map_fork_ready = true;
+    return 0;
+}
+
 // A few-stream step's mapping half that needs nothing of the current scan's
 // odometry, issued on the side stream at the step's start, beside its
 // projection, features and odometry: extractSurroundingKeyFrames' selection
@@ -1130,8 +1142,7 @@ int map_side_fork(slo_ctx* ctx) {
     StreamState* st0 = v.st;
     auto fld = [&](int32_t StreamState::*f) { return &(st0->*f); };
     int r;
-    if ((r = vg_side_ready(ctx))) return r;   // (map_ws_ensure made it: nothing is created here)
-    SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SLO_CHECK(hipEventRecord(ctx->ev_fork, ctx->stream));   // (side: map_fork_prepare made it)
     SLO_CHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     {
         VgSide sd(ctx);

@@ -1228,6 +1228,14 @@ int fa_prep_init(slo_ctx* ctx) {
     SLO_CHECK(hipStreamCreateWithFlags(&ctx->prep_stream, hipStreamNonBlocking));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pfork, hipEventDisableTiming));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_pjoin, hipEventDisableTiming));
+    return 0;
+}
+
+// ring_stream and its events: only a context that steps through
+// slo_batch_process makes them (not the stage contexts of Mode S or
+// slo_pipeline, whose streams should each keep a hardware queue of their own)
+int fa_ring_init(slo_ctx* ctx) {
+    if (ctx->ring_stream) return 0;
     SLO_CHECK(hipStreamCreateWithFlags(&ctx->ring_stream, hipStreamNonBlocking));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_rfork, hipEventDisableTiming));
     SLO_CHECK(hipEventCreateWithFlags(&ctx->ev_rjoin, hipEventDisableTiming));
