@@ -400,8 +400,8 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
 // k_fa_sort (256 threads): the six sector sorts (std::sort on [sp, ep),
 // Q4/Q6).  Without equal curvatures a sort's result is unique, so a wave
 // bitonic-sorts each sector in registers; only a sector holding a tie is
-// sorted by one lane with the exact libstdc++ introsort restatement
-// (slo_introsort.h), whose order of equal keys is the reference's.  Then the
+// sorted by a wave with the exact libstdc++ introsort restatement
+// (slo_pclsort.h wave_sort), whose order of equal keys is the reference's.  Then the
 // pick eligibility that picks cannot change (curvature, ground flag) is
 // evaluated by all lanes and compacted into per-sector candidate lists in
 // visiting order (sharp ep..sp, flat sp..ep), stored for k_fa_pick.
@@ -413,13 +413,14 @@ __device__ inline void bitonic_sort_wave(Smooth* a, int n, int lane, int* tie_fl
 // wave ballot: a sector's picks only label that sector's own points, so
 // collecting after all six sectors equals the reference's interleaving.
 
-// WAVE_TIES (contexts of a few streams, whose scan waits for the slowest
-// ring): a tie sector is sorted by a whole wave with slo_pclsort.h's exact
-// std::sort restatement (wave_sort: the same introsort steps, partitions taken
+// A tie sector is sorted by a whole wave with slo_pclsort.h's exact std::sort
+// restatement (wave_sort: the same introsort steps, partitions taken
 // lane-parallel) on (curvature order key << 32 | index) items in place of the
 // sector's entries — SmoothLess compares the curvature alone, as the PCL
-// sort's items compare their high words — instead of by one lane.
-template <bool WAVE_TIES>
+// sort's items compare their high words.  (Round 6: one lane ran
+// slo_sort::std_sort_small on it while the workgroup waited — 193 us per
+// launch on one stream, 62 with the wave; C3's fa_sort 10.5 -> 6.5 ms per
+// instrumented pass at 29.5 KB of LDS against 18.7.)
 __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     const int s = blockIdx.y;
     const int ring = blockIdx.x;
@@ -485,7 +486,7 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
     }
     __syncthreads();
     SORT_STAMP(1)
-    if constexpr (WAVE_TIES) {   // ties (or a long sector): the exact sort, a wave each
+    {   // ties (or a long sector): the exact sort, a wave each
         constexpr int kTieMax = 2048;   // the wave path's longest sector
         __shared__ unsigned short ttbl[4][kTieMax / 2 + 1];
         __shared__ slo_pcl::WaveSmem tws[4];
@@ -515,12 +516,6 @@ __global__ void __launch_bounds__(256) k_fa_sort(DevView v) {
         }
         __syncthreads();
         if (tid == 0 && s_terr) atomicOr(&v.st[s].err, SLO_ERR_SORT);
-    } else {
-        if (tid < 6 && s_tie[tid]) {   // ties (or a very long sector): the exact introsort, one lane each
-            const int sp = sec_sp(rs, re, tid), ep = sec_ep(rs, re, tid);
-            slo_sort::std_sort_small(&lsm[sp - lo], ep - sp, SmoothLess());
-        }
-        __syncthreads();
     }
     SORT_STAMP(2)
     // ---- candidate lists: point indices as window offsets, in visiting order
@@ -1240,8 +1235,7 @@ int fa_features_run(slo_ctx* ctx, bool fork) {
     SLO_LAUNCH(ctx, "fa_imu_start", k_fa_imu_start, dim3((S + 63) / 64), dim3(64), 0, v);
     SLO_LAUNCH(ctx, "fa_points", k_fa_points, gh, dim3(T), 0, v);
     SLO_LAUNCH(ctx, "fa_extract_stale", k_fa_extract_stale, dim3(1, S), dim3(256), 0, v);
-    if (S <= SLO_PREP_DEFER_STREAMS) SLO_LAUNCH(ctx, "fa_sort", k_fa_sort<true>, dim3(R, S), dim3(256), 0, v);
-    else SLO_LAUNCH(ctx, "fa_sort", k_fa_sort<false>, dim3(R, S), dim3(256), 0, v);
+    SLO_LAUNCH(ctx, "fa_sort", k_fa_sort, dim3(R, S), dim3(256), 0, v);
     SLO_LAUNCH(ctx, "fa_pick", k_fa_pick, dim3(R, S), dim3(64), 0, v);
     if (!fork || !ctx->ring_stream) return fa_ring_ds_launch(ctx, 0);
     SLO_CHECK(hipEventRecord(ctx->ev_rfork, ctx->stream));
