@@ -277,6 +277,7 @@ int slo_create(const slo_config* cfg, int hip_device, int n_streams, slo_ctx** o
     c.add(&v.cur_st, S * v.cap_st);
     c.add(&v.cur_st_ds, S * v.cap_st);
     c.add(&v.mo_part, S * SLO_MO_BLOCKS * SLO_MO_PART);
+    c.add(&v.tick, S);
     v.cap_q = v.cap_less_sharp + v.cap_st;
     c.add(&v.mo_nn, S * (size_t)v.cap_q * 5);
     c.add(&v.mo_perm, S * (size_t)v.cap_q);

@@ -225,6 +225,7 @@ struct DevView {
     float4* cur_st;      // [S][cap_st]     laserCloudSurfTotalLast
     float4* cur_st_ds;   // [S][cap_st]
     double* mo_part;     // [S][MO_BLOCKS][SLO_MO_PART] partial A^T A / A^T b (double-double) + count
+    int32_t* tick;       // [S] arrivals of a fused odometry launch's search workgroups (k_fa_fused, 0 between launches)
     int cap_q;           // mapping queries per stream: cap_less_sharp + cap_st
     int32_t* mo_nn;      // [S][cap_q][5] 5-NN map indices of each query (-1: rejected)
     int32_t* mo_perm;    // [S][cap_q] the queries grouped by their body-frame 2 m cell (k_mo_perm): the order

@@ -753,13 +753,13 @@ __global__ void __launch_bounds__(256) k_fa_search_surf(DevView v, int nb) {
 #ifndef SLO_ODO_FEW
 #define SLO_ODO_FEW 8   // at most this many streams: k_fa_search_surf_few
 #endif
+#ifndef SLO_ODO_FUSED
+#define SLO_ODO_FUSED 1   // ... and k_fa_fused (a search and its iterations in one launch)
+#endif
 __device__ inline bool walk_better(float d, int c, int t, const WalkBest& w) {
     return d < w.d || (d == w.d && (c < w.cls || (c == w.cls && t < w.t)));
 }
-__global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
-    int s, chunk;
-    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
-    if (s >= v.S) return;
+__device__ __forceinline__ void search_surf_few_block(const DevView& v, int s, int chunk) {
     const StreamState& st = v.st[s];
     if (st.odo_phase != 0) return;
     constexpr int QPB = 256 / SURF_QL;   // queries per workgroup
@@ -832,6 +832,12 @@ __global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
     ind[3 * i + 1] = found ? w.index() : -1;
     ind[3 * i + 2] = found ? w3.index() : -1;
 }
+__global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    search_surf_few_block(v, s, chunk);
+}
 
 // findCorrespondingCornerFeatures (FA:1044-1153): one workgroup = 64 queries
 // (consecutive in x order, sharp_perm) x 4 waves.  1-NN by brute force over
@@ -844,10 +850,7 @@ __global__ void __launch_bounds__(256) k_fa_search_surf_few(DevView v, int nb) {
 // result of the reference's exact nearest neighbour with ties to the lowest
 // index.  Then the 2nd point: wave w walks ring cscan + {-2, -1, +1, +2}[w]
 // and the four WalkBests merge in LDS.
-__global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
-    int s, chunk;
-    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
-    if (s >= v.S) return;
+__device__ __forceinline__ void search_corner_block(const DevView& v, int s, int chunk) {
     const StreamState& st = v.st[s];
     if (st.odo_phase != 1) return;
     const int nq = st.n_sharp;
@@ -949,12 +952,17 @@ __global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
     int32_t* indc = v.ind_corner + (size_t)s * v.cap_sharp * 2;
     indc[2 * i] = found ? bi : -1; indc[2 * i + 1] = found ? wb.index() : -1;
 }
+__global__ void __launch_bounds__(256) k_fa_search_corner(DevView v, int nb) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    search_corner_block(v, s, chunk);
+}
 
 // iterations iter0 .. iter0+4 of calculateTransformationSurf (FA:1270-1377)
 // or ...Corner (FA:1379-1478) for one stream
 template <int PH>
-__global__ void __launch_bounds__(256) k_fa_iter(DevView v, int iter0) {
-    const int s = blockIdx.x;
+__device__ __forceinline__ void fa_iter_block(const DevView& v, int s, int iter0) {
     StreamState& st = v.st[s];
     if (st.odo_phase != PH) return;
     const int tid = threadIdx.x, T = blockDim.x;
@@ -1084,6 +1092,34 @@ __global__ void __launch_bounds__(256) k_fa_iter(DevView v, int iter0) {
         for (int k = 0; k < 6; ++k) st.transformCur[k] = tc[k];
         if (s_ctl == 2 || iterCount >= 25) st.odo_phase = PH + 1;
     }
+}
+template <int PH>
+__global__ void __launch_bounds__(256) k_fa_iter(DevView v, int iter0) {
+    fa_iter_block<PH>(v, blockIdx.x, iter0);
+}
+
+// A context of a few streams: the correspondence search of iteration iter0
+// and the iterations iter0 .. iter0+4 after it in one launch — the stream's
+// last search workgroup to finish (a device-scope fence, then a ticket in
+// DevView::tick) runs k_fa_iter's workgroup.  Half the odometry's launches,
+// most of them empty once the stream has converged (a launch is ~5 us).
+template <int PH>
+__global__ void __launch_bounds__(256) k_fa_fused(DevView v, int nb, int iter0) {
+    int s, chunk;
+    xcd_stream_chunk(blockIdx.x, nb, s, chunk);
+    if (s >= v.S) return;
+    if (v.st[s].odo_phase != PH) return;   // every workgroup of the stream: the iterations would return too
+    if (PH == 0) search_surf_few_block(v, s, chunk);
+    else search_corner_block(v, s, chunk);
+    __shared__ int last;
+    __threadfence();   // this workgroup's correspondences, before its ticket
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(&v.tick[s], 1) == nb - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();   // every workgroup's correspondences, after the last ticket
+    if (threadIdx.x == 0) v.tick[s] = 0;   // (the next launch reads it after this one's end)
+    fa_iter_block<PH>(v, s, iter0);
 }
 
 // integrateTransformation (FA:1697-1725) + publishCloudsLast (FA:1759-1788)
@@ -1294,14 +1330,21 @@ int fa_odometry_run(slo_ctx* ctx, bool first_scan, bool fuse, bool defer) {
         const bool few = S <= SLO_ODO_FEW && !SLO_SURF_LINEAR;
         const int nbs = few ? (v.cap_flat + 255 / SURF_QL) / (256 / SURF_QL) : (v.cap_flat + 255) / 256;
         const int nbc = (v.cap_sharp + 63) / 64;
-        for (int b = 0; b < 5; ++b) {
-            if (few) SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf_few, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
-            else SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
-            SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
-        }
-        for (int b = 0; b < 5; ++b) {
-            SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
-            SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
+        if (few && SLO_ODO_FUSED && !(ctx->timing && !ctx->timing_only.empty())) {   // (a timing filter times each kernel)
+            for (int b = 0; b < 5; ++b)
+                SLO_LAUNCH(ctx, "fa_surf", k_fa_fused<0>, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs, 5 * b);
+            for (int b = 0; b < 5; ++b)
+                SLO_LAUNCH(ctx, "fa_corner", k_fa_fused<1>, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc, 5 * b);
+        } else {
+            for (int b = 0; b < 5; ++b) {
+                if (few) SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf_few, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
+                else SLO_LAUNCH(ctx, "fa_search_surf", k_fa_search_surf, dim3(xcd_grid(S, nbs)), dim3(256), 0, v, nbs);
+                SLO_LAUNCH(ctx, "fa_iter_surf", k_fa_iter<0>, dim3(S), dim3(256), 0, v, 5 * b);
+            }
+            for (int b = 0; b < 5; ++b) {
+                SLO_LAUNCH(ctx, "fa_search_corner", k_fa_search_corner, dim3(xcd_grid(S, nbc)), dim3(256), 0, v, nbc);
+                SLO_LAUNCH(ctx, "fa_iter_corner", k_fa_iter<1>, dim3(S), dim3(256), 0, v, 5 * b);
+            }
         }
     }
     if (int r = fa_ring_join(ctx)) return r;   // the less-flat cloud, forked by fa_features_run
